@@ -1,0 +1,303 @@
+/*
+ * emu_rx.h — C-ABI of the MI355X receive path (parse + Namespace/Client classify).
+ *
+ * Drop-in boundary for TRex-EMU's rx hot path.  The entry points replace, one for one,
+ * the Go surface listed below (paths relative to the reference tree):
+ *
+ *   emurx_rx_stream()        VethIFZmq.OnRxStream         src/emu/core/veth_zmq.go:277-320
+ *                            + per frame CThreadCtx.HandleRxPacket  src/emu/core/thread_ctx.go:365-375
+ *                            + Parser.ParsePacket / parsePacketL4   src/emu/core/parser.go:583-959
+ *                            + CThreadCtx.GetNs                     src/emu/core/thread_ctx.go:772-784
+ *                            + CNSCtx.CLookupBy{Mac,IPv4,IPv6,IPv6LocalGlobal} src/emu/core/ns_ctx.go:262-329
+ *                            (down to, not including, the ParserCb call: plugins stay in Go)
+ *   emurx_classify_dev()     the same, device-resident (frames + descriptors already in HBM)
+ *   emurx_register()         Parser.Register               src/emu/core/parser.go:528-565
+ *   emurx_ns_add/remove()    CThreadCtx.AddNs/RemoveNs      src/emu/core/thread_ctx.go:786-812
+ *   emurx_ns_set_plugins()   ns.PluginCtx presence          src/emu/core/plugin_ctx.go:257-265
+ *   emurx_client_add/remove  CNSCtx.AddClient/RemoveClient  src/emu/core/ns_ctx.go:332-440
+ *   emurx_client_update_*    CNSCtx.UpdateClientIpv4/Ipv6/DIpv6 src/emu/core/ns_ctx.go:442-533
+ *   emurx_client_set_ra()    CClient.Ipv6Router prefix      src/emu/core/client_ctx.go:60-66,279-295
+ *   emurx_hist_to_counters() ParserStats accumulation       src/emu/core/parser.go:67-119
+ *
+ * Conventions: plain C types, no exceptions or aborts cross the ABI; every call returns
+ * EMURX_OK (0) or a negative EMURX_E* code (mirrors PARSER_OK/PARSER_ERR, parser.go:41-44).
+ * Single caller thread per handle (the Go main goroutine, thread_ctx.go:397-419); every entry
+ * point re-binds the handle's device, so goroutine OS-thread migration is harmless.
+ */
+#ifndef EMU_RX_H
+#define EMU_RX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EMURX_ABI_VERSION 1
+
+/* ---- return codes -------------------------------------------------------------------- */
+#define EMURX_OK 0
+#define EMURX_EINVAL (-22)   /* bad argument */
+#define EMURX_ENOMEM (-12)   /* host or device allocation failed / capacity exceeded */
+#define EMURX_EEXIST (-17)   /* key already present (AddNs / AddClient duplicate) */
+#define EMURX_ENOENT (-2)    /* key not present */
+#define EMURX_EDEVICE (-5)   /* HIP runtime error */
+#define EMURX_ENOSPC (-28)   /* output buffer too small */
+
+#define EMURX_ID_NONE 0xFFFFFFFFu
+
+/* ---- limits (src/emu/core/mbuf.go:44-56, veth_zmq.go:8-22) ----------------------------- */
+#define EMURX_MAX_FRAME 9216u      /* MAX_PACKET_SIZE: MbufPoll.Alloc panics above */
+#define EMURX_ZMQ_MAGIC 0xBEEFu    /* ZMQ_PACKET_HEADER_MAGIC */
+
+/* ---- parser callbacks: order of the Parser struct fields, parser.go:509-520 ------------ */
+enum emurx_cb {
+    EMURX_CB_ARP = 0,
+    EMURX_CB_ICMP = 1,
+    EMURX_CB_IGMP = 2,
+    EMURX_CB_DHCP = 3,
+    EMURX_CB_DHCPSRV = 4,
+    EMURX_CB_DHCPV6 = 5,
+    EMURX_CB_MDNS = 6,
+    EMURX_CB_TCP = 7,
+    EMURX_CB_UDP = 8,
+    EMURX_CB_ICMPV6 = 9,
+    EMURX_CB_EAPOL = 10,
+    EMURX_CB_PPP = 11,
+    EMURX_NUM_CB = 12,
+    EMURX_CB_NONE = 0xFF
+};
+/* output queues: one per callback + one for every frame that reaches no callback */
+#define EMURX_Q_DROP 12
+#define EMURX_NUM_QUEUES 13
+
+/* ---- plugins whose per-Namespace / per-Client presence gates a callback --------------- */
+enum emurx_plugin {
+    EMURX_PLUG_ARP = 0,       /* "arp"       */
+    EMURX_PLUG_ICMP = 1,      /* "icmp"      */
+    EMURX_PLUG_IGMP = 2,      /* "igmp"      */
+    EMURX_PLUG_DHCP = 3,      /* "dhcp"      */
+    EMURX_PLUG_DHCPSRV = 4,   /* "dhcpsrv"   */
+    EMURX_PLUG_DHCPV6 = 5,    /* "dhcpv6"    */
+    EMURX_PLUG_MDNS = 6,      /* "mdns"      */
+    EMURX_PLUG_TRANSPORT = 7, /* "transport" */
+    EMURX_PLUG_IPV6 = 8,      /* "ipv6"      */
+    EMURX_PLUG_DOT1X = 9,     /* "dot1x"     */
+    EMURX_PLUG_PPP = 10,      /* "ppp"       */
+    EMURX_NUM_PLUG = 11
+};
+#define EMURX_PLUG_ALL ((1u << EMURX_NUM_PLUG) - 1u)
+
+/* ---- per-frame parse outcome (one per distinct return path of ParsePacket) ------------ */
+enum emurx_status {
+    EMURX_ST_OK = 0,                 /* callback `proto` invoked                             */
+    EMURX_ST_NOT_SUPPORTED = 1,      /* callback unregistered -> parserNotSupported, :524     */
+    EMURX_ST_PACKET_TOO_SHORT = 2,   /* errPacketIsTooShort        :770                       */
+    EMURX_ST_EAPOL_TOO_SHORT = 3,    /* errEAPolTooShort           :781                       */
+    EMURX_ST_ARP_TOO_SHORT = 4,      /* errArpTooShort             :792                       */
+    EMURX_ST_DOT1Q_TOO_SHORT = 5,    /* errDot1qTooShort           :802                       */
+    EMURX_ST_TOO_MANY_DOT1Q = 6,     /* errToManyDot1q             :806                       */
+    EMURX_ST_IPV4_TOO_SHORT = 7,     /* errIPv4TooShort            :824,846                   */
+    EMURX_ST_IPV4_HDR_TOO_SHORT = 8, /* errIPv4HeaderTooShort      :829,838,842               */
+    EMURX_ST_IPV4_FRAGMENT = 9,      /* errIPv4Fragment            :833                       */
+    EMURX_ST_IPV4_CS = 10,           /* errIPv4cs                  :854                       */
+    EMURX_ST_IPV6_TOO_SHORT = 11,    /* errIPv6TooShort            :866-877,894-926           */
+    EMURX_ST_IPV6_HOPLIMIT = 12,     /* errIPv6HopLimitDrop        :879                       */
+    EMURX_ST_IPV6_EMPTY = 13,        /* errIPv6Empty               :943                       */
+    EMURX_ST_IPV6_JUMBO = 14,        /* errIPv6OptJumbo            :938                       */
+    EMURX_ST_IPV6_FRAGMENT = 15,     /* errIPv6Fragment            :934                       */
+    EMURX_ST_ICMPV4_TOO_SHORT = 16,  /* errIcmpv4TooShort (ICMP and IGMP) :592,607            */
+    EMURX_ST_ICMPV4_CS = 17,         /* errIcmpv4Cse               :597                       */
+    EMURX_ST_TCP_TOO_SHORT = 18,     /* errTcpTooShort             :615,621                   */
+    EMURX_ST_TCP_CS = 19,            /* tcpCsErr                   :628                       */
+    EMURX_ST_UDP_TOO_SHORT = 20,     /* errUdpTooShort             :637                       */
+    EMURX_ST_UDP_CS = 21,            /* udpCsErr                   :644                       */
+    EMURX_ST_ICMPV6_TOO_SHORT = 22,  /* errIcmpv6TooShort          :685                       */
+    EMURX_ST_ICMPV6_CS = 23,         /* errIcmpv6Cse               :689                       */
+    EMURX_ST_ICMPV6_UNSUPPORTED = 24,/* errIcmpv6Unsupported       :715                       */
+    EMURX_ST_L4_UNSUPPORTED = 25,    /* errL4ProtoUnsupported      :720                       */
+    EMURX_ST_L3_UNSUPPORTED = 26,    /* errL3ProtoUnsupported      :954                       */
+    /* inputs on which the reference Go code panics: defined here, no counters */
+    EMURX_ST_PANIC_L4LEN = 27,       /* IPv4 totlen < IHL, span slice p[L4:L4+l4len] :597,628,644,689 */
+    EMURX_ST_PANIC_IPV6_OPT = 28,    /* processIpv6Options reads p[i+1] past the header :738  */
+    EMURX_ST_PANIC_NIL_EAPOL = 29,   /* EAPOL with dot1x unregistered: nil ParserCb :789       */
+    EMURX_ST_PANIC_MBUF = 30,        /* ZMQ frame > 9216 B: MbufPoll.Alloc panics, mbuf.go:106 */
+    EMURX_NUM_STATUS = 31
+};
+
+/* ---- lookup outcome of the callback's Namespace/Client rule (record.flags bits 4..6) -- */
+enum emurx_lookup {
+    EMURX_LK_NONE = 0,             /* not attempted: no callback is invoked for the frame */
+    EMURX_LK_NO_NS = 1,            /* GetNs(ps.Tun) == nil                                */
+    EMURX_LK_NS_NO_PLUGIN = 2,     /* ns.PluginCtx.Get(<plugin>) == nil                   */
+    EMURX_LK_NS_LEVEL = 3,         /* namespace-level dispatch, no client key (igmp, mdns,
+                                      ipv6 non-echo, arp reply)                           */
+    EMURX_LK_NO_CLIENT = 4,        /* the rule's key resolved no (acceptable) client     */
+    EMURX_LK_CLIENT_NO_PLUGIN = 5, /* client found, client.PluginCtx.Get(<plugin>) == nil */
+    EMURX_LK_CLIENT = 6            /* client_id is valid                                  */
+};
+#define EMURX_FLAG_RTALERT 0x01u   /* IPV6_M_RTALERT_ML, parser.go:48 */
+#define EMURX_FLAG_LK_SHIFT 4
+#define EMURX_FLAG_LK_MASK 0x70u
+
+/* ---- wire/device data structures ------------------------------------------------------ */
+/* frame descriptor: byte offset of the frame in the batch buffer, its length and vport.
+   (The ZMQ per-frame header 0xAA|vport|len, veth_zmq.go:296-305, carries the same fields.) */
+typedef struct emurx_desc {
+    uint32_t off;
+    uint16_t len;
+    uint8_t vport;
+    uint8_t pad;
+} emurx_desc;
+
+/* 32-byte record, one per frame, in frame order.  The numeric fields are exactly the
+   ParserPacketState the reference hands to a ParserCb (parser.go:51-61) plus the
+   CTunnelData that makes ps.Tun (thread_ctx.go:37-40), the callback tag, the outcome and
+   the resolved Namespace / Client ids. */
+typedef struct emurx_rec {
+    uint32_t ns_id;     /* id given at emurx_ns_add, or EMURX_ID_NONE                      */
+    uint32_t client_id; /* id given at emurx_client_add, or EMURX_ID_NONE                  */
+    uint32_t vlan[2];   /* CTunnelData.Vlans: (TPID<<16)|VID, PCP/DEI cleared, 0 if absent */
+    uint16_t vport;     /* CTunnelData.Vport                                               */
+    uint16_t l3;        /* ParserPacketState.L3                                            */
+    uint16_t l4;        /* ParserPacketState.L4                                            */
+    uint16_t l7;        /* ParserPacketState.L7                                            */
+    uint16_t l7_len;    /* ParserPacketState.L7Len (uint16 wraparound preserved)           */
+    uint8_t next_hdr;   /* ParserPacketState.NextHeader                                    */
+    uint8_t proto;      /* enum emurx_cb of the callback reached, EMURX_CB_NONE on errors  */
+    uint8_t status;     /* enum emurx_status                                               */
+    uint8_t flags;      /* bit0 EMURX_FLAG_RTALERT (ps.Flags); bits 4..6 enum emurx_lookup */
+    uint16_t rsv;
+} emurx_rec;
+
+/* Outcome histogram: EMURX_HIST_BINS × {pkts, bytes}.  Bin = hist_bin(status, proto).
+   Counter deltas are derived from it by emurx_hist_to_counters(). */
+#define EMURX_HIST_BINS 64
+#define EMURX_HIST_BIN(status, proto) \
+    ((status) <= EMURX_ST_NOT_SUPPORTED ? (unsigned)(status) * EMURX_NUM_CB + (unsigned)(proto) \
+                                        : 2u * EMURX_NUM_CB + (unsigned)(status) - 2u)
+
+/* ParserStats in declaration order, parser.go:67-119 (all uint64). */
+enum emurx_parser_counter {
+    EMURX_PC_errInternalHandler = 0, EMURX_PC_errParser, EMURX_PC_errEAPolTooShort,
+    EMURX_PC_errArpTooShort, EMURX_PC_errIcmpv4TooShort, EMURX_PC_errIgmpv4TooShort,
+    EMURX_PC_errUdpTooShort, EMURX_PC_errTcpTooShort, EMURX_PC_errDot1qTooShort,
+    EMURX_PC_errToManyDot1q, EMURX_PC_errIPv4TooShort, EMURX_PC_errIPv4HeaderTooShort,
+    EMURX_PC_errIPv4Fragment, EMURX_PC_errIPv4cs, EMURX_PC_errTCP, EMURX_PC_errUDP,
+    EMURX_PC_eapolPkts, EMURX_PC_eapolBytes, EMURX_PC_arpPkts, EMURX_PC_arpBytes,
+    EMURX_PC_icmpPkts, EMURX_PC_icmpBytes, EMURX_PC_igmpPkts, EMURX_PC_igmpBytes,
+    EMURX_PC_dhcpPkts, EMURX_PC_dhcpBytes, EMURX_PC_dhcpSrvPkts, EMURX_PC_dhcpSrvBytes,
+    EMURX_PC_mDnsPkts, EMURX_PC_mDnsBytes, EMURX_PC_tcpPkts, EMURX_PC_tcpBytes,
+    EMURX_PC_udpPkts, EMURX_PC_udpBytes, EMURX_PC_udpCsErr, EMURX_PC_tcpCsErr,
+    EMURX_PC_errIPv6TooShort, EMURX_PC_errIPv6HopLimitDrop, EMURX_PC_errIPv6Empty,
+    EMURX_PC_errIPv6OptJumbo, EMURX_PC_errIPv6Fragment, EMURX_PC_errIcmpv6TooShort,
+    EMURX_PC_errIcmpv6Cse, EMURX_PC_errIcmpv4Cse, EMURX_PC_errIcmpv6Unsupported,
+    EMURX_PC_Icmpv6Pkt, EMURX_PC_Icmpv6Bytes, EMURX_PC_errL4ProtoUnsupported,
+    EMURX_PC_errL3ProtoUnsupported, EMURX_PC_errPacketIsTooShort,
+    EMURX_NUM_PARSER_COUNTERS
+};
+
+typedef struct emurx_counters {
+    uint64_t parser[EMURX_NUM_PARSER_COUNTERS]; /* ParserStats deltas (parse-side errParser
+                                                   included; callback returns are added by
+                                                   the caller, thread_ctx.go:365-375)      */
+    uint64_t rx_pkts;      /* VethStats.RxPkts    veth_zmq.go:233 */
+    uint64_t rx_bytes;     /* VethStats.RxBytes   veth_zmq.go:234 */
+    uint64_t rx_batch;     /* VethStats.RxBatch   veth_zmq.go:278 */
+    uint64_t rx_parse_err; /* VethStats.RxParseErr veth_zmq.go:281-312 */
+    uint64_t ref_panic;    /* frames with an EMURX_ST_PANIC_* status (reference would abort) */
+} emurx_counters;
+
+typedef struct emurx_cfg {
+    int device;            /* HIP device ordinal */
+    uint32_t max_ns;       /* ns ids must be < max_ns */
+    uint32_t max_clients;  /* client ids must be < max_clients */
+    uint32_t max_frames;   /* frames per batch (device scratch is sized for it) */
+    uint32_t max_bytes;    /* bytes per host batch (emurx_rx_stream staging) */
+} emurx_cfg;
+
+/* Device-resident outputs of one batch (all pointers are device memory). */
+typedef struct emurx_dev_out {
+    emurx_rec* rec;        /* [n] records, frame order                                  */
+    uint32_t* qlist;       /* [EMURX_NUM_QUEUES * qcap] frame indices; queue q starts at q*qcap */
+    uint32_t qcap;         /* >= n */
+    uint32_t* qcount;      /* [16] frames per queue (first 13 used)                      */
+    uint64_t* hist;        /* [2 * EMURX_HIST_BINS] {pkts, bytes} per bin; ACCUMULATED    */
+} emurx_dev_out;
+
+typedef struct emurx_ctx emurx_t;
+
+/* ---- lifecycle --------------------------------------------------------------------- */
+int emurx_abi_version(void);
+int emurx_open(const emurx_cfg* cfg, emurx_t** out);
+void emurx_close(emurx_t* h);
+const char* emurx_strerror(int code);
+
+/* ---- parser registration (Parser.Register / Init, parser.go:528-581) ------------------ */
+int emurx_register(emurx_t* h, const char* protocol);     /* "arp","icmp",...,"transport" */
+int emurx_set_callbacks_mask(emurx_t* h, uint32_t mask);  /* bit i = enum emurx_cb i live */
+uint32_t emurx_get_callbacks_mask(const emurx_t* h);
+
+/* ---- table sync (control plane runs on the same goroutine as rx) ---------- */
+/* key = CTunnelKey bytes (thread_ctx.go:58,92-97): [0:2] vport LE, [2:4] 0, [4:8] Vlans[0] LE,
+   [8:12] Vlans[1] LE. */
+int emurx_ns_add(emurx_t* h, const uint8_t key[12], uint32_t ns_id, uint32_t plugin_mask);
+int emurx_ns_remove(emurx_t* h, const uint8_t key[12]);
+int emurx_ns_set_plugins(emurx_t* h, uint32_t ns_id, uint32_t plugin_mask);
+/* ipv4 / ipv6 / dhcpv6 may be NULL or all-zero (= absent, as Ipv4Key.IsZero etc.). */
+int emurx_client_add(emurx_t* h, uint32_t ns_id, uint32_t client_id, const uint8_t mac[6],
+                     const uint8_t ipv4[4], const uint8_t ipv6[16], const uint8_t dhcpv6[16],
+                     uint32_t plugin_mask);
+int emurx_client_remove(emurx_t* h, uint32_t ns_id, const uint8_t mac[6]);
+int emurx_client_set_plugins(emurx_t* h, uint32_t client_id, uint32_t plugin_mask);
+int emurx_client_update_ipv4(emurx_t* h, uint32_t client_id, const uint8_t ipv4[4]);
+int emurx_client_update_ipv6(emurx_t* h, uint32_t client_id, const uint8_t ipv6[16]);
+int emurx_client_update_dipv6(emurx_t* h, uint32_t client_id, const uint8_t dhcpv6[16]);
+int emurx_client_set_ra(emurx_t* h, uint32_t client_id, const uint8_t prefix[16],
+                        uint8_t prefix_len);
+/* Upload pending table deltas to the device (enqueued on `stream`, or the handle's own
+   stream when NULL).  Called implicitly by emurx_rx_stream. */
+int emurx_sync(emurx_t* h, void* stream);
+
+/* ---- data path ---------------------------------------------------------------------- */
+/* Host batch, ZMQ wire format (veth_zmq.go:8-22).  Decodes the stream exactly like
+   OnRxStream (uint16 running offset, abort-on-header-error), stages it in pinned memory,
+   parses + classifies on the GPU and returns records in frame order plus per-queue frame
+   index lists.  out_qoff[q]..out_qoff[q+1] indexes out_qlist for queue q
+   (out_qoff has EMURX_NUM_QUEUES+1 entries).  *n_out = frames decoded.  `delta` receives
+   the ParserStats + VethStats deltas of this batch. */
+int emurx_rx_stream(emurx_t* h, const uint8_t* msg, size_t len, emurx_rec* out_rec,
+                    uint32_t* out_qlist, uint32_t out_cap, uint32_t* n_out,
+                    uint32_t out_qoff[EMURX_NUM_QUEUES + 1], emurx_counters* delta);
+
+/* Device-resident batch: frames (d_frames) and descriptors (d_desc) already in HBM.
+   Enqueues parse+classify+compaction on `stream` (hipStream_t, NULL = handle stream) and
+   returns without synchronising.  out->hist is accumulated into (zero it to reset). */
+int emurx_classify_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_desc,
+                       uint32_t n, const emurx_dev_out* out, void* stream);
+
+/* Device-resident, parse only (no table lookups): records with ns_id/client_id NONE and
+   lookup EMURX_LK_NONE.  Used by the multi-GPU path before the Namespace all-to-all. */
+int emurx_parse_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_desc,
+                    uint32_t n, const emurx_dev_out* out, void* stream);
+
+/* Build descriptors for a ZMQ message on the host (the sequential offset walk of
+   OnRxStream).  Returns frames decoded in *n_out; *parse_err = 1 when the walk stopped on a
+   header error (RxParseErr).  Frames longer than EMURX_MAX_FRAME stop the walk with
+   *parse_err = 2 (the reference panics there). */
+int emurx_zmq_descriptors(const uint8_t* msg, size_t len, emurx_desc* out, uint32_t cap,
+                          uint32_t* n_out, int* parse_err);
+
+/* ParserStats delta from an outcome histogram (pure host arithmetic). */
+void emurx_hist_to_counters(const uint64_t hist[2 * EMURX_HIST_BINS], emurx_counters* out);
+
+/* Wall time of the last emurx_classify_dev's kernels measured with HIP events on the
+   launch stream (ms); -1 if timing is off.  Timing is enabled by emurx_set_timing(h, 1). */
+int emurx_set_timing(emurx_t* h, int enable);
+int emurx_last_kernel_ms(emurx_t* h, float* parse_ms, float* compact_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EMU_RX_H */

@@ -1,0 +1,166 @@
+"""ctypes binding of the C-ABI declared in include/emu_rx.h (libemurx.so).
+
+The shared library is built in-tree by `make -C trex-emu_amd` (or __graft_entry__.build()).
+Loading fails loudly when it is missing: there is no CPU fallback for the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+PKG_ROOT = Path(__file__).resolve().parent.parent          # trex-emu_amd/
+REPO_ROOT = PKG_ROOT.parent
+LIB_PATH = PKG_ROOT / "lib" / "libemurx.so"
+
+# ---- constants (emu_rx.h) ---------------------------------------------------------------
+EMURX_OK = 0
+EMURX_EINVAL, EMURX_ENOMEM, EMURX_EEXIST, EMURX_ENOENT = -22, -12, -17, -2
+EMURX_EDEVICE, EMURX_ENOSPC = -5, -28
+ID_NONE = 0xFFFFFFFF
+MAX_FRAME = 9216
+
+CB_NAMES = ["arp", "icmp", "igmp", "dhcp", "dhcpsrv", "dhcpv6", "mdns", "tcp", "udp",
+            "icmpv6", "eapol", "ppp"]
+(CB_ARP, CB_ICMP, CB_IGMP, CB_DHCP, CB_DHCPSRV, CB_DHCPV6, CB_MDNS, CB_TCP, CB_UDP,
+ CB_ICMPV6, CB_EAPOL, CB_PPP) = range(12)
+NUM_CB = 12
+CB_NONE = 0xFF
+Q_DROP = 12
+NUM_QUEUES = 13
+
+PLUG_NAMES = ["arp", "icmp", "igmp", "dhcp", "dhcpsrv", "dhcpv6", "mdns", "transport", "ipv6",
+              "dot1x", "ppp"]
+PLUG_ALL = (1 << len(PLUG_NAMES)) - 1
+
+STATUS_NAMES = [
+    "OK", "NOT_SUPPORTED", "PACKET_TOO_SHORT", "EAPOL_TOO_SHORT", "ARP_TOO_SHORT",
+    "DOT1Q_TOO_SHORT", "TOO_MANY_DOT1Q", "IPV4_TOO_SHORT", "IPV4_HDR_TOO_SHORT", "IPV4_FRAGMENT",
+    "IPV4_CS", "IPV6_TOO_SHORT", "IPV6_HOPLIMIT", "IPV6_EMPTY", "IPV6_JUMBO", "IPV6_FRAGMENT",
+    "ICMPV4_TOO_SHORT", "ICMPV4_CS", "TCP_TOO_SHORT", "TCP_CS", "UDP_TOO_SHORT", "UDP_CS",
+    "ICMPV6_TOO_SHORT", "ICMPV6_CS", "ICMPV6_UNSUPPORTED", "L4_UNSUPPORTED", "L3_UNSUPPORTED",
+    "PANIC_L4LEN", "PANIC_IPV6_OPT", "PANIC_NIL_EAPOL", "PANIC_MBUF"]
+ST = {n: i for i, n in enumerate(STATUS_NAMES)}
+LOOKUP_NAMES = ["NONE", "NO_NS", "NS_NO_PLUGIN", "NS_LEVEL", "NO_CLIENT", "CLIENT_NO_PLUGIN",
+                "CLIENT"]
+LK = {n: i for i, n in enumerate(LOOKUP_NAMES)}
+FLAG_RTALERT = 0x01
+
+PARSER_COUNTER_NAMES = [
+    "errInternalHandler", "errParser", "errEAPolTooShort", "errArpTooShort", "errIcmpv4TooShort",
+    "errIgmpv4TooShort", "errUdpTooShort", "errTcpTooShort", "errDot1qTooShort", "errToManyDot1q",
+    "errIPv4TooShort", "errIPv4HeaderTooShort", "errIPv4Fragment", "errIPv4cs", "errTCP", "errUDP",
+    "eapolPkts", "eapolBytes", "arpPkts", "arpBytes", "icmpPkts", "icmpBytes", "igmpPkts",
+    "igmpBytes", "dhcpPkts", "dhcpBytes", "dhcpSrvPkts", "dhcpSrvBytes", "mDnsPkts", "mDnsBytes",
+    "tcpPkts", "tcpBytes", "udpPkts", "udpBytes", "udpCsErr", "tcpCsErr", "errIPv6TooShort",
+    "errIPv6HopLimitDrop", "errIPv6Empty", "errIPv6OptJumbo", "errIPv6Fragment",
+    "errIcmpv6TooShort", "errIcmpv6Cse", "errIcmpv4Cse", "errIcmpv6Unsupported", "Icmpv6Pkt",
+    "Icmpv6Bytes", "errL4ProtoUnsupported", "errL3ProtoUnsupported", "errPacketIsTooShort"]
+NUM_PARSER_COUNTERS = len(PARSER_COUNTER_NAMES)
+HIST_BINS = 64
+
+# ---- record / descriptor layouts --------------------------------------------------------
+REC_DTYPE = np.dtype([
+    ("ns_id", "<u4"), ("client_id", "<u4"), ("vlan0", "<u4"), ("vlan1", "<u4"),
+    ("vport", "<u2"), ("l3", "<u2"), ("l4", "<u2"), ("l7", "<u2"), ("l7_len", "<u2"),
+    ("next_hdr", "u1"), ("proto", "u1"), ("status", "u1"), ("flags", "u1"), ("rsv", "<u2")])
+assert REC_DTYPE.itemsize == 32
+DESC_DTYPE = np.dtype([("off", "<u4"), ("len", "<u2"), ("vport", "u1"), ("pad", "u1")])
+assert DESC_DTYPE.itemsize == 8
+
+
+class Cfg(C.Structure):
+    _fields_ = [("device", C.c_int), ("max_ns", C.c_uint32), ("max_clients", C.c_uint32),
+                ("max_frames", C.c_uint32), ("max_bytes", C.c_uint32)]
+
+
+class Counters(C.Structure):
+    _fields_ = [("parser", C.c_uint64 * NUM_PARSER_COUNTERS), ("rx_pkts", C.c_uint64),
+                ("rx_bytes", C.c_uint64), ("rx_batch", C.c_uint64),
+                ("rx_parse_err", C.c_uint64), ("ref_panic", C.c_uint64)]
+
+    def as_dict(self):
+        d = {n: int(self.parser[i]) for i, n in enumerate(PARSER_COUNTER_NAMES)}
+        for k in ("rx_pkts", "rx_bytes", "rx_batch", "rx_parse_err", "ref_panic"):
+            d[k] = int(getattr(self, k))
+        return d
+
+
+class DevOut(C.Structure):
+    _fields_ = [("rec", C.c_void_p), ("qlist", C.c_void_p), ("qcap", C.c_uint32),
+                ("qcount", C.c_void_p), ("hist", C.c_void_p)]
+
+
+# (name, restype, argtypes) — every symbol include/emu_rx.h declares
+_P = C.c_void_p
+_U8P = C.c_void_p
+SIGNATURES = [
+    ("emurx_abi_version", C.c_int, []),
+    ("emurx_open", C.c_int, [C.POINTER(Cfg), C.POINTER(C.c_void_p)]),
+    ("emurx_close", None, [_P]),
+    ("emurx_strerror", C.c_char_p, [C.c_int]),
+    ("emurx_register", C.c_int, [_P, C.c_char_p]),
+    ("emurx_set_callbacks_mask", C.c_int, [_P, C.c_uint32]),
+    ("emurx_get_callbacks_mask", C.c_uint32, [_P]),
+    ("emurx_ns_add", C.c_int, [_P, _U8P, C.c_uint32, C.c_uint32]),
+    ("emurx_ns_remove", C.c_int, [_P, _U8P]),
+    ("emurx_ns_set_plugins", C.c_int, [_P, C.c_uint32, C.c_uint32]),
+    ("emurx_client_add", C.c_int, [_P, C.c_uint32, C.c_uint32, _U8P, _U8P, _U8P, _U8P, C.c_uint32]),
+    ("emurx_client_remove", C.c_int, [_P, C.c_uint32, _U8P]),
+    ("emurx_client_set_plugins", C.c_int, [_P, C.c_uint32, C.c_uint32]),
+    ("emurx_client_update_ipv4", C.c_int, [_P, C.c_uint32, _U8P]),
+    ("emurx_client_update_ipv6", C.c_int, [_P, C.c_uint32, _U8P]),
+    ("emurx_client_update_dipv6", C.c_int, [_P, C.c_uint32, _U8P]),
+    ("emurx_client_set_ra", C.c_int, [_P, C.c_uint32, _U8P, C.c_uint8]),
+    ("emurx_sync", C.c_int, [_P, _P]),
+    ("emurx_rx_stream", C.c_int, [_P, _U8P, C.c_size_t, _P, _P, C.c_uint32,
+                                  C.POINTER(C.c_uint32), _P, C.POINTER(Counters)]),
+    ("emurx_classify_dev", C.c_int, [_P, _P, _P, C.c_uint32, C.POINTER(DevOut), _P]),
+    ("emurx_parse_dev", C.c_int, [_P, _P, _P, C.c_uint32, C.POINTER(DevOut), _P]),
+    ("emurx_zmq_descriptors", C.c_int, [_U8P, C.c_size_t, _P, C.c_uint32,
+                                        C.POINTER(C.c_uint32), C.POINTER(C.c_int)]),
+    ("emurx_hist_to_counters", None, [_P, C.POINTER(Counters)]),
+    ("emurx_set_timing", C.c_int, [_P, C.c_int]),
+    ("emurx_last_kernel_ms", C.c_int, [_P, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
+]
+
+_lib = None
+
+
+def load(path: str | os.PathLike | None = None):
+    """Load libemurx.so (raises OSError when it was not built)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path else LIB_PATH
+    if not p.exists():
+        raise OSError(f"libemurx.so not built at {p}: run `make -C {PKG_ROOT}` "
+                      "(there is no CPU fallback for the product path)")
+    lib = C.CDLL(str(p), mode=C.RTLD_GLOBAL)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(rc: int, what: str = ""):
+    if rc != EMURX_OK:
+        msg = load().emurx_strerror(rc).decode()
+        raise RuntimeError(f"{what}: emurx error {rc} ({msg})")
+    return rc
+
+
+def ptr(a) -> int | None:
+    """Address of a numpy array / bytes / torch tensor (None passes NULL)."""
+    if a is None:
+        return None
+    if hasattr(a, "data_ptr"):
+        return a.data_ptr()
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    raise TypeError(f"pass numpy arrays or tensors, not {type(a)}")
