@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""Benchmark: Mpkt/s of device-resident rx parse+classify (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config B|C|E] [--frames F]
+
+A step = one batch through the hot path: emurx_classify_dev (k_parse: decode + checksums +
+Namespace/Client lookups + records; k_scan + k_compact: stable per-callback queues;
+outcome histogram) over F frames already resident in HBM.  Default workload = config B
+(1M x 64 B untagged IPv4/UDP, 1 Namespace / 1 Client), the configuration the metric is
+quoted on.  For N > 1 (torchrun, one rank per GPU) every rank processes its own F-frame
+shard against replicated tables: frames are independent, so there is no data-path
+collective (weak scaling); value = frames over all ranks / max-over-ranks time.
+
+The JSON line carries `roofline` (algorithmic bytes per frame = frame_len + 8 B descriptor
++ 32 B record, over the parse kernel's mean HIP-event duration on the launch stream) and
+`cpu_baseline` (the oracle, a single-threaded C restatement of the Go path, timed on this
+host's cores over a bounded sample of the same workload; rank 0 at N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "trex-emu_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+METRIC = "Mpkt/s device-resident rx parse+classify, 1M×64B batch, 1/2/4/8 MI355X"
+
+
+def parse_args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="B", choices=["B", "C", "E"])
+    ap.add_argument("--frames", type=int, default=1 << 20, help="frames per GPU per step")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--host-path", action="store_true",
+                    help="also time the host-inclusive path (pinned H2D + kernels + D2H)")
+    return ap.parse_args()
+
+
+def workload(cfg, n, rank):
+    from emurx import synth
+    if cfg == "B":
+        return synth.config_b(n, seed=synth.SEED_B + rank)
+    if cfg == "C":
+        return synth.config_c(n, rank=rank)
+    return synth.config_e(n, rank=rank)
+
+
+def cpu_baseline(w, budget_s):
+    """Oracle (C restatement of the Go path) on 1 host core over repeated passes of a
+    bounded sample of the same frames.  Test infrastructure: imported only here."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import numpy as np
+    import pyoracle
+    from emurx import synth
+    pyoracle.build()
+    o = pyoracle.Oracle()
+    synth.load_tables(w, o)
+    sample = min(len(w["desc"]), 1 << 18)
+    desc = np.ascontiguousarray(w["desc"][:sample])
+    o.rx_batch(w["buf"], desc[:1024])  # warm
+    frames, t0 = 0, time.perf_counter()
+    while True:
+        o.rx_batch(w["buf"], desc)
+        frames += sample
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": round(frames / el / 1e6, 3), "unit": "Mpkt/s", "cores": 1, "kind": "port",
+            "sample": f"{sample} frames of config {w['name']} x {frames // sample} passes "
+                      f"({el:.1f} s), oracle/emurx_oracle.c rx_batch (parse + classify + queues + counters)"}
+
+
+def main():
+    a = parse_args()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", str(a.gpus)))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus and "RANK" in os.environ:
+        print(f"warning: WORLD_SIZE={world} != --gpus {a.gpus}", file=sys.stderr)
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from emurx import abi
+    from emurx.rx import RxPath
+
+    n = a.frames
+    w = workload(a.config, n, rank)
+    max_ns = max(4096, len(w["ns"]))
+    max_cl = max(65536, len(w["clients"]["cid"]))
+    rx = RxPath(local, max_ns=max_ns, max_clients=max_cl, max_frames=n)
+    rx.register_all()
+    from emurx import synth
+    synth.load_tables(w, rx)
+
+    dev = torch.device("cuda", local)
+    buf = torch.from_numpy(w["buf"]).to(dev)
+    desc = torch.from_numpy(w["desc"].view(np.uint8).copy()).to(dev)
+    rec = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    qlist = torch.empty(n, dtype=torch.int32, device=dev)
+    qoff = torch.empty(16, dtype=torch.int32, device=dev)
+    hist = torch.zeros(2 * abi.HIST_BINS, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    rx.sync(stream.cuda_stream)
+
+    def step():
+        hist.zero_()
+        rx.classify_dev(buf, desc, n, rec, qlist, qoff, hist, stream=stream)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    # sanity of the outcome on this rank (counts only; parity lives in tests/)
+    h = hist.cpu().numpy().view(np.uint64)
+    assert int(h[0::2].sum()) == n, "histogram does not cover the batch"
+
+    rx.set_timing(a.steps + 8)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    pk, cp = rx.kernel_times()
+    rx.set_timing(0)
+
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    total_frames = n * a.steps * world
+    value = total_frames / el / 1e6
+    ms_per_step = el / a.steps * 1e3
+
+    # roofline of the dominant kernel (k_parse): algorithmic bytes per launch / mean duration
+    alg_bytes = w["nbytes"] + 8 * n + 32 * n
+    parse_s = float(np.mean(pk)) * 1e-3 if len(pk) else float("nan")
+    achieved = alg_bytes / parse_s / 1e9
+    traffic = None
+    pmc = ROOT / "profiles" / f"pmc_config{a.config}.json"
+    if pmc.exists():
+        try:
+            traffic = json.loads(pmc.read_text()).get("k_parse_hbm_bytes_per_launch")
+        except Exception:  # noqa: BLE001
+            traffic = None
+
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "Mpkt/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded, valid wire-format frames)",
+        "config": {
+            "workload": {"B": "B: 1M x 64B untagged IPv4/UDP, 1 ns / 1 client",
+                         "C": "C: 1M mixed dot1q/QinQ IPv4/IPv6, 4K ns / 64K clients",
+                         "E": "E: IMIX 64/594/1518 TCP/UDP, 4K ns / 64K clients"}[a.config],
+            "frames_per_gpu": n,
+            "frame_bytes_per_gpu": w["nbytes"],
+            "parallelism": f"frame shards x{world}, replicated tables, no collective",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "kernel": "k_parse",
+            "alg_bytes_per_launch": alg_bytes,
+            "kernel_ms_mean": round(parse_s * 1e3, 5),
+            "compact_ms_mean": round(float(np.mean(cp)), 5) if len(cp) else None,
+        },
+    }
+    if a.host_path:
+        out["host_inclusive"] = host_path_rate(rx, w)
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(w, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    rx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def host_path_rate(rx, w, msgs=200):
+    """emurx_rx_stream over ZMQ-sized messages (64 frames, as TRex sends them): pinned
+    H2D + kernels + D2H + host decode, synchronous per message."""
+    import numpy as np
+    from emurx import frames as F
+    d = w["desc"][: 64 * msgs]
+    fr = [w["buf"][x["off"]:x["off"] + x["len"]].tobytes() for x in d]
+    batch = [F.zmq_pack(fr[i:i + 64]) for i in range(0, len(fr), 64)]
+    rx.on_rx_stream(batch[0])
+    t0 = time.perf_counter()
+    for m in batch:
+        rx.on_rx_stream(m, cap=64)
+    el = time.perf_counter() - t0
+    return {"mpkts": round(len(fr) / el / 1e6, 4), "frames_per_msg": 64, "msgs": len(batch)}
+
+
+if __name__ == "__main__":
+    main()

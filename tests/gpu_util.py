@@ -1,0 +1,99 @@
+"""Helpers shared by the GPU tests: run the device path through the C-ABI and fetch the
+outputs, build tables for frame sets."""
+import numpy as np
+
+from emurx import abi
+
+
+def to_dev(a: np.ndarray, pad: int = 64):
+    import torch
+    b = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
+    t = torch.zeros(b.size + pad, dtype=torch.uint8, device="cuda")
+    if b.size:
+        t[: b.size] = torch.from_numpy(b.copy()).to("cuda")
+    return t
+
+
+def run_dev(rx, buf, desc, classify=True):
+    """-> rec, qlist, qoff(14), hist(2*64) as numpy, via emurx_classify_dev / parse_dev."""
+    import torch
+    n = len(desc)
+    tb, td = to_dev(buf), to_dev(desc)
+    rec = torch.zeros(max(n, 1) * 32, dtype=torch.uint8, device="cuda")
+    qlist = torch.zeros(max(n, 1), dtype=torch.int32, device="cuda")
+    qoff = torch.full((16,), -1, dtype=torch.int32, device="cuda")
+    hist = torch.zeros(2 * abi.HIST_BINS, dtype=torch.int64, device="cuda")
+    rx.classify_dev(tb, td, n, rec, qlist, qoff, hist, classify=classify)
+    torch.cuda.synchronize()
+    r = rec.cpu().numpy()[: n * 32].view(abi.REC_DTYPE)
+    return (r, qlist.cpu().numpy()[:n].view(np.uint32), qoff.cpu().numpy()[:14].view(np.uint32),
+            hist.cpu().numpy().view(np.uint64))
+
+
+def rec_diff(a, b, limit=5):
+    """Human-readable first differences between two record arrays."""
+    a = np.asarray(a)
+    b = np.asarray(b)
+    if len(a) != len(b):
+        return f"length {len(a)} != {len(b)}"
+    A = np.ascontiguousarray(a).view(np.uint8).reshape(-1, 32)
+    B = np.ascontiguousarray(b).view(np.uint8).reshape(-1, 32)
+    bad = np.nonzero((A != B).any(1))[0]
+    out = [f"{len(bad)} differing records"]
+    for i in bad[:limit]:
+        fa = {k: int(a[i][k]) for k in abi.REC_DTYPE.names}
+        fb = {k: int(b[i][k]) for k in abi.REC_DTYPE.names}
+        out.append(f"  [{i}] gpu={fa}\n       orc={fb}")
+    return "\n".join(out)
+
+
+def frames_tables(frames, vport=1):
+    """Namespace + Client tables derived from a frame set: a Namespace per distinct
+    (vport, tags) and, for unicast destination MACs, a client owning that MAC and the
+    frame's destination IPv4 / IPv6 (deduplicated)."""
+    from emurx import frames as F
+    import struct
+    ns = {}
+    clients = {}
+    used4, used6 = set(), set()
+    for f in frames:
+        if len(f) < 14:
+            continue
+        et = struct.unpack(">H", f[12:14])[0]
+        off, vl = 14, []
+        while et in (0x8100, 0x88A8) and len(f) >= off + 4 and len(vl) < 2:
+            vl.append(struct.unpack(">I", f[off - 2:off + 2])[0] & 0xFFFF0FFF)
+            et = struct.unpack(">H", f[off + 2:off + 4])[0]
+            off += 4
+        vl += [0] * (2 - len(vl))
+        key = F.tunnel_key(vport, vl[0], vl[1])
+        nsid = ns.setdefault(key, len(ns))
+        dmac = bytes(f[0:6])
+        if dmac[0] & 1 or dmac == bytes(6):
+            continue
+        ip4 = ip6 = None
+        if et == 0x0800 and len(f) >= off + 20:
+            ip4 = bytes(f[off + 16:off + 20])
+        if et == 0x86DD and len(f) >= off + 40:
+            ip6 = bytes(f[off + 24:off + 40])
+        k = (nsid, dmac)
+        if k not in clients:
+            if ip4 is not None and ((nsid, ip4) in used4 or ip4 == bytes(4)):
+                ip4 = None
+            if ip6 is not None and ((nsid, ip6) in used6 or ip6 == bytes(16)):
+                ip6 = None
+            if ip4:
+                used4.add((nsid, ip4))
+            if ip6:
+                used6.add((nsid, ip6))
+            clients[k] = (len(clients), ip4, ip6)
+    return ns, clients
+
+
+def load_frame_tables(targets, ns, clients, plug_ns=abi.PLUG_ALL, plug_cl=abi.PLUG_ALL):
+    for t in targets:
+        for key, nsid in ns.items():
+            assert t.ns_add(key, nsid, plug_ns) == 0
+        for (nsid, mac), (cid, ip4, ip6) in clients.items():
+            p = plug_cl if cid % 7 else plug_cl & ~(1 << 7)  # some clients without transport
+            assert t.client_add(nsid, cid, mac, ip4, ip6, None, p) == 0

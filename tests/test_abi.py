@@ -1,0 +1,125 @@
+"""C-ABI checks that need no GPU: libemurx.so loads, exports every function declared in
+include/emu_rx.h, record/descriptor layouts match, and the host-only entry points
+(ZMQ descriptor walk, histogram -> ParserStats) agree with the oracle."""
+import ctypes as C
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from emurx import abi
+from emurx import frames as F
+
+ROOT = Path(__file__).resolve().parent.parent
+HEADER = ROOT / "include" / "emu_rx.h"
+
+
+def declared_functions():
+    txt = HEADER.read_text()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(emurx_[a-z0-9_]+)\s*\(", txt)) - {"emurx_desc", "emurx_rec"})
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not abi.LIB_PATH.exists():
+        import subprocess
+        subprocess.run(["make", "-s", "-C", str(abi.PKG_ROOT)], check=True)
+    return abi.load()
+
+
+def test_exports_every_declared_symbol(lib):
+    names = declared_functions()
+    assert len(names) >= 20
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    bound = {s[0] for s in abi.SIGNATURES}
+    assert set(names) == bound, set(names) ^ bound
+
+
+def test_abi_version(lib):
+    assert lib.emurx_abi_version() == 1
+
+
+def test_layouts():
+    import pyoracle
+    assert abi.REC_DTYPE.itemsize == 32 and abi.DESC_DTYPE.itemsize == 8
+    assert abi.REC_DTYPE == pyoracle.REC_DTYPE and abi.DESC_DTYPE == pyoracle.DESC_DTYPE
+    assert C.sizeof(abi.Counters) == 8 * (abi.NUM_PARSER_COUNTERS + 5)
+    # field offsets as emu_rx.h lays emurx_rec out
+    off = {n: abi.REC_DTYPE.fields[n][1] for n in abi.REC_DTYPE.names}
+    assert off["vport"] == 16 and off["l7_len"] == 24 and off["next_hdr"] == 26
+    assert off["status"] == 28 and off["flags"] == 29
+
+
+def test_strerror(lib):
+    assert lib.emurx_strerror(0) == b"ok"
+    assert lib.emurx_strerror(-22) == b"invalid argument"
+
+
+def test_open_rejects_bad_cfg(lib):
+    h = C.c_void_p()
+    cfg = abi.Cfg(0, 0, 0, 0, 0)
+    assert lib.emurx_open(C.byref(cfg), C.byref(h)) == abi.EMURX_EINVAL
+
+
+def _rand_msgs(rng, count=300):
+    msgs = []
+    for _ in range(count):
+        nf = int(rng.integers(0, 12))
+        fr = [rng.integers(0, 256, int(rng.integers(0, 300)), dtype=np.uint8).tobytes() for _ in range(nf)]
+        m = bytearray(F.zmq_pack(fr, list(rng.integers(0, 256, nf))))
+        k = int(rng.integers(0, 6))
+        if k == 0 and len(m) > 6:
+            m = m[: int(rng.integers(0, len(m)))]            # truncated
+        elif k == 1 and len(m) > 8:
+            m[int(rng.integers(4, len(m)))] ^= 0xFF           # corrupted header byte maybe
+        elif k == 2:
+            m[1] ^= 0x01                                       # bad batch magic
+        elif k == 3:
+            m[2:4] = (nf + 3).to_bytes(2, "big")               # count larger than present
+        msgs.append(bytes(m))
+    # quirks: > 64 KB stream (uint16 running offset), oversized frame
+    msgs.append(F.zmq_pack([bytes(9000)] * 9))
+    msgs.append(F.zmq_pack([bytes(65000)]))
+    msgs.append(F.zmq_pack([bytes(9217)]))
+    msgs.append(b"")
+    return msgs
+
+
+def test_zmq_descriptors_match_oracle(lib):
+    import pyoracle
+    from emurx.rx import zmq_descriptors
+    rng = np.random.default_rng(7)
+    for m in _rand_msgs(rng):
+        a = zmq_descriptors(m)
+        b = pyoracle.zmq_descriptors(m)
+        assert a[0] == b[0] and a[2] == b[2]
+        assert a[1].tobytes() == b[1].tobytes()
+
+
+def test_hist_to_counters_matches_oracle(lib):
+    """Counters derived from the outcome histogram (device path) == the oracle's per-frame
+    increments, over every edge-case frame and the golden corpus."""
+    import edge_frames as E
+    import pyoracle
+    from emurx.rx import hist_to_counters
+    from test_oracle_corpus import corpus_batch
+    frames = [c[1] for c in E.cases()]
+    buf, desc = F.pack_frames(frames)
+    cbuf, cdesc, _ = corpus_batch()
+    for mask in ((1 << 12) - 1, (1 << 12) - 1 - (1 << abi.CB_PPP) - (1 << abi.CB_EAPOL), 0):
+        for b, d in ((buf, desc), (cbuf, cdesc)):
+            o = pyoracle.Oracle(mask)
+            rec, _, _, cnt = o.rx_batch(b, d)
+            hist = np.zeros(2 * abi.HIST_BINS, np.uint64)
+            for r, ln in zip(rec, d["len"]):
+                st, pr = int(r["status"]), int(r["proto"])
+                binx = st * 12 + pr if st <= 1 else 24 + st - 2
+                hist[2 * binx] += 1
+                hist[2 * binx + 1] += int(ln)
+            got = hist_to_counters(hist)
+            want = pyoracle.counters_dict(cnt)
+            for k in abi.PARSER_COUNTER_NAMES + ["ref_panic"]:
+                assert got[k] == want[k], (mask, k)

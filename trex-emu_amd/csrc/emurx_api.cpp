@@ -1,0 +1,675 @@
+// emurx_api.cpp — C-ABI of the MI355X receive path (include/emu_rx.h).
+//
+// Owns the Namespace / Client tables (host copies with the Go maps' semantics, flattened
+// into the device layout of emurx_tables.h on emurx_sync), the device scratch of a batch,
+// and the host batch entry point that replaces VethIFZmq.OnRxStream's per-frame loop
+// (src/emu/core/veth_zmq.go:277-320).  No exception or abort crosses the ABI.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/emu_rx.h"
+#include "emurx_kernels.h"
+#include "emurx_tables.h"
+
+namespace {
+
+uint32_t pow2_at_least(uint64_t v) {
+    uint64_t p = 16;
+    while (p < v) p <<= 1;
+    return (uint32_t)p;
+}
+uint32_t le32(const uint8_t* p) { return p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24); }
+uint16_t be16(const uint8_t* p) { return (uint16_t)((p[0] << 8) | p[1]); }
+uint32_t be32(const uint8_t* p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+bool zero(const uint8_t* p, int n) {
+    for (int i = 0; i < n; ++i)
+        if (p[i]) return false;
+    return true;
+}
+
+// table keys: (ns_id, address words) — the per-Namespace Go maps flattened into one
+struct K5 {
+    uint32_t w[5];
+    bool operator==(const K5& o) const { return !memcmp(w, o.w, sizeof(w)); }
+};
+struct K5Hash {
+    size_t operator()(const K5& k) const { return emurx_hash(k.w[0], k.w[1], k.w[2], k.w[3], k.w[4]); }
+};
+using Map = std::unordered_map<K5, uint32_t, K5Hash>;
+
+K5 key_ns(const uint8_t* k12) { return K5{{le32(k12), le32(k12 + 4), le32(k12 + 8), 0, 0}}; }
+K5 key_mac(uint32_t ns, const uint8_t* m) {
+    return K5{{ns, le32(m), (uint32_t)(m[4] | (m[5] << 8)), 0, 0}};
+}
+K5 key_ip4(uint32_t ns, const uint8_t* ip) { return K5{{ns, le32(ip), 0, 0, 0}}; }
+K5 key_ip6(uint32_t ns, const uint8_t* ip) {
+    return K5{{ns, le32(ip), le32(ip + 4), le32(ip + 8), le32(ip + 12)}};
+}
+
+struct NsInfo {
+    bool alive = false;
+    uint8_t key[12] = {0};
+    uint32_t plugins = 0;
+    std::vector<uint32_t> order;  // clientHead dlist (insertion order)
+};
+struct ClientInfo {
+    bool alive = false;
+    uint32_t ns = 0;
+    uint8_t mac[6] = {0}, ipv4[4] = {0}, ipv6[16] = {0}, dhcpv6[16] = {0};
+    uint32_t plugins = 0;
+    bool has_ra = false;
+    uint8_t ra_prefix[16] = {0};
+    uint8_t ra_plen = 0;
+};
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    int alloc(size_t count) {
+        if (count <= n && p) return 0;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        if (hipMalloc((void**)&p, std::max<size_t>(count, 1) * sizeof(T)) != hipSuccess) return -1;
+        n = count;
+        return 0;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+template <class T>
+struct PinBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    int alloc(size_t count) {
+        if (count <= n && p) return 0;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+        if (hipHostMalloc((void**)&p, std::max<size_t>(count, 1) * sizeof(T), hipHostMallocDefault) != hipSuccess)
+            return -1;
+        n = count;
+        return 0;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+}  // namespace
+
+struct emurx_ctx {
+    emurx_cfg cfg{};
+    hipStream_t stream = nullptr;
+    uint32_t cb_mask = 0;  // Parser.Init: every callback parserNotSupported (eapol nil)
+
+    // authoritative tables (Go map semantics)
+    Map ns_map, mac_map, ip4_map, ip6_map;
+    std::vector<NsInfo> ns;
+    std::vector<ClientInfo> cl;
+    bool dirty = true;
+
+    // device tables
+    uint32_t ns_slots = 0, mac_slots = 0, ip4_slots = 0, ip6_slots = 0;
+    DevBuf<uint32_t> d_ns, d_nsinfo, d_mac, d_ip4, d_ip6, d_client;
+    std::vector<uint32_t> h_ns, h_nsinfo, h_mac, h_ip4, h_ip6, h_client;
+
+    // batch scratch
+    DevBuf<emurx_rec> d_rec_scratch;
+    DevBuf<uint8_t> d_qtag;
+    DevBuf<uint32_t> d_tile_cnt, d_tile_off;
+
+    // host batch staging (emurx_rx_stream)
+    PinBuf<uint8_t> h_msg;
+    PinBuf<emurx_desc> h_desc;
+    PinBuf<uint32_t> h_qoff;
+    PinBuf<uint64_t> h_hist;
+    DevBuf<uint8_t> d_msg;
+    DevBuf<emurx_desc> d_desc;
+    DevBuf<emurx_rec> d_rec;
+    DevBuf<uint32_t> d_qlist, d_qoff;
+    DevBuf<uint64_t> d_hist;
+
+    // timing ring: 3 events per batch (before parse, after parse, after compaction)
+    std::vector<hipEvent_t> ev;
+    uint32_t slots = 0, ev_head = 0, ev_count = 0;
+
+    emurx_dev_tables tables() const {
+        emurx_dev_tables T{};
+        T.ns_tab = d_ns.p;
+        T.ns_info = d_nsinfo.p;
+        T.mac_tab = d_mac.p;
+        T.ip4_tab = d_ip4.p;
+        T.ip6_tab = d_ip6.p;
+        T.client = d_client.p;
+        T.ns_mask = ns_slots - 1;
+        T.mac_mask = mac_slots - 1;
+        T.ip4_mask = ip4_slots - 1;
+        T.ip6_mask = ip6_slots - 1;
+        T.max_ns = cfg.max_ns;
+        T.max_clients = cfg.max_clients;
+        T.cb_mask = cb_mask;
+        return T;
+    }
+};
+
+namespace {
+
+int bind(emurx_t* h) { return hipSetDevice(h->cfg.device) == hipSuccess ? EMURX_OK : EMURX_EDEVICE; }
+
+// open-addressing insert into a flat table (slot = `words` uint32, key in the first
+// words, value in the last word; EMURX_EMPTY marks a free slot)
+void flat_put(std::vector<uint32_t>& t, uint32_t mask, uint32_t words, uint32_t h, const uint32_t* e) {
+    uint32_t i = h & mask;
+    while (t[(size_t)i * words + words - 1] != EMURX_EMPTY) i = (i + 1) & mask;
+    memcpy(&t[(size_t)i * words], e, words * sizeof(uint32_t));
+}
+
+int rebuild_and_upload(emurx_t* h, hipStream_t st) {
+    if (!h->dirty) return EMURX_OK;
+    (void)hipStreamSynchronize(st);  // previous upload may still read the staging vectors
+    const uint32_t E = EMURX_EMPTY;
+    h->h_ns.assign((size_t)h->ns_slots * 4, 0);
+    for (size_t i = 0; i < h->ns_slots; ++i) h->h_ns[i * 4 + 3] = E;
+    for (auto& kv : h->ns_map) {
+        uint32_t e[4] = {kv.first.w[0], kv.first.w[1], kv.first.w[2], kv.second};
+        flat_put(h->h_ns, h->ns_slots - 1, 4, emurx_ns_hash(e[0], e[1], e[2]), e);
+    }
+    h->h_nsinfo.assign((size_t)h->cfg.max_ns * 4, 0);
+    for (uint32_t i = 0; i < h->ns.size(); ++i) {
+        const NsInfo& n = h->ns[i];
+        h->h_nsinfo[i * 4 + 0] = n.alive ? n.plugins : 0;
+        h->h_nsinfo[i * 4 + 1] = (n.alive && !n.order.empty()) ? n.order.front() : EMURX_ID_NONE;
+    }
+    auto fill4 = [&](std::vector<uint32_t>& t, uint32_t slots, const Map& m, int kind) {
+        t.assign((size_t)slots * 4, 0);
+        for (size_t i = 0; i < slots; ++i) t[i * 4 + 3] = E;
+        for (auto& kv : m) {
+            uint32_t e[4] = {kv.first.w[0], kv.first.w[1], kv.first.w[2], kv.second};
+            uint32_t hh = kind == 0 ? emurx_mac_hash(e[0], e[1], e[2]) : emurx_ip4_hash(e[0], e[1]);
+            if (kind == 1) e[2] = 0;
+            flat_put(t, slots - 1, 4, hh, e);
+        }
+    };
+    fill4(h->h_mac, h->mac_slots, h->mac_map, 0);
+    fill4(h->h_ip4, h->ip4_slots, h->ip4_map, 1);
+    h->h_ip6.assign((size_t)h->ip6_slots * 8, 0);
+    for (size_t i = 0; i < h->ip6_slots; ++i) h->h_ip6[i * 8 + 7] = E;
+    for (auto& kv : h->ip6_map) {
+        const uint32_t* w = kv.first.w;
+        uint32_t e[8] = {w[0], w[1], w[2], w[3], w[4], 0, 0, kv.second};
+        flat_put(h->h_ip6, h->ip6_slots - 1, 8, emurx_ip6_hash(w[0], w[1], w[2], w[3], w[4]), e);
+    }
+    h->h_client.assign((size_t)h->cfg.max_clients * 8, 0);
+    for (uint32_t i = 0; i < h->cl.size(); ++i) {
+        const ClientInfo& c = h->cl[i];
+        if (!c.alive) continue;
+        uint32_t* o = &h->h_client[(size_t)i * 8];
+        o[0] = le32(c.mac);
+        o[1] = (uint32_t)(c.mac[4] | (c.mac[5] << 8));
+        o[2] = c.plugins;
+        o[3] = (c.has_ra ? 1u : 0u) | ((uint32_t)c.ra_plen << 8);
+        o[4] = le32(c.ra_prefix);
+        o[5] = le32(c.ra_prefix + 4);
+    }
+    struct {
+        uint32_t* d;
+        std::vector<uint32_t>* h;
+    } up[] = {{h->d_ns.p, &h->h_ns},   {h->d_nsinfo.p, &h->h_nsinfo}, {h->d_mac.p, &h->h_mac},
+              {h->d_ip4.p, &h->h_ip4}, {h->d_ip6.p, &h->h_ip6},       {h->d_client.p, &h->h_client}};
+    for (auto& u : up)
+        if (hipMemcpyAsync(u.d, u.h->data(), u.h->size() * 4, hipMemcpyHostToDevice, st) != hipSuccess)
+            return EMURX_EDEVICE;
+    if (hipStreamSynchronize(st) != hipSuccess) return EMURX_EDEVICE;
+    h->dirty = false;
+    return EMURX_OK;
+}
+
+int ensure_scratch(emurx_t* h, uint32_t n) {
+    uint32_t tiles = (n + EMURX_TILE - 1) / EMURX_TILE;
+    if (h->d_rec_scratch.alloc(n) || h->d_qtag.alloc(n) || h->d_tile_cnt.alloc((size_t)tiles * 16 + 16) ||
+        h->d_tile_off.alloc((size_t)tiles * 16 + 16))
+        return EMURX_ENOMEM;
+    return EMURX_OK;
+}
+
+int run_dev(emurx_t* h, const uint8_t* frames, const emurx_desc* desc, uint32_t n,
+            const emurx_dev_out* out, void* stream, bool classify) {
+    if (!h || !out || !out->hist || (n && (!frames || !desc))) return EMURX_EINVAL;
+    if (n > h->cfg.max_frames) return EMURX_ENOMEM;
+    int rc = bind(h);
+    if (rc) return rc;
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    if (classify && (rc = rebuild_and_upload(h, st))) return rc;
+    if ((rc = ensure_scratch(h, std::max<uint32_t>(n, 1)))) return rc;
+    emurx_dev_tables T = h->tables();
+    hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
+    if (h->slots) {
+        const uint32_t s = h->ev_head;
+        e0 = h->ev[3 * s];
+        e1 = h->ev[3 * s + 1];
+        e2 = h->ev[3 * s + 2];
+        h->ev_head = (s + 1) % h->slots;
+        h->ev_count = std::min(h->ev_count + 1, h->slots);
+    }
+    int r = emurx_launch_batch(frames, desc, n, T, classify, *out, h->d_rec_scratch.p, h->d_qtag.p,
+                               h->d_tile_cnt.p, h->d_tile_off.p, st, e0, e1, e2);
+    return r ? EMURX_EDEVICE : EMURX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int emurx_abi_version(void) { return EMURX_ABI_VERSION; }
+
+const char* emurx_strerror(int code) {
+    switch (code) {
+    case EMURX_OK: return "ok";
+    case EMURX_EINVAL: return "invalid argument";
+    case EMURX_ENOMEM: return "out of memory / capacity exceeded";
+    case EMURX_EEXIST: return "already exists";
+    case EMURX_ENOENT: return "not found";
+    case EMURX_EDEVICE: return "HIP runtime error";
+    case EMURX_ENOSPC: return "output buffer too small";
+    default: return "unknown error";
+    }
+}
+
+int emurx_open(const emurx_cfg* cfg, emurx_t** out) {
+    if (!cfg || !out || cfg->max_ns == 0 || cfg->max_clients == 0 || cfg->max_frames == 0) return EMURX_EINVAL;
+    emurx_t* h = new (std::nothrow) emurx_ctx();
+    if (!h) return EMURX_ENOMEM;
+    h->cfg = *cfg;
+    if (h->cfg.max_bytes == 0) h->cfg.max_bytes = 1u << 20;
+    int rc = bind(h);
+    if (rc) { delete h; return rc; }
+    if (hipStreamCreate(&h->stream) != hipSuccess) { delete h; return EMURX_EDEVICE; }
+    h->ns_slots = pow2_at_least(2ull * cfg->max_ns);
+    h->mac_slots = pow2_at_least(2ull * cfg->max_clients);
+    h->ip4_slots = pow2_at_least(2ull * cfg->max_clients);
+    h->ip6_slots = pow2_at_least(4ull * cfg->max_clients);
+    h->ns.resize(cfg->max_ns);
+    h->cl.resize(cfg->max_clients);
+    if (h->d_ns.alloc((size_t)h->ns_slots * 4) || h->d_nsinfo.alloc((size_t)cfg->max_ns * 4) ||
+        h->d_mac.alloc((size_t)h->mac_slots * 4) || h->d_ip4.alloc((size_t)h->ip4_slots * 4) ||
+        h->d_ip6.alloc((size_t)h->ip6_slots * 8) || h->d_client.alloc((size_t)cfg->max_clients * 8)) {
+        emurx_close(h);
+        return EMURX_ENOMEM;
+    }
+    h->dirty = true;
+    if ((rc = rebuild_and_upload(h, h->stream))) { emurx_close(h); return rc; }
+    *out = h;
+    return EMURX_OK;
+}
+
+void emurx_close(emurx_t* h) {
+    if (!h) return;
+    bind(h);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    h->d_ns.release(); h->d_nsinfo.release(); h->d_mac.release(); h->d_ip4.release();
+    h->d_ip6.release(); h->d_client.release();
+    h->d_rec_scratch.release(); h->d_qtag.release(); h->d_tile_cnt.release(); h->d_tile_off.release();
+    h->h_msg.release(); h->h_desc.release(); h->h_qoff.release(); h->h_hist.release();
+    h->d_msg.release(); h->d_desc.release(); h->d_rec.release(); h->d_qlist.release();
+    h->d_qoff.release(); h->d_hist.release();
+    for (auto& e : h->ev)
+        if (e) (void)hipEventDestroy(e);
+    h->ev.clear();
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+// Parser.Register parser.go:528-565 (unknown names are ignored, as in Go)
+int emurx_register(emurx_t* h, const char* p) {
+    if (!h || !p) return EMURX_EINVAL;
+    static const struct { const char* name; uint32_t bits; } tab[] = {
+        {"arp", 1u << EMURX_CB_ARP},         {"icmp", 1u << EMURX_CB_ICMP},
+        {"igmp", 1u << EMURX_CB_IGMP},       {"dhcp", 1u << EMURX_CB_DHCP},
+        {"dhcpsrv", 1u << EMURX_CB_DHCPSRV}, {"icmpv6", 1u << EMURX_CB_ICMPV6},
+        {"dhcpv6", 1u << EMURX_CB_DHCPV6},   {"dot1x", 1u << EMURX_CB_EAPOL},
+        {"mdns", 1u << EMURX_CB_MDNS},       {"ppp", 1u << EMURX_CB_PPP},
+        {"transport", (1u << EMURX_CB_TCP) | (1u << EMURX_CB_UDP)}};
+    for (auto& t : tab)
+        if (!strcmp(p, t.name)) h->cb_mask |= t.bits;
+    return EMURX_OK;
+}
+int emurx_set_callbacks_mask(emurx_t* h, uint32_t mask) {
+    if (!h) return EMURX_EINVAL;
+    h->cb_mask = mask & ((1u << EMURX_NUM_CB) - 1u);
+    return EMURX_OK;
+}
+uint32_t emurx_get_callbacks_mask(const emurx_t* h) { return h ? h->cb_mask : 0; }
+
+// ---- tables ------------------------------------------------------------------------------
+// CThreadCtx.AddNs thread_ctx.go:786-795
+int emurx_ns_add(emurx_t* h, const uint8_t key[12], uint32_t ns_id, uint32_t plugin_mask) {
+    if (!h || !key) return EMURX_EINVAL;
+    if (ns_id >= h->cfg.max_ns) return EMURX_ENOMEM;
+    K5 k = key_ns(key);
+    if (h->ns_map.count(k) || h->ns[ns_id].alive) return EMURX_EEXIST;
+    NsInfo& n = h->ns[ns_id];
+    n.alive = true;
+    memcpy(n.key, key, 12);
+    n.plugins = plugin_mask;
+    n.order.clear();
+    h->ns_map[k] = ns_id;
+    h->dirty = true;
+    return EMURX_OK;
+}
+// CThreadCtx.RemoveNs thread_ctx.go:797-812 (refused while clients are active)
+int emurx_ns_remove(emurx_t* h, const uint8_t key[12]) {
+    if (!h || !key) return EMURX_EINVAL;
+    auto it = h->ns_map.find(key_ns(key));
+    if (it == h->ns_map.end()) return EMURX_ENOENT;
+    NsInfo& n = h->ns[it->second];
+    if (!n.order.empty()) return EMURX_EEXIST;
+    n.alive = false;
+    h->ns_map.erase(it);
+    h->dirty = true;
+    return EMURX_OK;
+}
+int emurx_ns_set_plugins(emurx_t* h, uint32_t ns_id, uint32_t plugin_mask) {
+    if (!h) return EMURX_EINVAL;
+    if (ns_id >= h->cfg.max_ns || !h->ns[ns_id].alive) return EMURX_ENOENT;
+    h->ns[ns_id].plugins = plugin_mask;
+    h->dirty = true;
+    return EMURX_OK;
+}
+
+// CNSCtx.AddClient ns_ctx.go:332-389
+int emurx_client_add(emurx_t* h, uint32_t ns_id, uint32_t cid, const uint8_t mac[6],
+                     const uint8_t ipv4[4], const uint8_t ipv6[16], const uint8_t dhcpv6[16],
+                     uint32_t plugin_mask) {
+    static const uint8_t z[16] = {0};
+    if (!h || !mac) return EMURX_EINVAL;
+    if (ns_id >= h->cfg.max_ns || !h->ns[ns_id].alive) return EMURX_ENOENT;
+    if (cid >= h->cfg.max_clients) return EMURX_ENOMEM;
+    if (!ipv4) ipv4 = z;
+    if (!ipv6) ipv6 = z;
+    if (!dhcpv6) dhcpv6 = z;
+    if (zero(mac, 6)) return EMURX_EINVAL;
+    if (h->mac_map.count(key_mac(ns_id, mac))) return EMURX_EEXIST;
+    bool has4 = !zero(ipv4, 4), has6 = !zero(ipv6, 16), has6d = !zero(dhcpv6, 16);
+    if (has4 && h->ip4_map.count(key_ip4(ns_id, ipv4))) return EMURX_EEXIST;
+    if (has6 && h->ip6_map.count(key_ip6(ns_id, ipv6))) return EMURX_EEXIST;
+    if (has6d && h->ip6_map.count(key_ip6(ns_id, dhcpv6))) return EMURX_EEXIST;
+    if (h->cl[cid].alive) return EMURX_EEXIST;
+    ClientInfo& c = h->cl[cid];
+    c = ClientInfo();
+    c.alive = true;
+    c.ns = ns_id;
+    c.plugins = plugin_mask;
+    memcpy(c.mac, mac, 6);
+    memcpy(c.ipv4, ipv4, 4);
+    memcpy(c.ipv6, ipv6, 16);
+    memcpy(c.dhcpv6, dhcpv6, 16);
+    h->mac_map[key_mac(ns_id, mac)] = cid;
+    if (has4) h->ip4_map[key_ip4(ns_id, ipv4)] = cid;
+    if (has6) h->ip6_map[key_ip6(ns_id, ipv6)] = cid;
+    if (has6d) h->ip6_map[key_ip6(ns_id, dhcpv6)] = cid;
+    h->ns[ns_id].order.push_back(cid);
+    h->dirty = true;
+    return EMURX_OK;
+}
+
+// CNSCtx.RemoveClient ns_ctx.go:392-440 (map entries are deleted by key)
+int emurx_client_remove(emurx_t* h, uint32_t ns_id, const uint8_t mac[6]) {
+    if (!h || !mac) return EMURX_EINVAL;
+    if (ns_id >= h->cfg.max_ns || !h->ns[ns_id].alive) return EMURX_ENOENT;
+    if (zero(mac, 6)) return EMURX_EINVAL;
+    auto it = h->mac_map.find(key_mac(ns_id, mac));
+    if (it == h->mac_map.end()) return EMURX_ENOENT;
+    uint32_t cid = it->second;
+    ClientInfo& c = h->cl[cid];
+    h->mac_map.erase(it);
+    auto& ord = h->ns[ns_id].order;
+    ord.erase(std::remove(ord.begin(), ord.end(), cid), ord.end());
+    if (!zero(c.ipv4, 4)) h->ip4_map.erase(key_ip4(ns_id, c.ipv4));
+    if (!zero(c.ipv6, 16)) h->ip6_map.erase(key_ip6(ns_id, c.ipv6));
+    if (!zero(c.dhcpv6, 16)) h->ip6_map.erase(key_ip6(ns_id, c.dhcpv6));
+    c.alive = false;
+    h->dirty = true;
+    return EMURX_OK;
+}
+
+int emurx_client_set_plugins(emurx_t* h, uint32_t cid, uint32_t plugin_mask) {
+    if (!h) return EMURX_EINVAL;
+    if (cid >= h->cfg.max_clients || !h->cl[cid].alive) return EMURX_ENOENT;
+    h->cl[cid].plugins = plugin_mask;
+    h->dirty = true;
+    return EMURX_OK;
+}
+
+// CNSCtx.UpdateClientIpv4 / Ipv6 / DIpv6 ns_ctx.go:442-533
+static int update_addr(emurx_t* h, uint32_t cid, int which, const uint8_t* nw) {
+    if (!h || !nw) return EMURX_EINVAL;
+    if (cid >= h->cfg.max_clients || !h->cl[cid].alive) return EMURX_ENOENT;
+    ClientInfo& c = h->cl[cid];
+    const int n = which == 4 ? 4 : 16;
+    uint8_t* cur = which == 4 ? c.ipv4 : (which == 6 ? c.ipv6 : c.dhcpv6);
+    Map& m = which == 4 ? h->ip4_map : h->ip6_map;
+    auto key = [&](const uint8_t* a) { return which == 4 ? key_ip4(c.ns, a) : key_ip6(c.ns, a); };
+    if (!memcmp(cur, nw, n)) return EMURX_OK;
+    h->dirty = true;
+    if (!zero(cur, n)) {
+        auto it = m.find(key(cur));
+        if (it == m.end()) { memset(cur, 0, n); return EMURX_ENOENT; }
+        m.erase(it);
+    }
+    if (!zero(nw, n)) {
+        if (m.count(key(nw))) { memset(cur, 0, n); return EMURX_EEXIST; }
+        m[key(nw)] = cid;
+    }
+    memcpy(cur, nw, n);
+    return EMURX_OK;
+}
+int emurx_client_update_ipv4(emurx_t* h, uint32_t cid, const uint8_t ipv4[4]) { return update_addr(h, cid, 4, ipv4); }
+int emurx_client_update_ipv6(emurx_t* h, uint32_t cid, const uint8_t ipv6[16]) { return update_addr(h, cid, 6, ipv6); }
+int emurx_client_update_dipv6(emurx_t* h, uint32_t cid, const uint8_t d[16]) { return update_addr(h, cid, 7, d); }
+
+int emurx_client_set_ra(emurx_t* h, uint32_t cid, const uint8_t prefix[16], uint8_t plen) {
+    if (!h || !prefix) return EMURX_EINVAL;
+    if (cid >= h->cfg.max_clients || !h->cl[cid].alive) return EMURX_ENOENT;
+    ClientInfo& c = h->cl[cid];
+    c.has_ra = true;
+    memcpy(c.ra_prefix, prefix, 16);
+    c.ra_plen = plen;
+    h->dirty = true;
+    return EMURX_OK;
+}
+
+int emurx_sync(emurx_t* h, void* stream) {
+    if (!h) return EMURX_EINVAL;
+    int rc = bind(h);
+    if (rc) return rc;
+    return rebuild_and_upload(h, stream ? (hipStream_t)stream : h->stream);
+}
+
+// ---- data path ---------------------------------------------------------------------------
+// the offset walk of VethIFZmq.OnRxStream veth_zmq.go:277-320 (uint16 running offset)
+int emurx_zmq_descriptors(const uint8_t* msg, size_t len, emurx_desc* out, uint32_t cap,
+                          uint32_t* n_out, int* parse_err) {
+    if (!n_out || !parse_err || (len && !msg)) return EMURX_EINVAL;
+    *n_out = 0;
+    *parse_err = 0;
+    const uint32_t blen = (uint32_t)len;
+    if (blen < 4) { *parse_err = 1; return EMURX_OK; }
+    uint32_t header = be32(msg);
+    if ((header >> 16) != EMURX_ZMQ_MAGIC) { *parse_err = 1; return EMURX_OK; }
+    const int pkts = (int)(header & 0xffff);
+    uint16_t of = 4;
+    for (int i = 0; i < pkts; ++i) {
+        if (blen < (uint32_t)(uint16_t)(of + 4)) { *parse_err = 1; return EMURX_OK; }
+        if ((uint16_t)(of + 4) < of) { *parse_err = 2; return EMURX_OK; }
+        header = be32(msg + of);
+        if ((header & 0xff000000u) != 0xAA000000u) { *parse_err = 1; return EMURX_OK; }
+        const uint8_t vport = (uint8_t)(header >> 16);
+        const uint16_t plen = (uint16_t)header;
+        if (blen < (uint32_t)(uint16_t)(of + 4 + plen)) { *parse_err = 1; return EMURX_OK; }
+        if (plen > EMURX_MAX_FRAME) { *parse_err = 2; return EMURX_OK; }
+        if ((uint16_t)(of + 4 + plen) < (uint16_t)(of + 4)) { *parse_err = 2; return EMURX_OK; }
+        if (*n_out >= cap) return EMURX_ENOSPC;
+        out[*n_out] = emurx_desc{(uint32_t)(uint16_t)(of + 4), plen, vport, 0};
+        ++*n_out;
+        of = (uint16_t)(of + 4 + plen);
+    }
+    return EMURX_OK;
+}
+
+void emurx_hist_to_counters(const uint64_t hist[2 * EMURX_HIST_BINS], emurx_counters* c) {
+    if (!hist || !c) return;
+    uint64_t* s = c->parser;
+    for (uint32_t st = 0; st < EMURX_NUM_STATUS; ++st) {
+        for (uint32_t cb = 0; cb < (st <= EMURX_ST_NOT_SUPPORTED ? (uint32_t)EMURX_NUM_CB : 1u); ++cb) {
+            const uint32_t b = st <= EMURX_ST_NOT_SUPPORTED ? EMURX_HIST_BIN(st, cb) : EMURX_HIST_BIN(st, 0);
+            const uint64_t pk = hist[2 * b], by = hist[2 * b + 1];
+            if (!pk) continue;
+            if (st >= EMURX_ST_PANIC_L4LEN) { c->ref_panic += pk; continue; }
+            if (st <= EMURX_ST_NOT_SUPPORTED) {
+                switch (cb) {  // parser.go:602-713 / :787-799
+                case EMURX_CB_ARP: s[EMURX_PC_arpPkts] += pk; s[EMURX_PC_arpBytes] += by; break;
+                case EMURX_CB_ICMP: s[EMURX_PC_icmpPkts] += pk; s[EMURX_PC_icmpBytes] += by; break;
+                case EMURX_CB_IGMP: s[EMURX_PC_igmpPkts] += pk; s[EMURX_PC_igmpBytes] += by; break;
+                case EMURX_CB_TCP: s[EMURX_PC_tcpPkts] += pk; s[EMURX_PC_tcpBytes] += by; break;
+                case EMURX_CB_ICMPV6: s[EMURX_PC_Icmpv6Pkt] += pk; s[EMURX_PC_Icmpv6Bytes] += by; break;
+                case EMURX_CB_EAPOL: s[EMURX_PC_eapolPkts] += pk; s[EMURX_PC_eapolBytes] += by; break;
+                case EMURX_CB_PPP: break;
+                default:
+                    s[EMURX_PC_udpPkts] += pk; s[EMURX_PC_udpBytes] += by;
+                    if (cb == EMURX_CB_MDNS) { s[EMURX_PC_mDnsPkts] += pk; s[EMURX_PC_mDnsBytes] += by; }
+                    if (cb == EMURX_CB_DHCP || cb == EMURX_CB_DHCPV6) { s[EMURX_PC_dhcpPkts] += pk; s[EMURX_PC_dhcpBytes] += by; }
+                    if (cb == EMURX_CB_DHCPSRV) { s[EMURX_PC_dhcpSrvPkts] += pk; s[EMURX_PC_dhcpSrvBytes] += by; }
+                }
+                if (st == EMURX_ST_NOT_SUPPORTED) s[EMURX_PC_errParser] += pk;
+                continue;
+            }
+            static const int err_counter[EMURX_NUM_STATUS] = {
+                -1, -1, EMURX_PC_errPacketIsTooShort, EMURX_PC_errEAPolTooShort, EMURX_PC_errArpTooShort,
+                EMURX_PC_errDot1qTooShort, EMURX_PC_errToManyDot1q, EMURX_PC_errIPv4TooShort,
+                EMURX_PC_errIPv4HeaderTooShort, EMURX_PC_errIPv4Fragment, EMURX_PC_errIPv4cs,
+                EMURX_PC_errIPv6TooShort, EMURX_PC_errIPv6HopLimitDrop, EMURX_PC_errIPv6Empty,
+                EMURX_PC_errIPv6OptJumbo, EMURX_PC_errIPv6Fragment, EMURX_PC_errIcmpv4TooShort,
+                EMURX_PC_errIcmpv4Cse, EMURX_PC_errTcpTooShort, EMURX_PC_tcpCsErr, EMURX_PC_errUdpTooShort,
+                EMURX_PC_udpCsErr, EMURX_PC_errIcmpv6TooShort, EMURX_PC_errIcmpv6Cse,
+                EMURX_PC_errIcmpv6Unsupported, EMURX_PC_errL4ProtoUnsupported,
+                EMURX_PC_errL3ProtoUnsupported, -1, -1, -1, -1};
+            s[err_counter[st]] += pk;
+            s[EMURX_PC_errParser] += pk;  // HandleRxPacket thread_ctx.go:368-369
+        }
+    }
+}
+
+int emurx_classify_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_desc, uint32_t n,
+                       const emurx_dev_out* out, void* stream) {
+    return run_dev(h, d_frames, d_desc, n, out, stream, true);
+}
+int emurx_parse_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_desc, uint32_t n,
+                    const emurx_dev_out* out, void* stream) {
+    return run_dev(h, d_frames, d_desc, n, out, stream, false);
+}
+
+int emurx_rx_stream(emurx_t* h, const uint8_t* msg, size_t len, emurx_rec* out_rec,
+                    uint32_t* out_qlist, uint32_t out_cap, uint32_t* n_out,
+                    uint32_t out_qoff[EMURX_NUM_QUEUES + 1], emurx_counters* delta) {
+    if (!h || !n_out || !out_qoff || !delta || (len && !msg)) return EMURX_EINVAL;
+    memset(delta, 0, sizeof(*delta));
+    *n_out = 0;
+    int rc = bind(h);
+    if (rc) return rc;
+    const uint32_t cap = std::min(out_cap, h->cfg.max_frames);
+    if (h->h_desc.alloc(std::max<uint32_t>(cap, 1)) || h->h_msg.alloc(len + 64) || h->h_qoff.alloc(16) ||
+        h->h_hist.alloc(2 * EMURX_HIST_BINS) || h->d_msg.alloc(len + 64) || h->d_desc.alloc(std::max<uint32_t>(cap, 1)) ||
+        h->d_rec.alloc(std::max<uint32_t>(cap, 1)) || h->d_qlist.alloc(std::max<uint32_t>(cap, 1)) ||
+        h->d_qoff.alloc(16) || h->d_hist.alloc(2 * EMURX_HIST_BINS))
+        return EMURX_ENOMEM;
+    int perr = 0;
+    uint32_t n = 0;
+    rc = emurx_zmq_descriptors(msg, len, h->h_desc.p, cap, &n, &perr);
+    if (rc) return rc;
+    delta->rx_batch = 1;  // VethStats.RxBatch veth_zmq.go:278
+    if (perr == 1) delta->rx_parse_err = 1;
+    if (perr == 2) delta->ref_panic += 1;
+    for (uint32_t i = 0; i < n; ++i) {  // VethIFZmq.OnRx veth_zmq.go:233-234
+        delta->rx_pkts++;
+        delta->rx_bytes += h->h_desc.p[i].len;
+    }
+    *n_out = n;
+    hipStream_t st = h->stream;
+    if ((rc = rebuild_and_upload(h, st))) return rc;
+    if (n == 0) {
+        memset(out_qoff, 0, sizeof(uint32_t) * (EMURX_NUM_QUEUES + 1));
+        return EMURX_OK;
+    }
+    if (!out_rec || !out_qlist) return EMURX_EINVAL;
+    memcpy(h->h_msg.p, msg, len);
+    memset(h->h_msg.p + len, 0, 64);
+    emurx_dev_out o{h->d_rec.p, h->d_qlist.p, h->d_qoff.p, h->d_hist.p};
+    bool ok = hipMemcpyAsync(h->d_msg.p, h->h_msg.p, len + 64, hipMemcpyHostToDevice, st) == hipSuccess &&
+              hipMemcpyAsync(h->d_desc.p, h->h_desc.p, (size_t)n * sizeof(emurx_desc), hipMemcpyHostToDevice, st) == hipSuccess &&
+              hipMemsetAsync(h->d_hist.p, 0, 2 * EMURX_HIST_BINS * sizeof(uint64_t), st) == hipSuccess;
+    if (!ok) return EMURX_EDEVICE;
+    if ((rc = run_dev(h, h->d_msg.p, h->d_desc.p, n, &o, st, true))) return rc;
+    ok = hipMemcpyAsync(out_rec, h->d_rec.p, (size_t)n * sizeof(emurx_rec), hipMemcpyDeviceToHost, st) == hipSuccess &&
+         hipMemcpyAsync(out_qlist, h->d_qlist.p, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost, st) == hipSuccess &&
+         hipMemcpyAsync(h->h_qoff.p, h->d_qoff.p, 16 * sizeof(uint32_t), hipMemcpyDeviceToHost, st) == hipSuccess &&
+         hipMemcpyAsync(h->h_hist.p, h->d_hist.p, 2 * EMURX_HIST_BINS * sizeof(uint64_t), hipMemcpyDeviceToHost, st) == hipSuccess &&
+         hipStreamSynchronize(st) == hipSuccess;
+    if (!ok) return EMURX_EDEVICE;
+    memcpy(out_qoff, h->h_qoff.p, sizeof(uint32_t) * (EMURX_NUM_QUEUES + 1));
+    emurx_hist_to_counters(h->h_hist.p, delta);
+    return EMURX_OK;
+}
+
+int emurx_set_timing(emurx_t* h, uint32_t slots) {
+    if (!h) return EMURX_EINVAL;
+    int rc = bind(h);
+    if (rc) return rc;
+    (void)hipStreamSynchronize(h->stream);
+    for (auto& e : h->ev)
+        if (e) (void)hipEventDestroy(e);
+    h->ev.assign((size_t)slots * 3, nullptr);
+    for (auto& e : h->ev)
+        if (hipEventCreate(&e) != hipSuccess) { h->slots = 0; return EMURX_EDEVICE; }
+    h->slots = slots;
+    h->ev_head = h->ev_count = 0;
+    return EMURX_OK;
+}
+
+int emurx_kernel_times(emurx_t* h, float* parse_ms, float* compact_ms, uint32_t cap, uint32_t* n_out) {
+    if (!h || !n_out || (cap && (!parse_ms || !compact_ms))) return EMURX_EINVAL;
+    *n_out = 0;
+    if (!h->slots || !h->ev_count) return EMURX_OK;
+    int rc = bind(h);
+    if (rc) return rc;
+    const uint32_t last = (h->ev_head + h->slots - 1) % h->slots;
+    if (hipEventSynchronize(h->ev[3 * last + 2]) != hipSuccess) return EMURX_EDEVICE;
+    const uint32_t n = std::min(h->ev_count, cap);
+    const uint32_t first = (h->ev_head + h->slots - h->ev_count) % h->slots;
+    for (uint32_t k = 0; k < n; ++k) {
+        const uint32_t s = (first + (h->ev_count - n) + k) % h->slots;
+        if (hipEventElapsedTime(&parse_ms[k], h->ev[3 * s], h->ev[3 * s + 1]) != hipSuccess ||
+            hipEventElapsedTime(&compact_ms[k], h->ev[3 * s + 1], h->ev[3 * s + 2]) != hipSuccess)
+            return EMURX_EDEVICE;
+    }
+    *n_out = n;
+    h->ev_count = 0;
+    return EMURX_OK;
+}
+
+}  // extern "C"

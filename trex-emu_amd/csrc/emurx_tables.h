@@ -1,0 +1,74 @@
+// emurx_tables.h — device-resident Namespace / Client tables (layout shared by the host
+// builder in emurx_api.cpp and the HIP kernels in emurx_kernels.hip).
+//
+// They mirror the reference's Go maps:
+//   MapNsT        map[CTunnelKey]*CNSCtx   src/emu/core/thread_ctx.go:139
+//   MapClientMAC  map[MACKey]*CClient      src/emu/core/ns_ctx.go:110-112  (per Namespace)
+//   MapClientIPv4 map[Ipv4Key]*CClient
+//   MapClientIPv6 map[Ipv6Key]*CClient     (static Ipv6 and Dhcpv6 addresses, ns_ctx.go:377-383)
+// as flat open-addressing arrays (linear probing, load factor <= 1/2, power-of-two size).
+// A per-Namespace client map becomes one global map keyed by (ns_id, key).  Every entry is
+// 16 B (IPv6: 32 B) so a probe is one 16-byte load; the tables are read-only during a
+// batch and sit in L2 / Infinity Cache (64K clients = 1 MiB MAC table).
+#pragma once
+#include <stdint.h>
+
+#ifndef EMURX_HD
+#if defined(__HIPCC__)
+#define EMURX_HD __host__ __device__ __forceinline__
+#else
+#define EMURX_HD static inline
+#endif
+#endif
+
+#define EMURX_EMPTY 0xFFFFFFFFu
+
+// 32-bit mix of up to five key words (murmur3 finaliser over a multiplicative combine).
+EMURX_HD uint32_t emurx_fmix(uint32_t h) {
+    h ^= h >> 16; h *= 0x85EBCA6Bu;
+    h ^= h >> 13; h *= 0xC2B2AE35u;
+    h ^= h >> 16;
+    return h;
+}
+EMURX_HD uint32_t emurx_hash(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t e) {
+    uint32_t h = a * 0x9E3779B1u;
+    h = (h ^ (h >> 15)) + b * 0x85EBCA77u;
+    h = (h ^ (h >> 13)) + c * 0xC2B2AE3Du;
+    h = (h ^ (h >> 16)) + d * 0x27D4EB2Fu;
+    h = (h ^ (h >> 15)) + e * 0x165667B1u;
+    return emurx_fmix(h);
+}
+
+// Entry layouts (uint32 words):
+//  ns   [4]: vport_word, vlan0, vlan1, ns_id           (key = CTunnelKey as 3 LE words)
+//  mac  [4]: ns_id, mac[0..3] LE, mac[4..5] LE, client_id
+//  ip4  [4]: ns_id, ipv4 bytes LE, 0, client_id
+//  ip6  [8]: ns_id, ip[0..3], ip[4..7], ip[8..11], ip[12..15], 0, 0, client_id
+//  ns_info   [4]: plugin_mask, first_client, 0, 0
+//  client    [8]: mac_lo, mac_hi, plugin_mask, ra (bit0 has_ra, bits 8..15 prefix_len),
+//                 ra_prefix[0..3], ra_prefix[4..7], 0, 0
+EMURX_HD uint32_t emurx_ns_hash(uint32_t w0, uint32_t w1, uint32_t w2) {
+    return emurx_hash(w0, w1, w2, 0x6E73u, 0);
+}
+EMURX_HD uint32_t emurx_mac_hash(uint32_t ns, uint32_t lo, uint32_t hi) {
+    return emurx_hash(ns, lo, hi, 0x6D6163u, 0);
+}
+EMURX_HD uint32_t emurx_ip4_hash(uint32_t ns, uint32_t ip) {
+    return emurx_hash(ns, ip, 0x697034u, 0, 0);
+}
+EMURX_HD uint32_t emurx_ip6_hash(uint32_t ns, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    return emurx_hash(ns, a ^ 0x697036u, b, c, d);
+}
+
+struct emurx_dev_tables {
+    const uint32_t* ns_tab;   // 4 words per slot
+    const uint32_t* ns_info;  // 4 words per ns id
+    const uint32_t* mac_tab;  // 4 words per slot
+    const uint32_t* ip4_tab;  // 4 words per slot
+    const uint32_t* ip6_tab;  // 8 words per slot
+    const uint32_t* client;   // 8 words per client id
+    uint32_t ns_mask, mac_mask, ip4_mask, ip6_mask;
+    uint32_t max_ns, max_clients;
+    uint32_t cb_mask;         // registered callbacks (Parser.Register)
+    uint32_t pad;
+};

@@ -1,0 +1,179 @@
+"""RxPath — Python surface of the C-ABI, shaped like the reference's rx entry points.
+
+    RxPath.register(name)         Parser.Register          src/emu/core/parser.go:528-565
+    RxPath.ns_add / ns_remove     CThreadCtx.AddNs/RemoveNs src/emu/core/thread_ctx.go:786-812
+    RxPath.client_add / remove    CNSCtx.AddClient/RemoveClient src/emu/core/ns_ctx.go:332-440
+    RxPath.on_rx_stream(msg)      VethIFZmq.OnRxStream     src/emu/core/veth_zmq.go:277-320
+    RxPath.classify_dev(...)      the same, device-resident (frames already in HBM)
+
+Device memory is plain torch CUDA tensors (plumbing only); every call goes through
+libemurx.so — there is no Python or CPU implementation of the data path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+
+
+def _u8(x, n):
+    if x is None:
+        return None
+    a = np.frombuffer(bytes(x), dtype=np.uint8).copy()
+    if a.size != n:
+        raise ValueError(f"expected {n} bytes, got {a.size}")
+    return a
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
+
+
+class RxPath:
+    def __init__(self, device: int = 0, max_ns: int = 4096, max_clients: int = 65536,
+                 max_frames: int = 1 << 20, max_bytes: int = 1 << 20):
+        self.lib = abi.load()
+        cfg = abi.Cfg(device, max_ns, max_clients, max_frames, max_bytes)
+        h = C.c_void_p()
+        abi.check(self.lib.emurx_open(C.byref(cfg), C.byref(h)), "emurx_open")
+        self.h = h
+        self.cfg = cfg
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.emurx_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    # ---- registration ----------------------------------------------------------------
+    def register(self, protocol: str):
+        return abi.check(self.lib.emurx_register(self.h, protocol.encode()), "register")
+
+    def register_all(self):
+        for p in ("arp", "icmp", "igmp", "dhcp", "dhcpsrv", "icmpv6", "dhcpv6", "dot1x", "mdns",
+                  "ppp", "transport"):
+            self.register(p)
+
+    def set_callbacks_mask(self, mask: int):
+        return abi.check(self.lib.emurx_set_callbacks_mask(self.h, mask), "set_callbacks_mask")
+
+    @property
+    def callbacks_mask(self) -> int:
+        return int(self.lib.emurx_get_callbacks_mask(self.h))
+
+    # ---- tables (return codes are passed through: they mirror Go's error returns) ------
+    def ns_add(self, key: bytes, ns_id: int, plugins: int = abi.PLUG_ALL) -> int:
+        k = _u8(key, 12)
+        return self.lib.emurx_ns_add(self.h, _p(k), ns_id, plugins)
+
+    def ns_remove(self, key: bytes) -> int:
+        k = _u8(key, 12)
+        return self.lib.emurx_ns_remove(self.h, _p(k))
+
+    def ns_set_plugins(self, ns_id: int, plugins: int) -> int:
+        return self.lib.emurx_ns_set_plugins(self.h, ns_id, plugins)
+
+    def client_add(self, ns_id, cid, mac, ipv4=None, ipv6=None, dhcpv6=None,
+                   plugins: int = abi.PLUG_ALL) -> int:
+        a = [_u8(mac, 6), _u8(ipv4, 4), _u8(ipv6, 16), _u8(dhcpv6, 16)]
+        return self.lib.emurx_client_add(self.h, ns_id, cid, *[_p(x) for x in a], plugins)
+
+    def client_remove(self, ns_id, mac) -> int:
+        m = _u8(mac, 6)
+        return self.lib.emurx_client_remove(self.h, ns_id, _p(m))
+
+    def client_set_plugins(self, cid, plugins) -> int:
+        return self.lib.emurx_client_set_plugins(self.h, cid, plugins)
+
+    def client_update_ipv4(self, cid, ip) -> int:
+        a = _u8(ip, 4)
+        return self.lib.emurx_client_update_ipv4(self.h, cid, _p(a))
+
+    def client_update_ipv6(self, cid, ip) -> int:
+        a = _u8(ip, 16)
+        return self.lib.emurx_client_update_ipv6(self.h, cid, _p(a))
+
+    def client_update_dipv6(self, cid, ip) -> int:
+        a = _u8(ip, 16)
+        return self.lib.emurx_client_update_dipv6(self.h, cid, _p(a))
+
+    def client_set_ra(self, cid, prefix, plen) -> int:
+        a = _u8(prefix, 16)
+        return self.lib.emurx_client_set_ra(self.h, cid, _p(a), plen)
+
+    def sync(self, stream=None):
+        return abi.check(self.lib.emurx_sync(self.h, stream), "sync")
+
+    # ---- host batch (ZMQ message) ------------------------------------------------------
+    def on_rx_stream(self, msg: bytes, cap: int | None = None):
+        cap = cap or int(self.cfg.max_frames)
+        m = np.frombuffer(bytes(msg), dtype=np.uint8).copy() if len(msg) else np.zeros(1, np.uint8)
+        rec = np.zeros(cap, dtype=abi.REC_DTYPE)
+        qlist = np.zeros(cap, dtype=np.uint32)
+        qoff = np.zeros(abi.NUM_QUEUES + 1, dtype=np.uint32)
+        cnt = abi.Counters()
+        n = C.c_uint32()
+        abi.check(self.lib.emurx_rx_stream(self.h, _p(m), len(msg), _p(rec), _p(qlist), cap,
+                                           C.byref(n), _p(qoff), C.byref(cnt)), "rx_stream")
+        k = n.value
+        return rec[:k], qlist[:k], qoff, cnt
+
+    # ---- device-resident batch -----------------------------------------------------------
+    def classify_dev(self, frames, desc, n: int, rec=None, qlist=None, qoff=None, hist=None,
+                     stream=None, classify: bool = True):
+        """frames/desc/rec/qlist/qoff/hist: device tensors (or raw device addresses)."""
+        out = abi.DevOut(_addr(rec), _addr(qlist), _addr(qoff), _addr(hist))
+        fn = self.lib.emurx_classify_dev if classify else self.lib.emurx_parse_dev
+        return abi.check(fn(self.h, _addr(frames), _addr(desc), n, C.byref(out),
+                            _stream(stream)), "classify_dev")
+
+    def set_timing(self, slots: int = 1024):
+        return abi.check(self.lib.emurx_set_timing(self.h, slots), "set_timing")
+
+    def kernel_times(self, cap: int = 1 << 16):
+        """(parse_ms[], compact_ms[]) of the batches since the previous call."""
+        a = np.zeros(cap, np.float32)
+        b = np.zeros(cap, np.float32)
+        n = C.c_uint32()
+        abi.check(self.lib.emurx_kernel_times(self.h, _p(a), _p(b), cap, C.byref(n)), "kernel_times")
+        return a[: n.value], b[: n.value]
+
+
+def _addr(x):
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    return x.data_ptr()
+
+
+def _stream(s):
+    if s is None:
+        return None
+    if isinstance(s, int):
+        return s
+    return s.cuda_stream
+
+
+def zmq_descriptors(msg: bytes, cap: int = 1 << 16):
+    lib = abi.load()
+    m = np.frombuffer(bytes(msg), dtype=np.uint8).copy() if len(msg) else np.zeros(1, np.uint8)
+    d = np.zeros(cap, dtype=abi.DESC_DTYPE)
+    n, e = C.c_uint32(), C.c_int()
+    rc = lib.emurx_zmq_descriptors(_p(m), len(msg), _p(d), cap, C.byref(n), C.byref(e))
+    return rc, d[:n.value], e.value
+
+
+def hist_to_counters(hist: np.ndarray) -> dict:
+    lib = abi.load()
+    h = np.ascontiguousarray(hist, dtype=np.uint64)
+    cnt = abi.Counters()
+    lib.emurx_hist_to_counters(_p(h), C.byref(cnt))
+    return cnt.as_dict()
