@@ -218,14 +218,15 @@ typedef struct emurx_cfg {
 } emurx_cfg;
 
 /* Device-resident outputs of one batch (all pointers are device memory).
-   Per-callback queues are stable (frame order inside a queue) and packed back to back:
-   queue q = qlist[qoff[q] .. qoff[q+1]).  rec/qlist/qoff may individually be NULL to skip
-   that output (hist is required). */
+   Each callback owns a region of qlist: queue q holds the indices of its frames, in frame
+   order, at qlist[q*qcap .. q*qcap + qcount[q]) (queue EMURX_Q_DROP = no callback).
+   rec / qlist / qcount may individually be NULL to skip that output; hist is required. */
 typedef struct emurx_dev_out {
-    emurx_rec* rec;        /* [n] records, frame order                                  */
-    uint32_t* qlist;       /* [n] frame indices grouped by queue                        */
-    uint32_t* qoff;        /* [16] queue start offsets (EMURX_NUM_QUEUES + 1 used)       */
-    uint64_t* hist;        /* [2 * EMURX_HIST_BINS] {pkts, bytes} per bin; ACCUMULATED    */
+    emurx_rec* rec;        /* [n] records, frame order                                   */
+    uint32_t* qlist;       /* [EMURX_NUM_QUEUES * qcap] frame indices                     */
+    uint32_t qcap;         /* region size per queue, >= n                                 */
+    uint32_t* qcount;      /* [16] frames per queue (first 13 used)                       */
+    uint64_t* hist;        /* [2 * EMURX_HIST_BINS] {pkts, bytes} per bin; ACCUMULATED     */
 } emurx_dev_out;
 
 typedef struct emurx_ctx emurx_t;
@@ -276,8 +277,9 @@ int emurx_rx_stream(emurx_t* h, const uint8_t* msg, size_t len, emurx_rec* out_r
 /* Device-resident batch: frames (d_frames) and descriptors (d_desc) already in HBM.
    Enqueues parse+classify+compaction on `stream` (hipStream_t, NULL = handle stream) and
    returns without synchronising.  out->hist is accumulated into (zero it to reset).
-   n <= cfg.max_frames.  The frame buffer must stay readable up to the next 64-byte
-   boundary past its last byte (frames are staged with 16-byte loads). */
+   n <= cfg.max_frames, out->qcap >= n.  The frame buffer must stay readable up to the
+   next 64-byte boundary past its last byte (frames are staged with 16-byte loads).
+   One kernel launch, no host synchronisation: capturable in a hipGraph. */
 int emurx_classify_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_desc,
                        uint32_t n, const emurx_dev_out* out, void* stream);
 
@@ -298,12 +300,15 @@ void emurx_hist_to_counters(const uint64_t hist[2 * EMURX_HIST_BINS], emurx_coun
 
 /* Kernel timing with HIP events recorded on the launch stream around every batch.
    emurx_set_timing(h, slots): slots > 0 keeps the last `slots` batches (ring), 0 disables.
-   emurx_kernel_times(): waits for the most recent batch, returns the parse-kernel and
-   compaction (scan + compact) times in ms of the batches recorded since the previous call
-   (oldest first, at most min(cap, slots)) and resets the ring. */
+   emurx_kernel_times(): waits for the most recent batch and returns, per batch recorded
+   since the previous call (oldest first, at most min(cap, slots)), the device time in ms of
+   the parse/classify kernel and of the queue kernel; then resets the ring. */
 int emurx_set_timing(emurx_t* h, uint32_t slots);
-int emurx_kernel_times(emurx_t* h, float* parse_ms, float* compact_ms, uint32_t cap,
-                       uint32_t* n_out);
+int emurx_kernel_times(emurx_t* h, float* rx_ms, float* q_ms, uint32_t cap, uint32_t* n_out);
+
+/* Sticky device error flag (reserved: no current kernel raises it; 0 = healthy).
+   Synchronises the device. */
+int emurx_device_error(emurx_t* h, int* error);
 
 #ifdef __cplusplus
 }

@@ -15,19 +15,27 @@ def to_dev(a: np.ndarray, pad: int = 64):
 
 
 def run_dev(rx, buf, desc, classify=True):
-    """-> rec, qlist, qoff(14), hist(2*64) as numpy, via emurx_classify_dev / parse_dev."""
+    """-> rec, qlist (packed in queue order), qoff(14), hist(2*64) as numpy, via
+    emurx_classify_dev / emurx_parse_dev (per-queue regions of qcap = n entries)."""
     import torch
     n = len(desc)
+    cap = max(n, 1)
     tb, td = to_dev(buf), to_dev(desc)
-    rec = torch.zeros(max(n, 1) * 32, dtype=torch.uint8, device="cuda")
-    qlist = torch.zeros(max(n, 1), dtype=torch.int32, device="cuda")
-    qoff = torch.full((16,), -1, dtype=torch.int32, device="cuda")
+    rec = torch.zeros(cap * 32, dtype=torch.uint8, device="cuda")
+    qlist = torch.full((abi.NUM_QUEUES * cap,), -1, dtype=torch.int32, device="cuda")
+    qcount = torch.full((16,), -1, dtype=torch.int32, device="cuda")
     hist = torch.zeros(2 * abi.HIST_BINS, dtype=torch.int64, device="cuda")
-    rx.classify_dev(tb, td, n, rec, qlist, qoff, hist, classify=classify)
+    rx.classify_dev(tb, td, n, rec, qlist, cap, qcount, hist, classify=classify)
     torch.cuda.synchronize()
+    assert rx.device_error() == 0
     r = rec.cpu().numpy()[: n * 32].view(abi.REC_DTYPE)
-    return (r, qlist.cpu().numpy()[:n].view(np.uint32), qoff.cpu().numpy()[:14].view(np.uint32),
-            hist.cpu().numpy().view(np.uint64))
+    cnt = qcount.cpu().numpy()[: abi.NUM_QUEUES].view(np.uint32).astype(np.int64)
+    ql = qlist.cpu().numpy().view(np.uint32)
+    qoff = np.zeros(abi.NUM_QUEUES + 1, np.uint32)
+    qoff[1:] = np.cumsum(cnt)
+    packed = np.concatenate([ql[q * cap:q * cap + cnt[q]] for q in range(abi.NUM_QUEUES)]) \
+        if n else np.zeros(0, np.uint32)
+    return r, packed.astype(np.uint32), qoff, hist.cpu().numpy().view(np.uint64)
 
 
 def rec_diff(a, b, limit=5):

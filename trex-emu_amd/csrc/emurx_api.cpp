@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <array>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <unordered_map>
@@ -129,23 +130,26 @@ struct emurx_ctx {
     DevBuf<uint32_t> d_ns, d_nsinfo, d_mac, d_ip4, d_ip6, d_client;
     std::vector<uint32_t> h_ns, h_nsinfo, h_mac, h_ip4, h_ip6, h_client;
 
-    // batch scratch
-    DevBuf<emurx_rec> d_rec_scratch;
+    // batch state (device): histogram shards (kept zero between launches), look-back
+    // granules (16 per tile, zero at allocation), launch control block
+    DevBuf<unsigned long long> d_hshard;
     DevBuf<uint8_t> d_qtag;
-    DevBuf<uint32_t> d_tile_cnt, d_tile_off;
+    DevBuf<uint32_t> d_tile_cnt, d_gsum;
+    DevBuf<emurx_ctl> d_ctl;
+    emurx_scratch scratch() const { return emurx_scratch{d_qtag.p, d_tile_cnt.p, d_gsum.p, d_hshard.p, d_ctl.p}; }
 
     // host batch staging (emurx_rx_stream)
     PinBuf<uint8_t> h_msg;
     PinBuf<emurx_desc> h_desc;
-    PinBuf<uint32_t> h_qoff;
+    PinBuf<uint32_t> h_qcount;
     PinBuf<uint64_t> h_hist;
     DevBuf<uint8_t> d_msg;
     DevBuf<emurx_desc> d_desc;
     DevBuf<emurx_rec> d_rec;
-    DevBuf<uint32_t> d_qlist, d_qoff;
+    DevBuf<uint32_t> d_qlist, d_qcount;
     DevBuf<uint64_t> d_hist;
 
-    // timing ring: 3 events per batch (before parse, after parse, after compaction)
+    // timing ring: 3 events per batch (before k_rx, between k_rx and k_q, after k_q)
     std::vector<hipEvent_t> ev;
     uint32_t slots = 0, ev_head = 0, ev_count = 0;
 
@@ -187,8 +191,13 @@ int rebuild_and_upload(emurx_t* h, hipStream_t st) {
     h->h_ns.assign((size_t)h->ns_slots * 4, 0);
     for (size_t i = 0; i < h->ns_slots; ++i) h->h_ns[i * 4 + 3] = E;
     for (auto& kv : h->ns_map) {
-        uint32_t e[4] = {kv.first.w[0], kv.first.w[1], kv.first.w[2], kv.second};
-        flat_put(h->h_ns, h->ns_slots - 1, 4, emurx_ns_hash(e[0], e[1], e[2]), e);
+        // a key with non-zero bytes [2:4] can never equal a parsed CTunnelKey (Set writes 0
+        // there, thread_ctx.go:93): it has no device slot.  The free upper half of the vport
+        // word carries the Namespace's plugin mask, so one probe answers GetNs + PluginCtx.Get.
+        if (kv.first.w[0] >> 16) continue;
+        uint32_t e[4] = {kv.first.w[0] | (h->ns[kv.second].plugins << 16), kv.first.w[1], kv.first.w[2],
+                         kv.second};
+        flat_put(h->h_ns, h->ns_slots - 1, 4, emurx_ns_hash(kv.first.w[0], e[1], e[2]), e);
     }
     h->h_nsinfo.assign((size_t)h->cfg.max_ns * 4, 0);
     for (uint32_t i = 0; i < h->ns.size(); ++i) {
@@ -203,6 +212,8 @@ int rebuild_and_upload(emurx_t* h, hipStream_t st) {
             uint32_t e[4] = {kv.first.w[0], kv.first.w[1], kv.first.w[2], kv.second};
             uint32_t hh = kind == 0 ? emurx_mac_hash(e[0], e[1], e[2]) : emurx_ip4_hash(e[0], e[1]);
             if (kind == 1) e[2] = 0;
+            // MAC slots carry the client's plugin mask in the free upper half of mac[4..5]
+            if (kind == 0) e[2] |= (h->cl[kv.second].plugins & 0xffffu) << 16;
             flat_put(t, slots - 1, 4, hh, e);
         }
     };
@@ -240,35 +251,24 @@ int rebuild_and_upload(emurx_t* h, hipStream_t st) {
     return EMURX_OK;
 }
 
-int ensure_scratch(emurx_t* h, uint32_t n) {
-    uint32_t tiles = (n + EMURX_TILE - 1) / EMURX_TILE;
-    if (h->d_rec_scratch.alloc(n) || h->d_qtag.alloc(n) || h->d_tile_cnt.alloc((size_t)tiles * 16 + 16) ||
-        h->d_tile_off.alloc((size_t)tiles * 16 + 16))
-        return EMURX_ENOMEM;
-    return EMURX_OK;
-}
-
 int run_dev(emurx_t* h, const uint8_t* frames, const emurx_desc* desc, uint32_t n,
             const emurx_dev_out* out, void* stream, bool classify) {
     if (!h || !out || !out->hist || (n && (!frames || !desc))) return EMURX_EINVAL;
     if (n > h->cfg.max_frames) return EMURX_ENOMEM;
+    if (out->qlist && out->qcap < n) return EMURX_EINVAL;
     int rc = bind(h);
     if (rc) return rc;
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
     if (classify && (rc = rebuild_and_upload(h, st))) return rc;
-    if ((rc = ensure_scratch(h, std::max<uint32_t>(n, 1)))) return rc;
     emurx_dev_tables T = h->tables();
-    hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
+    const hipEvent_t* ev = nullptr;
     if (h->slots) {
         const uint32_t s = h->ev_head;
-        e0 = h->ev[3 * s];
-        e1 = h->ev[3 * s + 1];
-        e2 = h->ev[3 * s + 2];
+        ev = &h->ev[3 * s];
         h->ev_head = (s + 1) % h->slots;
         h->ev_count = std::min(h->ev_count + 1, h->slots);
     }
-    int r = emurx_launch_batch(frames, desc, n, T, classify, *out, h->d_rec_scratch.p, h->d_qtag.p,
-                               h->d_tile_cnt.p, h->d_tile_off.p, st, e0, e1, e2);
+    int r = emurx_launch_batch(frames, desc, n, T, classify, *out, h->scratch(), st, ev);
     return r ? EMURX_EDEVICE : EMURX_OK;
 }
 
@@ -312,6 +312,19 @@ int emurx_open(const emurx_cfg* cfg, emurx_t** out) {
         emurx_close(h);
         return EMURX_ENOMEM;
     }
+    const size_t hs = (size_t)EMURX_HIST_SHARDS * 2 * EMURX_HIST_BINS;
+    const size_t tiles = ((size_t)cfg->max_frames + EMURX_TILE - 1) / EMURX_TILE;
+    const size_t ng = ((tiles + 63) / 64) * 16;
+    emurx_ctl ctl0{0, {0, 0, 0}};
+    if (const char* e = getenv("EMURX_DBG_KQ")) ctl0.rsv[1] = (uint32_t)atoi(e);  // ablation only
+    if (h->d_hshard.alloc(hs) || h->d_qtag.alloc(cfg->max_frames) || h->d_tile_cnt.alloc(tiles * 16) ||
+        h->d_gsum.alloc(ng) || h->d_ctl.alloc(1) ||
+        hipMemset(h->d_hshard.p, 0, hs * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(h->d_gsum.p, 0, ng * sizeof(uint32_t)) != hipSuccess ||
+        hipMemcpy(h->d_ctl.p, &ctl0, sizeof(ctl0), hipMemcpyHostToDevice) != hipSuccess) {
+        emurx_close(h);
+        return EMURX_ENOMEM;
+    }
     h->dirty = true;
     if ((rc = rebuild_and_upload(h, h->stream))) { emurx_close(h); return rc; }
     *out = h;
@@ -324,10 +337,11 @@ void emurx_close(emurx_t* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     h->d_ns.release(); h->d_nsinfo.release(); h->d_mac.release(); h->d_ip4.release();
     h->d_ip6.release(); h->d_client.release();
-    h->d_rec_scratch.release(); h->d_qtag.release(); h->d_tile_cnt.release(); h->d_tile_off.release();
-    h->h_msg.release(); h->h_desc.release(); h->h_qoff.release(); h->h_hist.release();
+    h->d_hshard.release(); h->d_qtag.release(); h->d_tile_cnt.release(); h->d_gsum.release();
+    h->d_ctl.release();
+    h->h_msg.release(); h->h_desc.release(); h->h_qcount.release(); h->h_hist.release();
     h->d_msg.release(); h->d_desc.release(); h->d_rec.release(); h->d_qlist.release();
-    h->d_qoff.release(); h->d_hist.release();
+    h->d_qcount.release(); h->d_hist.release();
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
     h->ev.clear();
@@ -592,11 +606,11 @@ int emurx_rx_stream(emurx_t* h, const uint8_t* msg, size_t len, emurx_rec* out_r
     *n_out = 0;
     int rc = bind(h);
     if (rc) return rc;
-    const uint32_t cap = std::min(out_cap, h->cfg.max_frames);
-    if (h->h_desc.alloc(std::max<uint32_t>(cap, 1)) || h->h_msg.alloc(len + 64) || h->h_qoff.alloc(16) ||
-        h->h_hist.alloc(2 * EMURX_HIST_BINS) || h->d_msg.alloc(len + 64) || h->d_desc.alloc(std::max<uint32_t>(cap, 1)) ||
-        h->d_rec.alloc(std::max<uint32_t>(cap, 1)) || h->d_qlist.alloc(std::max<uint32_t>(cap, 1)) ||
-        h->d_qoff.alloc(16) || h->d_hist.alloc(2 * EMURX_HIST_BINS))
+    const uint32_t cap = std::max<uint32_t>(std::min(out_cap, h->cfg.max_frames), 1);
+    if (h->h_desc.alloc(cap) || h->h_msg.alloc(len + 64) || h->h_qcount.alloc(16) ||
+        h->h_hist.alloc(2 * EMURX_HIST_BINS) || h->d_msg.alloc(len + 64) || h->d_desc.alloc(cap) ||
+        h->d_rec.alloc(cap) || h->d_qlist.alloc((size_t)EMURX_NUM_QUEUES * cap) || h->d_qcount.alloc(16) ||
+        h->d_hist.alloc(2 * EMURX_HIST_BINS))
         return EMURX_ENOMEM;
     int perr = 0;
     uint32_t n = 0;
@@ -619,19 +633,28 @@ int emurx_rx_stream(emurx_t* h, const uint8_t* msg, size_t len, emurx_rec* out_r
     if (!out_rec || !out_qlist) return EMURX_EINVAL;
     memcpy(h->h_msg.p, msg, len);
     memset(h->h_msg.p + len, 0, 64);
-    emurx_dev_out o{h->d_rec.p, h->d_qlist.p, h->d_qoff.p, h->d_hist.p};
+    emurx_dev_out o{h->d_rec.p, h->d_qlist.p, cap, h->d_qcount.p, h->d_hist.p};
     bool ok = hipMemcpyAsync(h->d_msg.p, h->h_msg.p, len + 64, hipMemcpyHostToDevice, st) == hipSuccess &&
               hipMemcpyAsync(h->d_desc.p, h->h_desc.p, (size_t)n * sizeof(emurx_desc), hipMemcpyHostToDevice, st) == hipSuccess &&
               hipMemsetAsync(h->d_hist.p, 0, 2 * EMURX_HIST_BINS * sizeof(uint64_t), st) == hipSuccess;
     if (!ok) return EMURX_EDEVICE;
     if ((rc = run_dev(h, h->d_msg.p, h->d_desc.p, n, &o, st, true))) return rc;
     ok = hipMemcpyAsync(out_rec, h->d_rec.p, (size_t)n * sizeof(emurx_rec), hipMemcpyDeviceToHost, st) == hipSuccess &&
-         hipMemcpyAsync(out_qlist, h->d_qlist.p, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost, st) == hipSuccess &&
-         hipMemcpyAsync(h->h_qoff.p, h->d_qoff.p, 16 * sizeof(uint32_t), hipMemcpyDeviceToHost, st) == hipSuccess &&
+         hipMemcpyAsync(h->h_qcount.p, h->d_qcount.p, 16 * sizeof(uint32_t), hipMemcpyDeviceToHost, st) == hipSuccess &&
          hipMemcpyAsync(h->h_hist.p, h->d_hist.p, 2 * EMURX_HIST_BINS * sizeof(uint64_t), hipMemcpyDeviceToHost, st) == hipSuccess &&
          hipStreamSynchronize(st) == hipSuccess;
     if (!ok) return EMURX_EDEVICE;
-    memcpy(out_qoff, h->h_qoff.p, sizeof(uint32_t) * (EMURX_NUM_QUEUES + 1));
+    // pack the per-queue regions back to back (out_qoff[q] .. out_qoff[q+1])
+    out_qoff[0] = 0;
+    for (int q = 0; q < EMURX_NUM_QUEUES; ++q) {
+        const uint32_t c = h->h_qcount.p[q];
+        if (c > n || out_qoff[q] + c > n) return EMURX_EDEVICE;
+        if (c && hipMemcpyAsync(out_qlist + out_qoff[q], h->d_qlist.p + (size_t)q * cap, (size_t)c * 4,
+                                hipMemcpyDeviceToHost, st) != hipSuccess)
+            return EMURX_EDEVICE;
+        out_qoff[q + 1] = out_qoff[q] + c;
+    }
+    if (hipStreamSynchronize(st) != hipSuccess) return EMURX_EDEVICE;
     emurx_hist_to_counters(h->h_hist.p, delta);
     return EMURX_OK;
 }
@@ -641,6 +664,7 @@ int emurx_set_timing(emurx_t* h, uint32_t slots) {
     int rc = bind(h);
     if (rc) return rc;
     (void)hipStreamSynchronize(h->stream);
+    (void)hipDeviceSynchronize();
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
     h->ev.assign((size_t)slots * 3, nullptr);
@@ -651,8 +675,8 @@ int emurx_set_timing(emurx_t* h, uint32_t slots) {
     return EMURX_OK;
 }
 
-int emurx_kernel_times(emurx_t* h, float* parse_ms, float* compact_ms, uint32_t cap, uint32_t* n_out) {
-    if (!h || !n_out || (cap && (!parse_ms || !compact_ms))) return EMURX_EINVAL;
+int emurx_kernel_times(emurx_t* h, float* rx_ms, float* q_ms, uint32_t cap, uint32_t* n_out) {
+    if (!h || !n_out || (cap && (!rx_ms || !q_ms))) return EMURX_EINVAL;
     *n_out = 0;
     if (!h->slots || !h->ev_count) return EMURX_OK;
     int rc = bind(h);
@@ -663,12 +687,24 @@ int emurx_kernel_times(emurx_t* h, float* parse_ms, float* compact_ms, uint32_t 
     const uint32_t first = (h->ev_head + h->slots - h->ev_count) % h->slots;
     for (uint32_t k = 0; k < n; ++k) {
         const uint32_t s = (first + (h->ev_count - n) + k) % h->slots;
-        if (hipEventElapsedTime(&parse_ms[k], h->ev[3 * s], h->ev[3 * s + 1]) != hipSuccess ||
-            hipEventElapsedTime(&compact_ms[k], h->ev[3 * s + 1], h->ev[3 * s + 2]) != hipSuccess)
+        if (hipEventElapsedTime(&rx_ms[k], h->ev[3 * s], h->ev[3 * s + 1]) != hipSuccess ||
+            hipEventElapsedTime(&q_ms[k], h->ev[3 * s + 1], h->ev[3 * s + 2]) != hipSuccess)
             return EMURX_EDEVICE;
     }
     *n_out = n;
     h->ev_count = 0;
+    return EMURX_OK;
+}
+
+int emurx_device_error(emurx_t* h, int* error) {
+    if (!h || !error) return EMURX_EINVAL;
+    int rc = bind(h);
+    if (rc) return rc;
+    emurx_ctl c{};
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(&c, h->d_ctl.p, sizeof(c), hipMemcpyDeviceToHost) != hipSuccess)
+        return EMURX_EDEVICE;
+    *error = (int)c.rsv[0];
     return EMURX_OK;
 }
 

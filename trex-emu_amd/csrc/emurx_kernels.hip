@@ -1,569 +1,85 @@
 // emurx_kernels.hip — CDNA4 (gfx950) kernels of the TRex-EMU receive path.
 //
-// One frame per lane, wave64.  Per batch:
-//   k_parse    descriptors -> per-wave LDS staging of the frames' bytes (coalesced 16-B
-//              loads of the wave's contiguous byte range) -> header decode + IPv4 / L4
-//              checksum (dword sums, see csum_span) -> Namespace / Client probes ->
-//              32-B record, queue tag, per-tile queue counts, outcome histogram.
-//   k_scan     exclusive scan of the per-tile queue counts (one workgroup).
-//   k_compact  stable per-callback queues of frame indices (ballot + popcount ranks).
-// No MFMA: there is no dense contraction on this path; it is HBM / issue bound.
-//
-// Control flow restates src/emu/core/parser.go:583-959 (ParsePacket, parsePacketL4,
-// processIpv6Options) and the per-callback lookup rules of src/emu/plugins/*; the CPU
-// oracle (oracle/emurx_oracle.c) is the line-by-line twin the parity tests compare with.
+// Two wait-free launches per batch (no workgroup ever waits for another):
+//   k_rx  one frame per lane, wave64: descriptors -> per-wave LDS staging of the frames'
+//         bytes (coalesced 16-B loads of the wave's contiguous byte range) -> header decode
+//         + IPv4 / L4 checksum -> Namespace / Client probes (emurx_parse.h) -> 32-B record,
+//         1-B queue tag, per-tile queue counts, per-group queue totals (atomic adds into
+//         one of ngroups = ntiles/64 rows), outcome-histogram shard.
+//   k_q   stable per-callback queues of frame indices: a tile's exclusive prefix is the
+//         totals of the groups before it (one lane per group) + the counts of its earlier
+//         group mates (one lane per tile) — two loads per lane, no scan launch, no chain;
+//         ranks inside the tile by wave ballots.  The last workgroup to finish folds the
+//         histogram shards into the caller's histogram and clears the group totals, so the
+//         pair of launches needs no host-side state (replayable from a hipGraph).
+// No MFMA: there is no dense contraction on this path; it is HBM / latency bound.
 #include <hip/hip_runtime.h>
 
 #include "../../include/emu_rx.h"
 #include "emurx_kernels.h"
+#include "emurx_parse.h"
 #include "emurx_tables.h"
 
 namespace emurx {
 
-constexpr int kWave = 64;
-constexpr int kBlock = 256;
-constexpr int kWaves = kBlock / kWave;
-constexpr uint32_t kStage = 8192;  // LDS bytes staged per wave (64 frames)
+static_assert(EMURX_TILE == kBlock, "one frame per lane per tile");
+constexpr uint32_t kGroup = 64;  // tiles per group total (one wave lane each)
 
-// ---------------------------------------------------------------------------------------
-// wave helpers
-// ---------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o));
-    return v;
-}
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
-    return v;
-}
-__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, o);
-        uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o);
-        v += ((uint64_t)hi << 32) | lo;
-    }
+    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
     return v;
 }
 
 // ---------------------------------------------------------------------------------------
-// RFC 1071 sum, restated for dword loads.
-// Go (layers/tcpip.go:76-94) adds big-endian byte pairs of the span into a uint32 and
-// folds; the span is valid iff the folded value is 0xffff.  Modulo 0xffff, 2^16 == 1 and
-// 256*256 == 1, so a little-endian dword at an aligned address contributes each byte with
-// weight 256^(address & 1).  Summing masked aligned dwords therefore gives
-//   S_go == T * 256^(1 - (span_start & 1))   (mod 0xffff)
-// and S_go + pseudo == 0 (mod 0xffff) with a non-zero total <=> Go's check passes.
-// ---------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t fold16(uint64_t s) {
-    uint32_t x = (uint32_t)(s & 0xffff) + (uint32_t)((s >> 16) & 0xffff) +
-                 (uint32_t)((s >> 32) & 0xffff) + (uint32_t)(s >> 48);
-    x = (x & 0xffff) + (x >> 16);
-    x = (x & 0xffff) + (x >> 16);
-    return x;  // <= 0xffff, == s mod 0xffff (0xffff stands for 0)
-}
-__device__ __forceinline__ uint32_t byte_mask(int sb, int eb) {  // bytes [sb, eb) of a dword
-    uint32_t lo = eb >= 4 ? 0xffffffffu : ((1u << (8 * max(eb, 0))) - 1u);
-    uint32_t hi = sb <= 0 ? 0xffffffffu : (sb >= 4 ? 0u : (0xffffffffu << (8 * sb)));
-    return lo & hi;
-}
-// true iff tcpipChecksum(span, pcs) == 0
-__device__ __forceinline__ bool csum_ok(uint64_t sum, bool all_zero, uint32_t a_start, uint32_t pcs) {
-    uint32_t t = fold16(sum);
-    if ((a_start & 1u) == 0) t = ((t << 8) | (t >> 8)) & 0xffffu;
-    uint32_t x = t + pcs;
-    x = (x & 0xffff) + (x >> 16);
-    x = (x & 0xffff) + (x >> 16);
-    x = (x & 0xffff) + (x >> 16);
-    return (x == 0xffffu || x == 0u) && !(all_zero && pcs == 0);
-}
-
-// ---------------------------------------------------------------------------------------
-// byte sources: the wave's LDS slab (fast path) or global memory (frames that do not fit)
-// ---------------------------------------------------------------------------------------
-struct LdsSrc {
-    const uint8_t* b8;    // block LDS
-    const uint32_t* b32;  // same array, dword view
-    uint32_t base;        // LDS byte index of frame byte 0 (== global address mod 16)
-    __device__ __forceinline__ uint32_t u8(uint32_t i) const { return b8[base + i]; }
-    __device__ __forceinline__ bool csum(uint32_t s, uint32_t n, uint32_t pcs) const {
-        uint32_t a = base + s, e = a + n;
-        uint32_t k0 = a >> 2, k1 = (e + 3) >> 2;
-        uint64_t sum = 0;
-        uint32_t orv = 0;
-        for (uint32_t k = k0; k < k1; ++k) {
-            uint32_t w = b32[k];
-            int rel = (int)(k << 2);
-            w &= byte_mask((int)a - rel, (int)e - rel);
-            sum += w;
-            orv |= w;
-        }
-        return csum_ok(sum, orv == 0, a, pcs);
-    }
-};
-struct GlbSrc {
-    const uint8_t* f;  // frame byte 0 (global)
-    __device__ __forceinline__ uint32_t u8(uint32_t i) const { return f[i]; }
-    __device__ __forceinline__ bool csum(uint32_t s, uint32_t n, uint32_t pcs) const {
-        uintptr_t a = (uintptr_t)(f + s), e = a + n;
-        const uint32_t* w32 = (const uint32_t*)(a & ~(uintptr_t)3);
-        uint32_t nw = (uint32_t)(((e + 3) & ~(uintptr_t)3) - (a & ~(uintptr_t)3)) >> 2;
-        uint64_t sum = 0;
-        uint32_t orv = 0;
-        int sa = (int)(a & 3);
-        int ee = (int)(e - (a & ~(uintptr_t)3));
-        for (uint32_t k = 0; k < nw; ++k) {
-            uint32_t w = w32[k];
-            int rel = (int)(k << 2);
-            w &= byte_mask(sa - rel, ee - rel);
-            sum += w;
-            orv |= w;
-        }
-        return csum_ok(sum, orv == 0, (uint32_t)a, pcs);
-    }
-};
-
-template <class S>
-__device__ __forceinline__ uint32_t be16(const S& s, uint32_t i) { return (s.u8(i) << 8) | s.u8(i + 1); }
-template <class S>
-__device__ __forceinline__ uint32_t be32(const S& s, uint32_t i) {
-    return (s.u8(i) << 24) | (s.u8(i + 1) << 16) | (s.u8(i + 2) << 8) | s.u8(i + 3);
-}
-template <class S>  // bytes i..i+3 as a little-endian word (the table key encoding)
-__device__ __forceinline__ uint32_t le32(const S& s, uint32_t i) {
-    return s.u8(i) | (s.u8(i + 1) << 8) | (s.u8(i + 2) << 16) | (s.u8(i + 3) << 24);
-}
-
-// ---------------------------------------------------------------------------------------
-// parse state == ParserPacketState + CTunnelData + outcome
-// ---------------------------------------------------------------------------------------
-struct Rec {
-    uint32_t ns, cl, vlan0, vlan1;
-    uint32_t vport, l3, l4, l7, l7len;
-    uint32_t nh, proto, status, flags;
-};
-
-__device__ __forceinline__ void invoke(Rec& r, uint32_t cb, uint32_t cb_mask) {
-    r.proto = cb;
-    if (cb_mask & (1u << cb)) r.status = EMURX_ST_OK;
-    else if (cb == EMURX_CB_EAPOL) r.status = EMURX_ST_PANIC_NIL_EAPOL;  // nil ParserCb :789
-    else r.status = EMURX_ST_NOT_SUPPORTED;                              // parserNotSupported
-}
-__device__ __forceinline__ void fail(Rec& r, uint32_t st) { r.status = st; r.proto = EMURX_CB_NONE; }
-
-__device__ __forceinline__ bool span_ok(uint32_t l4, uint32_t l4len) {
-    return ((l4 + l4len) & 0xffffu) >= l4;  // Go slice p[L4:L4+l4len] with uint16 end
-}
-
-// processIpv6Options parser.go:726-746; false on Go's out-of-range p[i+1]
-template <class S>
-__device__ bool ipv6_options(const S& s, uint32_t p0, int size, uint32_t& flags) {
-    int i = 0;
-    uint32_t nh = s.u8(p0);
-    for (;;) {
-        if (nh == 0) {
-            i++;
-        } else if (nh == 5) {
-            flags |= EMURX_FLAG_RTALERT;
-            return true;
-        } else {
-            if (i + 1 >= size) return false;
-            i = i + 2 + (int)s.u8(p0 + i + 1);
-        }
-        if (i > size - 1) return true;
-        nh = s.u8(p0 + i);
-    }
-}
-
-// Parser.parsePacketL4 parser.go:583-724
-template <class S>
-__device__ void parse_l4(const S& s, uint32_t len, Rec& r, uint32_t nextHdr, uint32_t pcs,
-                         uint32_t l4len, bool v6, uint32_t cb_mask) {
-    r.nh = nextHdr;
-    const uint32_t L4 = r.l4;
-    switch (nextHdr) {
-    case 1:  // ICMPv4
-        if (len < ((L4 + 8) & 0xffff)) { fail(r, EMURX_ST_ICMPV4_TOO_SHORT); return; }
-        if (!span_ok(L4, l4len)) { fail(r, EMURX_ST_PANIC_L4LEN); return; }
-        if (!s.csum(L4, l4len, 0)) { fail(r, EMURX_ST_ICMPV4_CS); return; }
-        r.l7 = (L4 + 8) & 0xffff;
-        invoke(r, EMURX_CB_ICMP, cb_mask);
-        return;
-    case 2:  // IGMP (no checksum in the parser)
-        if (len < ((L4 + 8) & 0xffff)) { fail(r, EMURX_ST_ICMPV4_TOO_SHORT); return; }
-        invoke(r, EMURX_CB_IGMP, cb_mask);
-        return;
-    case 6: {  // TCP
-        if (l4len < 20) { fail(r, EMURX_ST_TCP_TOO_SHORT); return; }
-        if (((L4 + 12) & 0xffff) >= len) { fail(r, EMURX_ST_PANIC_L4LEN); return; }
-        uint32_t tcplen = (s.u8((L4 + 12) & 0xffff) >> 4) << 2;
-        if (l4len < tcplen) { fail(r, EMURX_ST_TCP_TOO_SHORT); return; }
-        r.l7 = (L4 + tcplen) & 0xffff;
-        r.l7len = (l4len - tcplen) & 0xffff;
-        if (!span_ok(L4, l4len)) { fail(r, EMURX_ST_PANIC_L4LEN); return; }
-        if (!s.csum(L4, l4len, pcs)) { fail(r, EMURX_ST_TCP_CS); return; }
-        invoke(r, EMURX_CB_TCP, cb_mask);
-        return;
-    }
-    case 17: {  // UDP
-        if (len < ((L4 + 8) & 0xffff)) { fail(r, EMURX_ST_UDP_TOO_SHORT); return; }
-        r.l7len = (l4len - 8) & 0xffff;
-        if (be16(s, L4 + 6) > 0) {
-            if (!span_ok(L4, l4len)) { fail(r, EMURX_ST_PANIC_L4LEN); return; }
-            if (!s.csum(L4, l4len, pcs)) { fail(r, EMURX_ST_UDP_CS); return; }
-        }
-        r.l7 = (L4 + 8) & 0xffff;
-        uint32_t src = be16(s, L4), dst = be16(s, L4 + 2);
-        uint32_t cb = EMURX_CB_UDP;
-        if (dst == 5353) cb = EMURX_CB_MDNS;
-        else if (v6) { if (src == 547 && dst == 546) cb = EMURX_CB_DHCPV6; }
-        else if (src == 67 && dst == 68) cb = EMURX_CB_DHCP;
-        else if (dst == 67 && (src == 67 || src == 68)) cb = EMURX_CB_DHCPSRV;
-        invoke(r, cb, cb_mask);
-        return;
-    }
-    case 58: {  // ICMPv6
-        if (len < ((L4 + 4) & 0xffff)) { fail(r, EMURX_ST_ICMPV6_TOO_SHORT); return; }
-        if (!span_ok(L4, l4len)) { fail(r, EMURX_ST_PANIC_L4LEN); return; }
-        if (!s.csum(L4, l4len, pcs)) { fail(r, EMURX_ST_ICMPV6_CS); return; }
-        uint32_t t = s.u8(L4);
-        bool okt = (t >= 1 && t <= 4) || (t >= 128 && t <= 136);
-        if (okt) invoke(r, EMURX_CB_ICMPV6, cb_mask);
-        else fail(r, EMURX_ST_ICMPV6_UNSUPPORTED);
-        return;
-    }
-    default:
-        fail(r, EMURX_ST_L4_UNSUPPORTED);
-        return;
-    }
-}
-
-// pseudo-header partial sums: IPv4Header.GetPhCs ip4.go:49-58, IPv6Header.GetPhCs ip6.go:126-134
-template <class S>
-__device__ __forceinline__ uint32_t pair_sum(const S& s, uint32_t p, int n) {
-    uint32_t c = 0;
-    for (int i = 0; i < n; i += 2) c += be16(s, p + i);
-    return c;
-}
-
-// Parser.ParsePacket parser.go:756-959
-template <class S>
-__device__ void parse_packet(const S& s, uint32_t len, uint32_t vport, uint32_t cb_mask, Rec& r) {
-    r.ns = EMURX_ID_NONE; r.cl = EMURX_ID_NONE;
-    r.vlan0 = 0; r.vlan1 = 0; r.vport = vport;
-    r.l3 = r.l4 = r.l7 = r.l7len = 0;
-    r.nh = 0; r.proto = EMURX_CB_NONE; r.status = EMURX_ST_OK; r.flags = 0;
-    if (len < 14) { fail(r, EMURX_ST_PACKET_TOO_SHORT); return; }
-    uint32_t offset = 14;
-    uint32_t nextHdr = be16(s, 12);
-    int vlanIndex = 0;
-    for (;;) {
-        if (nextHdr == 0x8100 || nextHdr == 0x88A8) {
-            if (len < offset + 4) { fail(r, EMURX_ST_DOT1Q_TOO_SHORT); return; }
-            if (vlanIndex > 1) { fail(r, EMURX_ST_TOO_MANY_DOT1Q); return; }
-            uint32_t val = be32(s, offset - 2) & 0xffff0fffu;
-            if (vlanIndex == 0) r.vlan0 = val; else r.vlan1 = val;
-            vlanIndex++;
-            nextHdr = be16(s, offset + 2);
-            if (nextHdr == 0x8863 || nextHdr == 0x8864) { invoke(r, EMURX_CB_PPP, cb_mask); return; }
-            offset += 4;
-            continue;
-        }
-        if (nextHdr == 0x0800) {  // IPv4
-            r.l3 = offset;
-            if (len < offset + 20) { fail(r, EMURX_ST_IPV4_TOO_SHORT); return; }
-            uint32_t b0 = s.u8(offset);
-            if ((b0 >> 4) != 4) { fail(r, EMURX_ST_IPV4_HDR_TOO_SHORT); return; }
-            uint32_t frag = be16(s, offset + 6);
-            if ((frag & 0x1fff) != 0 || (frag & 0x2000) != 0) { fail(r, EMURX_ST_IPV4_FRAGMENT); return; }
-            uint32_t hdr = (b0 & 0xf) << 2;
-            if (hdr < 20) { fail(r, EMURX_ST_IPV4_HDR_TOO_SHORT); return; }
-            if (len < offset + hdr) { fail(r, EMURX_ST_IPV4_HDR_TOO_SHORT); return; }
-            uint32_t totlen = be16(s, offset + 2);
-            if (len < ((offset + totlen) & 0xffff)) { fail(r, EMURX_ST_IPV4_TOO_SHORT); return; }
-            if (!s.csum(offset, hdr, 0)) { fail(r, EMURX_ST_IPV4_CS); return; }
-            uint32_t l4len = (totlen - hdr) & 0xffff;
-            r.l4 = offset + hdr;
-            uint32_t proto = s.u8(offset + 9);
-            uint32_t pcs = pair_sum(s, offset + 12, 8) + proto + l4len;  // src, dst, 0|proto, len
-            parse_l4(s, len, r, proto, pcs, l4len, false, cb_mask);
-            return;
-        }
-        if (nextHdr == 0x86DD) {  // IPv6
-            r.l3 = offset;
-            if (len < offset + 40) { fail(r, EMURX_ST_IPV6_TOO_SHORT); return; }
-            if ((s.u8(offset) >> 4) != 6) { fail(r, EMURX_ST_IPV6_TOO_SHORT); return; }
-            uint32_t plen = be16(s, offset + 4);
-            if (len < ((offset + 40 + plen) & 0xffff)) { fail(r, EMURX_ST_IPV6_TOO_SHORT); return; }
-            if (s.u8(offset + 7) == 0) { fail(r, EMURX_ST_IPV6_HOPLIMIT); return; }
-            uint32_t l4 = offset + 40, l4len = plen, osize = 0;
-            uint32_t nh = s.u8(offset + 6);
-            for (;;) {
-                bool ext = nh == 0 || nh == 60 || nh == 43 || nh == 51 || nh == 50 || nh == 135 ||
-                           nh == 139 || nh == 140;
-                if (!ext) break;
-                if (l4len < 8) { fail(r, EMURX_ST_IPV6_TOO_SHORT); return; }
-                if (l4 + 2 > len) { fail(r, EMURX_ST_PANIC_L4LEN); return; }
-                uint32_t hl = (s.u8(l4 + 1) << 3) + 8;
-                if (l4len < hl) { fail(r, EMURX_ST_IPV6_TOO_SHORT); return; }
-                if (l4 + hl > len) { fail(r, EMURX_ST_PANIC_L4LEN); return; }
-                uint32_t nnh = s.u8(l4);
-                if (!ipv6_options(s, l4 + 2, (int)hl - 2, r.flags)) { fail(r, EMURX_ST_PANIC_IPV6_OPT); return; }
-                nh = nnh;
-                l4len -= hl;
-                osize += hl;
-                l4 += hl;
-            }
-            if (nh == 44) { fail(r, EMURX_ST_IPV6_FRAGMENT); return; }
-            if (nh == 194) { fail(r, EMURX_ST_IPV6_JUMBO); return; }
-            if (nh == 59) { fail(r, EMURX_ST_IPV6_EMPTY); return; }
-            r.l4 = l4;
-            uint32_t pcs = pair_sum(s, offset + 8, 32) + ((plen - osize) & 0xffff) + nh;
-            parse_l4(s, len, r, nh, pcs, l4len, true, cb_mask);
-            return;
-        }
-        if (nextHdr == 0x888E) {  // EAPOL
-            if (len < offset + 4) { fail(r, EMURX_ST_EAPOL_TOO_SHORT); return; }
-            r.l3 = offset;
-            invoke(r, EMURX_CB_EAPOL, cb_mask);
-            return;
-        }
-        if (nextHdr == 0x0806) {  // ARP, ARPHeaderSize 28
-            if (len < offset + 28) { fail(r, EMURX_ST_ARP_TOO_SHORT); return; }
-            r.l3 = offset;
-            invoke(r, EMURX_CB_ARP, cb_mask);
-            return;
-        }
-        if (nextHdr == 0x8863 || nextHdr == 0x8864) { invoke(r, EMURX_CB_PPP, cb_mask); return; }
-        fail(r, EMURX_ST_L3_UNSUPPORTED);
-        return;
-    }
-}
-
-// ---------------------------------------------------------------------------------------
-// Namespace / Client lookups (GetNs thread_ctx.go:777-784, CLookupBy* ns_ctx.go:262-329)
-// ---------------------------------------------------------------------------------------
-__device__ __forceinline__ uint4 ld4(const uint32_t* p) { return *reinterpret_cast<const uint4*>(p); }
-
-__device__ uint32_t probe_ns(const emurx_dev_tables& T, uint32_t w0, uint32_t w1, uint32_t w2) {
-    uint32_t i = emurx_ns_hash(w0, w1, w2) & T.ns_mask;
-    for (uint32_t k = 0; k <= T.ns_mask; ++k, i = (i + 1) & T.ns_mask) {
-        uint4 e = ld4(T.ns_tab + 4 * i);
-        if (e.w == EMURX_EMPTY) return EMURX_ID_NONE;
-        if (e.x == w0 && e.y == w1 && e.z == w2) return e.w;
-    }
-    return EMURX_ID_NONE;
-}
-__device__ uint32_t probe_mac(const emurx_dev_tables& T, uint32_t ns, uint32_t lo, uint32_t hi) {
-    if (lo == 0 && hi == 0) return EMURX_ID_NONE;  // MACKey.IsZero
-    uint32_t i = emurx_mac_hash(ns, lo, hi) & T.mac_mask;
-    for (uint32_t k = 0; k <= T.mac_mask; ++k, i = (i + 1) & T.mac_mask) {
-        uint4 e = ld4(T.mac_tab + 4 * i);
-        if (e.w == EMURX_EMPTY) return EMURX_ID_NONE;
-        if (e.x == ns && e.y == lo && e.z == hi) return e.w;
-    }
-    return EMURX_ID_NONE;
-}
-__device__ uint32_t probe_ip4(const emurx_dev_tables& T, uint32_t ns, uint32_t ip) {
-    if (ip == 0) return EMURX_ID_NONE;
-    uint32_t i = emurx_ip4_hash(ns, ip) & T.ip4_mask;
-    for (uint32_t k = 0; k <= T.ip4_mask; ++k, i = (i + 1) & T.ip4_mask) {
-        uint4 e = ld4(T.ip4_tab + 4 * i);
-        if (e.w == EMURX_EMPTY) return EMURX_ID_NONE;
-        if (e.x == ns && e.y == ip) return e.w;
-    }
-    return EMURX_ID_NONE;
-}
-__device__ uint32_t probe_ip6(const emurx_dev_tables& T, uint32_t ns, const uint32_t ip[4]) {
-    if ((ip[0] | ip[1] | ip[2] | ip[3]) == 0) return EMURX_ID_NONE;
-    uint32_t i = emurx_ip6_hash(ns, ip[0], ip[1], ip[2], ip[3]) & T.ip6_mask;
-    for (uint32_t k = 0; k <= T.ip6_mask; ++k, i = (i + 1) & T.ip6_mask) {
-        uint4 a = ld4(T.ip6_tab + 8 * i);
-        uint4 b = ld4(T.ip6_tab + 8 * i + 4);
-        if (b.w == EMURX_EMPTY) return EMURX_ID_NONE;
-        if (a.x == ns && a.y == ip[0] && a.z == ip[1] && a.w == ip[2] && b.x == ip[3]) return b.w;
-    }
-    return EMURX_ID_NONE;
-}
-
-__device__ __forceinline__ void set_lk(Rec& r, uint32_t lk) {
-    r.flags = (r.flags & ~EMURX_FLAG_LK_MASK) | (lk << EMURX_FLAG_LK_SHIFT);
-}
-__device__ __forceinline__ void client_result(const emurx_dev_tables& T, Rec& r, uint32_t cid,
-                                              uint32_t plug, bool check) {
-    if (cid == EMURX_ID_NONE) { set_lk(r, EMURX_LK_NO_CLIENT); return; }
-    r.cl = cid;
-    if (check && !(T.client[8 * cid + 2] & (1u << plug))) { set_lk(r, EMURX_LK_CLIENT_NO_PLUGIN); return; }
-    set_lk(r, EMURX_LK_CLIENT);
-}
-// CClient.IsUnicastToMe client_ctx.go:389-398 (frames here are always > 6 bytes)
-__device__ __forceinline__ bool unicast_to_me(const emurx_dev_tables& T, uint32_t cid,
-                                              uint32_t dlo, uint32_t dhi) {
-    return T.client[8 * cid + 0] == dlo && T.client[8 * cid + 1] == dhi;
-}
-
-// Go 1.18 net.IP.IsLinkLocalUnicast / IsGlobalUnicast for a 16-byte address (words LE)
-__device__ bool ip6_local_or_global(const uint32_t w[4]) {
-    uint32_t b0 = w[0] & 0xff, b1 = (w[0] >> 8) & 0xff;
-    bool v4in6 = w[0] == 0 && w[1] == 0 && (w[2] & 0xffff) == 0 && (w[2] >> 16) == 0xffffu;
-    if (v4in6) {
-        uint32_t v = w[3], c0 = v & 0xff, c1 = (v >> 8) & 0xff;
-        bool ll = c0 == 169 && c1 == 254;
-        if (ll) return true;
-        if (v == 0xffffffffu || v == 0 || c0 == 127 || (c0 & 0xf0) == 0xe0) return false;
-        return true;
-    }
-    bool ll = b0 == 0xfe && (b1 & 0xc0) == 0x80;
-    if (ll) return true;
-    if ((w[0] | w[1] | w[2] | w[3]) == 0) return false;                      // unspecified
-    if (w[0] == 0 && w[1] == 0 && w[2] == 0 && w[3] == 0x01000000u) return false;  // ::1
-    if (b0 == 0xff) return false;                                            // multicast
-    return true;
-}
-// CNSCtx.CLookupByIPv6LocalGlobal ns_ctx.go:288-316
-__device__ uint32_t lookup_ip6_lg(const emurx_dev_tables& T, uint32_t ns, const uint32_t w[4]) {
-    if (!ip6_local_or_global(w)) return EMURX_ID_NONE;
-    uint32_t b11 = (w[2] >> 24) & 0xff, b12 = w[3] & 0xff;
-    if (b11 == 0xff && b12 == 0xfe) {  // ExtractOnlyMac client_ctx.go:314-329
-        uint32_t m0 = (w[2] & 0xff) ^ 2, m1 = (w[2] >> 8) & 0xff, m2 = (w[2] >> 16) & 0xff;
-        uint32_t m3 = (w[3] >> 8) & 0xff, m4 = (w[3] >> 16) & 0xff, m5 = w[3] >> 24;
-        uint32_t lo = m0 | (m1 << 8) | (m2 << 16) | (m3 << 24), hi = m4 | (m5 << 8);
-        uint32_t cid = probe_mac(T, ns, lo, hi);
-        if (cid == EMURX_ID_NONE) return cid;
-        // CClient.IsValidPrefix client_ctx.go:279-295
-        if (w[0] == 0x000080feu && w[1] == 0) return cid;
-        const uint32_t* c = T.client + 8 * cid;
-        uint32_t ra = c[3];
-        if ((ra & 1u) && ((ra >> 8) & 0xff) == 64 && c[4] == w[0] && c[5] == w[1]) return cid;
-        return EMURX_ID_NONE;
-    }
-    return probe_ip6(T, ns, w);
-}
-// PluginDhcpNs.GetMacFromDhcp dhcp.go:863-891 + DHCPv4.DecodeFromBytes dhcpv4.go:125-172
-template <class S>
-__device__ bool dhcp_chaddr(const S& s, uint32_t len, const Rec& r, uint32_t& lo, uint32_t& hi) {
-    uint32_t d = r.l7, dlen = r.l7len;
-    if (dlen < 240) return false;
-    if (((d + dlen) & 0xffff) < d || d + dlen > len) return false;
-    if (be32(s, d + 236) != 0x63825363u) return false;
-    if (dlen > 240) {
-        uint32_t o = d + 240;
-        int stop = (int)dlen - 240, start = 0;
-        while (start < stop) {
-            uint32_t t = s.u8(o + start);
-            if (t == 255) break;
-            if (t == 0) { start++; continue; }
-            if (stop - start < 2) return false;
-            int l = (int)s.u8(o + start + 1);
-            if (l > stop - start - 2) return false;
-            start += l + 2;
-        }
-    }
-    if (s.u8(d + 1) != 1 || s.u8(d + 2) != 6) return false;
-    lo = le32(s, d + 28);
-    hi = s.u8(d + 32) | (s.u8(d + 33) << 8);
-    return true;
-}
-
-__constant__ uint8_t kCbPlugin[EMURX_NUM_CB] = {
-    EMURX_PLUG_ARP, EMURX_PLUG_ICMP, EMURX_PLUG_IGMP, EMURX_PLUG_DHCP, EMURX_PLUG_DHCPSRV,
-    EMURX_PLUG_DHCPV6, EMURX_PLUG_MDNS, EMURX_PLUG_TRANSPORT, EMURX_PLUG_TRANSPORT,
-    EMURX_PLUG_IPV6, EMURX_PLUG_DOT1X, EMURX_PLUG_PPP};
-
-template <class S>
-__device__ void classify(const S& s, uint32_t len, const emurx_dev_tables& T, Rec& r) {
-    if (r.status != EMURX_ST_OK) return;
-    uint32_t ns = probe_ns(T, r.vport, r.vlan0, r.vlan1);  // CTunnelKey words
-    if (ns == EMURX_ID_NONE) { set_lk(r, EMURX_LK_NO_NS); return; }
-    r.ns = ns;
-    uint32_t cb = r.proto, plug = kCbPlugin[cb];
-    const uint32_t* ni = T.ns_info + 4 * ns;
-    if (!(ni[0] & (1u << plug))) { set_lk(r, EMURX_LK_NS_NO_PLUGIN); return; }
-    uint32_t dlo = le32(s, 0), dhi = s.u8(4) | (s.u8(5) << 8);  // p[0:6]
-    bool bcast = dlo == 0xffffffffu && dhi == 0xffffu;
-    switch (cb) {
-    case EMURX_CB_ARP:  // arp.go:904-949
-        if (be16(s, r.l3 + 6) == 1) client_result(T, r, probe_ip4(T, ns, le32(s, r.l3 + 24)), plug, true);
-        else set_lk(r, EMURX_LK_NS_LEVEL);
-        return;
-    case EMURX_CB_ICMP: {  // icmp.go:396-427
-        uint32_t cid = probe_ip4(T, ns, le32(s, r.l3 + 16));
-        if (cid != EMURX_ID_NONE && !unicast_to_me(T, cid, dlo, dhi)) cid = EMURX_ID_NONE;
-        client_result(T, r, cid, plug, false);
-        return;
-    }
-    case EMURX_CB_IGMP:
-    case EMURX_CB_MDNS:
-        set_lk(r, EMURX_LK_NS_LEVEL);
-        return;
-    case EMURX_CB_DHCP: {  // dhcp.go:893-917
-        uint32_t lo = dlo, hi = dhi;
-        if (bcast && !dhcp_chaddr(s, len, r, lo, hi)) { set_lk(r, EMURX_LK_NO_CLIENT); return; }
-        client_result(T, r, probe_mac(T, ns, lo, hi), plug, true);
-        return;
-    }
-    case EMURX_CB_DHCPSRV:  // dhcpsrv.go:1798-1826
-        client_result(T, r, bcast ? ni[1] : probe_mac(T, ns, dlo, dhi), plug, true);
-        return;
-    case EMURX_CB_EAPOL: {  // dot1x.go:624-650, 01:80:c2:00:00:03
-        bool pae = dlo == 0x00c28001u && dhi == 0x0300u;
-        client_result(T, r, pae ? ni[1] : probe_mac(T, ns, dlo, dhi), plug, true);
-        return;
-    }
-    case EMURX_CB_ICMPV6: {  // ipv6.go:465-540
-        if (be16(s, r.l4) != 0x8000u) { set_lk(r, EMURX_LK_NS_LEVEL); return; }
-        if (r.l3 + 40 > len) { set_lk(r, EMURX_LK_NO_CLIENT); return; }
-        uint32_t w[4] = {le32(s, r.l3 + 24), le32(s, r.l3 + 28), le32(s, r.l3 + 32), le32(s, r.l3 + 36)};
-        uint32_t cid = lookup_ip6_lg(T, ns, w);
-        if (cid != EMURX_ID_NONE && !unicast_to_me(T, cid, dlo, dhi)) cid = EMURX_ID_NONE;
-        if (cid != EMURX_ID_NONE && s.u8(r.l3 + 8) == 0xff) cid = EMURX_ID_NONE;
-        client_result(T, r, cid, plug, false);
-        return;
-    }
-    default:  // dhcpv6, ppp, tcp, udp: client = MAC[dst] (plugin_transport.go:83-115 ...)
-        client_result(T, r, probe_mac(T, ns, dlo, dhi), plug, true);
-        return;
-    }
-}
-
-// ---------------------------------------------------------------------------------------
-// k_parse
+// k_rx: parse + classify, one tile of 256 frames per workgroup
 // ---------------------------------------------------------------------------------------
 template <bool kClassify>
-__global__ __launch_bounds__(kBlock) void k_parse(const uint8_t* __restrict__ frames,
-                                                  const emurx_desc* __restrict__ desc, uint32_t n,
-                                                  emurx_dev_tables T, emurx_rec* __restrict__ rec,
-                                                  uint8_t* __restrict__ qtag,
-                                                  uint32_t* __restrict__ tile_cnt,
-                                                  unsigned long long* __restrict__ hist) {
+__global__ __launch_bounds__(kBlock) void k_rx(const uint8_t* __restrict__ frames,
+                                               const emurx_desc* __restrict__ desc, uint32_t n,
+                                               emurx_dev_tables T, emurx_rec* __restrict__ rec,
+                                               uint8_t* __restrict__ qtag,
+                                               uint32_t* __restrict__ tile_cnt,
+                                               uint32_t* __restrict__ gsum,
+                                               unsigned long long* __restrict__ hshard) {
     __shared__ __attribute__((aligned(16))) uint32_t slab[kWaves * kStage / 4];
     __shared__ uint32_t s_qcnt[16];
     __shared__ unsigned long long s_hpk[EMURX_HIST_BINS], s_hby[EMURX_HIST_BINS];
 
     const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / kWave;
-    const uint32_t i = blockIdx.x * kBlock + tid;
+    const uint32_t tile = blockIdx.x;
+    const uint32_t i = tile * EMURX_TILE + tid;
     const bool valid = i < n;
     if (tid < 16) s_qcnt[tid] = 0;
     if (tid < EMURX_HIST_BINS) { s_hpk[tid] = 0; s_hby[tid] = 0; }
 
-    uint2 dd = valid ? *reinterpret_cast<const uint2*>(desc + i) : make_uint2(0, 0);
+    const uint2 dd = valid ? *reinterpret_cast<const uint2*>(desc + i) : make_uint2(0, 0);
     const uint32_t off = dd.x, len = dd.y & 0xffff, vport = (dd.y >> 16) & 0xff;
 
     // the wave's byte range [lo, hi) -> stage into LDS when it fits
-    uint32_t lo = wave_min_u32(valid ? off : 0xffffffffu);
-    uint32_t hi = wave_max_u32(valid ? off + len : 0u);
+    const uint32_t lo = wave_min_u32(valid ? off : 0xffffffffu);
+    const uint32_t hi = wave_max_u32(valid ? off + len : 0u);
     const uint32_t start = lo & ~15u;
     const uint32_t nvec = hi > lo ? (hi - start + 15) >> 4 : 0;
     const bool staged = nvec > 0 && nvec <= kStage / 16;
     uint4* wslab = reinterpret_cast<uint4*>(slab) + wv * (kStage / 16);
-    if (staged) {
+    if (staged) {  // all loads in flight before the first LDS write (one HBM round trip)
+        static_assert(kStage / 16 / kWave == 8, "staging unroll assumes 8 vectors per lane");
         const uint4* src = reinterpret_cast<const uint4*>(frames + start);
-        for (uint32_t v = lane; v < nvec; v += kWave) wslab[v] = src[v];
+        // clamped (always in-bounds) loads: no predication, duplicates hit the cache
+#define EMURX_LD(k) const uint4 v##k = src[min(lane + k * kWave, nvec - 1)]
+        EMURX_LD(0); EMURX_LD(1); EMURX_LD(2); EMURX_LD(3);
+        EMURX_LD(4); EMURX_LD(5); EMURX_LD(6); EMURX_LD(7);
+#undef EMURX_LD
+#define EMURX_ST(k) if (lane + k * kWave < nvec) wslab[lane + k * kWave] = v##k
+        EMURX_ST(0); EMURX_ST(1); EMURX_ST(2); EMURX_ST(3);
+        EMURX_ST(4); EMURX_ST(5); EMURX_ST(6); EMURX_ST(7);
+#undef EMURX_ST
     }
-    __syncthreads();
+    // each wave reads only its own slab: a wave-level barrier orders the LDS writes
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
     Rec r;
     if (valid) {
@@ -576,19 +92,21 @@ __global__ __launch_bounds__(kBlock) void k_parse(const uint8_t* __restrict__ fr
             parse_packet(s, len, vport, T.cb_mask, r);
             if (kClassify) classify(s, len, T, r);
         }
-        uint4* o = reinterpret_cast<uint4*>(rec + i);
-        o[0] = make_uint4(r.ns, r.cl, r.vlan0, r.vlan1);
-        o[1] = make_uint4(r.vport | (r.l3 << 16), r.l4 | (r.l7 << 16),
-                          r.l7len | (r.nh << 16) | (r.proto << 24), r.status | (r.flags << 8));
+        if (rec) {
+            uint4* o = reinterpret_cast<uint4*>(rec + i);
+            o[0] = make_uint4(r.ns, r.cl, r.vlan0, r.vlan1);
+            o[1] = make_uint4(r.vport | (r.l3 << 16), r.l4 | (r.l7 << 16),
+                              r.l7len | (r.nh << 16) | (r.proto << 24), r.status | (r.flags << 8));
+        }
     }
     const uint32_t q = valid ? (r.status == EMURX_ST_OK ? r.proto : EMURX_Q_DROP) : 0xffu;
     if (valid) qtag[i] = (uint8_t)q;
 
-    // per-wave queue counts -> block counts
+    // per-wave queue counts -> tile counts
     uint32_t mycnt = 0;
 #pragma unroll
     for (uint32_t qq = 0; qq < EMURX_NUM_QUEUES; ++qq) {
-        uint64_t m = __ballot(q == qq);
+        const uint64_t m = __ballot(q == qq);
         if (lane == qq) mycnt = (uint32_t)__popcll(m);
     }
     if (lane < EMURX_NUM_QUEUES && mycnt) atomicAdd(&s_qcnt[lane], mycnt);
@@ -608,116 +126,157 @@ __global__ __launch_bounds__(kBlock) void k_parse(const uint8_t* __restrict__ fr
         active &= ~m;
     }
     __syncthreads();
-    if (tid < 16) tile_cnt[blockIdx.x * 16 + tid] = s_qcnt[tid];
-    if (tid < EMURX_HIST_BINS && s_hpk[tid]) {
-        atomicAdd(&hist[2 * tid], s_hpk[tid]);
-        atomicAdd(&hist[2 * tid + 1], s_hby[tid]);
+    if (tid < 16) {
+        const uint32_t c = s_qcnt[tid];
+        tile_cnt[tile * 16 + tid] = c;
+        if (c) atomicAdd(&gsum[(tile / kGroup) * 16 + tid], c);
+    }
+    // one of EMURX_HIST_SHARDS copies per workgroup: same-address memory-side atomics from
+    // every workgroup would serialise
+    if (tid >= 64 && tid < 64 + EMURX_HIST_BINS && s_hpk[tid - 64]) {
+        const uint32_t b = tid - 64;
+        unsigned long long* hs = hshard + (size_t)(tile & (EMURX_HIST_SHARDS - 1)) * 2 * EMURX_HIST_BINS;
+        atomicAdd(&hs[2 * b], s_hpk[b]);
+        atomicAdd(&hs[2 * b + 1], s_hby[b]);
     }
 }
 
 // ---------------------------------------------------------------------------------------
-// k_scan: tile_cnt[T][16] -> tile_off[T][16] (absolute position in the packed qlist),
-// qoff[14].  One workgroup of 1024 threads; each thread owns a contiguous run of tiles.
+// k_q: stable per-callback queue regions (runs after k_rx: every count is final)
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_scan(const uint32_t* __restrict__ tile_cnt, uint32_t ntiles,
-                                               uint32_t* __restrict__ tile_off,
-                                               uint32_t* __restrict__ qoff) {
-    __shared__ uint32_t part[1024];
-    __shared__ uint32_t qtot[16], qbase[16];
-    const uint32_t t = threadIdx.x;
-    const uint32_t per = (ntiles + 1023) / 1024;
-    const uint32_t a = min(t * per, ntiles), b = min(a + per, ntiles);
-    for (uint32_t q = 0; q < EMURX_NUM_QUEUES; ++q) {
-        uint32_t s = 0;
-        for (uint32_t k = a; k < b; ++k) s += tile_cnt[k * 16 + q];
-        part[t] = s;
-        __syncthreads();
-        // Hillis-Steele inclusive scan over 1024 partials
-        for (uint32_t d = 1; d < 1024; d <<= 1) {
-            uint32_t v = t >= d ? part[t - d] : 0;
-            __syncthreads();
-            part[t] += v;
-            __syncthreads();
-        }
-        uint32_t run = part[t] - s;  // exclusive
-        if (t == 1023) qtot[q] = part[1023];
-        for (uint32_t k = a; k < b; ++k) {
-            tile_off[k * 16 + q] = run;
-            run += tile_cnt[k * 16 + q];
-        }
-        __syncthreads();
-    }
-    if (t == 0) {
-        uint32_t acc = 0;
-        for (uint32_t q = 0; q < EMURX_NUM_QUEUES; ++q) { qbase[q] = acc; qoff[q] = acc; acc += qtot[q]; }
-        qoff[EMURX_NUM_QUEUES] = acc;
-        qoff[14] = 0; qoff[15] = 0;
-    }
-    __syncthreads();
-    for (uint32_t k = a; k < b; ++k)
-        for (uint32_t q = 0; q < EMURX_NUM_QUEUES; ++q) tile_off[k * 16 + q] += qbase[q];
-}
-
-// ---------------------------------------------------------------------------------------
-// k_compact: stable queue lists of frame indices
-// ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_compact(const uint8_t* __restrict__ qtag, uint32_t n,
-                                                    const uint32_t* __restrict__ tile_off,
-                                                    uint32_t* __restrict__ qlist) {
-    __shared__ uint32_t s_wcnt[kWaves][16];
+__global__ __launch_bounds__(kBlock) void k_q(const uint8_t* __restrict__ qtag, uint32_t n,
+                                              uint32_t ntiles,
+                                              const uint32_t* __restrict__ tile_cnt,
+                                              uint32_t* __restrict__ gsum,
+                                              uint32_t* __restrict__ qlist, uint32_t qcap,
+                                              uint32_t* __restrict__ qcount,
+                                              unsigned long long* __restrict__ hshard,
+                                              unsigned long long* __restrict__ hist_out,
+                                              emurx_ctl* __restrict__ ctl) {
+    __shared__ uint32_t s_excl[16], s_wcnt[kWaves][16], s_last;
     const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / kWave;
-    const uint32_t i = blockIdx.x * kBlock + tid;
+    const uint32_t tile = blockIdx.x, g = tile / kGroup, j = tile % kGroup;
+    const uint32_t i = tile * EMURX_TILE + tid;
     const uint32_t q = i < n ? qtag[i] : 0xffu;
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const uint32_t dbg = ctl->rsv[1];  // EMURX_DBG_KQ ablation bits (0 in production)
+
+    if (wv == 0) {
+        // exclusive prefix of every queue over tiles [0, tile)
+        uint32_t part[EMURX_NUM_QUEUES];
+#pragma unroll
+        for (int k = 0; k < EMURX_NUM_QUEUES; ++k) part[k] = 0;
+        for (uint32_t g0 = 0; g0 < ((dbg & 1u) ? 0u : g); g0 += kWave) {  // full groups before ours
+            const uint32_t gl = g0 + lane;
+            if (gl < g) {
+                const uint4* p = reinterpret_cast<const uint4*>(gsum + (size_t)gl * 16);
+                const uint4 a = p[0], b = p[1], c = p[2], d = p[3];
+                part[0] += a.x; part[1] += a.y; part[2] += a.z; part[3] += a.w;
+                part[4] += b.x; part[5] += b.y; part[6] += b.z; part[7] += b.w;
+                part[8] += c.x; part[9] += c.y; part[10] += c.z; part[11] += c.w;
+                part[12] += d.x;
+            }
+        }
+        if (lane < j) {  // earlier tiles of our group
+            const uint4* p = reinterpret_cast<const uint4*>(tile_cnt + (size_t)(g * kGroup + lane) * 16);
+            const uint4 a = p[0], b = p[1], c = p[2], d = p[3];
+            part[0] += a.x; part[1] += a.y; part[2] += a.z; part[3] += a.w;
+            part[4] += b.x; part[5] += b.y; part[6] += b.z; part[7] += b.w;
+            part[8] += c.x; part[9] += c.y; part[10] += c.z; part[11] += c.w;
+            part[12] += d.x;
+        }
+        uint32_t mine = 0;
+#pragma unroll
+        for (int k = 0; k < EMURX_NUM_QUEUES; ++k) {
+            const uint32_t v = wave_sum_u32(part[k]);
+            if (lane == (uint32_t)k) mine = v;
+        }
+        if (lane < 16) {
+            s_excl[lane] = lane < EMURX_NUM_QUEUES ? mine : 0;
+            if (tile == ntiles - 1 && qcount)
+                qcount[lane] = lane < EMURX_NUM_QUEUES ? mine + tile_cnt[tile * 16 + lane] : 0;
+        }
+    }
+    // ranks inside the tile: per wave ballots, waves in order
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     uint32_t rank = 0, mycnt = 0;
 #pragma unroll
     for (uint32_t qq = 0; qq < EMURX_NUM_QUEUES; ++qq) {
-        uint64_t m = __ballot(q == qq);
+        const uint64_t m = __ballot(q == qq);
         if (q == qq) rank = (uint32_t)__popcll(m & lt);
         if (lane == qq) mycnt = (uint32_t)__popcll(m);
     }
-    if (lane < 16) s_wcnt[wv][lane] = lane < EMURX_NUM_QUEUES ? mycnt : 0;
+    if (lane < 16) s_wcnt[wv][lane] = mycnt;
     __syncthreads();
-    if (q < EMURX_NUM_QUEUES) {
-        uint32_t base = tile_off[blockIdx.x * 16 + q];
-        for (uint32_t w = 0; w < wv; ++w) base += s_wcnt[w][q];
-        qlist[base + rank] = i;
+    if (!(dbg & 8u) && qlist && q < EMURX_NUM_QUEUES) {
+        uint32_t pos = s_excl[q] + rank;
+        for (uint32_t w = 0; w < wv; ++w) pos += s_wcnt[w][q];
+        if (pos < qcap) qlist[(size_t)q * qcap + pos] = i;
+    }
+
+    // Last workgroup out folds the histogram shards and clears the group rows.  The done
+    // count is hierarchical: word 13 of each group row counts that group's workgroups and
+    // only a group's last one touches the global word (one returning atomic per address
+    // from every workgroup would serialise).  Nothing written here is read by another
+    // workgroup of this launch, so relaxed atomics suffice.
+    __syncthreads();  // this workgroup's gsum / tile_cnt reads are complete
+    const uint32_t ngroups = (ntiles + kGroup - 1) / kGroup;
+    if (tid == 0) {
+        const uint32_t gsize = min(kGroup, ntiles - g * kGroup);
+        uint32_t last = 0;
+        if (!(dbg & 4u) && atomicAdd(&gsum[g * 16 + EMURX_NUM_QUEUES], 1u) == gsize - 1)
+            last = atomicAdd(&ctl->done, 1u) == ngroups - 1;
+        s_last = last && !(dbg & 2u);
+    }
+    __syncthreads();
+    if (s_last) {
+        __shared__ unsigned long long s_half[2 * EMURX_HIST_BINS];
+        static_assert(kBlock == 2 * 2 * EMURX_HIST_BINS && EMURX_HIST_SHARDS == 64, "fold layout");
+        const uint32_t w = tid & (2 * EMURX_HIST_BINS - 1), h = tid / (2 * EMURX_HIST_BINS);
+        unsigned long long* p = hshard + (size_t)(32 * h) * 2 * EMURX_HIST_BINS + w;
+        unsigned long long v[32];
+#pragma unroll
+        for (int k = 0; k < 32; ++k) v[k] = p[(size_t)k * 2 * EMURX_HIST_BINS];  // 32 loads in flight
+        unsigned long long sum = 0;
+#pragma unroll
+        for (int k = 0; k < 32; ++k) {
+            sum += v[k];
+            if (v[k]) p[(size_t)k * 2 * EMURX_HIST_BINS] = 0;
+        }
+        if (h == 1) s_half[w] = sum;
+        __syncthreads();
+        if (h == 0 && (sum | s_half[w])) hist_out[w] += sum + s_half[w];
+        for (uint32_t k = tid; k < ngroups * 16; k += kBlock) gsum[k] = 0;
+        if (tid == 0) ctl->done = 0;
     }
 }
 
 }  // namespace emurx
 
 // ---------------------------------------------------------------------------------------
-// launchers (called by emurx_api.cpp)
+// launcher (called by emurx_api.cpp)
 // ---------------------------------------------------------------------------------------
 int emurx_launch_batch(const uint8_t* frames, const emurx_desc* desc, uint32_t n,
                        const emurx_dev_tables& T, bool classify, const emurx_dev_out& out,
-                       emurx_rec* rec_scratch, uint8_t* qtag, uint32_t* tile_cnt,
-                       uint32_t* tile_off, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1,
-                       hipEvent_t ev2) {
+                       const emurx_scratch& s, hipStream_t st, const hipEvent_t* ev) {
     using namespace emurx;
+    if (ev) (void)hipEventRecord(ev[0], st);
     if (n == 0) {
-        if (out.qoff) (void)hipMemsetAsync(out.qoff, 0, 16 * sizeof(uint32_t), st);
-        return 0;
+        if (out.qcount) (void)hipMemsetAsync(out.qcount, 0, 16 * sizeof(uint32_t), st);
+    } else {
+        const uint32_t ntiles = (n + EMURX_TILE - 1) / EMURX_TILE;
+        emurx_rec* rec = out.rec;
+        if (classify)
+            hipLaunchKernelGGL(k_rx<true>, dim3(ntiles), dim3(kBlock), 0, st, frames, desc, n, T, rec,
+                               s.qtag, s.tile_cnt, s.gsum, s.hshard);
+        else
+            hipLaunchKernelGGL(k_rx<false>, dim3(ntiles), dim3(kBlock), 0, st, frames, desc, n, T, rec,
+                               s.qtag, s.tile_cnt, s.gsum, s.hshard);
+        if (ev) (void)hipEventRecord(ev[1], st);
+        hipLaunchKernelGGL(k_q, dim3(ntiles), dim3(kBlock), 0, st, s.qtag, n, ntiles, s.tile_cnt, s.gsum,
+                           out.qlist, out.qcap, out.qcount, s.hshard,
+                           reinterpret_cast<unsigned long long*>(out.hist), s.ctl);
     }
-    const uint32_t ntiles = (n + kBlock - 1) / kBlock;
-    emurx_rec* rec = out.rec ? out.rec : rec_scratch;
-    if (ev0) (void)hipEventRecord(ev0, st);
-    if (classify)
-        hipLaunchKernelGGL(k_parse<true>, dim3(ntiles), dim3(kBlock), 0, st, frames, desc, n, T, rec,
-                           qtag, tile_cnt, reinterpret_cast<unsigned long long*>(out.hist));
-    else
-        hipLaunchKernelGGL(k_parse<false>, dim3(ntiles), dim3(kBlock), 0, st, frames, desc, n, T, rec,
-                           qtag, tile_cnt, reinterpret_cast<unsigned long long*>(out.hist));
-    if (ev1) (void)hipEventRecord(ev1, st);
-    if (out.qlist || out.qoff) {
-        uint32_t qoff_dummy_needed = out.qoff ? 0 : 1;
-        uint32_t* qoff = out.qoff ? out.qoff : tile_off + (size_t)ntiles * 16;  // scratch tail
-        (void)qoff_dummy_needed;
-        hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, tile_cnt, ntiles, tile_off, qoff);
-        if (out.qlist)
-            hipLaunchKernelGGL(k_compact, dim3(ntiles), dim3(kBlock), 0, st, qtag, n, tile_off, out.qlist);
-    }
-    if (ev2) (void)hipEventRecord(ev2, st);
+    if (ev && n == 0) (void)hipEventRecord(ev[1], st);
+    if (ev) (void)hipEventRecord(ev[2], st);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

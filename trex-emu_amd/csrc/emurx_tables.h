@@ -40,8 +40,8 @@ EMURX_HD uint32_t emurx_hash(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uin
 }
 
 // Entry layouts (uint32 words):
-//  ns   [4]: vport_word, vlan0, vlan1, ns_id           (key = CTunnelKey as 3 LE words)
-//  mac  [4]: ns_id, mac[0..3] LE, mac[4..5] LE, client_id
+//  ns   [4]: vport | ns_plugins << 16, vlan0, vlan1, ns_id   (key = CTunnelKey as 3 LE words)
+//  mac  [4]: ns_id, mac[0..3] LE, mac[4..5] LE | client_plugins << 16, client_id
 //  ip4  [4]: ns_id, ipv4 bytes LE, 0, client_id
 //  ip6  [8]: ns_id, ip[0..3], ip[4..7], ip[8..11], ip[12..15], 0, 0, client_id
 //  ns_info   [4]: plugin_mask, first_client, 0, 0

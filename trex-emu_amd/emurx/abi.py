@@ -89,8 +89,8 @@ class Counters(C.Structure):
 
 
 class DevOut(C.Structure):
-    _fields_ = [("rec", C.c_void_p), ("qlist", C.c_void_p), ("qoff", C.c_void_p),
-                ("hist", C.c_void_p)]
+    _fields_ = [("rec", C.c_void_p), ("qlist", C.c_void_p), ("qcap", C.c_uint32),
+                ("qcount", C.c_void_p), ("hist", C.c_void_p)]
 
 
 # (name, restype, argtypes) — every symbol include/emu_rx.h declares
@@ -124,6 +124,7 @@ SIGNATURES = [
     ("emurx_hist_to_counters", None, [_P, C.POINTER(Counters)]),
     ("emurx_set_timing", C.c_int, [_P, C.c_uint32]),
     ("emurx_kernel_times", C.c_int, [_P, _P, _P, C.c_uint32, C.POINTER(C.c_uint32)]),
+    ("emurx_device_error", C.c_int, [_P, C.POINTER(C.c_int)]),
 ]
 
 _lib = None

@@ -126,10 +126,11 @@ class RxPath:
         return rec[:k], qlist[:k], qoff, cnt
 
     # ---- device-resident batch -----------------------------------------------------------
-    def classify_dev(self, frames, desc, n: int, rec=None, qlist=None, qoff=None, hist=None,
-                     stream=None, classify: bool = True):
-        """frames/desc/rec/qlist/qoff/hist: device tensors (or raw device addresses)."""
-        out = abi.DevOut(_addr(rec), _addr(qlist), _addr(qoff), _addr(hist))
+    def classify_dev(self, frames, desc, n: int, rec=None, qlist=None, qcap: int = 0, qcount=None,
+                     hist=None, stream=None, classify: bool = True):
+        """frames/desc/rec/qlist/qcount/hist: device tensors (or raw device addresses).
+        Queue q's frame indices land in qlist[q*qcap : q*qcap + qcount[q]]."""
+        out = abi.DevOut(_addr(rec), _addr(qlist), qcap, _addr(qcount), _addr(hist))
         fn = self.lib.emurx_classify_dev if classify else self.lib.emurx_parse_dev
         return abi.check(fn(self.h, _addr(frames), _addr(desc), n, C.byref(out),
                             _stream(stream)), "classify_dev")
@@ -138,12 +139,18 @@ class RxPath:
         return abi.check(self.lib.emurx_set_timing(self.h, slots), "set_timing")
 
     def kernel_times(self, cap: int = 1 << 16):
-        """(parse_ms[], compact_ms[]) of the batches since the previous call."""
+        """(k_rx ms[], k_q ms[]) of every batch launched since the previous call (HIP events
+        on the launch stream)."""
         a = np.zeros(cap, np.float32)
         b = np.zeros(cap, np.float32)
         n = C.c_uint32()
         abi.check(self.lib.emurx_kernel_times(self.h, _p(a), _p(b), cap, C.byref(n)), "kernel_times")
         return a[: n.value], b[: n.value]
+
+    def device_error(self) -> int:
+        e = C.c_int()
+        abi.check(self.lib.emurx_device_error(self.h, C.byref(e)), "device_error")
+        return e.value
 
 
 def _addr(x):
