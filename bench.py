@@ -3,16 +3,16 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config B|C|E] [--frames F]
 
-A step = one batch through the hot path: emurx_classify_dev = k_rx (decode + checksums +
-Namespace/Client lookups + records + outcome histogram) + k_q (stable per-callback queues)
-over F frames already resident in HBM.  Default workload = config B
+A step = one batch through the hot path: emurx_classify_dev = one k_rx launch (decode +
+checksums + Namespace/Client lookups + 32-B records + stable per-callback queue segments +
+outcome histogram) over F frames already resident in HBM.  Default workload = config B
 (1M x 64 B untagged IPv4/UDP, 1 Namespace / 1 Client), the configuration the metric is
 quoted on.  For N > 1 (torchrun, one rank per GPU) every rank processes its own F-frame
 shard against replicated tables: frames are independent, so there is no data-path
 collective (weak scaling); value = frames over all ranks / max-over-ranks time.
 
 The JSON line carries `roofline` (algorithmic bytes per frame = frame_len + 8 B descriptor
-+ 32 B record, over the parse kernel's mean HIP-event duration on the launch stream) and
++ 32 B record + 4 B queue entry, over k_rx's mean HIP-event duration on the launch stream) and
 `cpu_baseline` (the oracle, a single-threaded C restatement of the Go path, timed on this
 host's cores over a bounded sample of the same workload; rank 0 at N=1 only).
 """
@@ -107,23 +107,25 @@ def main():
     buf = torch.from_numpy(w["buf"]).to(dev)
     desc = torch.from_numpy(w["desc"].view(np.uint8).copy()).to(dev)
     rec = torch.empty(n * 32, dtype=torch.uint8, device=dev)
-    qlist = torch.empty(abi.NUM_QUEUES * n, dtype=torch.int32, device=dev)
-    qcount = torch.empty(16, dtype=torch.int32, device=dev)
-    hist = torch.zeros(2 * abi.HIST_BINS, dtype=torch.int64, device=dev)  # accumulates
+    qcap = abi.queue_cap(n)
+    qlist = torch.empty(abi.NUM_QUEUES * qcap, dtype=torch.int32, device=dev)
+    tile_cnt = torch.empty(abi.ntiles(n) * 16, dtype=torch.int32, device=dev)
+    hist = torch.zeros(abi.HIST_SHARDS * 2 * abi.HIST_BINS, dtype=torch.int64, device=dev)  # accumulates
     stream = torch.cuda.current_stream(dev)
     rx.sync(stream.cuda_stream)
 
     def step():
-        rx.classify_dev(buf, desc, n, rec, qlist, n, qcount, hist, stream=stream)
+        rx.classify_dev(buf, desc, n, rec, qlist, qcap, tile_cnt, hist, stream=stream)
 
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
     # sanity of the outcome on this rank (counts only; parity lives in tests/)
-    h = hist.cpu().numpy().view(np.uint64)
+    from emurx.rx import hist_fold, pack_queues
+    h = hist_fold(hist.cpu().numpy().view(np.uint64))
     assert int(h[0::2].sum()) == n * a.warmup, "histogram does not cover the batches"
-    assert int(qcount.cpu().numpy()[:abi.NUM_QUEUES].sum()) == n
-    assert rx.device_error() == 0
+    _, qoff = pack_queues(qlist.cpu().numpy(), qcap, tile_cnt.cpu().numpy(), n)
+    assert int(qoff[-1]) == n, "queues do not cover the batch"
 
     rx.set_timing(a.steps + 8)
     if world > 1:
@@ -136,9 +138,8 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    pk, qk = rx.kernel_times()
+    pk = rx.kernel_times()
     rx.set_timing(0)
-    assert rx.device_error() == 0
 
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
@@ -149,7 +150,7 @@ def main():
     ms_per_step = el / a.steps * 1e3
 
     # roofline of the dominant kernel (k_rx): algorithmic bytes / its mean HIP-event duration
-    alg_bytes = w["nbytes"] + 8 * n + 32 * n
+    alg_bytes = w["nbytes"] + 8 * n + 32 * n + 4 * n
     parse_s = float(np.mean(pk)) * 1e-3 if len(pk) else float("nan")
     achieved = alg_bytes / parse_s / 1e9
     traffic = None
@@ -191,7 +192,7 @@ def main():
             "kernel": "k_rx",
             "alg_bytes_per_launch": alg_bytes,
             "kernel_ms_mean": round(parse_s * 1e3, 5),
-            "queue_kernel_ms_mean": round(float(np.mean(qk)), 5) if len(qk) else None,
+            "kernel_launches_timed": int(len(pk)),
         },
     }
     if a.host_path:

@@ -218,15 +218,21 @@ typedef struct emurx_cfg {
 } emurx_cfg;
 
 /* Device-resident outputs of one batch (all pointers are device memory).
-   Each callback owns a region of qlist: queue q holds the indices of its frames, in frame
-   order, at qlist[q*qcap .. q*qcap + qcount[q]) (queue EMURX_Q_DROP = no callback).
-   rec / qlist / qcount may individually be NULL to skip that output; hist is required. */
+   Frames are processed in tiles of EMURX_QUEUE_TILE (frame i is in tile i / TILE).  Each
+   callback owns a region of qlist, and each tile a segment of that region: the indices of
+   tile t's frames that reach callback q are, in frame order,
+       qlist[q*qcap + t*TILE .. q*qcap + t*TILE + tile_cnt[t*16 + q])
+   so queue q (EMURX_Q_DROP = no callback) is the concatenation of its segments over t.
+   The histogram is kept as EMURX_HIST_SHARDS accumulating copies (fold them with
+   emurx_hist_fold).  rec / qlist / tile_cnt may individually be NULL; hist is required. */
+#define EMURX_QUEUE_TILE 256
+#define EMURX_HIST_SHARDS 64
 typedef struct emurx_dev_out {
-    emurx_rec* rec;        /* [n] records, frame order                                   */
-    uint32_t* qlist;       /* [EMURX_NUM_QUEUES * qcap] frame indices                     */
-    uint32_t qcap;         /* region size per queue, >= n                                 */
-    uint32_t* qcount;      /* [16] frames per queue (first 13 used)                       */
-    uint64_t* hist;        /* [2 * EMURX_HIST_BINS] {pkts, bytes} per bin; ACCUMULATED     */
+    emurx_rec* rec;        /* [n] records, frame order                                     */
+    uint32_t* qlist;       /* [EMURX_NUM_QUEUES * qcap] frame indices                       */
+    uint32_t qcap;         /* per-queue region, >= ceil(n / TILE) * TILE                    */
+    uint32_t* tile_cnt;    /* [ceil(n / TILE) * 16] frames per (tile, queue), 13 used of 16  */
+    uint64_t* hist;        /* [EMURX_HIST_SHARDS * 2 * EMURX_HIST_BINS], ACCUMULATED         */
 } emurx_dev_out;
 
 typedef struct emurx_ctx emurx_t;
@@ -277,9 +283,10 @@ int emurx_rx_stream(emurx_t* h, const uint8_t* msg, size_t len, emurx_rec* out_r
 /* Device-resident batch: frames (d_frames) and descriptors (d_desc) already in HBM.
    Enqueues parse+classify+compaction on `stream` (hipStream_t, NULL = handle stream) and
    returns without synchronising.  out->hist is accumulated into (zero it to reset).
-   n <= cfg.max_frames, out->qcap >= n.  The frame buffer must stay readable up to the
-   next 64-byte boundary past its last byte (frames are staged with 16-byte loads).
-   One kernel launch, no host synchronisation: capturable in a hipGraph. */
+   n <= cfg.max_frames, out->qcap >= ceil(n / EMURX_QUEUE_TILE) * EMURX_QUEUE_TILE.  The
+   frame buffer must stay readable up to the next 64-byte boundary past its last byte
+   (frames are staged with 16-byte loads).  One kernel launch, no host synchronisation,
+   no handle state touched on the device: capturable in a hipGraph. */
 int emurx_classify_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_desc,
                        uint32_t n, const emurx_dev_out* out, void* stream);
 
@@ -297,18 +304,16 @@ int emurx_zmq_descriptors(const uint8_t* msg, size_t len, emurx_desc* out, uint3
 
 /* ParserStats delta from an outcome histogram (pure host arithmetic). */
 void emurx_hist_to_counters(const uint64_t hist[2 * EMURX_HIST_BINS], emurx_counters* out);
+/* Sum the EMURX_HIST_SHARDS copies of a device histogram (after a D2H copy). */
+void emurx_hist_fold(const uint64_t* shards, uint64_t out[2 * EMURX_HIST_BINS]);
 
 /* Kernel timing with HIP events recorded on the launch stream around every batch.
    emurx_set_timing(h, slots): slots > 0 keeps the last `slots` batches (ring), 0 disables.
-   emurx_kernel_times(): waits for the most recent batch and returns, per batch recorded
-   since the previous call (oldest first, at most min(cap, slots)), the device time in ms of
-   the parse/classify kernel and of the queue kernel; then resets the ring. */
+   emurx_kernel_times(): waits for the most recent batch and returns the device time in ms
+   of every batch recorded since the previous call (oldest first, at most min(cap, slots));
+   then resets the ring. */
 int emurx_set_timing(emurx_t* h, uint32_t slots);
-int emurx_kernel_times(emurx_t* h, float* rx_ms, float* q_ms, uint32_t cap, uint32_t* n_out);
-
-/* Sticky device error flag (reserved: no current kernel raises it; 0 = healthy).
-   Synchronises the device. */
-int emurx_device_error(emurx_t* h, int* error);
+int emurx_kernel_times(emurx_t* h, float* batch_ms, uint32_t cap, uint32_t* n_out);
 
 #ifdef __cplusplus
 }

@@ -14,28 +14,24 @@ def to_dev(a: np.ndarray, pad: int = 64):
     return t
 
 
-def run_dev(rx, buf, desc, classify=True):
+def run_dev(rx, buf, desc, classify=True, qcap=None):
     """-> rec, qlist (packed in queue order), qoff(14), hist(2*64) as numpy, via
-    emurx_classify_dev / emurx_parse_dev (per-queue regions of qcap = n entries)."""
+    emurx_classify_dev / emurx_parse_dev (per-tile queue segments, sharded histogram)."""
     import torch
+    from emurx.rx import hist_fold, pack_queues
     n = len(desc)
-    cap = max(n, 1)
+    qcap = qcap or max(abi.queue_cap(n), abi.QUEUE_TILE)
+    nt = max(abi.ntiles(n), 1)
     tb, td = to_dev(buf), to_dev(desc)
-    rec = torch.zeros(cap * 32, dtype=torch.uint8, device="cuda")
-    qlist = torch.full((abi.NUM_QUEUES * cap,), -1, dtype=torch.int32, device="cuda")
-    qcount = torch.full((16,), -1, dtype=torch.int32, device="cuda")
-    hist = torch.zeros(2 * abi.HIST_BINS, dtype=torch.int64, device="cuda")
-    rx.classify_dev(tb, td, n, rec, qlist, cap, qcount, hist, classify=classify)
+    rec = torch.zeros(max(n, 1) * 32, dtype=torch.uint8, device="cuda")
+    qlist = torch.full((abi.NUM_QUEUES * qcap,), -1, dtype=torch.int32, device="cuda")
+    tile_cnt = torch.full((nt * 16,), -1, dtype=torch.int32, device="cuda")
+    hist = torch.zeros(abi.HIST_SHARDS * 2 * abi.HIST_BINS, dtype=torch.int64, device="cuda")
+    rx.classify_dev(tb, td, n, rec, qlist, qcap, tile_cnt, hist, classify=classify)
     torch.cuda.synchronize()
-    assert rx.device_error() == 0
     r = rec.cpu().numpy()[: n * 32].view(abi.REC_DTYPE)
-    cnt = qcount.cpu().numpy()[: abi.NUM_QUEUES].view(np.uint32).astype(np.int64)
-    ql = qlist.cpu().numpy().view(np.uint32)
-    qoff = np.zeros(abi.NUM_QUEUES + 1, np.uint32)
-    qoff[1:] = np.cumsum(cnt)
-    packed = np.concatenate([ql[q * cap:q * cap + cnt[q]] for q in range(abi.NUM_QUEUES)]) \
-        if n else np.zeros(0, np.uint32)
-    return r, packed.astype(np.uint32), qoff, hist.cpu().numpy().view(np.uint64)
+    packed, qoff = pack_queues(qlist.cpu().numpy(), qcap, tile_cnt.cpu().numpy(), n)
+    return r, packed, qoff, hist_fold(hist.cpu().numpy().view(np.uint64))
 
 
 def rec_diff(a, b, limit=5):

@@ -123,3 +123,32 @@ def test_hist_to_counters_matches_oracle(lib):
             want = pyoracle.counters_dict(cnt)
             for k in abi.PARSER_COUNTER_NAMES + ["ref_panic"]:
                 assert got[k] == want[k], (mask, k)
+
+
+def test_hist_fold(lib):
+    from emurx.rx import hist_fold
+    rng = np.random.default_rng(5)
+    sh = rng.integers(0, 1 << 40, size=abi.HIST_SHARDS * 2 * abi.HIST_BINS, dtype=np.uint64)
+    want = sh.reshape(abi.HIST_SHARDS, -1).sum(0, dtype=np.uint64)
+    assert np.array_equal(hist_fold(sh), want)
+
+
+@pytest.mark.parametrize("n", [0, 1, 255, 256, 257, 1000])
+def test_pack_queues(n):
+    """Host concatenation of per-tile queue segments == a stable partition by queue (what
+    k_rx writes: tile t's frames of queue q at qlist[q*qcap + t*TILE + k], k < tile_cnt)."""
+    from emurx.rx import pack_queues
+    rng = np.random.default_rng(n)
+    q = rng.integers(0, abi.NUM_QUEUES, size=n)
+    qcap = abi.queue_cap(n) + 17
+    nt = max(abi.ntiles(n), 1)
+    qlist = np.full(abi.NUM_QUEUES * qcap, 0xDEADBEEF, np.uint32)
+    tile_cnt = np.zeros(nt * 16, np.uint32)
+    for i in range(n):
+        t = i // abi.QUEUE_TILE
+        qlist[q[i] * qcap + t * abi.QUEUE_TILE + tile_cnt[t * 16 + q[i]]] = i
+        tile_cnt[t * 16 + q[i]] += 1
+    packed, qoff = pack_queues(qlist, qcap, tile_cnt, n)
+    want = np.argsort(q, kind="stable").astype(np.uint32)
+    assert np.array_equal(packed, want)
+    assert np.array_equal(np.diff(qoff.astype(np.int64)), np.bincount(q, minlength=abi.NUM_QUEUES))

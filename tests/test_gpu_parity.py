@@ -207,6 +207,21 @@ def test_ragged_sizes(rxmod):
         check_batch(rx, o, buf, desc)
 
 
+def test_queue_region_capacity(rxmod):
+    """A per-queue region larger than the minimum leaves the segments in place; one smaller
+    than ceil(n / TILE) * TILE is refused before any launch."""
+    rx, o = new_pair(rxmod)
+    frames = [c[1] for c in E.cases()]
+    sel = [frames[i % len(frames)] for i in range(700)]
+    buf, desc = F.pack_frames(sel)
+    orec, oq, oqoff, _ = o.rx_batch(buf, desc)
+    rec, qlist, qoff, _ = run_dev(rx, buf, desc, qcap=abi.queue_cap(700) + 3 * abi.QUEUE_TILE + 5)
+    assert rec.tobytes() == orec.tobytes()
+    assert np.array_equal(qoff, oqoff) and np.array_equal(qlist, oq)
+    with pytest.raises(RuntimeError, match="invalid argument"):
+        run_dev(rx, buf, desc, qcap=700)
+
+
 # ---- table mutations between batches -------------------------------------------------------
 def test_table_updates(rxmod):
     w = synth.config_c(8192)

@@ -130,26 +130,18 @@ struct emurx_ctx {
     DevBuf<uint32_t> d_ns, d_nsinfo, d_mac, d_ip4, d_ip6, d_client;
     std::vector<uint32_t> h_ns, h_nsinfo, h_mac, h_ip4, h_ip6, h_client;
 
-    // batch state (device): histogram shards (kept zero between launches), look-back
-    // granules (16 per tile, zero at allocation), launch control block
-    DevBuf<unsigned long long> d_hshard;
-    DevBuf<uint8_t> d_qtag;
-    DevBuf<uint32_t> d_tile_cnt, d_gsum;
-    DevBuf<emurx_ctl> d_ctl;
-    emurx_scratch scratch() const { return emurx_scratch{d_qtag.p, d_tile_cnt.p, d_gsum.p, d_hshard.p, d_ctl.p}; }
-
-    // host batch staging (emurx_rx_stream)
+    // host batch staging (emurx_rx_stream): message, descriptors, and the batch outputs
     PinBuf<uint8_t> h_msg;
     PinBuf<emurx_desc> h_desc;
-    PinBuf<uint32_t> h_qcount;
+    PinBuf<uint32_t> h_qlist, h_tile_cnt;
     PinBuf<uint64_t> h_hist;
     DevBuf<uint8_t> d_msg;
     DevBuf<emurx_desc> d_desc;
     DevBuf<emurx_rec> d_rec;
-    DevBuf<uint32_t> d_qlist, d_qcount;
+    DevBuf<uint32_t> d_qlist, d_tile_cnt;
     DevBuf<uint64_t> d_hist;
 
-    // timing ring: 3 events per batch (before k_rx, between k_rx and k_q, after k_q)
+    // timing ring: 2 events per batch (around the k_rx launch)
     std::vector<hipEvent_t> ev;
     uint32_t slots = 0, ev_head = 0, ev_count = 0;
 
@@ -251,11 +243,14 @@ int rebuild_and_upload(emurx_t* h, hipStream_t st) {
     return EMURX_OK;
 }
 
+uint32_t ntiles(uint32_t n) { return (n + EMURX_QUEUE_TILE - 1) / EMURX_QUEUE_TILE; }
+size_t queue_cap(uint32_t n) { return (size_t)ntiles(n) * EMURX_QUEUE_TILE; }
+
 int run_dev(emurx_t* h, const uint8_t* frames, const emurx_desc* desc, uint32_t n,
             const emurx_dev_out* out, void* stream, bool classify) {
     if (!h || !out || !out->hist || (n && (!frames || !desc))) return EMURX_EINVAL;
     if (n > h->cfg.max_frames) return EMURX_ENOMEM;
-    if (out->qlist && out->qcap < n) return EMURX_EINVAL;
+    if (out->qlist && out->qcap < queue_cap(n)) return EMURX_EINVAL;
     int rc = bind(h);
     if (rc) return rc;
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
@@ -264,11 +259,11 @@ int run_dev(emurx_t* h, const uint8_t* frames, const emurx_desc* desc, uint32_t 
     const hipEvent_t* ev = nullptr;
     if (h->slots) {
         const uint32_t s = h->ev_head;
-        ev = &h->ev[3 * s];
+        ev = &h->ev[2 * s];
         h->ev_head = (s + 1) % h->slots;
         h->ev_count = std::min(h->ev_count + 1, h->slots);
     }
-    int r = emurx_launch_batch(frames, desc, n, T, classify, *out, h->scratch(), st, ev);
+    int r = emurx_launch_batch(frames, desc, n, T, classify, *out, st, ev);
     return r ? EMURX_EDEVICE : EMURX_OK;
 }
 
@@ -312,19 +307,6 @@ int emurx_open(const emurx_cfg* cfg, emurx_t** out) {
         emurx_close(h);
         return EMURX_ENOMEM;
     }
-    const size_t hs = (size_t)EMURX_HIST_SHARDS * 2 * EMURX_HIST_BINS;
-    const size_t tiles = ((size_t)cfg->max_frames + EMURX_TILE - 1) / EMURX_TILE;
-    const size_t ng = ((tiles + 63) / 64) * 16;
-    emurx_ctl ctl0{0, {0, 0, 0}};
-    if (const char* e = getenv("EMURX_DBG_KQ")) ctl0.rsv[1] = (uint32_t)atoi(e);  // ablation only
-    if (h->d_hshard.alloc(hs) || h->d_qtag.alloc(cfg->max_frames) || h->d_tile_cnt.alloc(tiles * 16) ||
-        h->d_gsum.alloc(ng) || h->d_ctl.alloc(1) ||
-        hipMemset(h->d_hshard.p, 0, hs * sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(h->d_gsum.p, 0, ng * sizeof(uint32_t)) != hipSuccess ||
-        hipMemcpy(h->d_ctl.p, &ctl0, sizeof(ctl0), hipMemcpyHostToDevice) != hipSuccess) {
-        emurx_close(h);
-        return EMURX_ENOMEM;
-    }
     h->dirty = true;
     if ((rc = rebuild_and_upload(h, h->stream))) { emurx_close(h); return rc; }
     *out = h;
@@ -337,11 +319,10 @@ void emurx_close(emurx_t* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     h->d_ns.release(); h->d_nsinfo.release(); h->d_mac.release(); h->d_ip4.release();
     h->d_ip6.release(); h->d_client.release();
-    h->d_hshard.release(); h->d_qtag.release(); h->d_tile_cnt.release(); h->d_gsum.release();
-    h->d_ctl.release();
-    h->h_msg.release(); h->h_desc.release(); h->h_qcount.release(); h->h_hist.release();
+    h->h_msg.release(); h->h_desc.release(); h->h_qlist.release(); h->h_tile_cnt.release();
+    h->h_hist.release();
     h->d_msg.release(); h->d_desc.release(); h->d_rec.release(); h->d_qlist.release();
-    h->d_qcount.release(); h->d_hist.release();
+    h->d_tile_cnt.release(); h->d_hist.release();
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
     h->ev.clear();
@@ -607,10 +588,11 @@ int emurx_rx_stream(emurx_t* h, const uint8_t* msg, size_t len, emurx_rec* out_r
     int rc = bind(h);
     if (rc) return rc;
     const uint32_t cap = std::max<uint32_t>(std::min(out_cap, h->cfg.max_frames), 1);
-    if (h->h_desc.alloc(cap) || h->h_msg.alloc(len + 64) || h->h_qcount.alloc(16) ||
-        h->h_hist.alloc(2 * EMURX_HIST_BINS) || h->d_msg.alloc(len + 64) || h->d_desc.alloc(cap) ||
-        h->d_rec.alloc(cap) || h->d_qlist.alloc((size_t)EMURX_NUM_QUEUES * cap) || h->d_qcount.alloc(16) ||
-        h->d_hist.alloc(2 * EMURX_HIST_BINS))
+    const size_t qcap_max = queue_cap(cap), hist_words = (size_t)EMURX_HIST_SHARDS * 2 * EMURX_HIST_BINS;
+    if (h->h_desc.alloc(cap) || h->h_msg.alloc(len + 64) || h->h_qlist.alloc(EMURX_NUM_QUEUES * qcap_max) ||
+        h->h_tile_cnt.alloc(ntiles(cap) * 16) || h->h_hist.alloc(hist_words) || h->d_msg.alloc(len + 64) ||
+        h->d_desc.alloc(cap) || h->d_rec.alloc(cap) || h->d_qlist.alloc(EMURX_NUM_QUEUES * qcap_max) ||
+        h->d_tile_cnt.alloc(ntiles(cap) * 16) || h->d_hist.alloc(hist_words))
         return EMURX_ENOMEM;
     int perr = 0;
     uint32_t n = 0;
@@ -633,30 +615,45 @@ int emurx_rx_stream(emurx_t* h, const uint8_t* msg, size_t len, emurx_rec* out_r
     if (!out_rec || !out_qlist) return EMURX_EINVAL;
     memcpy(h->h_msg.p, msg, len);
     memset(h->h_msg.p + len, 0, 64);
-    emurx_dev_out o{h->d_rec.p, h->d_qlist.p, cap, h->d_qcount.p, h->d_hist.p};
+    // queue regions sized for this batch, so the whole qlist comes back in one copy
+    const uint32_t nt = ntiles(n);
+    const size_t qcap = queue_cap(n);
+    emurx_dev_out o{h->d_rec.p, h->d_qlist.p, (uint32_t)qcap, h->d_tile_cnt.p, h->d_hist.p};
     bool ok = hipMemcpyAsync(h->d_msg.p, h->h_msg.p, len + 64, hipMemcpyHostToDevice, st) == hipSuccess &&
               hipMemcpyAsync(h->d_desc.p, h->h_desc.p, (size_t)n * sizeof(emurx_desc), hipMemcpyHostToDevice, st) == hipSuccess &&
-              hipMemsetAsync(h->d_hist.p, 0, 2 * EMURX_HIST_BINS * sizeof(uint64_t), st) == hipSuccess;
+              hipMemsetAsync(h->d_hist.p, 0, hist_words * sizeof(uint64_t), st) == hipSuccess;
     if (!ok) return EMURX_EDEVICE;
     if ((rc = run_dev(h, h->d_msg.p, h->d_desc.p, n, &o, st, true))) return rc;
     ok = hipMemcpyAsync(out_rec, h->d_rec.p, (size_t)n * sizeof(emurx_rec), hipMemcpyDeviceToHost, st) == hipSuccess &&
-         hipMemcpyAsync(h->h_qcount.p, h->d_qcount.p, 16 * sizeof(uint32_t), hipMemcpyDeviceToHost, st) == hipSuccess &&
-         hipMemcpyAsync(h->h_hist.p, h->d_hist.p, 2 * EMURX_HIST_BINS * sizeof(uint64_t), hipMemcpyDeviceToHost, st) == hipSuccess &&
+         hipMemcpyAsync(h->h_qlist.p, h->d_qlist.p, EMURX_NUM_QUEUES * qcap * 4, hipMemcpyDeviceToHost, st) == hipSuccess &&
+         hipMemcpyAsync(h->h_tile_cnt.p, h->d_tile_cnt.p, (size_t)nt * 16 * 4, hipMemcpyDeviceToHost, st) == hipSuccess &&
+         hipMemcpyAsync(h->h_hist.p, h->d_hist.p, hist_words * sizeof(uint64_t), hipMemcpyDeviceToHost, st) == hipSuccess &&
          hipStreamSynchronize(st) == hipSuccess;
     if (!ok) return EMURX_EDEVICE;
-    // pack the per-queue regions back to back (out_qoff[q] .. out_qoff[q+1])
-    out_qoff[0] = 0;
+    // concatenate each queue's per-tile segments (out_qoff[q] .. out_qoff[q+1])
+    uint32_t at = 0;
     for (int q = 0; q < EMURX_NUM_QUEUES; ++q) {
-        const uint32_t c = h->h_qcount.p[q];
-        if (c > n || out_qoff[q] + c > n) return EMURX_EDEVICE;
-        if (c && hipMemcpyAsync(out_qlist + out_qoff[q], h->d_qlist.p + (size_t)q * cap, (size_t)c * 4,
-                                hipMemcpyDeviceToHost, st) != hipSuccess)
-            return EMURX_EDEVICE;
-        out_qoff[q + 1] = out_qoff[q] + c;
+        out_qoff[q] = at;
+        for (uint32_t t = 0; t < nt; ++t) {
+            const uint32_t c = h->h_tile_cnt.p[t * 16 + q];
+            if (c > EMURX_QUEUE_TILE || at + c > n) return EMURX_EDEVICE;
+            memcpy(out_qlist + at, h->h_qlist.p + q * qcap + (size_t)t * EMURX_QUEUE_TILE, (size_t)c * 4);
+            at += c;
+        }
     }
-    if (hipStreamSynchronize(st) != hipSuccess) return EMURX_EDEVICE;
-    emurx_hist_to_counters(h->h_hist.p, delta);
+    out_qoff[EMURX_NUM_QUEUES] = at;
+    if (at != n) return EMURX_EDEVICE;
+    uint64_t hist[2 * EMURX_HIST_BINS];
+    emurx_hist_fold(h->h_hist.p, hist);
+    emurx_hist_to_counters(hist, delta);
     return EMURX_OK;
+}
+
+void emurx_hist_fold(const uint64_t* shards, uint64_t out[2 * EMURX_HIST_BINS]) {
+    for (int b = 0; b < 2 * EMURX_HIST_BINS; ++b) out[b] = 0;
+    if (!shards) return;
+    for (int s = 0; s < EMURX_HIST_SHARDS; ++s)
+        for (int b = 0; b < 2 * EMURX_HIST_BINS; ++b) out[b] += shards[(size_t)s * 2 * EMURX_HIST_BINS + b];
 }
 
 int emurx_set_timing(emurx_t* h, uint32_t slots) {
@@ -667,7 +664,7 @@ int emurx_set_timing(emurx_t* h, uint32_t slots) {
     (void)hipDeviceSynchronize();
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
-    h->ev.assign((size_t)slots * 3, nullptr);
+    h->ev.assign((size_t)slots * 2, nullptr);
     for (auto& e : h->ev)
         if (hipEventCreate(&e) != hipSuccess) { h->slots = 0; return EMURX_EDEVICE; }
     h->slots = slots;
@@ -675,36 +672,23 @@ int emurx_set_timing(emurx_t* h, uint32_t slots) {
     return EMURX_OK;
 }
 
-int emurx_kernel_times(emurx_t* h, float* rx_ms, float* q_ms, uint32_t cap, uint32_t* n_out) {
-    if (!h || !n_out || (cap && (!rx_ms || !q_ms))) return EMURX_EINVAL;
+int emurx_kernel_times(emurx_t* h, float* batch_ms, uint32_t cap, uint32_t* n_out) {
+    if (!h || !n_out || (cap && !batch_ms)) return EMURX_EINVAL;
     *n_out = 0;
     if (!h->slots || !h->ev_count) return EMURX_OK;
     int rc = bind(h);
     if (rc) return rc;
     const uint32_t last = (h->ev_head + h->slots - 1) % h->slots;
-    if (hipEventSynchronize(h->ev[3 * last + 2]) != hipSuccess) return EMURX_EDEVICE;
+    if (hipEventSynchronize(h->ev[2 * last + 1]) != hipSuccess) return EMURX_EDEVICE;
     const uint32_t n = std::min(h->ev_count, cap);
     const uint32_t first = (h->ev_head + h->slots - h->ev_count) % h->slots;
     for (uint32_t k = 0; k < n; ++k) {
         const uint32_t s = (first + (h->ev_count - n) + k) % h->slots;
-        if (hipEventElapsedTime(&rx_ms[k], h->ev[3 * s], h->ev[3 * s + 1]) != hipSuccess ||
-            hipEventElapsedTime(&q_ms[k], h->ev[3 * s + 1], h->ev[3 * s + 2]) != hipSuccess)
+        if (hipEventElapsedTime(&batch_ms[k], h->ev[2 * s], h->ev[2 * s + 1]) != hipSuccess)
             return EMURX_EDEVICE;
     }
     *n_out = n;
     h->ev_count = 0;
-    return EMURX_OK;
-}
-
-int emurx_device_error(emurx_t* h, int* error) {
-    if (!h || !error) return EMURX_EINVAL;
-    int rc = bind(h);
-    if (rc) return rc;
-    emurx_ctl c{};
-    if (hipDeviceSynchronize() != hipSuccess ||
-        hipMemcpy(&c, h->d_ctl.p, sizeof(c), hipMemcpyDeviceToHost) != hipSuccess)
-        return EMURX_EDEVICE;
-    *error = (int)c.rsv[0];
     return EMURX_OK;
 }
 

@@ -60,6 +60,8 @@ PARSER_COUNTER_NAMES = [
     "Icmpv6Bytes", "errL4ProtoUnsupported", "errL3ProtoUnsupported", "errPacketIsTooShort"]
 NUM_PARSER_COUNTERS = len(PARSER_COUNTER_NAMES)
 HIST_BINS = 64
+HIST_SHARDS = 64   # EMURX_HIST_SHARDS: accumulating copies of the device histogram
+QUEUE_TILE = 256   # EMURX_QUEUE_TILE: frames per tile / queue segment
 
 # ---- record / descriptor layouts --------------------------------------------------------
 REC_DTYPE = np.dtype([
@@ -90,7 +92,16 @@ class Counters(C.Structure):
 
 class DevOut(C.Structure):
     _fields_ = [("rec", C.c_void_p), ("qlist", C.c_void_p), ("qcap", C.c_uint32),
-                ("qcount", C.c_void_p), ("hist", C.c_void_p)]
+                ("tile_cnt", C.c_void_p), ("hist", C.c_void_p)]
+
+
+def ntiles(n: int) -> int:
+    return (n + QUEUE_TILE - 1) // QUEUE_TILE
+
+
+def queue_cap(n: int) -> int:
+    """Smallest per-queue region (DevOut.qcap) a batch of n frames accepts."""
+    return ntiles(n) * QUEUE_TILE
 
 
 # (name, restype, argtypes) — every symbol include/emu_rx.h declares
@@ -122,9 +133,9 @@ SIGNATURES = [
     ("emurx_zmq_descriptors", C.c_int, [_U8P, C.c_size_t, _P, C.c_uint32,
                                         C.POINTER(C.c_uint32), C.POINTER(C.c_int)]),
     ("emurx_hist_to_counters", None, [_P, C.POINTER(Counters)]),
+    ("emurx_hist_fold", None, [_P, _P]),
     ("emurx_set_timing", C.c_int, [_P, C.c_uint32]),
-    ("emurx_kernel_times", C.c_int, [_P, _P, _P, C.c_uint32, C.POINTER(C.c_uint32)]),
-    ("emurx_device_error", C.c_int, [_P, C.POINTER(C.c_int)]),
+    ("emurx_kernel_times", C.c_int, [_P, _P, C.c_uint32, C.POINTER(C.c_uint32)]),
 ]
 
 _lib = None

@@ -126,11 +126,12 @@ class RxPath:
         return rec[:k], qlist[:k], qoff, cnt
 
     # ---- device-resident batch -----------------------------------------------------------
-    def classify_dev(self, frames, desc, n: int, rec=None, qlist=None, qcap: int = 0, qcount=None,
+    def classify_dev(self, frames, desc, n: int, rec=None, qlist=None, qcap: int = 0, tile_cnt=None,
                      hist=None, stream=None, classify: bool = True):
-        """frames/desc/rec/qlist/qcount/hist: device tensors (or raw device addresses).
-        Queue q's frame indices land in qlist[q*qcap : q*qcap + qcount[q]]."""
-        out = abi.DevOut(_addr(rec), _addr(qlist), qcap, _addr(qcount), _addr(hist))
+        """frames/desc/rec/qlist/tile_cnt/hist: device tensors (or raw device addresses).
+        Tile t's frames of queue q land in qlist[q*qcap + t*QUEUE_TILE :][:tile_cnt[t*16+q]]
+        (see pack_queues); hist holds HIST_SHARDS accumulating copies (see hist_fold)."""
+        out = abi.DevOut(_addr(rec), _addr(qlist), qcap, _addr(tile_cnt), _addr(hist))
         fn = self.lib.emurx_classify_dev if classify else self.lib.emurx_parse_dev
         return abi.check(fn(self.h, _addr(frames), _addr(desc), n, C.byref(out),
                             _stream(stream)), "classify_dev")
@@ -139,18 +140,12 @@ class RxPath:
         return abi.check(self.lib.emurx_set_timing(self.h, slots), "set_timing")
 
     def kernel_times(self, cap: int = 1 << 16):
-        """(k_rx ms[], k_q ms[]) of every batch launched since the previous call (HIP events
-        on the launch stream)."""
+        """Device ms of every batch launched since the previous call (HIP events recorded on
+        the launch stream around the k_rx launch)."""
         a = np.zeros(cap, np.float32)
-        b = np.zeros(cap, np.float32)
         n = C.c_uint32()
-        abi.check(self.lib.emurx_kernel_times(self.h, _p(a), _p(b), cap, C.byref(n)), "kernel_times")
-        return a[: n.value], b[: n.value]
-
-    def device_error(self) -> int:
-        e = C.c_int()
-        abi.check(self.lib.emurx_device_error(self.h, C.byref(e)), "device_error")
-        return e.value
+        abi.check(self.lib.emurx_kernel_times(self.h, _p(a), cap, C.byref(n)), "kernel_times")
+        return a[: n.value]
 
 
 def _addr(x):
@@ -176,6 +171,32 @@ def zmq_descriptors(msg: bytes, cap: int = 1 << 16):
     n, e = C.c_uint32(), C.c_int()
     rc = lib.emurx_zmq_descriptors(_p(m), len(msg), _p(d), cap, C.byref(n), C.byref(e))
     return rc, d[:n.value], e.value
+
+
+def hist_fold(shards: np.ndarray) -> np.ndarray:
+    """[HIST_SHARDS * 2 * HIST_BINS] device histogram copies -> [2 * HIST_BINS] (C-ABI)."""
+    lib = abi.load()
+    s = np.ascontiguousarray(shards, dtype=np.uint64).reshape(-1)
+    assert s.size == abi.HIST_SHARDS * 2 * abi.HIST_BINS
+    out = np.zeros(2 * abi.HIST_BINS, np.uint64)
+    lib.emurx_hist_fold(_p(s), _p(out))
+    return out
+
+
+def pack_queues(qlist: np.ndarray, qcap: int, tile_cnt: np.ndarray, n: int):
+    """Per-tile queue segments -> (frame indices in queue order, qoff[NUM_QUEUES + 1]):
+    queue q = qlist_packed[qoff[q]:qoff[q+1]], frames in order (the host side of
+    emurx_rx_stream's packing)."""
+    nt = abi.ntiles(n)
+    ql = np.asarray(qlist).view(np.uint32).reshape(abi.NUM_QUEUES, -1)[:, : nt * abi.QUEUE_TILE]
+    cnt = np.asarray(tile_cnt).view(np.uint32).reshape(-1, 16)[:nt, : abi.NUM_QUEUES].astype(np.int64)
+    assert (cnt <= abi.QUEUE_TILE).all()
+    seg = ql.reshape(abi.NUM_QUEUES, nt, abi.QUEUE_TILE)
+    keep = np.arange(abi.QUEUE_TILE)[None, None, :] < cnt.T[:, :, None]
+    packed = seg[keep].astype(np.uint32)  # C order: queue, tile, slot
+    qoff = np.zeros(abi.NUM_QUEUES + 1, np.uint32)
+    qoff[1:] = np.cumsum(cnt.sum(0))
+    return packed, qoff
 
 
 def hist_to_counters(hist: np.ndarray) -> dict:
