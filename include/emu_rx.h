@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define EMURX_ABI_VERSION 1
+#define EMURX_ABI_VERSION 2
 
 /* ---- return codes -------------------------------------------------------------------- */
 #define EMURX_OK 0

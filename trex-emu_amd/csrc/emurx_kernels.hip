@@ -71,13 +71,13 @@ __global__ __launch_bounds__(kBlock) void k_rx(const uint8_t* __restrict__ frame
         if (staged) {
             LdsSrc s{reinterpret_cast<const uint8_t*>(slab), slab, wv * kStage + (off - start)};
             parse_packet(s, len, vport, T.cb_mask, r);
-            if (kClassify) classify(s, len, T, r);
+            if (kClassify && !(EMURX_ABL & 2)) classify(s, len, T, r);
         } else {
             GlbSrc s{frames + off};
             parse_packet(s, len, vport, T.cb_mask, r);
-            if (kClassify) classify(s, len, T, r);
+            if (kClassify && !(EMURX_ABL & 2)) classify(s, len, T, r);
         }
-        if (rec) {
+        if (rec && !(EMURX_ABL & 16)) {
             uint4* o = reinterpret_cast<uint4*>(rec + i);
             o[0] = make_uint4(r.ns, r.cl, r.vlan0, r.vlan1);
             o[1] = make_uint4(r.vport | (r.l3 << 16), r.l4 | (r.l7 << 16),
@@ -90,7 +90,7 @@ __global__ __launch_bounds__(kBlock) void k_rx(const uint8_t* __restrict__ frame
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     uint32_t rank = 0, mycnt = 0;
 #pragma unroll
-    for (uint32_t qq = 0; qq < EMURX_NUM_QUEUES; ++qq) {
+    for (uint32_t qq = 0; qq < ((EMURX_ABL & 8) ? 0 : EMURX_NUM_QUEUES); ++qq) {
         const uint64_t m = __ballot(q == qq);
         if (q == qq) rank = (uint32_t)__popcll(m & lt);
         if (lane == qq) mycnt = (uint32_t)__popcll(m);
@@ -99,7 +99,7 @@ __global__ __launch_bounds__(kBlock) void k_rx(const uint8_t* __restrict__ frame
 
     // outcome histogram: one LDS add per distinct (status, proto) bin per wave
     const uint32_t bin = valid ? EMURX_HIST_BIN(r.status, r.proto) : 0xffffffffu;
-    uint64_t active = __ballot(valid);
+    uint64_t active = (EMURX_ABL & 4) ? 0 : __ballot(valid);
     while (active) {
         const int leader = __ffsll((long long)active) - 1;
         const uint32_t b = (uint32_t)__shfl((int)bin, leader);
@@ -114,7 +114,7 @@ __global__ __launch_bounds__(kBlock) void k_rx(const uint8_t* __restrict__ frame
     __syncthreads();
 
     // this tile's segment of every queue: frames in (wave, lane) order == frame order
-    if (qlist && q < EMURX_NUM_QUEUES) {
+    if (qlist && q < EMURX_NUM_QUEUES && !(EMURX_ABL & 8)) {
         uint32_t pos = rank;
         for (uint32_t w = 0; w < wv; ++w) pos += s_wcnt[w][q];
         const size_t at = (size_t)q * qcap + (size_t)tile * EMURX_QUEUE_TILE + pos;

@@ -19,6 +19,10 @@ constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / kWave;
 constexpr uint32_t kStage = 8192;  // LDS bytes staged per wave (64 frames)
 
+#ifndef EMURX_ABL
+#define EMURX_ABL 0  // experiment-only stage ablation (tools/ablate.sh); 0 in every real build
+#endif
+
 // ---------------------------------------------------------------------------------------
 // wave helpers
 // ---------------------------------------------------------------------------------------
@@ -84,6 +88,7 @@ struct LdsSrc {
     uint32_t base;        // LDS byte index of frame byte 0 (== global address mod 16)
     __device__ __forceinline__ uint32_t u8(uint32_t i) const { return b8[base + i]; }
     __device__ __forceinline__ bool csum(uint32_t s, uint32_t n, uint32_t pcs) const {
+        if (EMURX_ABL & 1) return true;
         uint32_t a = base + s, e = a + n;
         uint32_t k0 = a >> 2, k1 = (e + 3) >> 2;
         uint64_t sum = 0;

@@ -146,7 +146,7 @@ def load(path: str | os.PathLike | None = None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = Path(path) if path else LIB_PATH
+    p = Path(path) if path else Path(os.environ.get("EMURX_LIB", LIB_PATH))
     if not p.exists():
         raise OSError(f"libemurx.so not built at {p}: run `make -C {PKG_ROOT}` "
                       "(there is no CPU fallback for the product path)")
