@@ -126,7 +126,7 @@ struct emurx_ctx {
     bool dirty = true;
 
     // device tables
-    uint32_t ns_slots = 0, mac_slots = 0, ip4_slots = 0, ip6_slots = 0;
+    uint32_t ns_buckets = 0, mac_buckets = 0, ip4_buckets = 0, ip6_buckets = 0;
     DevBuf<uint32_t> d_ns, d_nsinfo, d_mac, d_ip4, d_ip6, d_client;
     std::vector<uint32_t> h_ns, h_nsinfo, h_mac, h_ip4, h_ip6, h_client;
 
@@ -153,10 +153,10 @@ struct emurx_ctx {
         T.ip4_tab = d_ip4.p;
         T.ip6_tab = d_ip6.p;
         T.client = d_client.p;
-        T.ns_mask = ns_slots - 1;
-        T.mac_mask = mac_slots - 1;
-        T.ip4_mask = ip4_slots - 1;
-        T.ip6_mask = ip6_slots - 1;
+        T.ns_mask = ns_buckets - 1;
+        T.mac_mask = mac_buckets - 1;
+        T.ip4_mask = ip4_buckets - 1;
+        T.ip6_mask = ip6_buckets - 1;
         T.max_ns = cfg.max_ns;
         T.max_clients = cfg.max_clients;
         T.cb_mask = cb_mask;
@@ -168,20 +168,28 @@ namespace {
 
 int bind(emurx_t* h) { return hipSetDevice(h->cfg.device) == hipSuccess ? EMURX_OK : EMURX_EDEVICE; }
 
-// open-addressing insert into a flat table (slot = `words` uint32, key in the first
-// words, value in the last word; EMURX_EMPTY marks a free slot)
-void flat_put(std::vector<uint32_t>& t, uint32_t mask, uint32_t words, uint32_t h, const uint32_t* e) {
-    uint32_t i = h & mask;
-    while (t[(size_t)i * words + words - 1] != EMURX_EMPTY) i = (i + 1) & mask;
-    memcpy(&t[(size_t)i * words], e, words * sizeof(uint32_t));
+// open-addressing insert into a bucketed table (emurx_tables.h): first free slot of the
+// first bucket, in linear bucket order from the home bucket, that has one
+void bucket_put(std::vector<uint32_t>& t, uint32_t bmask, uint32_t words, uint32_t h, const uint32_t* e) {
+    const uint32_t per = EMURX_BUCKET_WORDS / words;
+    for (uint32_t b = h & bmask;; b = (b + 1) & bmask)
+        for (uint32_t k = 0; k < per; ++k) {
+            uint32_t* slot = &t[(size_t)b * EMURX_BUCKET_WORDS + k * words];
+            if (slot[words - 1] == EMURX_EMPTY) {
+                memcpy(slot, e, words * sizeof(uint32_t));
+                return;
+            }
+        }
+}
+void empty_table(std::vector<uint32_t>& t, uint32_t buckets, uint32_t words) {
+    t.assign((size_t)buckets * EMURX_BUCKET_WORDS, 0);
+    for (size_t i = words - 1; i < t.size(); i += words) t[i] = EMURX_EMPTY;
 }
 
 int rebuild_and_upload(emurx_t* h, hipStream_t st) {
     if (!h->dirty) return EMURX_OK;
     (void)hipStreamSynchronize(st);  // previous upload may still read the staging vectors
-    const uint32_t E = EMURX_EMPTY;
-    h->h_ns.assign((size_t)h->ns_slots * 4, 0);
-    for (size_t i = 0; i < h->ns_slots; ++i) h->h_ns[i * 4 + 3] = E;
+    empty_table(h->h_ns, h->ns_buckets, 4);
     for (auto& kv : h->ns_map) {
         // a key with non-zero bytes [2:4] can never equal a parsed CTunnelKey (Set writes 0
         // there, thread_ctx.go:93): it has no device slot.  The free upper half of the vport
@@ -189,7 +197,7 @@ int rebuild_and_upload(emurx_t* h, hipStream_t st) {
         if (kv.first.w[0] >> 16) continue;
         uint32_t e[4] = {kv.first.w[0] | (h->ns[kv.second].plugins << 16), kv.first.w[1], kv.first.w[2],
                          kv.second};
-        flat_put(h->h_ns, h->ns_slots - 1, 4, emurx_ns_hash(kv.first.w[0], e[1], e[2]), e);
+        bucket_put(h->h_ns, h->ns_buckets - 1, 4, emurx_tk_hash(kv.first.w[0], e[1], e[2]), e);
     }
     h->h_nsinfo.assign((size_t)h->cfg.max_ns * 4, 0);
     for (uint32_t i = 0; i < h->ns.size(); ++i) {
@@ -197,26 +205,30 @@ int rebuild_and_upload(emurx_t* h, hipStream_t st) {
         h->h_nsinfo[i * 4 + 0] = n.alive ? n.plugins : 0;
         h->h_nsinfo[i * 4 + 1] = (n.alive && !n.order.empty()) ? n.order.front() : EMURX_ID_NONE;
     }
-    auto fill4 = [&](std::vector<uint32_t>& t, uint32_t slots, const Map& m, int kind) {
-        t.assign((size_t)slots * 4, 0);
-        for (size_t i = 0; i < slots; ++i) t[i * 4 + 3] = E;
+    // client entries hash from their Namespace's tunnel key (emurx_tables.h)
+    auto tk_of = [&](uint32_t ns) {
+        const uint8_t* k = h->ns[ns].key;
+        return emurx_tk_hash(le32(k), le32(k + 4), le32(k + 8));
+    };
+    auto fill4 = [&](std::vector<uint32_t>& t, uint32_t buckets, const Map& m, int kind) {
+        empty_table(t, buckets, 4);
         for (auto& kv : m) {
             uint32_t e[4] = {kv.first.w[0], kv.first.w[1], kv.first.w[2], kv.second};
-            uint32_t hh = kind == 0 ? emurx_mac_hash(e[0], e[1], e[2]) : emurx_ip4_hash(e[0], e[1]);
+            const uint32_t tk = tk_of(e[0]);
+            uint32_t hh = kind == 0 ? emurx_mac_hash(tk, e[1], e[2]) : emurx_ip4_hash(tk, e[1]);
             if (kind == 1) e[2] = 0;
             // MAC slots carry the client's plugin mask in the free upper half of mac[4..5]
             if (kind == 0) e[2] |= (h->cl[kv.second].plugins & 0xffffu) << 16;
-            flat_put(t, slots - 1, 4, hh, e);
+            bucket_put(t, buckets - 1, 4, hh, e);
         }
     };
-    fill4(h->h_mac, h->mac_slots, h->mac_map, 0);
-    fill4(h->h_ip4, h->ip4_slots, h->ip4_map, 1);
-    h->h_ip6.assign((size_t)h->ip6_slots * 8, 0);
-    for (size_t i = 0; i < h->ip6_slots; ++i) h->h_ip6[i * 8 + 7] = E;
+    fill4(h->h_mac, h->mac_buckets, h->mac_map, 0);
+    fill4(h->h_ip4, h->ip4_buckets, h->ip4_map, 1);
+    empty_table(h->h_ip6, h->ip6_buckets, 8);
     for (auto& kv : h->ip6_map) {
         const uint32_t* w = kv.first.w;
         uint32_t e[8] = {w[0], w[1], w[2], w[3], w[4], 0, 0, kv.second};
-        flat_put(h->h_ip6, h->ip6_slots - 1, 8, emurx_ip6_hash(w[0], w[1], w[2], w[3], w[4]), e);
+        bucket_put(h->h_ip6, h->ip6_buckets - 1, 8, emurx_ip6_hash(tk_of(w[0]), w[1], w[2], w[3], w[4]), e);
     }
     h->h_client.assign((size_t)h->cfg.max_clients * 8, 0);
     for (uint32_t i = 0; i < h->cl.size(); ++i) {
@@ -295,15 +307,17 @@ int emurx_open(const emurx_cfg* cfg, emurx_t** out) {
     int rc = bind(h);
     if (rc) { delete h; return rc; }
     if (hipStreamCreate(&h->stream) != hipSuccess) { delete h; return EMURX_EDEVICE; }
-    h->ns_slots = pow2_at_least(2ull * cfg->max_ns);
-    h->mac_slots = pow2_at_least(2ull * cfg->max_clients);
-    h->ip4_slots = pow2_at_least(2ull * cfg->max_clients);
-    h->ip6_slots = pow2_at_least(4ull * cfg->max_clients);
+    // load factor <= 1/2 in slots: 4 slots (IPv6: 2) per 64-byte bucket
+    h->ns_buckets = pow2_at_least(2ull * cfg->max_ns) / 4;
+    h->mac_buckets = pow2_at_least(2ull * cfg->max_clients) / 4;
+    h->ip4_buckets = pow2_at_least(2ull * cfg->max_clients) / 4;
+    h->ip6_buckets = pow2_at_least(4ull * cfg->max_clients) / 2;
     h->ns.resize(cfg->max_ns);
     h->cl.resize(cfg->max_clients);
-    if (h->d_ns.alloc((size_t)h->ns_slots * 4) || h->d_nsinfo.alloc((size_t)cfg->max_ns * 4) ||
-        h->d_mac.alloc((size_t)h->mac_slots * 4) || h->d_ip4.alloc((size_t)h->ip4_slots * 4) ||
-        h->d_ip6.alloc((size_t)h->ip6_slots * 8) || h->d_client.alloc((size_t)cfg->max_clients * 8)) {
+    const size_t BW = EMURX_BUCKET_WORDS;
+    if (h->d_ns.alloc(h->ns_buckets * BW) || h->d_nsinfo.alloc((size_t)cfg->max_ns * 4) ||
+        h->d_mac.alloc(h->mac_buckets * BW) || h->d_ip4.alloc(h->ip4_buckets * BW) ||
+        h->d_ip6.alloc(h->ip6_buckets * BW) || h->d_client.alloc((size_t)cfg->max_clients * 8)) {
         emurx_close(h);
         return EMURX_ENOMEM;
     }

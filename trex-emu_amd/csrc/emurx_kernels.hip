@@ -7,6 +7,7 @@
 //         Namespace / Client probes (emurx_parse.h) -> 32-B record -> the frame's index in
 //         its callback's queue segment for this tile (rank by wave ballots, waves in order)
 //         -> per-tile queue counts -> outcome histogram (one of EMURX_HIST_SHARDS copies).
+//         Frames reach LDS by LDS-DMA (global_load_lds_dwordx4), with no VGPR round trip.
 // Queue q is the concatenation over tiles of qlist[q*qcap + t*TILE .. + tile_cnt[t][q]):
 // stable (frame order) without any cross-tile prefix, so no scan launch and no waiting.
 // No MFMA: there is no dense contraction on this path; it is HBM / latency bound.
@@ -21,6 +22,12 @@ namespace emurx {
 
 static_assert(EMURX_QUEUE_TILE == kBlock, "one frame per lane per tile");
 
+// LDS-DMA (global_load_lds_dwordx4): lane l's 16 source bytes land at dst + 16 * l
+__device__ __forceinline__ void glds16(const uint4* src, uint4* dst_wave_base) {
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst_wave_base, 16, 0, 0);
+}
+__device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0)
+
 template <bool kClassify>
 __global__ __launch_bounds__(kBlock) void k_rx(const uint8_t* __restrict__ frames,
                                                const emurx_desc* __restrict__ desc, uint32_t n,
@@ -30,38 +37,34 @@ __global__ __launch_bounds__(kBlock) void k_rx(const uint8_t* __restrict__ frame
                                                unsigned long long* __restrict__ hist) {
     __shared__ __attribute__((aligned(16))) uint32_t slab[kWaves * kStage / 4];
     __shared__ uint32_t s_wcnt[kWaves][16];
-    __shared__ unsigned long long s_hpk[EMURX_HIST_BINS], s_hby[EMURX_HIST_BINS];
+    __shared__ unsigned long long s_hist[kWaves][EMURX_HIST_BINS];  // {pkts << 40 | bytes}
 
     const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / kWave;
     const uint32_t tile = blockIdx.x;
     const uint32_t i = tile * EMURX_QUEUE_TILE + tid;
     const bool valid = i < n;
-    if (tid < EMURX_HIST_BINS) { s_hpk[tid] = 0; s_hby[tid] = 0; }
+    s_hist[wv][lane] = 0;  // each wave owns its copy: no cross-wave ordering needed
+    if (lane < 16) s_wcnt[wv][lane] = 0;
 
     const uint2 dd = valid ? *reinterpret_cast<const uint2*>(desc + i) : make_uint2(0, 0);
     const uint32_t off = dd.x, len = dd.y & 0xffff, vport = (dd.y >> 16) & 0xff;
 
-    // the wave's byte range [lo, hi) -> stage into LDS when it fits
+    // the wave's byte range [lo, hi) -> copied HBM -> LDS by LDS-DMA when it fits the slab
     const uint32_t lo = wave_min_u32(valid ? off : 0xffffffffu);
     const uint32_t hi = wave_max_u32(valid ? off + len : 0u);
     const uint32_t start = lo & ~15u;
     const uint32_t nvec = hi > lo ? (hi - start + 15) >> 4 : 0;
     const bool staged = nvec > 0 && nvec <= kStage / 16;
     uint4* wslab = reinterpret_cast<uint4*>(slab) + wv * (kStage / 16);
-    if (staged) {  // all loads in flight before the first LDS write (one HBM round trip)
-        static_assert(kStage / 16 / kWave == 8, "staging unroll assumes 8 vectors per lane");
+    if (staged) {  // all copies in flight before the wait; clamped sources stay in bounds
+        static_assert(kStage / 16 / kWave == 8, "staging assumes 8 vectors per lane");
         const uint4* src = reinterpret_cast<const uint4*>(frames + start);
-        // clamped (always in-bounds) loads: no predication, duplicates hit the cache
-#define EMURX_LD(k) const uint4 v##k = src[min(lane + k * kWave, nvec - 1)]
-        EMURX_LD(0); EMURX_LD(1); EMURX_LD(2); EMURX_LD(3);
-        EMURX_LD(4); EMURX_LD(5); EMURX_LD(6); EMURX_LD(7);
-#undef EMURX_LD
-#define EMURX_ST(k) if (lane + k * kWave < nvec) wslab[lane + k * kWave] = v##k
-        EMURX_ST(0); EMURX_ST(1); EMURX_ST(2); EMURX_ST(3);
-        EMURX_ST(4); EMURX_ST(5); EMURX_ST(6); EMURX_ST(7);
-#undef EMURX_ST
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k)
+            if (k * kWave < nvec) glds16(src + min(lane + k * kWave, nvec - 1), wslab + k * kWave);
+        wait_vm0();
     }
-    // each wave reads only its own slab: a wave-level barrier orders the LDS writes
+    // each wave reads only its own slab: a wave-level barrier orders it
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -83,33 +86,22 @@ __global__ __launch_bounds__(kBlock) void k_rx(const uint8_t* __restrict__ frame
             o[1] = make_uint4(r.vport | (r.l3 << 16), r.l4 | (r.l7 << 16),
                               r.l7len | (r.nh << 16) | (r.proto << 24), r.status | (r.flags << 8));
         }
+        // outcome histogram: one packed LDS add per frame into the wave's copy
+        if (!(EMURX_ABL & 4))
+            atomicAdd(&s_hist[wv][EMURX_HIST_BIN(r.status, r.proto)], (1ull << 40) | (unsigned long long)len);
     }
     const uint32_t q = valid ? (r.status == EMURX_ST_OK ? r.proto : EMURX_Q_DROP) : 0xffu;
 
-    // rank inside (wave, queue) and the wave's count per queue
-    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    uint32_t rank = 0, mycnt = 0;
-#pragma unroll
-    for (uint32_t qq = 0; qq < ((EMURX_ABL & 8) ? 0 : EMURX_NUM_QUEUES); ++qq) {
+    // rank inside (wave, queue): one ballot per distinct queue present in the wave
+    uint32_t rank = 0;
+    uint64_t left = (EMURX_ABL & 8) ? 0 : __ballot(valid);
+    while (left) {
+        const uint32_t lead = (uint32_t)__ffsll((long long)left) - 1;
+        const uint32_t qq = (uint32_t)__builtin_amdgcn_readlane((int)q, (int)lead);
         const uint64_t m = __ballot(q == qq);
-        if (q == qq) rank = (uint32_t)__popcll(m & lt);
-        if (lane == qq) mycnt = (uint32_t)__popcll(m);
-    }
-    if (lane < 16) s_wcnt[wv][lane] = mycnt;
-
-    // outcome histogram: one LDS add per distinct (status, proto) bin per wave
-    const uint32_t bin = valid ? EMURX_HIST_BIN(r.status, r.proto) : 0xffffffffu;
-    uint64_t active = (EMURX_ABL & 4) ? 0 : __ballot(valid);
-    while (active) {
-        const int leader = __ffsll((long long)active) - 1;
-        const uint32_t b = (uint32_t)__shfl((int)bin, leader);
-        const uint64_t m = __ballot(bin == b);
-        const uint64_t bytes = wave_sum_u64(bin == b ? (uint64_t)len : 0);
-        if ((int)lane == leader) {
-            atomicAdd(&s_hpk[b], (unsigned long long)__popcll(m));
-            atomicAdd(&s_hby[b], (unsigned long long)bytes);
-        }
-        active &= ~m;
+        if (q == qq) rank = mbcnt(m);
+        if (lane == lead) s_wcnt[wv][qq] = (uint32_t)__popcll(m);
+        left &= ~m;
     }
     __syncthreads();
 
@@ -125,11 +117,14 @@ __global__ __launch_bounds__(kBlock) void k_rx(const uint8_t* __restrict__ frame
             s_wcnt[0][tid] + s_wcnt[1][tid] + s_wcnt[2][tid] + s_wcnt[3][tid];
     // one of EMURX_HIST_SHARDS copies per workgroup: same-address memory-side atomics from
     // every workgroup would serialise; the shards are folded on the host
-    if (tid >= 64 && tid < 64 + EMURX_HIST_BINS && s_hpk[tid - 64]) {
+    if (tid >= 64 && tid < 64 + EMURX_HIST_BINS) {
         const uint32_t b = tid - 64;
-        unsigned long long* hs = hist + (size_t)(tile & (EMURX_HIST_SHARDS - 1)) * 2 * EMURX_HIST_BINS;
-        atomicAdd(&hs[2 * b], s_hpk[b]);
-        atomicAdd(&hs[2 * b + 1], s_hby[b]);
+        const unsigned long long v = s_hist[0][b] + s_hist[1][b] + s_hist[2][b] + s_hist[3][b];
+        if (v) {
+            unsigned long long* hs = hist + (size_t)(tile & (EMURX_HIST_SHARDS - 1)) * 2 * EMURX_HIST_BINS;
+            atomicAdd(&hs[2 * b], v >> 40);
+            atomicAdd(&hs[2 * b + 1], v & ((1ull << 40) - 1));
+        }
     }
 }
 

@@ -27,24 +27,31 @@ constexpr uint32_t kStage = 8192;  // LDS bytes staged per wave (64 frames)
 // wave helpers
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+// wave64 reductions on the DPP network (quad perms, row rotates, row broadcasts; result is
+// read from lane 63 into a scalar register): no LDS traffic, 6 VALU + 1 readlane
+template <int kCtrl, int kRowMask = 0xf>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, kCtrl, kRowMask, 0xf, false);
+}
+template <class Op>
+__device__ __forceinline__ uint32_t wave_reduce(uint32_t v, Op op) {
+    v = op(v, dpp<0xb1>(v));        // quad_perm [1,0,3,2]
+    v = op(v, dpp<0x4e>(v));        // quad_perm [2,3,0,1]
+    v = op(v, dpp<0x124>(v));       // row_ror:4
+    v = op(v, dpp<0x128>(v));       // row_ror:8
+    v = op(v, dpp<0x142, 0xa>(v));  // row_bcast:15
+    v = op(v, dpp<0x143, 0xc>(v));  // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o));
-    return v;
+    return wave_reduce(v, [](uint32_t x, uint32_t y) { return min(x, y); });
 }
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
-    return v;
+    return wave_reduce(v, [](uint32_t x, uint32_t y) { return max(x, y); });
 }
-__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, o);
-        uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o);
-        v += ((uint64_t)hi << 32) | lo;
-    }
-    return v;
+// lanes below this one in mask m
+__device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
 // ---------------------------------------------------------------------------------------
@@ -56,27 +63,40 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 //   S_go == T * 256^(1 - (span_start & 1))   (mod 0xffff)
 // and S_go + pseudo == 0 (mod 0xffff) with a non-zero total <=> Go's check passes.
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t fold16(uint64_t s) {
-    uint32_t x = (uint32_t)(s & 0xffff) + (uint32_t)((s >> 16) & 0xffff) +
-                 (uint32_t)((s >> 32) & 0xffff) + (uint32_t)(s >> 48);
+// v_sad_u16(w, 0, acc) = acc + (w & 0xffff) + (w >> 16): one VALU per dword, and
+// == sum of w (mod 0xffff) because 2^16 == 1.  Zero iff every masked byte is zero.
+__device__ __forceinline__ uint32_t sad16(uint32_t w, uint32_t acc) { return __builtin_amdgcn_sad_u16(w, 0u, acc); }
+__device__ __forceinline__ uint32_t fold16(uint32_t x) {
     x = (x & 0xffff) + (x >> 16);
     x = (x & 0xffff) + (x >> 16);
-    return x;  // <= 0xffff, == s mod 0xffff (0xffff stands for 0)
+    return x;  // <= 0xffff, == x mod 0xffff (0xffff stands for 0)
 }
-__device__ __forceinline__ uint32_t byte_mask(int sb, int eb) {  // bytes [sb, eb) of a dword
-    uint32_t lo = eb >= 4 ? 0xffffffffu : ((1u << (8 * max(eb, 0))) - 1u);
-    uint32_t hi = sb <= 0 ? 0xffffffffu : (sb >= 4 ? 0u : (0xffffffffu << (8 * sb)));
-    return lo & hi;
+// the sum of the span's big-endian 16-bit words (mod 0xffff) from its aligned-dword sum T
+__device__ __forceinline__ uint32_t be_domain(uint32_t T, uint32_t a_start) {
+    uint32_t t = fold16(T);
+    return (a_start & 1u) ? t : (((t << 8) | (t >> 8)) & 0xffffu);
 }
-// true iff tcpipChecksum(span, pcs) == 0
-__device__ __forceinline__ bool csum_ok(uint64_t sum, bool all_zero, uint32_t a_start, uint32_t pcs) {
-    uint32_t t = fold16(sum);
-    if ((a_start & 1u) == 0) t = ((t << 8) | (t >> 8)) & 0xffffu;
-    uint32_t x = t + pcs;
-    x = (x & 0xffff) + (x >> 16);
-    x = (x & 0xffff) + (x >> 16);
-    x = (x & 0xffff) + (x >> 16);
-    return (x == 0xffffu || x == 0u) && !(all_zero && pcs == 0);
+// tcpipChecksum(span, pcs) == 0  <=>  pcs + S == 0 (mod 0xffff) and the u32 sum is non-zero
+__device__ __forceinline__ bool csum_ok(uint32_t T, uint32_t a_start, uint32_t pcs) {
+    uint32_t x = fold16(be_domain(T, a_start) + pcs);
+    return (x == 0xffffu || x == 0u) && !(T == 0 && pcs == 0);
+}
+// sum over the bytes [a, a + n) of a dword array: head / body / tail masks, body unmasked
+template <class P>
+__device__ __forceinline__ uint32_t dword_sum(const P* w32, uint32_t a, uint32_t n) {
+    if (n == 0) return 0;
+    const uint32_t e = a + n, k0 = a >> 2, k1 = (e - 1) >> 2;
+    const uint32_t hm = 0xffffffffu << (8 * (a & 3));
+    const uint32_t tm = 0xffffffffu >> (8 * ((0u - e) & 3));
+    const uint32_t w0 = w32[k0] & hm;
+    if (k0 == k1) return sad16(w0 & tm, 0);
+    uint32_t acc = sad16(w0, 0), k = k0 + 1;
+    for (; k + 4 <= k1; k += 4) {
+        const uint32_t x0 = w32[k], x1 = w32[k + 1], x2 = w32[k + 2], x3 = w32[k + 3];
+        acc = sad16(x3, sad16(x2, sad16(x1, sad16(x0, acc))));
+    }
+    for (; k < k1; ++k) acc = sad16(w32[k], acc);
+    return sad16(w32[k1] & tm, acc);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -87,43 +107,29 @@ struct LdsSrc {
     const uint32_t* b32;  // same array, dword view
     uint32_t base;        // LDS byte index of frame byte 0 (== global address mod 16)
     __device__ __forceinline__ uint32_t u8(uint32_t i) const { return b8[base + i]; }
-    __device__ __forceinline__ bool csum(uint32_t s, uint32_t n, uint32_t pcs) const {
-        if (EMURX_ABL & 1) return true;
-        uint32_t a = base + s, e = a + n;
-        uint32_t k0 = a >> 2, k1 = (e + 3) >> 2;
-        uint64_t sum = 0;
-        uint32_t orv = 0;
-        for (uint32_t k = k0; k < k1; ++k) {
-            uint32_t w = b32[k];
-            int rel = (int)(k << 2);
-            w &= byte_mask((int)a - rel, (int)e - rel);
-            sum += w;
-            orv |= w;
-        }
-        return csum_ok(sum, orv == 0, a, pcs);
-    }
+    __device__ __forceinline__ uint32_t sum(uint32_t s, uint32_t n) const { return dword_sum(b32, base + s, n); }
+    __device__ __forceinline__ uint32_t at(uint32_t s) const { return base + s; }
 };
 struct GlbSrc {
     const uint8_t* f;  // frame byte 0 (global)
     __device__ __forceinline__ uint32_t u8(uint32_t i) const { return f[i]; }
-    __device__ __forceinline__ bool csum(uint32_t s, uint32_t n, uint32_t pcs) const {
-        uintptr_t a = (uintptr_t)(f + s), e = a + n;
-        const uint32_t* w32 = (const uint32_t*)(a & ~(uintptr_t)3);
-        uint32_t nw = (uint32_t)(((e + 3) & ~(uintptr_t)3) - (a & ~(uintptr_t)3)) >> 2;
-        uint64_t sum = 0;
-        uint32_t orv = 0;
-        int sa = (int)(a & 3);
-        int ee = (int)(e - (a & ~(uintptr_t)3));
-        for (uint32_t k = 0; k < nw; ++k) {
-            uint32_t w = w32[k];
-            int rel = (int)(k << 2);
-            w &= byte_mask(sa - rel, ee - rel);
-            sum += w;
-            orv |= w;
-        }
-        return csum_ok(sum, orv == 0, (uint32_t)a, pcs);
+    __device__ __forceinline__ uint32_t sum(uint32_t s, uint32_t n) const {
+        const uintptr_t a = (uintptr_t)(f + s);
+        return dword_sum(reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3), (uint32_t)(a & 3), n);
     }
+    __device__ __forceinline__ uint32_t at(uint32_t s) const { return (uint32_t)(uintptr_t)(f + s); }
 };
+// tcpipChecksum(p[s:s+n], pcs) == 0
+template <class S>
+__device__ __forceinline__ bool csum(const S& src, uint32_t s, uint32_t n, uint32_t pcs) {
+    if (EMURX_ABL & 1) return true;
+    return csum_ok(src.sum(s, n), src.at(s), pcs);
+}
+// sum of the big-endian 16-bit words of p[s:s+n] (n even), mod 0xffff: GetPhCs's address part
+template <class S>
+__device__ __forceinline__ uint32_t pseudo(const S& src, uint32_t s, uint32_t n) {
+    return be_domain(src.sum(s, n), src.at(s));
+}
 
 template <class S>
 __device__ __forceinline__ uint32_t be16(const S& s, uint32_t i) { return (s.u8(i) << 8) | s.u8(i + 1); }
@@ -187,7 +193,7 @@ __device__ void parse_l4(const S& s, uint32_t len, Rec& r, uint32_t nextHdr, uin
     case 1:  // ICMPv4
         if (len < ((L4 + 8) & 0xffff)) { fail(r, EMURX_ST_ICMPV4_TOO_SHORT); return; }
         if (!span_ok(L4, l4len)) { fail(r, EMURX_ST_PANIC_L4LEN); return; }
-        if (!s.csum(L4, l4len, 0)) { fail(r, EMURX_ST_ICMPV4_CS); return; }
+        if (!csum(s, L4, l4len, 0)) { fail(r, EMURX_ST_ICMPV4_CS); return; }
         r.l7 = (L4 + 8) & 0xffff;
         invoke(r, EMURX_CB_ICMP, cb_mask);
         return;
@@ -203,7 +209,7 @@ __device__ void parse_l4(const S& s, uint32_t len, Rec& r, uint32_t nextHdr, uin
         r.l7 = (L4 + tcplen) & 0xffff;
         r.l7len = (l4len - tcplen) & 0xffff;
         if (!span_ok(L4, l4len)) { fail(r, EMURX_ST_PANIC_L4LEN); return; }
-        if (!s.csum(L4, l4len, pcs)) { fail(r, EMURX_ST_TCP_CS); return; }
+        if (!csum(s, L4, l4len, pcs)) { fail(r, EMURX_ST_TCP_CS); return; }
         invoke(r, EMURX_CB_TCP, cb_mask);
         return;
     }
@@ -212,7 +218,7 @@ __device__ void parse_l4(const S& s, uint32_t len, Rec& r, uint32_t nextHdr, uin
         r.l7len = (l4len - 8) & 0xffff;
         if (be16(s, L4 + 6) > 0) {
             if (!span_ok(L4, l4len)) { fail(r, EMURX_ST_PANIC_L4LEN); return; }
-            if (!s.csum(L4, l4len, pcs)) { fail(r, EMURX_ST_UDP_CS); return; }
+            if (!csum(s, L4, l4len, pcs)) { fail(r, EMURX_ST_UDP_CS); return; }
         }
         r.l7 = (L4 + 8) & 0xffff;
         uint32_t src = be16(s, L4), dst = be16(s, L4 + 2);
@@ -227,7 +233,7 @@ __device__ void parse_l4(const S& s, uint32_t len, Rec& r, uint32_t nextHdr, uin
     case 58: {  // ICMPv6
         if (len < ((L4 + 4) & 0xffff)) { fail(r, EMURX_ST_ICMPV6_TOO_SHORT); return; }
         if (!span_ok(L4, l4len)) { fail(r, EMURX_ST_PANIC_L4LEN); return; }
-        if (!s.csum(L4, l4len, pcs)) { fail(r, EMURX_ST_ICMPV6_CS); return; }
+        if (!csum(s, L4, l4len, pcs)) { fail(r, EMURX_ST_ICMPV6_CS); return; }
         uint32_t t = s.u8(L4);
         bool okt = (t >= 1 && t <= 4) || (t >= 128 && t <= 136);
         if (okt) invoke(r, EMURX_CB_ICMPV6, cb_mask);
@@ -240,14 +246,9 @@ __device__ void parse_l4(const S& s, uint32_t len, Rec& r, uint32_t nextHdr, uin
     }
 }
 
-// pseudo-header partial sums: IPv4Header.GetPhCs ip4.go:49-58, IPv6Header.GetPhCs ip6.go:126-134
-template <class S>
-__device__ __forceinline__ uint32_t pair_sum(const S& s, uint32_t p, int n) {
-    uint32_t c = 0;
-    for (int i = 0; i < n; i += 2) c += be16(s, p + i);
-    return c;
-}
-
+// pseudo-header partial sums (IPv4Header.GetPhCs ip4.go:49-58, IPv6Header.GetPhCs
+// ip6.go:126-134) are taken mod 0xffff: the checksum verdict depends on the sum only mod
+// 0xffff, and with the protocol term (never 0 where a pseudo header is used) never zero.
 // Parser.ParsePacket parser.go:756-959
 template <class S>
 __device__ void parse_packet(const S& s, uint32_t len, uint32_t vport, uint32_t cb_mask, Rec& r) {
@@ -283,11 +284,11 @@ __device__ void parse_packet(const S& s, uint32_t len, uint32_t vport, uint32_t 
             if (len < offset + hdr) { fail(r, EMURX_ST_IPV4_HDR_TOO_SHORT); return; }
             uint32_t totlen = be16(s, offset + 2);
             if (len < ((offset + totlen) & 0xffff)) { fail(r, EMURX_ST_IPV4_TOO_SHORT); return; }
-            if (!s.csum(offset, hdr, 0)) { fail(r, EMURX_ST_IPV4_CS); return; }
+            if (!csum(s, offset, hdr, 0)) { fail(r, EMURX_ST_IPV4_CS); return; }
             uint32_t l4len = (totlen - hdr) & 0xffff;
             r.l4 = offset + hdr;
             uint32_t proto = s.u8(offset + 9);
-            uint32_t pcs = pair_sum(s, offset + 12, 8) + proto + l4len;  // src, dst, 0|proto, len
+            uint32_t pcs = pseudo(s, offset + 12, 8) + proto + l4len;  // src, dst, 0|proto, len
             parse_l4(s, len, r, proto, pcs, l4len, false, cb_mask);
             return;
         }
@@ -320,7 +321,7 @@ __device__ void parse_packet(const S& s, uint32_t len, uint32_t vport, uint32_t 
             if (nh == 194) { fail(r, EMURX_ST_IPV6_JUMBO); return; }
             if (nh == 59) { fail(r, EMURX_ST_IPV6_EMPTY); return; }
             r.l4 = l4;
-            uint32_t pcs = pair_sum(s, offset + 8, 32) + ((plen - osize) & 0xffff) + nh;
+            uint32_t pcs = pseudo(s, offset + 8, 32) + ((plen - osize) & 0xffff) + nh;
             parse_l4(s, len, r, nh, pcs, l4len, true, cb_mask);
             return;
         }
@@ -344,50 +345,75 @@ __device__ void parse_packet(const S& s, uint32_t len, uint32_t vport, uint32_t 
 
 // ---------------------------------------------------------------------------------------
 // Namespace / Client lookups (GetNs thread_ctx.go:777-784, CLookupBy* ns_ctx.go:262-329)
+// over the bucketed tables of emurx_tables.h.  A frame's Namespace bucket and its client
+// bucket both follow from the parsed tunnel key, so classify() issues the two 64-byte
+// bucket reads together and resolves them afterwards; overflow buckets are rare.
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ uint4 ld4(const uint32_t* p) { return *reinterpret_cast<const uint4*>(p); }
+struct Bucket {
+    uint4 s[4];
+};
+__device__ __forceinline__ Bucket ld_bucket(const uint32_t* tab, uint32_t b) {
+    const uint4* p = reinterpret_cast<const uint4*>(tab + (size_t)b * EMURX_BUCKET_WORDS);
+    return Bucket{{p[0], p[1], p[2], p[3]}};
+}
 
-// ns slot: {vport | ns_plugins << 16, vlan0, vlan1, ns_id} -> (ns_id, ns plugin mask)
-__device__ uint2 probe_ns(const emurx_dev_tables& T, uint32_t w0, uint32_t w1, uint32_t w2) {
-    uint32_t i = emurx_ns_hash(w0, w1, w2) & T.ns_mask;
-    for (uint32_t k = 0; k <= T.ns_mask; ++k, i = (i + 1) & T.ns_mask) {
-        uint4 e = ld4(T.ns_tab + 4 * i);
-        if (e.w == EMURX_EMPTY) break;
-        if ((e.x & 0xffffu) == w0 && e.y == w1 && e.z == w2) return make_uint2(e.w, e.x >> 16);
+// ns slot {vport | ns_plugins << 16, vlan0, vlan1, ns_id} -> (ns_id, ns plugin mask)
+__device__ uint2 resolve_ns(const emurx_dev_tables& T, uint32_t b, Bucket e, uint32_t w0, uint32_t w1,
+                            uint32_t w2) {
+    for (uint32_t n = 0;;) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint4 x = e.s[k];
+            if (x.w == EMURX_EMPTY) return make_uint2(EMURX_ID_NONE, 0);
+            if ((x.x & 0xffffu) == w0 && x.y == w1 && x.z == w2) return make_uint2(x.w, x.x >> 16);
+        }
+        if (++n > T.ns_mask) return make_uint2(EMURX_ID_NONE, 0);
+        b = (b + 1) & T.ns_mask;
+        e = ld_bucket(T.ns_tab, b);
     }
-    return make_uint2(EMURX_ID_NONE, 0);
 }
-// mac slot: {ns_id, mac[0..3], mac[4..5] | client_plugins << 16, client_id}
-__device__ uint2 probe_mac(const emurx_dev_tables& T, uint32_t ns, uint32_t lo, uint32_t hi) {
-    if (lo == 0 && hi == 0) return make_uint2(EMURX_ID_NONE, 0);  // MACKey.IsZero
-    uint32_t i = emurx_mac_hash(ns, lo, hi) & T.mac_mask;
-    for (uint32_t k = 0; k <= T.mac_mask; ++k, i = (i + 1) & T.mac_mask) {
-        uint4 e = ld4(T.mac_tab + 4 * i);
-        if (e.w == EMURX_EMPTY) break;
-        if (e.x == ns && e.y == lo && (e.z & 0xffffu) == hi) return make_uint2(e.w, e.z >> 16);
+// mac slot {ns_id, mac[0..3], mac[4..5] | client_plugins << 16, client_id} -> (cid, plugins)
+__device__ uint2 resolve_mac(const emurx_dev_tables& T, uint32_t b, Bucket e, uint32_t ns, uint32_t lo,
+                             uint32_t hi) {
+    for (uint32_t n = 0;;) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint4 x = e.s[k];
+            if (x.w == EMURX_EMPTY) return make_uint2(EMURX_ID_NONE, 0);
+            if (x.x == ns && x.y == lo && (x.z & 0xffffu) == hi) return make_uint2(x.w, x.z >> 16);
+        }
+        if (++n > T.mac_mask) return make_uint2(EMURX_ID_NONE, 0);
+        b = (b + 1) & T.mac_mask;
+        e = ld_bucket(T.mac_tab, b);
     }
-    return make_uint2(EMURX_ID_NONE, 0);
 }
-__device__ uint32_t probe_ip4(const emurx_dev_tables& T, uint32_t ns, uint32_t ip) {
-    if (ip == 0) return EMURX_ID_NONE;
-    uint32_t i = emurx_ip4_hash(ns, ip) & T.ip4_mask;
-    for (uint32_t k = 0; k <= T.ip4_mask; ++k, i = (i + 1) & T.ip4_mask) {
-        uint4 e = ld4(T.ip4_tab + 4 * i);
-        if (e.w == EMURX_EMPTY) return EMURX_ID_NONE;
-        if (e.x == ns && e.y == ip) return e.w;
+// ip4 slot {ns_id, ip, 0, client_id}
+__device__ uint32_t resolve_ip4(const emurx_dev_tables& T, uint32_t b, Bucket e, uint32_t ns, uint32_t ip) {
+    for (uint32_t n = 0;;) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint4 x = e.s[k];
+            if (x.w == EMURX_EMPTY) return EMURX_ID_NONE;
+            if (x.x == ns && x.y == ip) return x.w;
+        }
+        if (++n > T.ip4_mask) return EMURX_ID_NONE;
+        b = (b + 1) & T.ip4_mask;
+        e = ld_bucket(T.ip4_tab, b);
     }
-    return EMURX_ID_NONE;
 }
-__device__ __forceinline__ uint32_t probe_ip6(const emurx_dev_tables& T, uint32_t ns, const uint32_t ip[4]) {
-    if ((ip[0] | ip[1] | ip[2] | ip[3]) == 0) return EMURX_ID_NONE;
-    uint32_t i = emurx_ip6_hash(ns, ip[0], ip[1], ip[2], ip[3]) & T.ip6_mask;
-    for (uint32_t k = 0; k <= T.ip6_mask; ++k, i = (i + 1) & T.ip6_mask) {
-        uint4 a = ld4(T.ip6_tab + 8 * i);
-        uint4 b = ld4(T.ip6_tab + 8 * i + 4);
-        if (b.w == EMURX_EMPTY) return EMURX_ID_NONE;
-        if (a.x == ns && a.y == ip[0] && a.z == ip[1] && a.w == ip[2] && b.x == ip[3]) return b.w;
+// ip6 slot {ns_id, ip[0..3], ip[4..7], ip[8..11]} {ip[12..15], 0, 0, client_id}, 2 per bucket
+__device__ uint32_t resolve_ip6(const emurx_dev_tables& T, uint32_t b, Bucket e, uint32_t ns, const uint32_t w[4]) {
+    for (uint32_t n = 0;;) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const uint4 x = e.s[2 * k], y = e.s[2 * k + 1];
+            if (y.w == EMURX_EMPTY) return EMURX_ID_NONE;
+            if (x.x == ns && x.y == w[0] && x.z == w[1] && x.w == w[2] && y.x == w[3]) return y.w;
+        }
+        if (++n > T.ip6_mask) return EMURX_ID_NONE;
+        b = (b + 1) & T.ip6_mask;
+        e = ld_bucket(T.ip6_tab, b);
     }
-    return EMURX_ID_NONE;
 }
 
 __device__ __forceinline__ void set_lk(Rec& r, uint32_t lk) {
@@ -428,25 +454,6 @@ __device__ __forceinline__ bool ip6_local_or_global(const uint32_t w[4]) {
     if (b0 == 0xff) return false;                                            // multicast
     return true;
 }
-// CNSCtx.CLookupByIPv6LocalGlobal ns_ctx.go:288-316
-__device__ __forceinline__ uint32_t lookup_ip6_lg(const emurx_dev_tables& T, uint32_t ns, const uint32_t w[4]) {
-    if (!ip6_local_or_global(w)) return EMURX_ID_NONE;
-    uint32_t b11 = (w[2] >> 24) & 0xff, b12 = w[3] & 0xff;
-    if (b11 == 0xff && b12 == 0xfe) {  // ExtractOnlyMac client_ctx.go:314-329
-        uint32_t m0 = (w[2] & 0xff) ^ 2, m1 = (w[2] >> 8) & 0xff, m2 = (w[2] >> 16) & 0xff;
-        uint32_t m3 = (w[3] >> 8) & 0xff, m4 = (w[3] >> 16) & 0xff, m5 = w[3] >> 24;
-        uint32_t lo = m0 | (m1 << 8) | (m2 << 16) | (m3 << 24), hi = m4 | (m5 << 8);
-        uint32_t cid = probe_mac(T, ns, lo, hi).x;
-        if (cid == EMURX_ID_NONE) return cid;
-        // CClient.IsValidPrefix client_ctx.go:279-295
-        if (w[0] == 0x000080feu && w[1] == 0) return cid;
-        const uint32_t* c = T.client + 8 * cid;
-        uint32_t ra = c[3];
-        if ((ra & 1u) && ((ra >> 8) & 0xff) == 64 && c[4] == w[0] && c[5] == w[1]) return cid;
-        return EMURX_ID_NONE;
-    }
-    return probe_ip6(T, ns, w);
-}
 // PluginDhcpNs.GetMacFromDhcp dhcp.go:863-891 + DHCPv4.DecodeFromBytes dhcpv4.go:125-172
 template <class S>
 __device__ bool dhcp_chaddr(const S& s, uint32_t len, const Rec& r, uint32_t& lo, uint32_t& hi) {
@@ -478,67 +485,142 @@ __constant__ uint8_t kCbPlugin[EMURX_NUM_CB] = {
     EMURX_PLUG_DHCPV6, EMURX_PLUG_MDNS, EMURX_PLUG_TRANSPORT, EMURX_PLUG_TRANSPORT,
     EMURX_PLUG_IPV6, EMURX_PLUG_DOT1X, EMURX_PLUG_PPP};
 
+// what a callback's client rule looks up, decided from the frame alone (before the
+// Namespace is known, so both probes can be issued together)
+enum Key : uint32_t {
+    kNsLevel = 0,  // no client lookup (igmp, mdns, arp reply, icmpv6 non-echo)
+    kNoClient,     // the rule fails before any lookup (dhcp broadcast without chaddr, ...)
+    kFirst,        // ns.GetFirstClient (dhcpsrv broadcast, eapol PAE group address)
+    kMac,          // CLookupByMac(kw[0..1])
+    kEui,          // CLookupByIPv6LocalGlobal, EUI-64 form: MAC from the address + prefix rule
+    kIp4,          // CLookupByIPv4(kw[0])
+    kIp6,          // CLookupByIPv6(kw[0..3])
+};
+
 template <class S>
 __device__ void classify(const S& s, uint32_t len, const emurx_dev_tables& T, Rec& r) {
     if (r.status != EMURX_ST_OK) return;
-    const uint2 nsr = probe_ns(T, r.vport, r.vlan0, r.vlan1);  // CTunnelKey words
+    const uint32_t cb = r.proto, plug = kCbPlugin[cb];
+    const uint32_t dlo = le32(s, 0), dhi = s.u8(4) | (s.u8(5) << 8);  // p[0:6]
+    const bool bcast = dlo == 0xffffffffu && dhi == 0xffffu;
+
+    // ---- the client key of this callback's rule ----
+    uint32_t key = kMac, kw[4] = {dlo, dhi, 0, 0};
+    switch (cb) {
+    case EMURX_CB_ARP:  // arp.go:904-949: request -> IPv4 of the ARP target
+        if (be16(s, r.l3 + 6) == 1) { key = kIp4; kw[0] = le32(s, r.l3 + 24); }
+        else key = kNsLevel;
+        break;
+    case EMURX_CB_ICMP:  // icmp.go:396-427: IPv4 destination, then IsUnicastToMe
+        key = kIp4; kw[0] = le32(s, r.l3 + 16);
+        break;
+    case EMURX_CB_IGMP:
+    case EMURX_CB_MDNS:
+        key = kNsLevel;
+        break;
+    case EMURX_CB_DHCP:  // dhcp.go:893-917: broadcast -> chaddr
+        if (bcast && !dhcp_chaddr(s, len, r, kw[0], kw[1])) key = kNoClient;
+        break;
+    case EMURX_CB_DHCPSRV:  // dhcpsrv.go:1798-1826: broadcast -> GetFirstClient
+        if (bcast) key = kFirst;
+        break;
+    case EMURX_CB_EAPOL:  // dot1x.go:624-650: 01:80:c2:00:00:03 -> GetFirstClient
+        if (dlo == 0x00c28001u && dhi == 0x0300u) key = kFirst;
+        break;
+    case EMURX_CB_ICMPV6: {  // ipv6.go:465-540: echo request -> CLookupByIPv6LocalGlobal(dst)
+        if (be16(s, r.l4) != 0x8000u) { key = kNsLevel; break; }
+        if (r.l3 + 40 > len) { key = kNoClient; break; }
+        for (int k = 0; k < 4; ++k) kw[k] = le32(s, r.l3 + 24 + 4 * k);
+        if (!ip6_local_or_global(kw)) { key = kNoClient; break; }
+        if (((kw[2] >> 24) & 0xff) == 0xff && (kw[3] & 0xff) == 0xfe) {  // ExtractOnlyMac client_ctx.go:314-329
+            key = kEui;
+        } else {
+            key = kIp6;
+        }
+        break;
+    }
+    default:  // dhcpv6, ppp, tcp, udp: MAC[dst] (plugin_transport.go:83-115, ...)
+        break;
+    }
+    uint32_t mlo = kw[0], mhi = kw[1];  // the MAC probed for kMac / kEui
+    if (key == kEui) {
+        mlo = ((kw[2] & 0xff) ^ 2) | (((kw[2] >> 8) & 0xff) << 8) | (((kw[2] >> 16) & 0xff) << 16) |
+              (((kw[3] >> 8) & 0xff) << 24);
+        mhi = ((kw[3] >> 16) & 0xff) | ((kw[3] >> 24) << 8);
+    }
+    // zero keys never match (MACKey / Ipv4Key / Ipv6Key IsZero, ns_ctx.go:262-329)
+    if ((key == kMac || key == kEui) && mlo == 0 && mhi == 0) key = kNoClient;
+    if (key == kIp4 && kw[0] == 0) key = kNoClient;
+    if (key == kIp6 && (kw[0] | kw[1] | kw[2] | kw[3]) == 0) key = kNoClient;
+
+    // ---- issue the Namespace and client bucket reads together ----
+    const uint32_t tk = emurx_tk_hash(r.vport, r.vlan0, r.vlan1);  // CTunnelKey words
+    const uint32_t nb = tk & T.ns_mask;
+    const Bucket ne = ld_bucket(T.ns_tab, nb);
+    uint32_t cbk = 0;
+    Bucket ce{};
+    if (key == kMac || key == kEui) {
+        cbk = emurx_mac_hash(tk, mlo, mhi) & T.mac_mask;
+        ce = ld_bucket(T.mac_tab, cbk);
+    } else if (key == kIp4) {
+        cbk = emurx_ip4_hash(tk, kw[0]) & T.ip4_mask;
+        ce = ld_bucket(T.ip4_tab, cbk);
+    } else if (key == kIp6) {
+        cbk = emurx_ip6_hash(tk, kw[0], kw[1], kw[2], kw[3]) & T.ip6_mask;
+        ce = ld_bucket(T.ip6_tab, cbk);
+    }
+
+    // ---- GetNs + ns.PluginCtx.Get(plugin) ----
+    const uint2 nsr = resolve_ns(T, nb, ne, r.vport, r.vlan0, r.vlan1);
     const uint32_t ns = nsr.x;
     if (ns == EMURX_ID_NONE) { set_lk(r, EMURX_LK_NO_NS); return; }
     r.ns = ns;
-    uint32_t cb = r.proto, plug = kCbPlugin[cb];
     if (!(nsr.y & (1u << plug))) { set_lk(r, EMURX_LK_NS_NO_PLUGIN); return; }
-    uint32_t dlo = le32(s, 0), dhi = s.u8(4) | (s.u8(5) << 8);  // p[0:6]
-    bool bcast = dlo == 0xffffffffu && dhi == 0xffffu;
-    switch (cb) {
-    case EMURX_CB_ARP:  // arp.go:904-949
-        if (be16(s, r.l3 + 6) == 1) {
-            const uint32_t cid = probe_ip4(T, ns, le32(s, r.l3 + 24));
-            client_result(r, cid, client_plugins(T, cid), plug, true);
-        } else {
-            set_lk(r, EMURX_LK_NS_LEVEL);
-        }
-        return;
-    case EMURX_CB_ICMP: {  // icmp.go:396-427
-        uint32_t cid = probe_ip4(T, ns, le32(s, r.l3 + 16));
-        if (cid != EMURX_ID_NONE && !unicast_to_me(T, cid, dlo, dhi)) cid = EMURX_ID_NONE;
-        client_result(r, cid, 0, plug, false);
-        return;
-    }
-    case EMURX_CB_IGMP:
-    case EMURX_CB_MDNS:
+
+    // ---- the client rule ----
+    switch (key) {
+    case kNsLevel:
         set_lk(r, EMURX_LK_NS_LEVEL);
         return;
-    case EMURX_CB_DHCP: {  // dhcp.go:893-917
-        uint32_t lo = dlo, hi = dhi;
-        if (bcast && !dhcp_chaddr(s, len, r, lo, hi)) { set_lk(r, EMURX_LK_NO_CLIENT); return; }
-        const uint2 c = probe_mac(T, ns, lo, hi);
-        client_result(r, c.x, c.y, plug, true);
+    case kNoClient:
+        set_lk(r, EMURX_LK_NO_CLIENT);
+        return;
+    case kFirst: {
+        const uint32_t cid = T.ns_info[4 * ns + 1];
+        client_result(r, cid, client_plugins(T, cid), plug, true);
         return;
     }
-    case EMURX_CB_DHCPSRV:  // dhcpsrv.go:1798-1826: broadcast -> GetFirstClient
-    case EMURX_CB_EAPOL: {  // dot1x.go:624-650: 01:80:c2:00:00:03 -> GetFirstClient
-        const bool first = cb == EMURX_CB_DHCPSRV ? bcast : (dlo == 0x00c28001u && dhi == 0x0300u);
-        if (first) {
-            const uint32_t cid = T.ns_info[4 * ns + 1];
+    case kIp4: {
+        uint32_t cid = resolve_ip4(T, cbk, ce, ns, kw[0]);
+        if (cb == EMURX_CB_ARP) {
             client_result(r, cid, client_plugins(T, cid), plug, true);
-        } else {
-            const uint2 c = probe_mac(T, ns, dlo, dhi);
-            client_result(r, c.x, c.y, plug, true);
+        } else {  // icmp
+            if (cid != EMURX_ID_NONE && !unicast_to_me(T, cid, dlo, dhi)) cid = EMURX_ID_NONE;
+            client_result(r, cid, 0, plug, false);
         }
         return;
     }
-    case EMURX_CB_ICMPV6: {  // ipv6.go:465-540
-        if (be16(s, r.l4) != 0x8000u) { set_lk(r, EMURX_LK_NS_LEVEL); return; }
-        if (r.l3 + 40 > len) { set_lk(r, EMURX_LK_NO_CLIENT); return; }
-        uint32_t w[4] = {le32(s, r.l3 + 24), le32(s, r.l3 + 28), le32(s, r.l3 + 32), le32(s, r.l3 + 36)};
-        uint32_t cid = lookup_ip6_lg(T, ns, w);
+    case kEui:
+    case kIp6: {  // icmpv6 echo request
+        uint32_t cid;
+        if (key == kEui) {
+            cid = resolve_mac(T, cbk, ce, ns, mlo, mhi).x;
+            // CClient.IsValidPrefix client_ctx.go:279-295
+            if (cid != EMURX_ID_NONE && !(kw[0] == 0x000080feu && kw[1] == 0)) {
+                const uint32_t* c = T.client + 8 * cid;
+                const uint32_t ra = c[3];
+                if (!((ra & 1u) && ((ra >> 8) & 0xff) == 64 && c[4] == kw[0] && c[5] == kw[1])) cid = EMURX_ID_NONE;
+            }
+        } else {
+            cid = resolve_ip6(T, cbk, ce, ns, kw);
+        }
         if (cid != EMURX_ID_NONE && !unicast_to_me(T, cid, dlo, dhi)) cid = EMURX_ID_NONE;
         if (cid != EMURX_ID_NONE && s.u8(r.l3 + 8) == 0xff) cid = EMURX_ID_NONE;
         client_result(r, cid, 0, plug, false);
         return;
     }
-    default: {  // dhcpv6, ppp, tcp, udp: client = MAC[dst] (plugin_transport.go:83-115 ...)
-        const uint2 c = probe_mac(T, ns, dlo, dhi);
+    default: {  // kMac
+        const uint2 c = resolve_mac(T, cbk, ce, ns, mlo, mhi);
         client_result(r, c.x, c.y, plug, true);
         return;
     }

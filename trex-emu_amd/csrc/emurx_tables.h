@@ -6,10 +6,16 @@
 //   MapClientMAC  map[MACKey]*CClient      src/emu/core/ns_ctx.go:110-112  (per Namespace)
 //   MapClientIPv4 map[Ipv4Key]*CClient
 //   MapClientIPv6 map[Ipv6Key]*CClient     (static Ipv6 and Dhcpv6 addresses, ns_ctx.go:377-383)
-// as flat open-addressing arrays (linear probing, load factor <= 1/2, power-of-two size).
-// A per-Namespace client map becomes one global map keyed by (ns_id, key).  Every entry is
-// 16 B (IPv6: 32 B) so a probe is one 16-byte load; the tables are read-only during a
-// batch and sit in L2 / Infinity Cache (64K clients = 1 MiB MAC table).
+// as flat open-addressing arrays of 64-byte BUCKETS (one cache line; 4 slots of 16 B, IPv6:
+// 2 slots of 32 B), load factor <= 1/2, power-of-two bucket counts, linear probing over
+// buckets.  A lookup reads its home bucket with four 16-byte loads of one line and ends at
+// the first bucket that holds an empty slot.  Only exact-match semantics matter for parity
+// with the Go maps; the hash function is ours.
+//
+// The per-Namespace client maps become one global map per key kind, keyed by
+// (Namespace, address) and hashed from (CTunnelKey hash, address): a frame's client bucket
+// is known from its parsed tunnel key alone, so the Namespace and Client probes of one frame
+// are issued together (one memory round trip) and the Namespace id is compared afterwards.
 #pragma once
 #include <stdint.h>
 
@@ -22,6 +28,7 @@
 #endif
 
 #define EMURX_EMPTY 0xFFFFFFFFu
+#define EMURX_BUCKET_WORDS 16u  // 64 B
 
 // 32-bit mix of up to five key words (murmur3 finaliser over a multiplicative combine).
 EMURX_HD uint32_t emurx_fmix(uint32_t h) {
@@ -39,7 +46,7 @@ EMURX_HD uint32_t emurx_hash(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uin
     return emurx_fmix(h);
 }
 
-// Entry layouts (uint32 words):
+// Slot layouts (uint32 words; the last word of a slot is the value, EMURX_EMPTY = free):
 //  ns   [4]: vport | ns_plugins << 16, vlan0, vlan1, ns_id   (key = CTunnelKey as 3 LE words)
 //  mac  [4]: ns_id, mac[0..3] LE, mac[4..5] LE | client_plugins << 16, client_id
 //  ip4  [4]: ns_id, ipv4 bytes LE, 0, client_id
@@ -47,27 +54,29 @@ EMURX_HD uint32_t emurx_hash(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uin
 //  ns_info   [4]: plugin_mask, first_client, 0, 0
 //  client    [8]: mac_lo, mac_hi, plugin_mask, ra (bit0 has_ra, bits 8..15 prefix_len),
 //                 ra_prefix[0..3], ra_prefix[4..7], 0, 0
-EMURX_HD uint32_t emurx_ns_hash(uint32_t w0, uint32_t w1, uint32_t w2) {
+// Home buckets: ns = tk & ns_mask; client tables = hash(tk, address) & mask, where
+// tk = emurx_tk_hash(CTunnelKey words) of the client's Namespace.
+EMURX_HD uint32_t emurx_tk_hash(uint32_t w0, uint32_t w1, uint32_t w2) {
     return emurx_hash(w0, w1, w2, 0x6E73u, 0);
 }
-EMURX_HD uint32_t emurx_mac_hash(uint32_t ns, uint32_t lo, uint32_t hi) {
-    return emurx_hash(ns, lo, hi, 0x6D6163u, 0);
+EMURX_HD uint32_t emurx_mac_hash(uint32_t tk, uint32_t lo, uint32_t hi) {
+    return emurx_hash(tk, lo, hi, 0x6D6163u, 0);
 }
-EMURX_HD uint32_t emurx_ip4_hash(uint32_t ns, uint32_t ip) {
-    return emurx_hash(ns, ip, 0x697034u, 0, 0);
+EMURX_HD uint32_t emurx_ip4_hash(uint32_t tk, uint32_t ip) {
+    return emurx_hash(tk, ip, 0x697034u, 0, 0);
 }
-EMURX_HD uint32_t emurx_ip6_hash(uint32_t ns, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-    return emurx_hash(ns, a ^ 0x697036u, b, c, d);
+EMURX_HD uint32_t emurx_ip6_hash(uint32_t tk, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    return emurx_hash(tk, a ^ 0x697036u, b, c, d);
 }
 
 struct emurx_dev_tables {
-    const uint32_t* ns_tab;   // 4 words per slot
+    const uint32_t* ns_tab;   // [ns_mask + 1] buckets of 4 slots
     const uint32_t* ns_info;  // 4 words per ns id
-    const uint32_t* mac_tab;  // 4 words per slot
-    const uint32_t* ip4_tab;  // 4 words per slot
-    const uint32_t* ip6_tab;  // 8 words per slot
+    const uint32_t* mac_tab;  // [mac_mask + 1] buckets of 4 slots
+    const uint32_t* ip4_tab;  // [ip4_mask + 1] buckets of 4 slots
+    const uint32_t* ip6_tab;  // [ip6_mask + 1] buckets of 2 slots
     const uint32_t* client;   // 8 words per client id
-    uint32_t ns_mask, mac_mask, ip4_mask, ip6_mask;
+    uint32_t ns_mask, mac_mask, ip4_mask, ip6_mask;  // bucket count - 1
     uint32_t max_ns, max_clients;
     uint32_t cb_mask;         // registered callbacks (Parser.Register)
     uint32_t pad;
