@@ -39,6 +39,8 @@ def parse_args():
     ap.add_argument("--frames", type=int, default=1 << 20, help="frames per GPU per step")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--time-stride", type=int, default=4,
+                    help="record HIP events around every N-th launch of the timed region")
     ap.add_argument("--no-check", action="store_true",
                     help="skip the output sanity check (stage-ablation builds, tools/ablate.sh)")
     ap.add_argument("--host-path", action="store_true",
@@ -130,7 +132,7 @@ def main():
         _, qoff = pack_queues(qlist.cpu().numpy(), qcap, tile_cnt.cpu().numpy(), n)
         assert int(qoff[-1]) == n, "queues do not cover the batch"
 
-    rx.set_timing(a.steps + 8)
+    rx.set_timing(a.steps + 8, a.time_stride)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -196,6 +198,8 @@ def main():
             "alg_bytes_per_launch": alg_bytes,
             "kernel_ms_mean": round(parse_s * 1e3, 5),
             "kernel_launches_timed": int(len(pk)),
+            "kernel_time_source": f"HIP events on the launch stream around every {a.time_stride}-th "
+                                  "launch of the timed region",
         },
     }
     if a.host_path:

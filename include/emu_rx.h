@@ -283,8 +283,9 @@ int emurx_rx_stream(emurx_t* h, const uint8_t* msg, size_t len, emurx_rec* out_r
 /* Device-resident batch: frames (d_frames) and descriptors (d_desc) already in HBM.
    Enqueues parse+classify+compaction on `stream` (hipStream_t, NULL = handle stream) and
    returns without synchronising.  out->hist is accumulated into (zero it to reset).
-   n <= cfg.max_frames, out->qcap >= ceil(n / EMURX_QUEUE_TILE) * EMURX_QUEUE_TILE.  The
-   frame buffer must stay readable up to the next 64-byte boundary past its last byte
+   n <= cfg.max_frames, out->qcap >= ceil(n / EMURX_QUEUE_TILE) * EMURX_QUEUE_TILE.
+   d_frames must be 16-byte aligned and d_desc 8-byte aligned (EMURX_EINVAL otherwise), and
+   the frame buffer must stay readable up to the next 64-byte boundary past its last byte
    (frames are staged with 16-byte loads).  One kernel launch, no host synchronisation,
    no handle state touched on the device: capturable in a hipGraph. */
 int emurx_classify_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_desc,
@@ -308,11 +309,13 @@ void emurx_hist_to_counters(const uint64_t hist[2 * EMURX_HIST_BINS], emurx_coun
 void emurx_hist_fold(const uint64_t* shards, uint64_t out[2 * EMURX_HIST_BINS]);
 
 /* Kernel timing with HIP events recorded on the launch stream around every batch.
-   emurx_set_timing(h, slots): slots > 0 keeps the last `slots` batches (ring), 0 disables.
-   emurx_kernel_times(): waits for the most recent batch and returns the device time in ms
-   of every batch recorded since the previous call (oldest first, at most min(cap, slots));
+   emurx_set_timing(h, slots, stride): slots > 0 keeps the last `slots` timed batches (ring),
+   0 disables; every `stride`-th batch is timed (0 or 1 = every batch), so that a timed run
+   can keep most launches free of event markers.
+   emurx_kernel_times(): waits for the most recent timed batch and returns the device time in
+   ms of every batch timed since the previous call (oldest first, at most min(cap, slots));
    then resets the ring. */
-int emurx_set_timing(emurx_t* h, uint32_t slots);
+int emurx_set_timing(emurx_t* h, uint32_t slots, uint32_t stride);
 int emurx_kernel_times(emurx_t* h, float* batch_ms, uint32_t cap, uint32_t* n_out);
 
 #ifdef __cplusplus

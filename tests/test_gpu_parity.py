@@ -257,3 +257,17 @@ def test_configs(rxmod, cfg, n):
     if cfg == "config_b":
         assert (rec["status"] == 0).all() and (rec["proto"] == abi.CB_UDP).all()
         assert (rec["ns_id"] == 0).all() and (rec["client_id"] == 0).all()
+
+
+def test_kernel_timing_stride(rxmod):
+    """emurx_set_timing(slots, stride): every stride-th batch carries an event pair."""
+    rx, _ = new_pair(rxmod)
+    frames = [c[1] for c in E.cases()]
+    buf, desc = F.pack_frames(frames)
+    rx.set_timing(16, 2)
+    for _ in range(6):
+        run_dev(rx, buf, desc)
+    t = rx.kernel_times()
+    assert len(t) == 3 and (t > 0).all()
+    assert len(rx.kernel_times()) == 0
+    rx.set_timing(0)

@@ -143,7 +143,7 @@ struct emurx_ctx {
 
     // timing ring: 2 events per batch (around the k_rx launch)
     std::vector<hipEvent_t> ev;
-    uint32_t slots = 0, ev_head = 0, ev_count = 0;
+    uint32_t slots = 0, ev_head = 0, ev_count = 0, stride = 1, batch_seq = 0;
 
     emurx_dev_tables tables() const {
         emurx_dev_tables T{};
@@ -261,6 +261,7 @@ size_t queue_cap(uint32_t n) { return (size_t)ntiles(n) * EMURX_QUEUE_TILE; }
 int run_dev(emurx_t* h, const uint8_t* frames, const emurx_desc* desc, uint32_t n,
             const emurx_dev_out* out, void* stream, bool classify) {
     if (!h || !out || !out->hist || (n && (!frames || !desc))) return EMURX_EINVAL;
+    if (((uintptr_t)frames & 15) || ((uintptr_t)desc & 7)) return EMURX_EINVAL;  // 16-B staging loads
     if (n > h->cfg.max_frames) return EMURX_ENOMEM;
     if (out->qlist && out->qcap < queue_cap(n)) return EMURX_EINVAL;
     int rc = bind(h);
@@ -269,7 +270,7 @@ int run_dev(emurx_t* h, const uint8_t* frames, const emurx_desc* desc, uint32_t 
     if (classify && (rc = rebuild_and_upload(h, st))) return rc;
     emurx_dev_tables T = h->tables();
     const hipEvent_t* ev = nullptr;
-    if (h->slots) {
+    if (h->slots && (h->batch_seq++ % h->stride) == 0) {
         const uint32_t s = h->ev_head;
         ev = &h->ev[2 * s];
         h->ev_head = (s + 1) % h->slots;
@@ -670,7 +671,7 @@ void emurx_hist_fold(const uint64_t* shards, uint64_t out[2 * EMURX_HIST_BINS]) 
         for (int b = 0; b < 2 * EMURX_HIST_BINS; ++b) out[b] += shards[(size_t)s * 2 * EMURX_HIST_BINS + b];
 }
 
-int emurx_set_timing(emurx_t* h, uint32_t slots) {
+int emurx_set_timing(emurx_t* h, uint32_t slots, uint32_t stride) {
     if (!h) return EMURX_EINVAL;
     int rc = bind(h);
     if (rc) return rc;
@@ -682,7 +683,8 @@ int emurx_set_timing(emurx_t* h, uint32_t slots) {
     for (auto& e : h->ev)
         if (hipEventCreate(&e) != hipSuccess) { h->slots = 0; return EMURX_EDEVICE; }
     h->slots = slots;
-    h->ev_head = h->ev_count = 0;
+    h->stride = stride ? stride : 1;
+    h->ev_head = h->ev_count = h->batch_seq = 0;
     return EMURX_OK;
 }
 

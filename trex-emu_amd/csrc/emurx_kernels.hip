@@ -63,6 +63,14 @@ __global__ __launch_bounds__(kBlock) void k_rx(const uint8_t* __restrict__ frame
         for (uint32_t k = 0; k < 8; ++k)
             if (k * kWave < nvec) glds16(src + min(lane + k * kWave, nvec - 1), wslab + k * kWave);
         wait_vm0();
+    } else {  // too wide: each lane stages a 128-byte window of its own frame (headers)
+        const uintptr_t fa = (uintptr_t)(frames + off);
+        const uint4* src = reinterpret_cast<const uint4*>(fa & ~(uintptr_t)15);
+        const uint32_t nv = valid ? (uint32_t)(((fa & 15) + len + 15) >> 4) : 0;  // vectors of the frame
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k)
+            if (k < nv) glds16(src + k, wslab + k * kWave);
+        wait_vm0();
     }
     // each wave reads only its own slab: a wave-level barrier orders it
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -76,7 +84,9 @@ __global__ __launch_bounds__(kBlock) void k_rx(const uint8_t* __restrict__ frame
             parse_packet(s, len, vport, T.cb_mask, r);
             if (kClassify && !(EMURX_ABL & 2)) classify(s, len, T, r);
         } else {
-            GlbSrc s{frames + off};
+            const uint32_t head = (uint32_t)((uintptr_t)(frames + off) & 15);
+            WinSrc s{reinterpret_cast<const uint8_t*>(slab), slab, wv * kStage + lane * 16, head,
+                     min(8 * 16 - head, len), frames + off};
             parse_packet(s, len, vport, T.cb_mask, r);
             if (kClassify && !(EMURX_ABL & 2)) classify(s, len, T, r);
         }

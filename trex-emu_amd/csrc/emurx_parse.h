@@ -81,26 +81,60 @@ __device__ __forceinline__ bool csum_ok(uint32_t T, uint32_t a_start, uint32_t p
     uint32_t x = fold16(be_domain(T, a_start) + pcs);
     return (x == 0xffffu || x == 0u) && !(T == 0 && pcs == 0);
 }
-// sum over the bytes [a, a + n) of a dword array: head / body / tail masks, body unmasked
-template <class P>
-__device__ __forceinline__ uint32_t dword_sum(const P* w32, uint32_t a, uint32_t n) {
+// sum over the bytes [a, a + n) of a dword sequence w[k] (byte a at dword a >> 2):
+// head / body / tail masks, body unmasked
+template <class A>
+__device__ __forceinline__ uint32_t dword_sum(const A& w, uint32_t a, uint32_t n) {
     if (n == 0) return 0;
     const uint32_t e = a + n, k0 = a >> 2, k1 = (e - 1) >> 2;
     const uint32_t hm = 0xffffffffu << (8 * (a & 3));
     const uint32_t tm = 0xffffffffu >> (8 * ((0u - e) & 3));
-    const uint32_t w0 = w32[k0] & hm;
+    const uint32_t w0 = w[k0] & hm;
     if (k0 == k1) return sad16(w0 & tm, 0);
     uint32_t acc = sad16(w0, 0), k = k0 + 1;
     for (; k + 4 <= k1; k += 4) {
-        const uint32_t x0 = w32[k], x1 = w32[k + 1], x2 = w32[k + 2], x3 = w32[k + 3];
+        const uint32_t x0 = w[k], x1 = w[k + 1], x2 = w[k + 2], x3 = w[k + 3];
         acc = sad16(x3, sad16(x2, sad16(x1, sad16(x0, acc))));
     }
-    for (; k < k1; ++k) acc = sad16(w32[k], acc);
-    return sad16(w32[k1] & tm, acc);
+    for (; k < k1; ++k) acc = sad16(w[k], acc);
+    return sad16(w[k1] & tm, acc);
+}
+// bytes [lo, hi) of a 16-byte vector (indices may fall outside 0..16)
+__device__ __forceinline__ uint32_t keep(int lo, int hi, int d) {
+    const int a = lo - 4 * d, b = hi - 4 * d;
+    const uint32_t m1 = a <= 0 ? 0xffffffffu : (a >= 4 ? 0u : (0xffffffffu << (8 * a)));
+    const uint32_t m2 = b >= 4 ? 0xffffffffu : (b <= 0 ? 0u : (0xffffffffu >> (8 * (4 - b))));
+    return m1 & m2;
+}
+__device__ __forceinline__ uint32_t sad_vec(const uint4& x, uint32_t acc) {
+    return sad16(x.w, sad16(x.z, sad16(x.y, sad16(x.x, acc))));
+}
+__device__ __forceinline__ uint32_t sad_vec_masked(const uint4& x, int lo, int hi, uint32_t acc) {
+    return sad16(x.w & keep(lo, hi, 3), sad16(x.z & keep(lo, hi, 2),
+                 sad16(x.y & keep(lo, hi, 1), sad16(x.x & keep(lo, hi, 0), acc))));
+}
+// the same sum over global bytes p[0, n) with 16-byte loads, four in flight per step
+__device__ uint32_t glb_sum(const uint8_t* p, uint32_t n) {
+    if (n == 0) return 0;
+    const uintptr_t a = (uintptr_t)p, e = a + n;
+    const uint4* v = reinterpret_cast<const uint4*>(a & ~(uintptr_t)15);
+    const uint32_t nv = (uint32_t)((((e + 15) & ~(uintptr_t)15) - (a & ~(uintptr_t)15)) >> 4);
+    const int h = (int)(a & 15), t = 16 - (int)((0u - (uint32_t)e) & 15);  // keep [h, 16) / [0, t)
+    if (nv == 1) return sad_vec_masked(v[0], h, t, 0);
+    uint32_t acc = sad_vec_masked(v[0], h, 16, 0), k = 1;
+    for (; k + 4 <= nv - 1; k += 4) {
+        const uint4 x0 = v[k], x1 = v[k + 1], x2 = v[k + 2], x3 = v[k + 3];
+        acc = sad_vec(x3, sad_vec(x2, sad_vec(x1, sad_vec(x0, acc))));
+    }
+    for (; k < nv - 1; ++k) acc = sad_vec(v[k], acc);
+    return sad_vec_masked(v[nv - 1], 0, t, acc);
 }
 
 // ---------------------------------------------------------------------------------------
-// byte sources: the wave's LDS slab (fast path) or global memory (frames that do not fit)
+// byte sources.  LdsSrc: the wave's contiguous LDS copy of its frames (fast path).
+// WinSrc: waves whose frames do not fit the slab (IMIX, jumbo) — each lane holds a 128-byte
+// window of its own frame in LDS (headers), everything past it is read from global memory
+// (the checksum spans, with 16-byte loads).
 // ---------------------------------------------------------------------------------------
 struct LdsSrc {
     const uint8_t* b8;    // block LDS
@@ -110,12 +144,32 @@ struct LdsSrc {
     __device__ __forceinline__ uint32_t sum(uint32_t s, uint32_t n) const { return dword_sum(b32, base + s, n); }
     __device__ __forceinline__ uint32_t at(uint32_t s) const { return base + s; }
 };
-struct GlbSrc {
-    const uint8_t* f;  // frame byte 0 (global)
-    __device__ __forceinline__ uint32_t u8(uint32_t i) const { return f[i]; }
+// window layout: vector k of lane l at wave slab byte k * 1024 + l * 16 (LDS-DMA order)
+struct WinDw {
+    const uint32_t* p;  // slab dword of lane l's vector 0
+    __device__ __forceinline__ uint32_t operator[](uint32_t j) const { return p[((j >> 2) << 8) + (j & 3)]; }
+};
+struct WinSrc {
+    const uint8_t* b8;
+    const uint32_t* b32;
+    uint32_t wbase;     // LDS byte index of this lane's vector 0
+    uint32_t head;      // frame byte 0 within vector 0 (== global address mod 16)
+    uint32_t wlim;      // frame bytes [0, wlim) are in the window
+    const uint8_t* f;   // frame byte 0 (global)
+    __device__ __forceinline__ uint32_t u8(uint32_t i) const {
+        if (i < wlim) {
+            const uint32_t b = head + i;
+            return b8[wbase + ((b >> 4) << 10) + (b & 15)];
+        }
+        return f[i];
+    }
     __device__ __forceinline__ uint32_t sum(uint32_t s, uint32_t n) const {
-        const uintptr_t a = (uintptr_t)(f + s);
-        return dword_sum(reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3), (uint32_t)(a & 3), n);
+        const uint32_t e = s + n, m = min(e, wlim);
+        uint32_t acc = 0;
+        if (s < m) acc = dword_sum(WinDw{b32 + (wbase >> 2)}, head + s, m - s);
+        const uint32_t g = max(s, wlim);
+        if (e > g) acc += glb_sum(f + g, e - g);
+        return acc;
     }
     __device__ __forceinline__ uint32_t at(uint32_t s) const { return (uint32_t)(uintptr_t)(f + s); }
 };
@@ -185,7 +239,7 @@ __device__ bool ipv6_options(const S& s, uint32_t p0, int size, uint32_t& flags)
 
 // Parser.parsePacketL4 parser.go:583-724
 template <class S>
-__device__ void parse_l4(const S& s, uint32_t len, Rec& r, uint32_t nextHdr, uint32_t pcs,
+__device__ __forceinline__ void parse_l4(const S& s, uint32_t len, Rec& r, uint32_t nextHdr, uint32_t pcs,
                          uint32_t l4len, bool v6, uint32_t cb_mask) {
     r.nh = nextHdr;
     const uint32_t L4 = r.l4;
@@ -251,7 +305,7 @@ __device__ void parse_l4(const S& s, uint32_t len, Rec& r, uint32_t nextHdr, uin
 // 0xffff, and with the protocol term (never 0 where a pseudo header is used) never zero.
 // Parser.ParsePacket parser.go:756-959
 template <class S>
-__device__ void parse_packet(const S& s, uint32_t len, uint32_t vport, uint32_t cb_mask, Rec& r) {
+__device__ __forceinline__ void parse_packet(const S& s, uint32_t len, uint32_t vport, uint32_t cb_mask, Rec& r) {
     r.ns = EMURX_ID_NONE; r.cl = EMURX_ID_NONE;
     r.vlan0 = 0; r.vlan1 = 0; r.vport = vport;
     r.l3 = r.l4 = r.l7 = r.l7len = 0;
@@ -358,7 +412,7 @@ __device__ __forceinline__ Bucket ld_bucket(const uint32_t* tab, uint32_t b) {
 }
 
 // ns slot {vport | ns_plugins << 16, vlan0, vlan1, ns_id} -> (ns_id, ns plugin mask)
-__device__ uint2 resolve_ns(const emurx_dev_tables& T, uint32_t b, Bucket e, uint32_t w0, uint32_t w1,
+__device__ __forceinline__ uint2 resolve_ns(const emurx_dev_tables& T, uint32_t b, Bucket e, uint32_t w0, uint32_t w1,
                             uint32_t w2) {
     for (uint32_t n = 0;;) {
 #pragma unroll
@@ -373,7 +427,7 @@ __device__ uint2 resolve_ns(const emurx_dev_tables& T, uint32_t b, Bucket e, uin
     }
 }
 // mac slot {ns_id, mac[0..3], mac[4..5] | client_plugins << 16, client_id} -> (cid, plugins)
-__device__ uint2 resolve_mac(const emurx_dev_tables& T, uint32_t b, Bucket e, uint32_t ns, uint32_t lo,
+__device__ __forceinline__ uint2 resolve_mac(const emurx_dev_tables& T, uint32_t b, Bucket e, uint32_t ns, uint32_t lo,
                              uint32_t hi) {
     for (uint32_t n = 0;;) {
 #pragma unroll
@@ -388,7 +442,7 @@ __device__ uint2 resolve_mac(const emurx_dev_tables& T, uint32_t b, Bucket e, ui
     }
 }
 // ip4 slot {ns_id, ip, 0, client_id}
-__device__ uint32_t resolve_ip4(const emurx_dev_tables& T, uint32_t b, Bucket e, uint32_t ns, uint32_t ip) {
+__device__ __forceinline__ uint32_t resolve_ip4(const emurx_dev_tables& T, uint32_t b, Bucket e, uint32_t ns, uint32_t ip) {
     for (uint32_t n = 0;;) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -402,7 +456,7 @@ __device__ uint32_t resolve_ip4(const emurx_dev_tables& T, uint32_t b, Bucket e,
     }
 }
 // ip6 slot {ns_id, ip[0..3], ip[4..7], ip[8..11]} {ip[12..15], 0, 0, client_id}, 2 per bucket
-__device__ uint32_t resolve_ip6(const emurx_dev_tables& T, uint32_t b, Bucket e, uint32_t ns, const uint32_t w[4]) {
+__device__ __forceinline__ uint32_t resolve_ip6(const emurx_dev_tables& T, uint32_t b, Bucket e, uint32_t ns, const uint32_t w[4]) {
     for (uint32_t n = 0;;) {
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
@@ -498,7 +552,7 @@ enum Key : uint32_t {
 };
 
 template <class S>
-__device__ void classify(const S& s, uint32_t len, const emurx_dev_tables& T, Rec& r) {
+__device__ __forceinline__ void classify(const S& s, uint32_t len, const emurx_dev_tables& T, Rec& r) {
     if (r.status != EMURX_ST_OK) return;
     const uint32_t cb = r.proto, plug = kCbPlugin[cb];
     const uint32_t dlo = le32(s, 0), dhi = s.u8(4) | (s.u8(5) << 8);  // p[0:6]

@@ -134,7 +134,7 @@ SIGNATURES = [
                                         C.POINTER(C.c_uint32), C.POINTER(C.c_int)]),
     ("emurx_hist_to_counters", None, [_P, C.POINTER(Counters)]),
     ("emurx_hist_fold", None, [_P, _P]),
-    ("emurx_set_timing", C.c_int, [_P, C.c_uint32]),
+    ("emurx_set_timing", C.c_int, [_P, C.c_uint32, C.c_uint32]),
     ("emurx_kernel_times", C.c_int, [_P, _P, C.c_uint32, C.POINTER(C.c_uint32)]),
 ]
 

@@ -136,8 +136,9 @@ class RxPath:
         return abi.check(fn(self.h, _addr(frames), _addr(desc), n, C.byref(out),
                             _stream(stream)), "classify_dev")
 
-    def set_timing(self, slots: int = 1024):
-        return abi.check(self.lib.emurx_set_timing(self.h, slots), "set_timing")
+    def set_timing(self, slots: int = 1024, stride: int = 1):
+        """Time every `stride`-th batch with HIP events (0 slots disables)."""
+        return abi.check(self.lib.emurx_set_timing(self.h, slots, stride), "set_timing")
 
     def kernel_times(self, cap: int = 1 << 16):
         """Device ms of every batch launched since the previous call (HIP events recorded on
