@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Benchmark: Mpkt/s of device-resident rx parse+classify (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config B|C|E] [--frames F]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config B|C|D|E] [--frames F]
+                    [--exchange] [--backend nccl|gloo]
 
 A step = one batch through the hot path: emurx_classify_dev = one k_rx launch (decode +
 checksums + Namespace/Client lookups + 32-B records + stable per-callback queue segments +
@@ -10,6 +11,11 @@ outcome histogram) over F frames already resident in HBM.  Default workload = co
 quoted on.  For N > 1 (torchrun, one rank per GPU) every rank processes its own F-frame
 shard against replicated tables: frames are independent, so there is no data-path
 collective (weak scaling); value = frames over all ranks / max-over-ranks time.
+
+--exchange (default for config D: 2M frames per GPU, 32K Namespaces / 1M Clients) adds the
+Namespace-partitioned exchange to every step: emurx_route_dev packs the records whose
+Namespace was found into the owners' regions and an equal-split all-to-all (RCCL over
+xGMI) delivers them, with the per-region counts in a second all-to-all.
 
 The JSON line carries `roofline` (algorithmic bytes per frame = frame_len + 8 B descriptor
 + 32 B record + 4 B queue entry, over k_rx's mean HIP-event duration on the launch stream) and
@@ -35,8 +41,13 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="B", choices=["B", "C", "E"])
-    ap.add_argument("--frames", type=int, default=1 << 20, help="frames per GPU per step")
+    ap.add_argument("--config", default="B", choices=["B", "C", "D", "E"])
+    ap.add_argument("--frames", type=int, default=None,
+                    help="frames per GPU per step (default 1M; config D: 2M = 16M over 8 GPUs)")
+    ap.add_argument("--exchange", action="store_true",
+                    help="route records to their Namespace owners each step (default for D)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: rehearse the multi-rank path with ranks sharing a GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--time-stride", type=int, default=4,
@@ -54,6 +65,8 @@ def workload(cfg, n, rank):
         return synth.config_b(n, seed=synth.SEED_B + rank)
     if cfg == "C":
         return synth.config_c(n, rank=rank)
+    if cfg == "D":
+        return synth.config_d(n, rank=rank)
     return synth.config_e(n, rank=rank)
 
 
@@ -92,9 +105,16 @@ def main():
     import numpy as np
     import torch
     import torch.distributed as dist
+    if a.frames is None:
+        a.frames = (1 << 21) if a.config == "D" else (1 << 20)
+    a.exchange = a.exchange or a.config == "D"
+    local = local % max(torch.cuda.device_count(), 1)  # gloo rehearsal: ranks may share a GPU
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     from emurx import abi
     from emurx.rx import RxPath
 
@@ -118,8 +138,30 @@ def main():
     stream = torch.cuda.current_stream(dev)
     rx.sync(stream.cuda_stream)
 
+    xch = None
+    if a.exchange:
+        from emurx import exchange as X
+        cap = X.capacity(n, world)
+        send = torch.empty(world * cap * X.REC_BYTES, dtype=torch.uint8, device=dev)
+        send_count = torch.zeros(world, dtype=torch.int32, device=dev)
+        xch = dict(cap=cap, recv=None, recv_count=None, ev=[], timing=False, k=0)
+
     def step():
         rx.classify_dev(buf, desc, n, rec, qlist, qcap, tile_cnt, hist, stream=stream)
+        if xch is not None:
+            ev = None
+            if xch["timing"] and xch["k"] % a.time_stride == 0:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record(stream)
+            xch["k"] += 1
+            rx.route_dev(rec, n, world, rank, xch["cap"], send, send_count, stream=stream)
+            if world > 1:
+                xch["recv"], xch["recv_count"] = X.exchange(send, send_count, xch["cap"])
+            else:
+                xch["recv"], xch["recv_count"] = send, send_count
+            if ev is not None:
+                ev[1].record(stream)
+                xch["ev"].append(ev)
 
     for _ in range(a.warmup):
         step()
@@ -131,8 +173,12 @@ def main():
         assert int(h[0::2].sum()) == n * a.warmup, "histogram does not cover the batches"
         _, qoff = pack_queues(qlist.cpu().numpy(), qcap, tile_cnt.cpu().numpy(), n)
         assert int(qoff[-1]) == n, "queues do not cover the batch"
+        if xch is not None:
+            xcheck(xch, rec, n, world, rank, dist, torch, dev)
 
     rx.set_timing(a.steps + 8, a.time_stride)
+    if xch is not None:
+        xch["timing"] = True
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -147,7 +193,7 @@ def main():
     rx.set_timing(0)
 
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        t = torch.tensor([el], dtype=torch.float64, device=dev if a.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     total_frames = n * a.steps * world
@@ -181,11 +227,14 @@ def main():
         "data": "synthetic (seeded, valid wire-format frames)",
         "config": {
             "workload": {"B": "B: 1M x 64B untagged IPv4/UDP, 1 ns / 1 client",
+                         "D": "D: 2M mixed dot1q/QinQ IPv4/IPv6 per GPU (16M over 8), 32K ns / 1M clients",
                          "C": "C: 1M mixed dot1q/QinQ IPv4/IPv6, 4K ns / 64K clients",
                          "E": "E: IMIX 64/594/1518 TCP/UDP, 4K ns / 64K clients"}[a.config],
             "frames_per_gpu": n,
             "frame_bytes_per_gpu": w["nbytes"],
-            "parallelism": f"frame shards x{world}, replicated tables, no collective",
+            "parallelism": (f"frame shards x{world}, replicated tables, Namespace-owner all-to-all "
+                            f"({a.backend})" if a.exchange else
+                            f"frame shards x{world}, replicated tables, no collective"),
         },
         "roofline": {
             "bound": "hbm",
@@ -202,6 +251,15 @@ def main():
                                   "launch of the timed region",
         },
     }
+    if xch is not None:
+        xm = [e0.elapsed_time(e1) for e0, e1 in xch["ev"]]
+        out["exchange"] = {
+            "route_plus_all_to_all_ms_mean": round(float(np.mean(xm)), 5) if xm else None,
+            "steps_timed": len(xm),
+            "records_per_region_cap": xch["cap"],
+            "record_bytes": 40,
+            "collective": f"all_to_all_single x2 ({a.backend})" if world > 1 else "none (1 rank)",
+        }
     if a.host_path:
         out["host_inclusive"] = host_path_rate(rx, w)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -211,6 +269,21 @@ def main():
     rx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def xcheck(xch, rec, n, world, rank, dist, torch, dev):
+    """Exchange sanity (counts only; the packing is parity-tested in tests/): every routed
+    record arrives once, within capacity."""
+    import numpy as np
+    cnt = xch["recv_count"].cpu().numpy().astype(np.int64)
+    assert (cnt <= xch["cap"]).all(), f"exchange overflow {cnt} > {xch['cap']}"
+    r = rec.cpu().numpy().view(np.dtype([("ns", "<u4"), ("rest", "V28")]))
+    routed = torch.tensor([int((r["ns"] != 0xFFFFFFFF).sum()), int(cnt.sum())], dtype=torch.int64)
+    if world > 1:
+        routed = routed.to(dev) if dist.get_backend() == "nccl" else routed
+        dist.all_reduce(routed)
+    routed = routed.cpu().numpy()
+    assert routed[0] == routed[1], f"sent {routed[0]} != received {routed[1]}"
 
 
 def host_path_rate(rx, w, msgs=200):

@@ -318,6 +318,30 @@ void emurx_hist_fold(const uint64_t* shards, uint64_t out[2 * EMURX_HIST_BINS]);
 int emurx_set_timing(emurx_t* h, uint32_t slots, uint32_t stride);
 int emurx_kernel_times(emurx_t* h, float* batch_ms, uint32_t cap, uint32_t* n_out);
 
+/* ---- Namespace-partitioned exchange (multi-GPU, one process per GPU) -------------------
+   Frames shard by input offset across the GPUs of a node; each Namespace is owned by one
+   partition, emurx_ns_owner(key) = a hash of its CTunnelKey (thread_ctx.go:92-97) mapped
+   onto [0, n_parts).  After a batch is classified, emurx_route_dev packs every record whose
+   Namespace was found (ns_id != EMURX_ID_NONE) into the send region of its owner:
+       send[d * cap .. d * cap + send_count[d])   in frame order, as emurx_route_rec
+   An equal-split all-to-all (RCCL over xGMI; n_parts regions of `cap` records) then delivers
+   each record to the GPU that owns its Namespace, with send_count exchanged alongside so the
+   receiver knows how many of each region are valid.  send_count[d] > cap means the region
+   overflowed (records past cap were not written): the caller must raise cap and resend.
+   Records without a Namespace stay with the receiving GPU (they are in its counters). */
+#define EMURX_MAX_PARTS 8
+typedef struct emurx_route_rec {
+    emurx_rec rec;       /* the classified record                                        */
+    uint32_t src_index;  /* frame index in the source GPU's batch                        */
+    uint32_t src_rank;   /* source partition                                             */
+} emurx_route_rec;       /* 40 bytes */
+
+uint32_t emurx_ns_owner(const uint8_t key[12], uint32_t n_parts);
+/* d_rec: the batch's records (device), n frames; d_send: [n_parts * cap] (device);
+   d_send_count: [n_parts] (device).  Three kernel launches on `stream`, no host sync. */
+int emurx_route_dev(emurx_t* h, const emurx_rec* d_rec, uint32_t n, uint32_t n_parts, uint32_t my_rank,
+                    uint32_t cap, emurx_route_rec* d_send, uint32_t* d_send_count, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -23,6 +23,16 @@ def oracle_built():
 
 
 @pytest.fixture(scope="session")
+def lib():
+    """libemurx.so loaded (built first if missing); loading touches no GPU."""
+    from emurx import abi
+    if not abi.LIB_PATH.exists():
+        import subprocess
+        subprocess.run(["make", "-s", "-C", str(abi.PKG_ROOT)], check=True)
+    return abi.load()
+
+
+@pytest.fixture(scope="session")
 def gpu_ok():
     import torch
     if not torch.cuda.is_available():

@@ -21,14 +21,6 @@ def declared_functions():
     return sorted(set(re.findall(r"\b(emurx_[a-z0-9_]+)\s*\(", txt)) - {"emurx_desc", "emurx_rec"})
 
 
-@pytest.fixture(scope="module")
-def lib():
-    if not abi.LIB_PATH.exists():
-        import subprocess
-        subprocess.run(["make", "-s", "-C", str(abi.PKG_ROOT)], check=True)
-    return abi.load()
-
-
 def test_exports_every_declared_symbol(lib):
     names = declared_functions()
     assert len(names) >= 20

@@ -271,3 +271,57 @@ def test_kernel_timing_stride(rxmod):
     assert len(t) == 3 and (t > 0).all()
     assert len(rx.kernel_times()) == 0
     rx.set_timing(0)
+
+
+# ---- Namespace-partitioned exchange: device packing (emurx_route_dev) ---------------------
+@pytest.mark.parametrize("n_parts,my_rank", [(1, 0), (2, 1), (3, 2), (8, 5)])
+def test_route_dev(rxmod, n_parts, my_rank):
+    """Send regions packed on the device == the host restatement, over config C records
+    (unknown Namespaces stay local); includes a batch size that is not a tile multiple."""
+    import torch
+    import route_ref
+    from emurx import exchange as X
+    n = 20000 + 77
+    w = synth.config_c(n, rank=my_rank)
+    rx, o = new_pair(rxmod)
+    synth.load_tables(w, rx)
+    synth.load_tables(w, o)
+    orec, _, _, _ = o.rx_batch(w["buf"], w["desc"])
+    rec = torch.from_numpy(orec.view(np.uint8).copy()).cuda()
+    cap = X.capacity(n, n_parts)
+    send = torch.full((n_parts * cap * X.REC_BYTES,), 0xEE, dtype=torch.uint8, device="cuda")
+    cnt = torch.full((n_parts,), -1, dtype=torch.int32, device="cuda")
+    rx.route_dev(rec, n, n_parts, my_rank, cap, send, cnt)
+    torch.cuda.synchronize()
+    got_cnt = cnt.cpu().numpy()
+    s = send.cpu().numpy().view(abi.ROUTE_REC_DTYPE).reshape(n_parts, cap)
+    want = route_ref.route(orec, n_parts, my_rank)
+    assert list(got_cnt) == [len(x) for x in want]
+    for d in range(n_parts):
+        assert s[d, : got_cnt[d]].tobytes() == want[d].tobytes(), d
+    assert sum(got_cnt) == int((orec["ns_id"] != abi.ID_NONE).sum())
+
+
+def test_route_dev_overflow(rxmod):
+    """A region smaller than its records: the count reports the true total, nothing is
+    written past the region."""
+    import torch
+    import route_ref
+    n = 5000
+    w = synth.config_c(n)
+    rx, o = new_pair(rxmod)
+    synth.load_tables(w, o)
+    orec, _, _, _ = o.rx_batch(w["buf"], w["desc"])
+    rec = torch.from_numpy(orec.view(np.uint8).copy()).cuda()
+    cap = 1000
+    send = torch.full((2 * cap * 40 + 4096,), 0xEE, dtype=torch.uint8, device="cuda")
+    cnt = torch.zeros(2, dtype=torch.int32, device="cuda")
+    rx.route_dev(rec, n, 2, 0, cap, send, cnt)
+    torch.cuda.synchronize()
+    want = route_ref.route(orec, 2, 0)
+    assert list(cnt.cpu().numpy()) == [len(x) for x in want] and min(len(x) for x in want) > cap
+    s = send.cpu().numpy()
+    assert (s[2 * cap * 40:] == 0xEE).all()
+    r = s[: 2 * cap * 40].view(abi.ROUTE_REC_DTYPE).reshape(2, cap)
+    for d in range(2):
+        assert r[d].tobytes() == want[d][:cap].tobytes()

@@ -31,6 +31,12 @@ for what in "${@:-all}"; do
   prof|all)
     run prof_B 600 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof_B -o run --output-format csv \
         -- python bench.py --steps 50 --warmup 5 --no-cpu-baseline; stop_on_fault $? ;;&
+  exchange)
+    run bench_D1 900 python bench.py --config D --steps 50 --warmup 5 --no-cpu-baseline; stop_on_fault $?
+    run bench_D2_gloo 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port 29533 bench.py --gpus 2 --config D --backend gloo --frames 262144 --steps 10 --warmup 2; stop_on_fault $?
+    run bench_B2_gloo 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port 29534 bench.py --gpus 2 --backend gloo --steps 20 --warmup 2; stop_on_fault $? ;;
   pmc)
     for c in FETCH_SIZE WRITE_SIZE; do
       run pmc_$c 600 rocprofv3 --pmc $c -T -d gpurun_out/pmc_$c -o run --output-format csv \

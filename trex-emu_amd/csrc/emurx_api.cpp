@@ -141,6 +141,9 @@ struct emurx_ctx {
     DevBuf<uint32_t> d_qlist, d_tile_cnt;
     DevBuf<uint64_t> d_hist;
 
+    // Namespace-partition packing scratch (emurx_route_dev)
+    DevBuf<uint32_t> d_route_cnt, d_route_off;
+
     // timing ring: 2 events per batch (around the k_rx launch)
     std::vector<hipEvent_t> ev;
     uint32_t slots = 0, ev_head = 0, ev_count = 0, stride = 1, batch_seq = 0;
@@ -338,6 +341,7 @@ void emurx_close(emurx_t* h) {
     h->h_hist.release();
     h->d_msg.release(); h->d_desc.release(); h->d_rec.release(); h->d_qlist.release();
     h->d_tile_cnt.release(); h->d_hist.release();
+    h->d_route_cnt.release(); h->d_route_off.release();
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
     h->ev.clear();
@@ -706,6 +710,29 @@ int emurx_kernel_times(emurx_t* h, float* batch_ms, uint32_t cap, uint32_t* n_ou
     *n_out = n;
     h->ev_count = 0;
     return EMURX_OK;
+}
+
+uint32_t emurx_ns_owner(const uint8_t key[12], uint32_t n_parts) {
+    if (!key || n_parts == 0) return 0;
+    return emurx_owner(emurx_tk_hash(le32(key), le32(key + 4), le32(key + 8)), n_parts);
+}
+
+int emurx_route_dev(emurx_t* h, const emurx_rec* d_rec, uint32_t n, uint32_t n_parts, uint32_t my_rank,
+                    uint32_t cap, emurx_route_rec* d_send, uint32_t* d_send_count, void* stream) {
+    if (!h || !d_send_count || n_parts == 0 || n_parts > EMURX_MAX_PARTS || my_rank >= n_parts ||
+        (n && (!d_rec || !d_send || cap == 0)))
+        return EMURX_EINVAL;
+    if (((uintptr_t)d_rec & 15) || ((uintptr_t)d_send & 7)) return EMURX_EINVAL;
+    int rc = bind(h);
+    if (rc) return rc;
+    const size_t tiles = ((size_t)n + EMURX_QUEUE_TILE - 1) / EMURX_QUEUE_TILE;
+    if (h->d_route_cnt.alloc(std::max<size_t>(tiles, 1) * 16) || h->d_route_off.alloc(std::max<size_t>(tiles, 1) * 16))
+        return EMURX_ENOMEM;
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    return emurx_launch_route(d_rec, n, n_parts, my_rank, cap, d_send, d_send_count, h->d_route_cnt.p,
+                              h->d_route_off.p, st)
+               ? EMURX_EDEVICE
+               : EMURX_OK;
 }
 
 }  // extern "C"

@@ -81,3 +81,9 @@ struct emurx_dev_tables {
     uint32_t cb_mask;         // registered callbacks (Parser.Register)
     uint32_t pad;
 };
+
+// Namespace partition of a tunnel-key hash among n_parts GPUs (multiply-high: uniform for a
+// well-mixed hash, no division)
+EMURX_HD uint32_t emurx_owner(uint32_t tk, uint32_t n_parts) {
+    return (uint32_t)(((uint64_t)tk * n_parts) >> 32);
+}

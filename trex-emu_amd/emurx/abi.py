@@ -69,6 +69,9 @@ REC_DTYPE = np.dtype([
     ("vport", "<u2"), ("l3", "<u2"), ("l4", "<u2"), ("l7", "<u2"), ("l7_len", "<u2"),
     ("next_hdr", "u1"), ("proto", "u1"), ("status", "u1"), ("flags", "u1"), ("rsv", "<u2")])
 assert REC_DTYPE.itemsize == 32
+ROUTE_REC_DTYPE = np.dtype([("rec", REC_DTYPE), ("src_index", "<u4"), ("src_rank", "<u4")])
+assert ROUTE_REC_DTYPE.itemsize == 40
+MAX_PARTS = 8
 DESC_DTYPE = np.dtype([("off", "<u4"), ("len", "<u2"), ("vport", "u1"), ("pad", "u1")])
 assert DESC_DTYPE.itemsize == 8
 
@@ -136,6 +139,8 @@ SIGNATURES = [
     ("emurx_hist_fold", None, [_P, _P]),
     ("emurx_set_timing", C.c_int, [_P, C.c_uint32, C.c_uint32]),
     ("emurx_kernel_times", C.c_int, [_P, _P, C.c_uint32, C.POINTER(C.c_uint32)]),
+    ("emurx_ns_owner", C.c_uint32, [_U8P, C.c_uint32]),
+    ("emurx_route_dev", C.c_int, [_P, _P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P]),
 ]
 
 _lib = None

@@ -149,6 +149,21 @@ class RxPath:
         return a[: n.value]
 
 
+    # ---- Namespace-partitioned exchange ---------------------------------------------------
+    def route_dev(self, rec, n: int, n_parts: int, my_rank: int, cap: int, send, send_count, stream=None):
+        """Pack the batch's records with a Namespace into their owners' send regions
+        (send[d*cap:][:send_count[d]], frame order; include/emu_rx.h emurx_route_dev)."""
+        return abi.check(self.lib.emurx_route_dev(self.h, _addr(rec), n, n_parts, my_rank, cap, _addr(send),
+                                                  _addr(send_count), _stream(stream)), "route_dev")
+
+
+def ns_owner(key: bytes, n_parts: int) -> int:
+    """Partition (GPU) owning the Namespace with this 12-byte CTunnelKey."""
+    k = np.frombuffer(bytes(key), np.uint8).copy()
+    assert k.size == 12
+    return int(abi.load().emurx_ns_owner(_p(k), n_parts))
+
+
 def _addr(x):
     if x is None:
         return None
