@@ -46,6 +46,8 @@ def parse_args():
                     help="frames per GPU per step (default 1M; config D: 2M = 16M over 8 GPUs)")
     ap.add_argument("--exchange", action="store_true",
                     help="route records to their Namespace owners each step (default for D)")
+    ap.add_argument("--no-exchange-run", action="store_true",
+                    help="at N > 1, skip the extra config-D Namespace-exchange measurement")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the multi-rank path with ranks sharing a GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
@@ -115,11 +117,36 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group("gloo")
+    out, rx, w = measure(a, a.config, a.frames, a.exchange, a.steps, a.warmup, rank, world, local, dist, torch)
+    if world > 1 and a.config == "B" and not a.no_exchange_run:
+        # evidence for the Namespace-owner all-to-all at N > 1: config D
+        # shards with the exchange in every step; the headline value stays config B's
+        try:
+            rx.close()
+            xo, rx, _ = measure(a, "D", 1 << 21, True, max(10, a.steps // 4), max(2, a.warmup // 4),
+                                rank, world, local, dist, torch)
+            out["namespace_exchange"] = {k: xo[k] for k in ("value", "unit", "ms_per_step", "steps", "config",
+                                                              "exchange")}
+            out["namespace_exchange"]["k_rx_ms_mean"] = xo["roofline"]["kernel_ms_mean"]
+        except Exception as e:  # noqa: BLE001 - report, keep the headline line
+            out["namespace_exchange"] = {"error": repr(e)[:300]}
+    if a.host_path:
+        out["host_inclusive"] = host_path_rate(rx, w)
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(w, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    rx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def measure(a, cfg, n, exchange, steps, warmup, rank, world, local, dist, torch):
+    """Run `steps` timed batches of workload `cfg` (n frames per rank) -> (JSON dict, rx, w)."""
+    import numpy as np
     from emurx import abi
     from emurx.rx import RxPath
-
-    n = a.frames
-    w = workload(a.config, n, rank)
+    w = workload(cfg, n, rank)
     max_ns = max(4096, len(w["ns"]))
     max_cl = max(65536, len(w["clients"]["cid"]))
     rx = RxPath(local, max_ns=max_ns, max_clients=max_cl, max_frames=n)
@@ -139,7 +166,7 @@ def main():
     rx.sync(stream.cuda_stream)
 
     xch = None
-    if a.exchange:
+    if exchange:
         from emurx import exchange as X
         cap = X.capacity(n, world)
         send = torch.empty(world * cap * X.REC_BYTES, dtype=torch.uint8, device=dev)
@@ -163,27 +190,27 @@ def main():
                 ev[1].record(stream)
                 xch["ev"].append(ev)
 
-    for _ in range(a.warmup):
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize()
     # sanity of the outcome on this rank (counts only; parity lives in tests/)
     if not a.no_check:
         from emurx.rx import hist_fold, pack_queues
         h = hist_fold(hist.cpu().numpy().view(np.uint64))
-        assert int(h[0::2].sum()) == n * a.warmup, "histogram does not cover the batches"
+        assert int(h[0::2].sum()) == n * warmup, "histogram does not cover the batches"
         _, qoff = pack_queues(qlist.cpu().numpy(), qcap, tile_cnt.cpu().numpy(), n)
         assert int(qoff[-1]) == n, "queues do not cover the batch"
         if xch is not None:
             xcheck(xch, rec, n, world, rank, dist, torch, dev)
 
-    rx.set_timing(a.steps + 8, a.time_stride)
+    rx.set_timing(steps + 8, a.time_stride)
     if xch is not None:
         xch["timing"] = True
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    for _ in range(steps):
         step()
     torch.cuda.synchronize()
     if world > 1:
@@ -196,16 +223,16 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device=dev if a.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    total_frames = n * a.steps * world
+    total_frames = n * steps * world
     value = total_frames / el / 1e6
-    ms_per_step = el / a.steps * 1e3
+    ms_per_step = el / steps * 1e3
 
     # roofline of the dominant kernel (k_rx): algorithmic bytes / its mean HIP-event duration
     alg_bytes = w["nbytes"] + 8 * n + 32 * n + 4 * n
     parse_s = float(np.mean(pk)) * 1e-3 if len(pk) else float("nan")
     achieved = alg_bytes / parse_s / 1e9
     traffic = None
-    pmc = ROOT / "profiles" / f"pmc_config{a.config}.json"
+    pmc = ROOT / "profiles" / f"pmc_config{cfg}.json"
     if pmc.exists():
         try:
             traffic = json.loads(pmc.read_text()).get("k_rx_hbm_bytes_per_launch")
@@ -217,8 +244,8 @@ def main():
         "value": round(value, 2),
         "unit": "Mpkt/s",
         "n_gpus": world,
-        "steps": a.steps,
-        "warmup": a.warmup,
+        "steps": steps,
+        "warmup": warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
         "scaling": "weak",
@@ -229,11 +256,11 @@ def main():
             "workload": {"B": "B: 1M x 64B untagged IPv4/UDP, 1 ns / 1 client",
                          "D": "D: 2M mixed dot1q/QinQ IPv4/IPv6 per GPU (16M over 8), 32K ns / 1M clients",
                          "C": "C: 1M mixed dot1q/QinQ IPv4/IPv6, 4K ns / 64K clients",
-                         "E": "E: IMIX 64/594/1518 TCP/UDP, 4K ns / 64K clients"}[a.config],
+                         "E": "E: IMIX 64/594/1518 TCP/UDP, 4K ns / 64K clients"}[cfg],
             "frames_per_gpu": n,
             "frame_bytes_per_gpu": w["nbytes"],
             "parallelism": (f"frame shards x{world}, replicated tables, Namespace-owner all-to-all "
-                            f"({a.backend})" if a.exchange else
+                            f"({a.backend})" if exchange else
                             f"frame shards x{world}, replicated tables, no collective"),
         },
         "roofline": {
@@ -260,15 +287,7 @@ def main():
             "record_bytes": 40,
             "collective": f"all_to_all_single x2 ({a.backend})" if world > 1 else "none (1 rank)",
         }
-    if a.host_path:
-        out["host_inclusive"] = host_path_rate(rx, w)
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(w, a.cpu_seconds)
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    rx.close()
-    if world > 1:
-        dist.destroy_process_group()
+    return out, rx, w
 
 
 def xcheck(xch, rec, n, world, rank, dist, torch, dev):

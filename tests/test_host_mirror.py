@@ -1,0 +1,43 @@
+"""The reference's parser tests (parser_test.go) over the C++ host mirror
+(trex-emu_amd/host/emu_core.*) and the HIP path behind the C-ABI."""
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+BIN = ROOT / "trex-emu_amd" / "build" / "test_parser"
+KAT = ROOT / "tests" / "golden" / "kat_frames.bin"
+
+
+def _build():
+    subprocess.run(["make", "-s", "-C", str(ROOT / "trex-emu_amd")], check=True)
+
+
+def test_host_mirror_builds():
+    _build()
+    assert BIN.exists() and KAT.exists()
+
+
+@pytest.mark.gpu
+def test_parser_go_tests_on_gpu(gpu_ok):
+    _build()
+    r = subprocess.run([str(BIN), str(KAT)], capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    for name in ("TestParserArp1", "TestParserIcmp", "TestParserDhcp1", "TestParserDhcpInvalidCs",
+                 "TestNsClientLookup", "TestOnRxStream"):
+        assert f"PASS {name}" in r.stdout
+
+
+def test_kat_fixture_is_current():
+    """tests/golden/kat_frames.bin == what tests/golden/make_kat_frames.py writes now."""
+    import struct
+    import sys
+    sys.path.insert(0, str(ROOT / "tests" / "golden"))
+    import make_kat_frames as M
+    b = bytearray(struct.pack("<I", len(M.frames())))
+    for name, f, vp in M.frames():
+        n = name.encode()
+        b += struct.pack("<H", len(n)) + n + struct.pack("<HI", vp, len(f)) + bytes(f)
+    assert KAT.read_bytes() == bytes(b)

@@ -37,6 +37,12 @@ for what in "${@:-all}"; do
         --master-port 29533 bench.py --gpus 2 --config D --backend gloo --frames 262144 --steps 10 --warmup 2; stop_on_fault $?
     run bench_B2_gloo 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
         --master-port 29534 bench.py --gpus 2 --backend gloo --steps 20 --warmup 2; stop_on_fault $? ;;
+  rehearse)
+    run bench_B2x_gloo 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port 29535 bench.py --gpus 2 --backend gloo --steps 20 --warmup 2; stop_on_fault $? ;;&
+  profD)
+    run prof_D 900 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof_D -o run --output-format csv \
+        -- python bench.py --config D --steps 20 --warmup 3 --no-cpu-baseline; stop_on_fault $? ;;
   pmc)
     for c in FETCH_SIZE WRITE_SIZE; do
       run pmc_$c 600 rocprofv3 --pmc $c -T -d gpurun_out/pmc_$c -o run --output-format csv \

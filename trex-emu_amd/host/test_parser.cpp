@@ -1,0 +1,270 @@
+// test_parser.cpp — the reference's parser tests (src/emu/core/parser_test.go), restated over
+// the C++ host mirror (emu_core.h) and therefore over the HIP path behind the C-ABI.
+// Frames: tests/golden/kat_frames.bin (rebuilt byte-for-byte from the Go tests by
+// tests/golden/make_kat_frames.py).  Needs a GPU; run by tests/test_host_mirror.py.
+//
+//   test_parser <kat_frames.bin>      exit 0 and "PASS <name>" per test
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <functional>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "emu_core.h"
+
+using namespace emu;
+
+namespace {
+
+struct Kat {
+    uint16_t vport;
+    std::vector<uint8_t> data;
+};
+std::map<std::string, Kat> g_kat;
+
+void load(const char* path) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) throw std::runtime_error(std::string("cannot open ") + path);
+    auto rd = [&](void* p, size_t n) {
+        if (!f.read((char*)p, n)) throw std::runtime_error("short fixture");
+    };
+    uint32_t count;
+    rd(&count, 4);
+    for (uint32_t i = 0; i < count; ++i) {
+        uint16_t nl;
+        rd(&nl, 2);
+        std::string name(nl, '\0');
+        rd(&name[0], nl);
+        Kat k;
+        uint32_t len;
+        rd(&k.vport, 2);
+        rd(&len, 4);
+        k.data.resize(len);
+        rd(k.data.data(), len);
+        g_kat[name] = k;
+    }
+}
+
+Mbuf frame(const std::string& name) {
+    const Kat& k = g_kat.at(name);
+    Mbuf m;
+    m.Append(k.data);
+    m.SetVPort(k.vport);
+    return m;
+}
+
+struct Fatal : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+#define FATALF(...)                                     \
+    do {                                                \
+        char b_[256];                                   \
+        snprintf(b_, sizeof b_, __VA_ARGS__);           \
+        throw Fatal(b_);                                \
+    } while (0)
+
+// parser_test.go:14-33
+int arp = 0;
+CTunnelKey lastTun;
+uint16_t lastL3, lastL4, lastL7;
+uint32_t lastNs, lastClient;
+uint8_t lastLookup;
+int arpSupported(ParserPacketState* ps) {
+    arp++;
+    lastL3 = ps->L3;
+    lastL4 = ps->L4;
+    lastL7 = ps->L7;
+    lastTun = *ps->Tun;
+    lastNs = ps->NsId;
+    lastClient = ps->ClientId;
+    lastLookup = ps->Lookup;
+    return -1;
+}
+
+CTunnelKey tunOf(uint16_t vport, uint32_t v0, uint32_t v1) {
+    CTunnelData d;
+    d.Vport = vport;
+    d.Vlans[0] = v0;
+    d.Vlans[1] = v1;
+    CTunnelKey k;
+    k.Set(d);
+    return k;
+}
+
+// ---- parser_test.go ---------------------------------------------------------------------
+void TestParserDot1Q_PPP() {  // :35-75
+    CThreadCtx tctx;
+    Parser parser;
+    parser.Init(&tctx);
+    Mbuf m1 = frame("test_parser_dot1q_ppp");
+    if (parser.ParsePacket(&m1) != PARSER_ERR) FATALF("ppp is parserNotSupported after Init");
+}
+
+void TestParser_PPP() {  // :77-112
+    CThreadCtx tctx;
+    Parser parser;
+    parser.Init(&tctx);
+    Mbuf m1 = frame("test_parser_ppp");
+    if (parser.ParsePacket(&m1) != PARSER_ERR) FATALF("ppp is parserNotSupported after Init");
+}
+
+void TestParserArp() {  // :114-171
+    CThreadCtx tctx;
+    Parser parser;
+    parser.tctx = &tctx;
+    parser.arp = arpSupported;
+    Mbuf m1 = frame("test_parser_arp");
+    arp = 0;
+    parser.ParsePacket(&m1);
+    if (arp != 0) FATALF(" arp cb should not be called (three tags)");
+    if (parser.stats.get("errToManyDot1q") != 1) FATALF(" errToManyDot1q should be 1 ");
+}
+
+void TestParserArp1() {  // :173-234
+    CThreadCtx tctx;
+    Parser parser;
+    parser.tctx = &tctx;
+    parser.arp = arpSupported;
+    Mbuf m1 = frame("test_parser_arp1");
+    arp = 0;
+    parser.ParsePacket(&m1);
+    if (arp != 1) FATALF(" arp cb should be called ");
+    if (lastTun != tunOf(7, 0x81000007, 0x81000fff)) FATALF(" ERROR expected last tun is not right %s", lastTun.String().c_str());
+}
+
+void TestParserIcmp() {  // :236-303
+    CThreadCtx tctx;
+    Parser parser;
+    parser.tctx = &tctx;
+    parser.icmp = arpSupported;
+    Mbuf m1 = frame("test_parser_icmp");
+    arp = 0;
+    parser.ParsePacket(&m1);
+    if (arp != 1) FATALF(" cb should be called ");
+    if (lastTun != tunOf(7, 0x81000007, 0x81000fff)) FATALF(" ERROR expected last tun is not right ");
+    if (lastL3 != 22 || lastL4 != 42 || lastL7 != 50) FATALF(" ERROR expected [22 42 50] != [%u %u %u] ", lastL3, lastL4, lastL7);
+}
+
+void TestParserDhcp1() {  // :305-388
+    CThreadCtx tctx;
+    Parser parser;
+    parser.tctx = &tctx;
+    parser.dhcp = arpSupported;
+    Mbuf m1 = frame("test_parser_dhcp1");
+    arp = 0;
+    parser.ParsePacket(&m1);
+    if (arp != 1) FATALF(" cb should be called ");
+    if (lastTun != tunOf(7, 0x81000007, 0x81000001)) FATALF(" ERROR expected last tun is not right ");
+    if (lastL3 != 22 || lastL4 != 42 || lastL7 != 50) FATALF(" ERROR expected [22 42 50] != [%u %u %u] ", lastL3, lastL4, lastL7);
+}
+
+void TestParserDhcpInvalidCs() {  // :390-454
+    CThreadCtx tctx;
+    Parser parser;
+    parser.tctx = &tctx;
+    parser.dhcp = arpSupported;
+    Mbuf m1 = frame("test_parser_dhcp_invalid_cs");
+    arp = 0;
+    parser.ParsePacket(&m1);
+    if (parser.stats.get("errIPv4cs") != 1) FATALF(" ipv4 checksum should be wrong ");
+}
+
+void TestParserIpv6Option() {  // :465-491 (the Go test asserts nothing; SURVEY.md §8c: RA flag, L4 66, bad csum)
+    CThreadCtx tctx;
+    Parser parser;
+    parser.tctx = &tctx;
+    parser.icmpv6 = arpSupported;
+    Mbuf m1 = frame("test_parser_ipv6_option");
+    arp = 0;
+    parser.ParsePacket(&m1);
+    if (arp != 0 || parser.stats.get("errIcmpv6Cse") != 1) FATALF(" icmpv6 checksum of the capture is wrong ");
+}
+
+// ---- beyond parser_test.go: the lookups and the batch entry point -----------------------
+void TestNsClientLookup() {  // GetNs + CLookupByIPv4 + IsUnicastToMe (icmp.go:396-427)
+    CThreadCtx tctx;
+    Parser parser;
+    parser.tctx = &tctx;
+    parser.icmp = arpSupported;
+    const int ns = tctx.AddNs(tunOf(7, 0x81000007, 0x81000fff));
+    const uint8_t mac[6] = {0, 2, 2, 2, 2, 2}, ip[4] = {48, 0, 0, 1};
+    const int cid = tctx.AddClient((uint32_t)ns, mac, ip);
+    if (ns < 0 || cid < 0) FATALF(" AddNs / AddClient failed %d %d", ns, cid);
+    Mbuf m1 = frame("test_parser_icmp");
+    arp = 0;
+    parser.ParsePacket(&m1);
+    if (arp != 1 || lastNs != (uint32_t)ns || lastClient != (uint32_t)cid || lastLookup != EMURX_LK_CLIENT)
+        FATALF(" lookup ns %u client %u lk %u ", lastNs, lastClient, lastLookup);
+    // the namespace gone: GetNs == nil
+    if (tctx.RemoveNs(tunOf(7, 0x81000007, 0x81000fff)) != EMURX_OK) FATALF(" RemoveNs ");
+    parser.ParsePacket(&m1);
+    if (lastNs != EMURX_ID_NONE || lastLookup != EMURX_LK_NO_NS) FATALF(" removed ns still found ");
+}
+
+void TestOnRxStream() {  // veth_zmq.go:277-320 + HandleRxPacket, callbacks in frame order
+    CThreadCtx tctx;
+    tctx.parser.Init(&tctx);
+    std::vector<std::string> order;
+    tctx.parser.icmp = [&](ParserPacketState* ps) { order.push_back("icmp"); return arpSupported(ps); };
+    tctx.parser.dhcp = [&](ParserPacketState* ps) { order.push_back("dhcp"); return 0; };
+    tctx.parser.arp = [&](ParserPacketState*) { order.push_back("arp"); return -2; };
+    const char* names[] = {"test_parser_icmp", "test_parser_arp1", "test_parser_dhcp1", "test_parser_arp",
+                           "test_parser_dhcp_invalid_cs", "test_parser_ppp", "test_parser_icmp"};
+    std::vector<std::vector<uint8_t>> fr;
+    std::vector<uint16_t> vp;
+    uint64_t bytes = 0;
+    for (const char* n : names) {
+        fr.push_back(g_kat.at(n).data);
+        vp.push_back(g_kat.at(n).vport);
+        bytes += g_kat.at(n).data.size();
+    }
+    tctx.veth.OnRxStream(ZmqPack(fr, vp));
+    const std::vector<std::string> want = {"icmp", "arp", "dhcp", "icmp"};
+    if (order != want) FATALF(" callback order ");
+    const VethStats& s = tctx.veth.stats;
+    if (s.RxBatch != 1 || s.RxPkts != 7 || s.RxBytes != bytes || s.RxParseErr != 0) FATALF(" veth stats ");
+    const ParserStats& p = tctx.parser.stats;
+    // errParser: 2 icmp callbacks returning -1, the too-many-dot1q and bad-csum frames, the
+    // ppp frame (parserNotSupported); errInternalHandler: the arp callback's -2
+    if (p.get("errParser") != 5 || p.get("errInternalHandler") != 1) FATALF(" errParser %lu errInternalHandler %lu",
+        (unsigned long)p.get("errParser"), (unsigned long)p.get("errInternalHandler"));
+    if (p.get("icmpPkts") != 2 || p.get("errToManyDot1q") != 1 || p.get("errIPv4cs") != 1) FATALF(" counters ");
+    // a truncated message: RxParseErr, the walk stops (veth_zmq.go:296-312)
+    std::vector<uint8_t> bad = ZmqPack(fr, vp);
+    bad.resize(bad.size() - 5);
+    order.clear();
+    tctx.veth.OnRxStream(bad);
+    if (tctx.veth.stats.RxParseErr != 1 || order.size() != 3) FATALF(" truncated message ");
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc < 2) {
+        fprintf(stderr, "usage: %s kat_frames.bin\n", argv[0]);
+        return 2;
+    }
+    load(argv[1]);
+    const std::vector<std::pair<const char*, std::function<void()>>> tests = {
+        {"TestParserDot1Q_PPP", TestParserDot1Q_PPP}, {"TestParser_PPP", TestParser_PPP},
+        {"TestParserArp", TestParserArp},             {"TestParserArp1", TestParserArp1},
+        {"TestParserIcmp", TestParserIcmp},           {"TestParserDhcp1", TestParserDhcp1},
+        {"TestParserDhcpInvalidCs", TestParserDhcpInvalidCs},
+        {"TestParserIpv6Option", TestParserIpv6Option}, {"TestNsClientLookup", TestNsClientLookup},
+        {"TestOnRxStream", TestOnRxStream}};
+    int failed = 0;
+    for (auto& t : tests) {
+        try {
+            t.second();
+            printf("PASS %s\n", t.first);
+        } catch (const std::exception& e) {
+            printf("FAIL %s: %s\n", t.first, e.what());
+            failed++;
+        }
+    }
+    printf("%s: %zu tests, %d failed\n", failed ? "FAIL" : "ok", tests.size(), failed);
+    return failed ? 1 : 0;
+}
