@@ -142,7 +142,7 @@ struct emurx_ctx {
     DevBuf<uint64_t> d_hist;
 
     // Namespace-partition packing scratch (emurx_route_dev)
-    DevBuf<uint32_t> d_route_cnt, d_route_off;
+    DevBuf<uint32_t> d_route_cnt, d_route_grp, d_route_goff;  // grp: zero between batches
 
     // timing ring: 2 events per batch (around the k_rx launch)
     std::vector<hipEvent_t> ev;
@@ -341,7 +341,7 @@ void emurx_close(emurx_t* h) {
     h->h_hist.release();
     h->d_msg.release(); h->d_desc.release(); h->d_rec.release(); h->d_qlist.release();
     h->d_tile_cnt.release(); h->d_hist.release();
-    h->d_route_cnt.release(); h->d_route_off.release();
+    h->d_route_cnt.release(); h->d_route_grp.release(); h->d_route_goff.release();
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
     h->ev.clear();
@@ -726,11 +726,16 @@ int emurx_route_dev(emurx_t* h, const emurx_rec* d_rec, uint32_t n, uint32_t n_p
     int rc = bind(h);
     if (rc) return rc;
     const size_t tiles = ((size_t)n + EMURX_QUEUE_TILE - 1) / EMURX_QUEUE_TILE;
-    if (h->d_route_cnt.alloc(std::max<size_t>(tiles, 1) * 16) || h->d_route_off.alloc(std::max<size_t>(tiles, 1) * 16))
-        return EMURX_ENOMEM;
+    if (tiles > 1024u * 64u) return EMURX_EINVAL;  // 16M frames per batch
+    const size_t gw = 1024 * 16;
+    if (!h->d_route_grp.p) {
+        if (h->d_route_grp.alloc(gw) || hipMemset(h->d_route_grp.p, 0, gw * sizeof(uint32_t)) != hipSuccess)
+            return EMURX_ENOMEM;
+    }
+    if (h->d_route_cnt.alloc(std::max<size_t>(tiles, 1) * 16) || h->d_route_goff.alloc(gw)) return EMURX_ENOMEM;
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
     return emurx_launch_route(d_rec, n, n_parts, my_rank, cap, d_send, d_send_count, h->d_route_cnt.p,
-                              h->d_route_off.p, st)
+                              h->d_route_grp.p, h->d_route_goff.p, st)
                ? EMURX_EDEVICE
                : EMURX_OK;
 }

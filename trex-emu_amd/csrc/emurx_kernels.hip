@@ -78,18 +78,22 @@ __global__ __launch_bounds__(kBlock) void k_rx(const uint8_t* __restrict__ frame
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
     Rec r;
-    if (valid) {
-        if (staged) {
+    r.dlen = 0;
+    if (staged) {  // wave-uniform branch
+        if (valid) {
             LdsSrc s{reinterpret_cast<const uint8_t*>(slab), slab, wv * kStage + (off - start)};
             parse_packet(s, len, vport, T.cb_mask, r);
             if (kClassify && !(EMURX_ABL & 2)) classify(s, len, T, r);
-        } else {
-            const uint32_t head = (uint32_t)((uintptr_t)(frames + off) & 15);
-            WinSrc s{reinterpret_cast<const uint8_t*>(slab), slab, wv * kStage + lane * 16, head,
-                     min(8 * 16 - head, len), frames + off};
-            parse_packet(s, len, vport, T.cb_mask, r);
-            if (kClassify && !(EMURX_ABL & 2)) classify(s, len, T, r);
         }
+    } else {
+        const uint32_t head = (uint32_t)((uintptr_t)(frames + off) & 15);
+        WinSrc s{reinterpret_cast<const uint8_t*>(slab), slab, wv * kStage + lane * 16, head,
+                 min(8 * 16 - head, len), frames + off};
+        if (valid) parse_packet(s, len, vport, T.cb_mask, r);
+        coop_checksum(r, frames + off);  // the wave's long L4 spans, converged
+        if (valid && kClassify && !(EMURX_ABL & 2)) classify(s, len, T, r);
+    }
+    if (valid) {
         if (rec && !(EMURX_ABL & 16)) {
             uint4* o = reinterpret_cast<uint4*>(rec + i);
             o[0] = make_uint4(r.ns, r.cl, r.vlan0, r.vlan1);

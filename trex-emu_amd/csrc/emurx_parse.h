@@ -23,6 +23,17 @@ constexpr uint32_t kStage = 8192;  // LDS bytes staged per wave (64 frames)
 #define EMURX_ABL 0  // experiment-only stage ablation (tools/ablate.sh); 0 in every real build
 #endif
 
+// loads through the global address space (global_load_*): pointers rebuilt from integers or
+// kept in a struct would otherwise compile to flat loads, which also count on lgkmcnt and
+// make the compiler serialise them with LDS traffic
+typedef unsigned emurx_v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 gld16(const void* p) {
+    const emurx_v4u v = *(const __attribute__((address_space(1))) emurx_v4u*)p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint32_t gld4(const void* p) { return *(const __attribute__((address_space(1))) uint32_t*)p; }
+__device__ __forceinline__ uint32_t gld1(const void* p) { return *(const __attribute__((address_space(1))) uint8_t*)p; }
+
 // ---------------------------------------------------------------------------------------
 // wave helpers
 // ---------------------------------------------------------------------------------------
@@ -114,20 +125,21 @@ __device__ __forceinline__ uint32_t sad_vec_masked(const uint4& x, int lo, int h
                  sad16(x.y & keep(lo, hi, 1), sad16(x.x & keep(lo, hi, 0), acc))));
 }
 // the same sum over global bytes p[0, n) with 16-byte loads, four in flight per step
-__device__ uint32_t glb_sum(const uint8_t* p, uint32_t n) {
+__device__ __forceinline__ uint32_t glb_sum(const uint8_t* p, uint32_t n) {
     if (n == 0) return 0;
     const uintptr_t a = (uintptr_t)p, e = a + n;
-    const uint4* v = reinterpret_cast<const uint4*>(a & ~(uintptr_t)15);
+    const uint8_t* v = reinterpret_cast<const uint8_t*>(a & ~(uintptr_t)15);
     const uint32_t nv = (uint32_t)((((e + 15) & ~(uintptr_t)15) - (a & ~(uintptr_t)15)) >> 4);
     const int h = (int)(a & 15), t = 16 - (int)((0u - (uint32_t)e) & 15);  // keep [h, 16) / [0, t)
-    if (nv == 1) return sad_vec_masked(v[0], h, t, 0);
-    uint32_t acc = sad_vec_masked(v[0], h, 16, 0), k = 1;
+    if (nv == 1) return sad_vec_masked(gld16(v), h, t, 0);
+    uint32_t acc = sad_vec_masked(gld16(v), h, 16, 0), k = 1;
     for (; k + 4 <= nv - 1; k += 4) {
-        const uint4 x0 = v[k], x1 = v[k + 1], x2 = v[k + 2], x3 = v[k + 3];
+        const uint4 x0 = gld16(v + 16 * k), x1 = gld16(v + 16 * (k + 1)), x2 = gld16(v + 16 * (k + 2)),
+                    x3 = gld16(v + 16 * (k + 3));
         acc = sad_vec(x3, sad_vec(x2, sad_vec(x1, sad_vec(x0, acc))));
     }
-    for (; k < nv - 1; ++k) acc = sad_vec(v[k], acc);
-    return sad_vec_masked(v[nv - 1], 0, t, acc);
+    for (; k < nv - 1; ++k) acc = sad_vec(gld16(v + 16 * k), acc);
+    return sad_vec_masked(gld16(v + 16 * (nv - 1)), 0, t, acc);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -161,7 +173,7 @@ struct WinSrc {
             const uint32_t b = head + i;
             return b8[wbase + ((b >> 4) << 10) + (b & 15)];
         }
-        return f[i];
+        return gld1(f + i);
     }
     __device__ __forceinline__ uint32_t sum(uint32_t s, uint32_t n) const {
         const uint32_t e = s + n, m = min(e, wlim);
@@ -203,6 +215,9 @@ struct Rec {
     uint32_t ns, cl, vlan0, vlan1;
     uint32_t vport, l3, l4, l7, l7len;
     uint32_t nh, proto, status, flags;
+    // L4 checksum deferred to the wave-cooperative pass (WinSrc spans past the window):
+    // bytes [dstart, dstart + dlen) with pseudo sum dpcs; on failure the outcome becomes dfail
+    uint32_t dstart, dlen, dpcs, dfail;
 };
 
 __device__ __forceinline__ void invoke(Rec& r, uint32_t cb, uint32_t cb_mask) {
@@ -215,6 +230,24 @@ __device__ __forceinline__ void fail(Rec& r, uint32_t st) { r.status = st; r.pro
 
 __device__ __forceinline__ bool span_ok(uint32_t l4, uint32_t l4len) {
     return ((l4 + l4len) & 0xffffu) >= l4;  // Go slice p[L4:L4+l4len] with uint16 end
+}
+
+// the L4 checksum of parsePacketL4.  LdsSrc: now.  WinSrc: now when the span lies in the
+// lane's window, else deferred to coop_checksum() (the caller proceeds as if it passed; the
+// cooperative pass applies `fail_st` afterwards, see settle_deferred)
+template <class S>
+__device__ __forceinline__ bool csum_l4(const S& s, Rec& r, uint32_t at, uint32_t n, uint32_t pcs, uint32_t fail_st) {
+    return csum(s, at, n, pcs);
+}
+template <>
+__device__ __forceinline__ bool csum_l4<WinSrc>(const WinSrc& s, Rec& r, uint32_t at, uint32_t n, uint32_t pcs,
+                                                uint32_t fail_st) {
+    if (at + n <= s.wlim || n == 0) return csum(s, at, n, pcs);
+    r.dstart = at;
+    r.dlen = n;
+    r.dpcs = pcs;
+    r.dfail = fail_st;
+    return true;
 }
 
 // processIpv6Options parser.go:726-746; false on Go's out-of-range p[i+1]
@@ -247,7 +280,7 @@ __device__ __forceinline__ void parse_l4(const S& s, uint32_t len, Rec& r, uint3
     case 1:  // ICMPv4
         if (len < ((L4 + 8) & 0xffff)) { fail(r, EMURX_ST_ICMPV4_TOO_SHORT); return; }
         if (!span_ok(L4, l4len)) { fail(r, EMURX_ST_PANIC_L4LEN); return; }
-        if (!csum(s, L4, l4len, 0)) { fail(r, EMURX_ST_ICMPV4_CS); return; }
+        if (!csum_l4(s, r, L4, l4len, 0, EMURX_ST_ICMPV4_CS)) { fail(r, EMURX_ST_ICMPV4_CS); return; }
         r.l7 = (L4 + 8) & 0xffff;
         invoke(r, EMURX_CB_ICMP, cb_mask);
         return;
@@ -263,7 +296,7 @@ __device__ __forceinline__ void parse_l4(const S& s, uint32_t len, Rec& r, uint3
         r.l7 = (L4 + tcplen) & 0xffff;
         r.l7len = (l4len - tcplen) & 0xffff;
         if (!span_ok(L4, l4len)) { fail(r, EMURX_ST_PANIC_L4LEN); return; }
-        if (!csum(s, L4, l4len, pcs)) { fail(r, EMURX_ST_TCP_CS); return; }
+        if (!csum_l4(s, r, L4, l4len, pcs, EMURX_ST_TCP_CS)) { fail(r, EMURX_ST_TCP_CS); return; }
         invoke(r, EMURX_CB_TCP, cb_mask);
         return;
     }
@@ -272,7 +305,7 @@ __device__ __forceinline__ void parse_l4(const S& s, uint32_t len, Rec& r, uint3
         r.l7len = (l4len - 8) & 0xffff;
         if (be16(s, L4 + 6) > 0) {
             if (!span_ok(L4, l4len)) { fail(r, EMURX_ST_PANIC_L4LEN); return; }
-            if (!csum(s, L4, l4len, pcs)) { fail(r, EMURX_ST_UDP_CS); return; }
+            if (!csum_l4(s, r, L4, l4len, pcs, EMURX_ST_UDP_CS)) { fail(r, EMURX_ST_UDP_CS); return; }
         }
         r.l7 = (L4 + 8) & 0xffff;
         uint32_t src = be16(s, L4), dst = be16(s, L4 + 2);
@@ -287,7 +320,7 @@ __device__ __forceinline__ void parse_l4(const S& s, uint32_t len, Rec& r, uint3
     case 58: {  // ICMPv6
         if (len < ((L4 + 4) & 0xffff)) { fail(r, EMURX_ST_ICMPV6_TOO_SHORT); return; }
         if (!span_ok(L4, l4len)) { fail(r, EMURX_ST_PANIC_L4LEN); return; }
-        if (!csum(s, L4, l4len, pcs)) { fail(r, EMURX_ST_ICMPV6_CS); return; }
+        if (!csum_l4(s, r, L4, l4len, pcs, EMURX_ST_ICMPV6_CS)) { fail(r, EMURX_ST_ICMPV6_CS); return; }
         uint32_t t = s.u8(L4);
         bool okt = (t >= 1 && t <= 4) || (t >= 128 && t <= 136);
         if (okt) invoke(r, EMURX_CB_ICMPV6, cb_mask);
@@ -310,6 +343,7 @@ __device__ __forceinline__ void parse_packet(const S& s, uint32_t len, uint32_t 
     r.vlan0 = 0; r.vlan1 = 0; r.vport = vport;
     r.l3 = r.l4 = r.l7 = r.l7len = 0;
     r.nh = 0; r.proto = EMURX_CB_NONE; r.status = EMURX_ST_OK; r.flags = 0;
+    r.dlen = 0;
     if (len < 14) { fail(r, EMURX_ST_PACKET_TOO_SHORT); return; }
     uint32_t offset = 14;
     uint32_t nextHdr = be16(s, 12);
@@ -398,6 +432,82 @@ __device__ __forceinline__ void parse_packet(const S& s, uint32_t len, uint32_t 
 }
 
 // ---------------------------------------------------------------------------------------
+// Wave-cooperative L4 checksums for the WinSrc path (long spans, IMIX / jumbo frames): the
+// 64 lanes stream one frame's span at a time with coalesced 16-byte loads, eight frames in
+// flight, and reduce it on the DPP network; the owner lane settles its outcome.  Replaces
+// a per-lane serial walk of up to ~90 dependent loads.  Called with the wave converged.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+    return wave_reduce(v, [](uint32_t x, uint32_t y) { return x + y; });
+}
+__device__ __forceinline__ void settle_deferred(Rec& r, bool ok) {
+    if (ok) return;
+    const uint32_t st = r.dfail;
+    if (st == EMURX_ST_ICMPV4_CS || st == EMURX_ST_UDP_CS) r.l7 = 0;  // Go sets L7 after the check
+    fail(r, st);
+}
+// lane-indexed vector k of a span of nv vectors (bytes [h, t) of the first / last): the load
+// is clamped in bounds and issued unconditionally, the contribution masked afterwards
+__device__ __forceinline__ uint4 span_load(const uint8_t* v, uint32_t nv, uint32_t k) {
+    return gld16(v + 16 * min(k, nv - 1));
+}
+__device__ __forceinline__ uint32_t span_sum(const uint4& x, uint32_t nv, int h, int t, uint32_t k) {
+    if (k >= nv) return 0;
+    return sad_vec_masked(x, k == 0 ? h : 0, k == nv - 1 ? t : 16, 0);
+}
+__device__ __forceinline__ void coop_checksum(Rec& r, const uint8_t* f) {
+    const uint32_t lane = lane_id();
+    const uintptr_t my = (uintptr_t)(f + r.dstart);
+    uint64_t pend = __ballot(r.dlen != 0);
+    while (pend) {
+        constexpr int kB = 8;  // frames in flight
+        uint32_t J[kB], nv[kB];
+        int h[kB], t[kB];
+        const uint8_t* base[kB];
+        uint4 xa[kB], xb[kB];
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {  // wave-uniform: frame, span geometry (scalar registers)
+            J[k] = pend ? (uint32_t)__ffsll((long long)pend) - 1 : 64u;
+            if (pend) pend &= pend - 1;
+            nv[k] = 0;
+            base[k] = f;
+            h[k] = 0;
+            t[k] = 16;
+            if (J[k] < 64) {
+                const uint32_t alo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)my, (int)J[k]);
+                const uint32_t ahi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(my >> 32), (int)J[k]);
+                const uint32_t n = (uint32_t)__builtin_amdgcn_readlane((int)r.dlen, (int)J[k]);
+                const uintptr_t a = ((uintptr_t)ahi << 32) | alo, e = a + n;
+                base[k] = reinterpret_cast<const uint8_t*>(a & ~(uintptr_t)15);
+                nv[k] = (uint32_t)((((e + 15) & ~(uintptr_t)15) - (a & ~(uintptr_t)15)) >> 4);
+                h[k] = (int)(a & 15);
+                t[k] = 16 - (int)((0u - (uint32_t)e) & 15);
+            }
+        }
+        // every frame's first two vectors per lane in flight before the first use
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+            if (nv[k]) {
+                xa[k] = span_load(base[k], nv[k], lane);
+                xb[k] = span_load(base[k], nv[k], lane + 64);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+            if (J[k] >= 64) continue;
+            uint32_t acc = span_sum(xa[k], nv[k], h[k], t[k], lane) + span_sum(xb[k], nv[k], h[k], t[k], lane + 64);
+            for (uint32_t v = 128; v < nv[k]; v += 64)  // spans past 2 KiB (jumbo frames)
+                acc += span_sum(span_load(base[k], nv[k], v + lane), nv[k], h[k], t[k], v + lane);
+            const uint32_t T = wave_sum_u32(acc);
+            if (lane == J[k]) {
+                settle_deferred(r, csum_ok(T, (uint32_t)my, r.dpcs));
+                r.dlen = 0;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
 // Namespace / Client lookups (GetNs thread_ctx.go:777-784, CLookupBy* ns_ctx.go:262-329)
 // over the bucketed tables of emurx_tables.h.  A frame's Namespace bucket and its client
 // bucket both follow from the parsed tunnel key, so classify() issues the two 64-byte
@@ -407,8 +517,8 @@ struct Bucket {
     uint4 s[4];
 };
 __device__ __forceinline__ Bucket ld_bucket(const uint32_t* tab, uint32_t b) {
-    const uint4* p = reinterpret_cast<const uint4*>(tab + (size_t)b * EMURX_BUCKET_WORDS);
-    return Bucket{{p[0], p[1], p[2], p[3]}};
+    const uint32_t* p = tab + (size_t)b * EMURX_BUCKET_WORDS;
+    return Bucket{{gld16(p), gld16(p + 4), gld16(p + 8), gld16(p + 12)}};
 }
 
 // ns slot {vport | ns_plugins << 16, vlan0, vlan1, ns_id} -> (ns_id, ns plugin mask)
@@ -482,12 +592,12 @@ __device__ __forceinline__ void client_result(Rec& r, uint32_t cid, uint32_t cpl
     set_lk(r, EMURX_LK_CLIENT);
 }
 __device__ __forceinline__ uint32_t client_plugins(const emurx_dev_tables& T, uint32_t cid) {
-    return cid == EMURX_ID_NONE ? 0u : T.client[8 * cid + 2];
+    return cid == EMURX_ID_NONE ? 0u : gld4(T.client + 8 * cid + 2);
 }
 // CClient.IsUnicastToMe client_ctx.go:389-398 (frames here are always > 6 bytes)
 __device__ __forceinline__ bool unicast_to_me(const emurx_dev_tables& T, uint32_t cid,
                                               uint32_t dlo, uint32_t dhi) {
-    return T.client[8 * cid + 0] == dlo && T.client[8 * cid + 1] == dhi;
+    return gld4(T.client + 8 * cid + 0) == dlo && gld4(T.client + 8 * cid + 1) == dhi;
 }
 
 // Go 1.18 net.IP.IsLinkLocalUnicast / IsGlobalUnicast for a 16-byte address (words LE)
@@ -640,7 +750,7 @@ __device__ __forceinline__ void classify(const S& s, uint32_t len, const emurx_d
         set_lk(r, EMURX_LK_NO_CLIENT);
         return;
     case kFirst: {
-        const uint32_t cid = T.ns_info[4 * ns + 1];
+        const uint32_t cid = gld4(T.ns_info + 4 * ns + 1);
         client_result(r, cid, client_plugins(T, cid), plug, true);
         return;
     }

@@ -4,10 +4,13 @@
 // GPU that owns that Namespace (emurx_owner of its CTunnelKey hash).  Three
 // launches build the all-to-all send buffer in frame order per destination:
 //   k_route<false>  per tile of 256 records: destination of each record, counts per
-//                   (tile, destination)                                   -> tile_cnt
-//   k_route_scan    one workgroup: exclusive prefix over tiles per destination -> tile_off,
-//                   totals -> send_count
-//   k_route<true>   same ranks again (wave ballots, no atomics) -> send[d * cap + offset]
+//                   (tile, destination) -> tile_cnt, and per group of 64 tiles -> grp (one
+//                   atomic per tile and destination, 64 tiles per address)
+//   k_route_scan    one workgroup, one lane per group: exclusive prefix over groups ->
+//                   grp_off, totals -> send_count; clears grp for the next batch
+//   k_route<true>   tile offset = grp_off + the counts of the group's earlier tiles (one
+//                   coalesced load + wave reductions), ranks by wave ballots (no atomics)
+//                   -> send[d * cap + offset]
 // The exchange itself (an equal-split all-to-all over RCCL) is issued by the caller on the
 // same stream.  Bytes: 32 B read twice + 40 B written per routed record.
 #include <hip/hip_runtime.h>
@@ -19,15 +22,17 @@
 
 namespace emurx {
 
-constexpr uint32_t kScanThreads = 1024;
+constexpr uint32_t kScanThreads = 1024;  // groups per batch (64 tiles each): 16M frames
+constexpr uint32_t kGroup = 64;          // tiles per group
 
 template <bool kPack>
 __global__ __launch_bounds__(kBlock) void k_route(const emurx_rec* __restrict__ rec, uint32_t n,
                                                   uint32_t n_parts, uint32_t my_rank,
-                                                  uint32_t* __restrict__ tile_cnt,
-                                                  const uint32_t* __restrict__ tile_off,
+                                                  uint32_t* __restrict__ tile_cnt, uint32_t* __restrict__ grp,
+                                                  const uint32_t* __restrict__ grp_off,
                                                   emurx_route_rec* __restrict__ send, uint32_t cap) {
     __shared__ uint32_t s_wcnt[kWaves][16];
+    __shared__ uint32_t s_toff[EMURX_MAX_PARTS];
     const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / kWave, tile = blockIdx.x;
     const uint32_t i = tile * kBlock + tid;
     if (lane < 16) s_wcnt[wv][lane] = 0;
@@ -39,6 +44,22 @@ __global__ __launch_bounds__(kBlock) void k_route(const emurx_rec* __restrict__ 
     }
     // {ns, client, vlan0, vlan1} {vport | l3 << 16, ...}
     const uint32_t d = a.x != EMURX_ID_NONE ? emurx_owner(emurx_tk_hash(b.x & 0xffffu, a.z, a.w), n_parts) : 0xffu;
+    if (kPack && wv == 0) {  // this tile's offset: group offset + the group's earlier tiles
+        const uint32_t g0 = tile & ~(kGroup - 1);
+        uint4 x = make_uint4(0, 0, 0, 0), y = x;
+        if (g0 + lane < tile) {
+            const uint4* p = reinterpret_cast<const uint4*>(tile_cnt + (g0 + lane) * 16);
+            x = p[0];
+            y = p[1];
+        }
+        const uint32_t c[EMURX_MAX_PARTS] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+#pragma unroll
+        for (uint32_t k = 0; k < EMURX_MAX_PARTS; ++k) {
+            if (k >= n_parts) break;
+            const uint32_t sum = wave_reduce(c[k], [](uint32_t u, uint32_t v) { return u + v; });
+            if (lane == 0) s_toff[k] = grp_off[(tile / kGroup) * 16 + k] + sum;
+        }
+    }
     uint32_t rank = 0;
     uint64_t left = __ballot(d != 0xffu);
     while (left) {
@@ -51,11 +72,15 @@ __global__ __launch_bounds__(kBlock) void k_route(const emurx_rec* __restrict__ 
     }
     __syncthreads();
     if (!kPack) {
-        if (tid < 16) tile_cnt[tile * 16 + tid] = s_wcnt[0][tid] + s_wcnt[1][tid] + s_wcnt[2][tid] + s_wcnt[3][tid];
+        if (tid < 16) {
+            const uint32_t c = s_wcnt[0][tid] + s_wcnt[1][tid] + s_wcnt[2][tid] + s_wcnt[3][tid];
+            tile_cnt[tile * 16 + tid] = c;
+            if (c) atomicAdd(&grp[(tile / kGroup) * 16 + tid], c);
+        }
         return;
     }
     if (d == 0xffu) return;
-    uint32_t pos = tile_off[tile * 16 + d] + rank;
+    uint32_t pos = s_toff[d] + rank;
     for (uint32_t w = 0; w < wv; ++w) pos += s_wcnt[w][d];
     if (pos >= cap) return;  // overflow: send_count[d] > cap tells the caller
     uint32_t* o = reinterpret_cast<uint32_t*>(send + (size_t)d * cap + pos);  // 40 B, 8-B aligned
@@ -66,73 +91,59 @@ __global__ __launch_bounds__(kBlock) void k_route(const emurx_rec* __restrict__ 
     reinterpret_cast<uint2*>(o)[4] = make_uint2(i, my_rank);
 }
 
-// exclusive prefix over tiles of tile_cnt[t][d], d < n_parts; one workgroup of 1024 lanes,
-// each owning a contiguous run of tiles
-__global__ __launch_bounds__(kScanThreads) void k_route_scan(const uint32_t* __restrict__ tile_cnt,
-                                                              uint32_t ntiles, uint32_t n_parts,
-                                                              uint32_t* __restrict__ tile_off,
+// exclusive prefix over groups of grp[g][d], d < n_parts; one lane per group; leaves grp zero
+__global__ __launch_bounds__(kScanThreads) void k_route_scan(uint32_t* __restrict__ grp, uint32_t ngroups,
+                                                              uint32_t n_parts, uint32_t* __restrict__ grp_off,
                                                               uint32_t* __restrict__ send_count) {
-    __shared__ uint32_t s[EMURX_MAX_PARTS][kScanThreads];
+    __shared__ uint32_t s_wsum[EMURX_MAX_PARTS][kScanThreads / kWave];
+    __shared__ uint32_t s_ex[EMURX_MAX_PARTS][kScanThreads];
     const uint32_t t = threadIdx.x, lane = lane_id(), wv = t / kWave;
-    const uint32_t per = (ntiles + kScanThreads - 1) / kScanThreads;
-    const uint32_t t0 = min(t * per, ntiles), t1 = min(t0 + per, ntiles);
-    uint32_t run[EMURX_MAX_PARTS];
-#pragma unroll
-    for (uint32_t d = 0; d < EMURX_MAX_PARTS; ++d) run[d] = 0;
-    for (uint32_t k = t0; k < t1; ++k) {
-        const uint4* p = reinterpret_cast<const uint4*>(tile_cnt + k * 16);
-        const uint4 x = p[0], y = p[1];
-        run[0] += x.x; run[1] += x.y; run[2] += x.z; run[3] += x.w;
-        run[4] += y.x; run[5] += y.y; run[6] += y.z; run[7] += y.w;
+    uint4 x = make_uint4(0, 0, 0, 0), y = x;
+    if (t < ngroups) {
+        uint4* p = reinterpret_cast<uint4*>(grp + t * 16);
+        x = p[0];
+        y = p[1];
+        p[0] = make_uint4(0, 0, 0, 0);
+        p[1] = make_uint4(0, 0, 0, 0);
     }
-#pragma unroll
-    for (uint32_t d = 0; d < EMURX_MAX_PARTS; ++d) s[d][t] = run[d];
-    __syncthreads();
-    // wave d scans destination d's 1024 run totals: 16 per lane, then across lanes
-    if (wv < n_parts) {
-        const uint32_t d = wv;
-        uint32_t v[16], sum = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < 16; ++k) { v[k] = s[d][lane * 16 + k]; sum += v[k]; }
-        uint32_t incl = sum;
+    for (uint32_t k = 0; k < n_parts; ++k) {  // inclusive wave scan per destination
+        const uint32_t v = k == 0 ? x.x : k == 1 ? x.y : k == 2 ? x.z : k == 3 ? x.w
+                         : k == 4 ? y.x : k == 5 ? y.y : k == 6 ? y.z : y.w;
+        uint32_t incl = v;
 #pragma unroll
         for (uint32_t o = 1; o < kWave; o <<= 1) {
             const uint32_t up = (uint32_t)__shfl_up((int)incl, o);
             if (lane >= o) incl += up;
         }
-        uint32_t ex = incl - sum;
-#pragma unroll
-        for (uint32_t k = 0; k < 16; ++k) { s[d][lane * 16 + k] = ex; ex += v[k]; }
-        if (lane == kWave - 1) send_count[d] = incl;
+        if (lane == kWave - 1) s_wsum[k][wv] = incl;
+        s_ex[k][t] = incl - v;
     }
     __syncthreads();
-    uint32_t base[EMURX_MAX_PARTS];
-#pragma unroll
-    for (uint32_t d = 0; d < EMURX_MAX_PARTS; ++d) base[d] = s[d][t];
-    for (uint32_t k = t0; k < t1; ++k) {
-        const uint4* p = reinterpret_cast<const uint4*>(tile_cnt + k * 16);
-        const uint4 x = p[0], y = p[1];
-        uint4* q = reinterpret_cast<uint4*>(tile_off + k * 16);
-        q[0] = make_uint4(base[0], base[1], base[2], base[3]);
-        q[1] = make_uint4(base[4], base[5], base[6], base[7]);
-        base[0] += x.x; base[1] += x.y; base[2] += x.z; base[3] += x.w;
-        base[4] += y.x; base[5] += y.y; base[6] += y.z; base[7] += y.w;
+    for (uint32_t k = 0; k < n_parts; ++k) {
+        uint32_t before = 0, total = 0;
+        for (uint32_t w = 0; w < kScanThreads / kWave; ++w) {
+            const uint32_t sw = s_wsum[k][w];
+            before += w < wv ? sw : 0;
+            total += sw;
+        }
+        if (t < ngroups) grp_off[t * 16 + k] = before + s_ex[k][t];
+        if (t == 0) send_count[k] = total;
     }
 }
 
 }  // namespace emurx
 
 int emurx_launch_route(const emurx_rec* rec, uint32_t n, uint32_t n_parts, uint32_t my_rank, uint32_t cap,
-                       emurx_route_rec* send, uint32_t* send_count, uint32_t* tile_cnt, uint32_t* tile_off,
-                       hipStream_t st) {
+                       emurx_route_rec* send, uint32_t* send_count, uint32_t* tile_cnt, uint32_t* grp,
+                       uint32_t* grp_off, hipStream_t st) {
     using namespace emurx;
-    const uint32_t ntiles = (n + kBlock - 1) / kBlock;
+    const uint32_t ntiles = (n + kBlock - 1) / kBlock, ngroups = (ntiles + kGroup - 1) / kGroup;
     if (n == 0) return hipMemsetAsync(send_count, 0, n_parts * sizeof(uint32_t), st) == hipSuccess ? 0 : -1;
-    hipLaunchKernelGGL(k_route<false>, dim3(ntiles), dim3(kBlock), 0, st, rec, n, n_parts, my_rank, tile_cnt,
+    if (ngroups > kScanThreads) return -1;
+    hipLaunchKernelGGL(k_route<false>, dim3(ntiles), dim3(kBlock), 0, st, rec, n, n_parts, my_rank, tile_cnt, grp,
                        (const uint32_t*)nullptr, send, cap);
-    hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(kScanThreads), 0, st, tile_cnt, ntiles, n_parts, tile_off,
-                       send_count);
-    hipLaunchKernelGGL(k_route<true>, dim3(ntiles), dim3(kBlock), 0, st, rec, n, n_parts, my_rank, tile_cnt,
-                       tile_off, send, cap);
+    hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(kScanThreads), 0, st, grp, ngroups, n_parts, grp_off, send_count);
+    hipLaunchKernelGGL(k_route<true>, dim3(ntiles), dim3(kBlock), 0, st, rec, n, n_parts, my_rank, tile_cnt, grp,
+                       grp_off, send, cap);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

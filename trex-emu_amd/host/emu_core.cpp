@@ -206,6 +206,7 @@ int CThreadCtx::AddClient(uint32_t ns, const uint8_t mac[6], const uint8_t ipv4[
     ++next_client_;
     return (int)id;
 }
+int CThreadCtx::RemoveClient(uint32_t ns, const uint8_t mac[6]) { return emurx_client_remove(h_, ns, mac); }
 void CThreadCtx::HandleRxPacket(Mbuf* m) {
     const int r = parser.ParsePacket(m);
     if (r < 0) {

@@ -124,9 +124,10 @@ public:
 
     // ids are dense and owned here, as the Go side assigns them (thread_ctx.go:786, ns_ctx.go:332)
     int AddNs(const CTunnelKey& key, uint32_t plugins = 0x7FF);  // -> ns id, or EMURX_E*
-    int RemoveNs(const CTunnelKey& key);
+    int RemoveNs(const CTunnelKey& key);  // EMURX_EEXIST while it has clients (thread_ctx.go:803)
     int AddClient(uint32_t ns, const uint8_t mac[6], const uint8_t ipv4[4] = nullptr,
                   const uint8_t ipv6[16] = nullptr, uint32_t plugins = 0x7FF);  // -> client id
+    int RemoveClient(uint32_t ns, const uint8_t mac[6]);  // ns_ctx.go RemoveClient
     void HandleRxPacket(Mbuf* m);  // thread_ctx.go:365-375
     emurx_t* rx() const { return h_; }
 

@@ -198,7 +198,11 @@ void TestNsClientLookup() {  // GetNs + CLookupByIPv4 + IsUnicastToMe (icmp.go:3
     parser.ParsePacket(&m1);
     if (arp != 1 || lastNs != (uint32_t)ns || lastClient != (uint32_t)cid || lastLookup != EMURX_LK_CLIENT)
         FATALF(" lookup ns %u client %u lk %u ", lastNs, lastClient, lastLookup);
-    // the namespace gone: GetNs == nil
+    // RemoveNs refuses while clients are active (thread_ctx.go:803-805); then GetNs == nil
+    if (tctx.RemoveNs(tunOf(7, 0x81000007, 0x81000fff)) != EMURX_EEXIST) FATALF(" RemoveNs with clients ");
+    if (tctx.RemoveClient((uint32_t)ns, mac) != EMURX_OK) FATALF(" RemoveClient ");
+    parser.ParsePacket(&m1);
+    if (lastNs != (uint32_t)ns || lastLookup != EMURX_LK_NO_CLIENT) FATALF(" removed client still found ");
     if (tctx.RemoveNs(tunOf(7, 0x81000007, 0x81000fff)) != EMURX_OK) FATALF(" RemoveNs ");
     parser.ParsePacket(&m1);
     if (lastNs != EMURX_ID_NONE || lastLookup != EMURX_LK_NO_NS) FATALF(" removed ns still found ");
