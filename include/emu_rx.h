@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define EMURX_ABI_VERSION 2
+#define EMURX_ABI_VERSION 3
 
 /* ---- return codes -------------------------------------------------------------------- */
 #define EMURX_OK 0
@@ -148,8 +148,11 @@ typedef struct emurx_desc {
     uint32_t off;
     uint16_t len;
     uint8_t vport;
-    uint8_t pad;
+    uint8_t pad;   /* 0, or EMURX_DESC_HOLE */
 } emurx_desc;
+/* pad value of an empty descriptor slot: no frame, no record, no queue entry, not counted
+   (the batched ingest leaves one for every frame a message announced but did not carry) */
+#define EMURX_DESC_HOLE 0xFFu
 
 /* 32-byte record, one per frame, in frame order.  The numeric fields are exactly the
    ParserPacketState the reference hands to a ParserCb (parser.go:51-61) plus the
@@ -302,6 +305,50 @@ int emurx_parse_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_des
    *parse_err = 2 (the reference panics there). */
 int emurx_zmq_descriptors(const uint8_t* msg, size_t len, emurx_desc* out, uint32_t cap,
                           uint32_t* n_out, int* parse_err);
+
+/* ---- batched host ingest: many ZMQ messages per GPU round trip -------
+   The per-message loop of VethIFZmq.OnRxStream (veth_zmq.go:277-320) over a whole batch of
+   messages, with the framing walk on the GPU (one lane per message, same uint16 offset and
+   abort-on-header-error rules as emurx_zmq_descriptors), then parse + classify (k_rx), then
+   the per-callback queues packed on the GPU.  Two slots let the caller fill one pinned
+   staging buffer while the other slot's batch is in flight:
+
+       buf = emurx_ingest_buffer(h, s, bytes)    pinned host memory owned by the library
+       ... the caller writes ZMQ messages into buf (the receive copy it does anyway) ...
+       emurx_ingest_submit(h, s, msgs, nmsg)     H2D + 4 launches + D2H, returns at once
+       emurx_ingest_wait(h, s, &res)             results of slot s, valid until its next submit
+
+   Frames are numbered in message order, then wire order (the order the Go loop handles
+   them).  res.desc[i].off is the frame's offset in the slot's buffer.  Counters in res.delta
+   are those of OnRxStream called once per message (RxBatch = nmsg). */
+#define EMURX_INGEST_SLOTS 2
+#define EMURX_MSG_OK 0u          /* every announced frame decoded                           */
+#define EMURX_MSG_PARSE_ERR 1u   /* RxParseErr: the walk stopped on a header error           */
+#define EMURX_MSG_PANIC 2u       /* the reference panics: frame > 9216 B or offset wrap      */
+typedef struct emurx_msg {
+    uint32_t off; /* message start in the slot buffer (any alignment) */
+    uint32_t len; /* message bytes                                    */
+} emurx_msg;
+typedef struct emurx_ingest_result {
+    const emurx_rec* rec;        /* [n_frames] records, frame order                         */
+    const emurx_desc* desc;      /* [n_frames] frame offset / length / vport in the buffer  */
+    const uint32_t* qlist;       /* [n_frames] frame indices grouped by queue (qoff)        */
+    const uint32_t* msg_frames;  /* [n_msgs] frames decoded from each message               */
+    const uint8_t* msg_status;   /* [n_msgs] EMURX_MSG_*                                    */
+    uint32_t n_frames;
+    uint32_t n_msgs;
+    uint32_t qoff[EMURX_NUM_QUEUES + 1];
+    emurx_counters delta;        /* ParserStats + VethStats deltas of the batch             */
+} emurx_ingest_result;
+/* Pinned staging buffer of slot s (0 <= s < EMURX_INGEST_SLOTS) with room for `bytes`
+   (grown on demand; not while the slot has a batch in flight). */
+int emurx_ingest_buffer(emurx_t* h, uint32_t slot, size_t bytes, uint8_t** buf);
+/* Enqueue the slot's messages.  EMURX_ENOSPC when the messages could announce more frames
+   than cfg.max_frames (split the batch); EMURX_EINVAL for a message outside the buffer or a
+   slot still in flight. */
+int emurx_ingest_submit(emurx_t* h, uint32_t slot, const emurx_msg* msgs, uint32_t nmsg);
+/* Wait for the slot's batch and point `res` at its results (library-owned pinned memory). */
+int emurx_ingest_wait(emurx_t* h, uint32_t slot, emurx_ingest_result* res);
 
 /* ParserStats delta from an outcome histogram (pure host arithmetic). */
 void emurx_hist_to_counters(const uint64_t hist[2 * EMURX_HIST_BINS], emurx_counters* out);

@@ -325,3 +325,121 @@ def test_route_dev_overflow(rxmod):
     r = s[: 2 * cap * 40].view(abi.ROUTE_REC_DTYPE).reshape(2, cap)
     for d in range(2):
         assert r[d].tobytes() == want[d][:cap].tobytes()
+
+
+# ---- batched host ingest: device framing walk + k_rx + device queue packing ---------------
+def oracle_messages(o, msgs):
+    """What the ingest of `msgs` must return: OnRxStream per message (the oracle's), frames
+    numbered across the messages, queues as a stable partition of the whole batch."""
+    import collections
+    import pyoracle
+    recs, nfr, status, tot = [], [], [], collections.Counter()
+    for m in msgs:
+        rec, _, _, cnt = o.rx_stream(m)
+        recs.append(rec)
+        nfr.append(len(rec))
+        status.append(pyoracle.zmq_descriptors(m)[2])
+        tot.update(pyoracle.counters_dict(cnt))
+    rec = np.concatenate(recs) if recs else np.zeros(0, abi.REC_DTYPE)
+    q = np.where(rec["status"] == 0, rec["proto"], abi.Q_DROP).astype(np.int64)
+    qoff = np.zeros(abi.NUM_QUEUES + 1, np.uint32)
+    qoff[1:] = np.cumsum(np.bincount(q, minlength=abi.NUM_QUEUES))
+    return rec, np.argsort(q, kind="stable").astype(np.uint32), qoff, nfr, status, dict(tot)
+
+
+def place_messages(rx, slot, msgs, rng):
+    """Write messages into the slot's pinned buffer at unaligned offsets -> MSG_DTYPE table."""
+    gaps = rng.integers(0, 8, len(msgs))
+    buf = rx.ingest_buffer(slot, sum(len(m) for m in msgs) + int(gaps.sum()))
+    tab = np.zeros(len(msgs), abi.MSG_DTYPE)
+    at = 0
+    for i, (m, g) in enumerate(zip(msgs, gaps)):
+        at += int(g)
+        buf[at:at + len(m)] = np.frombuffer(m, np.uint8)
+        tab[i] = (at, len(m))
+        at += len(m)
+    return tab
+
+
+def check_ingest(res, o, msgs, tab):
+    import pyoracle
+    rec, qlist, qoff, nfr, status, cnt = oracle_messages(o, msgs)
+    assert res["rec"].tobytes() == rec.tobytes(), rec_diff(res["rec"], rec)
+    assert np.array_equal(res["qoff"], qoff) and np.array_equal(res["qlist"], qlist)
+    assert list(res["msg_frames"]) == nfr and list(res["msg_status"]) == status
+    want_desc = [pyoracle.zmq_descriptors(m)[1].copy() for m in msgs]
+    for d, t in zip(want_desc, tab):
+        d["off"] += t["off"]
+    want_desc = np.concatenate(want_desc) if want_desc else np.zeros(0, abi.DESC_DTYPE)
+    assert res["desc"].tobytes() == want_desc.tobytes()
+    assert res["counters"] == cnt
+
+
+def test_ingest_messages(rxmod):
+    """Valid, truncated, corrupted, over-announcing, oversized and > 64 KiB messages in one
+    batch at unaligned offsets: records, descriptors, queues, per-message frame counts and
+    status, and every counter equal the oracle's OnRxStream per message."""
+    import test_abi
+    rng = np.random.default_rng(0x16E5)
+    frames = [c[1] for c in E.cases()] + corpus_frames()[:3000]
+    msgs = test_abi._rand_msgs(rng, 200)
+    for i in range(0, len(frames), 57):
+        msgs.append(F.zmq_pack(frames[i:i + 57], [1] * len(frames[i:i + 57])))
+    msgs = [msgs[i] for i in rng.permutation(len(msgs))]
+    rx, o = new_pair(rxmod)
+    ns, cl = frames_tables(frames, vport=1)
+    load_frame_tables([rx, o], ns, cl)
+    tab = place_messages(rx, 0, msgs, rng)
+    rx.ingest_submit(0, tab)
+    res = rx.ingest_wait(0)
+    assert res["n"] > 3000 and (res["msg_status"] != 0).sum() > 50   # holes and aborts exercised
+    check_ingest(res, o, msgs, tab)
+
+
+def test_ingest_two_slots_pipelined(rxmod):
+    """Config C frames as 64-frame messages, three batches over the two slots with one batch
+    always in flight while the next is staged; each equals the oracle."""
+    rng = np.random.default_rng(9)
+    w = synth.config_c(30000)
+    rx, o = new_pair(rxmod)
+    synth.load_tables(w, rx)
+    synth.load_tables(w, o)
+    fr = [w["buf"][d["off"]:d["off"] + d["len"]].tobytes() for d in w["desc"]]
+    vp = [int(v) for v in w["desc"]["vport"]]
+    msgs = [F.zmq_pack(fr[i:i + 64], vp[i:i + 64]) for i in range(0, len(fr), 64)]
+    parts = [msgs[:150], msgs[150:300], msgs[300:]]
+    tabs = [None, None]
+    tabs[0] = place_messages(rx, 0, parts[0], rng)
+    rx.ingest_submit(0, tabs[0])
+    tabs[1] = place_messages(rx, 1, parts[1], rng)
+    rx.ingest_submit(1, tabs[1])
+    check_ingest(rx.ingest_wait(0), o, parts[0], tabs[0])
+    t2 = place_messages(rx, 0, parts[2], rng)
+    rx.ingest_submit(0, t2)
+    check_ingest(rx.ingest_wait(1), o, parts[1], tabs[1])
+    check_ingest(rx.ingest_wait(0), o, parts[2], t2)
+
+
+def test_ingest_limits(rxmod):
+    """No messages; a batch that could announce more frames than max_frames (ENOSPC, nothing
+    enqueued); wait without a submit (EINVAL); a message outside the buffer (EINVAL)."""
+    from emurx.rx import RxPath
+    rx = RxPath(0, max_ns=16, max_clients=16, max_frames=100)
+    rx.ingest_buffer(0, 64)
+    rx.ingest_submit(0, np.zeros(0, abi.MSG_DTYPE))
+    res = rx.ingest_wait(0)
+    assert res["n"] == 0 and res["counters"]["rx_batch"] == 0 and (res["qoff"] == 0).all()
+    m = F.zmq_pack([bytes(60)] * 101)
+    buf = rx.ingest_buffer(0, len(m))
+    buf[:] = np.frombuffer(m, np.uint8)
+    with pytest.raises(RuntimeError, match="output buffer too small"):
+        rx.ingest_submit(0, [(0, len(m))])
+    with pytest.raises(RuntimeError, match="invalid argument"):
+        rx.ingest_wait(0)
+    with pytest.raises(RuntimeError, match="invalid argument"):
+        rx.ingest_submit(0, [(8, len(m))])
+    m = F.zmq_pack([bytes(60)] * 100)
+    buf[: len(m)] = np.frombuffer(m, np.uint8)
+    rx.ingest_submit(0, [(0, len(m))])
+    res = rx.ingest_wait(0)
+    assert res["n"] == 100 and res["counters"]["errL3ProtoUnsupported"] == 100

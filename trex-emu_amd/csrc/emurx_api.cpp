@@ -112,6 +112,40 @@ struct PinBuf {
     }
 };
 
+// One in-flight batch of the batched ZMQ ingest: pinned staging + device scratch + results.
+struct IngestSlot {
+    hipStream_t st = nullptr;
+    hipEvent_t done = nullptr;
+    bool pending = false;
+    uint32_t nmsg = 0, slots = 0;  // messages and descriptor slots of the batch in flight
+    PinBuf<uint8_t> h_buf;         // messages, written by the caller (+64 B pad)
+    PinBuf<uint32_t> h_ctl;        // emurx_msg[nmsg], slot_base[nmsg + 1]
+    PinBuf<uint32_t> h_stat, h_qlist, h_qoff, h_mframes;
+    PinBuf<uint8_t> h_mstatus;
+    PinBuf<emurx_rec> h_rec;
+    PinBuf<emurx_desc> h_desc;
+    PinBuf<uint64_t> h_hist;
+    DevBuf<uint8_t> d_buf;
+    DevBuf<uint32_t> d_ctl, d_stat, d_qlist, d_tile_cnt, d_seg_off, d_packed, d_qoff;
+    DevBuf<emurx_desc> d_desc;
+    DevBuf<emurx_rec> d_rec;
+    DevBuf<uint64_t> d_hist, d_hist_out;  // d_hist: zero between batches (k_qscan clears it)
+    std::vector<uint32_t> remap;          // slot -> frame index, only when a message fell short
+    void release() {
+        if (st) (void)hipStreamSynchronize(st);
+        h_buf.release(); h_ctl.release(); h_stat.release(); h_qlist.release(); h_qoff.release();
+        h_mframes.release(); h_mstatus.release(); h_rec.release(); h_desc.release(); h_hist.release();
+        d_buf.release(); d_ctl.release(); d_stat.release(); d_qlist.release(); d_tile_cnt.release();
+        d_seg_off.release(); d_packed.release(); d_qoff.release(); d_desc.release(); d_rec.release();
+        d_hist.release(); d_hist_out.release();
+        if (done) (void)hipEventDestroy(done);
+        if (st) (void)hipStreamDestroy(st);
+        done = nullptr;
+        st = nullptr;
+        pending = false;
+    }
+};
+
 }  // namespace
 
 struct emurx_ctx {
@@ -130,16 +164,8 @@ struct emurx_ctx {
     DevBuf<uint32_t> d_ns, d_nsinfo, d_mac, d_ip4, d_ip6, d_client;
     std::vector<uint32_t> h_ns, h_nsinfo, h_mac, h_ip4, h_ip6, h_client;
 
-    // host batch staging (emurx_rx_stream): message, descriptors, and the batch outputs
-    PinBuf<uint8_t> h_msg;
-    PinBuf<emurx_desc> h_desc;
-    PinBuf<uint32_t> h_qlist, h_tile_cnt;
-    PinBuf<uint64_t> h_hist;
-    DevBuf<uint8_t> d_msg;
-    DevBuf<emurx_desc> d_desc;
-    DevBuf<emurx_rec> d_rec;
-    DevBuf<uint32_t> d_qlist, d_tile_cnt;
-    DevBuf<uint64_t> d_hist;
+    // batched host ingest: EMURX_INGEST_SLOTS public slots + one private to emurx_rx_stream
+    IngestSlot ing[EMURX_INGEST_SLOTS + 1];
 
     // Namespace-partition packing scratch (emurx_route_dev)
     DevBuf<uint32_t> d_route_cnt, d_route_grp, d_route_goff;  // grp: zero between batches
@@ -283,6 +309,144 @@ int run_dev(emurx_t* h, const uint8_t* frames, const emurx_desc* desc, uint32_t 
     return r ? EMURX_EDEVICE : EMURX_OK;
 }
 
+// ---- batched ZMQ ingest (emurx_ingest_*; emurx_rx_stream uses the private last slot) ----
+int ingest_buffer(emurx_t* h, uint32_t slot, size_t bytes, uint8_t** buf) {
+    IngestSlot& s = h->ing[slot];
+    if (s.pending || bytes > 0xFFFFFFFFull - 64) return EMURX_EINVAL;
+    if (s.h_buf.alloc(bytes + 64) || s.d_buf.alloc(bytes + 64)) return EMURX_ENOMEM;
+    *buf = s.h_buf.p;
+    return EMURX_OK;
+}
+
+int ingest_submit(emurx_t* h, uint32_t slot, const emurx_msg* msgs, uint32_t nmsg) {
+    IngestSlot& s = h->ing[slot];
+    if (s.pending || (nmsg && (!msgs || !s.h_buf.p))) return EMURX_EINVAL;
+    int rc = bind(h);
+    if (rc) return rc;
+    if (!s.st && hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking) != hipSuccess) return EMURX_EDEVICE;
+    if (!s.done && hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) return EMURX_EDEVICE;
+    const size_t cap = s.h_buf.p ? s.h_buf.n - 64 : 0;
+    if (s.h_ctl.alloc((size_t)3 * nmsg + 1)) return EMURX_ENOMEM;
+    uint32_t* ctl = s.h_ctl.p;
+    uint32_t* base = ctl + 2 * (size_t)nmsg;
+    uint64_t S = 0;
+    size_t end = 0;
+    for (uint32_t m = 0; m < nmsg; ++m) {
+        const uint64_t e = (uint64_t)msgs[m].off + msgs[m].len;
+        if (e > cap) return EMURX_EINVAL;
+        end = std::max<size_t>(end, (size_t)e);
+        ctl[2 * m] = msgs[m].off;
+        ctl[2 * m + 1] = msgs[m].len;
+        base[m] = (uint32_t)S;
+        // descriptor slots: the frames the header announces, at most one per 4 bytes of the
+        // first 64 KiB (the uint16 running offset never passes 65535 on an accepted frame)
+        const uint8_t* p = s.h_buf.p + msgs[m].off;
+        const uint32_t len = msgs[m].len;
+        if (len >= 4 && (be32(p) >> 16) == EMURX_ZMQ_MAGIC)
+            S += std::min<uint32_t>(be32(p) & 0xffff, (std::min<uint32_t>(len, 65536) - 4) / 4);
+        if (S > h->cfg.max_frames) return EMURX_ENOSPC;
+    }
+    base[nmsg] = (uint32_t)S;
+    const uint32_t n = (uint32_t)S, nt = ntiles(n);
+    const size_t qcap = std::max<size_t>(queue_cap(n), EMURX_QUEUE_TILE);
+    const size_t hw = (size_t)EMURX_HIST_SHARDS * 2 * EMURX_HIST_BINS;
+    const bool fresh_hist = !s.d_hist.p;
+    if (s.d_ctl.alloc((size_t)3 * nmsg + 1) || s.d_stat.alloc(nmsg) || s.d_desc.alloc(n) || s.d_rec.alloc(n) ||
+        s.d_qlist.alloc(EMURX_NUM_QUEUES * qcap) || s.d_tile_cnt.alloc((size_t)std::max<uint32_t>(nt, 1) * 16) ||
+        s.d_seg_off.alloc((size_t)std::max<uint32_t>(nt, 1) * 16) || s.d_packed.alloc(n) || s.d_qoff.alloc(16) ||
+        s.d_hist.alloc(hw) || s.d_hist_out.alloc(2 * EMURX_HIST_BINS) || s.h_stat.alloc(nmsg) ||
+        s.h_rec.alloc(n) || s.h_desc.alloc(n) || s.h_qlist.alloc(n) || s.h_qoff.alloc(16) ||
+        s.h_hist.alloc(2 * EMURX_HIST_BINS) || s.h_mframes.alloc(nmsg) || s.h_mstatus.alloc(nmsg))
+        return EMURX_ENOMEM;
+    if (h->dirty) {  // batches in flight read the device tables: let them finish first
+        for (auto& o : h->ing)
+            if (o.st) (void)hipStreamSynchronize(o.st);
+        if ((rc = rebuild_and_upload(h, h->stream))) return rc;
+    }
+    hipStream_t st = s.st;
+    const auto H2D = hipMemcpyHostToDevice, D2H = hipMemcpyDeviceToHost;
+    bool ok = true;
+    if (fresh_hist) ok = ok && hipMemsetAsync(s.d_hist.p, 0, hw * sizeof(uint64_t), st) == hipSuccess;
+    ok = ok && hipMemcpyAsync(s.d_ctl.p, ctl, ((size_t)3 * nmsg + 1) * 4, H2D, st) == hipSuccess;
+    if (end) ok = ok && hipMemcpyAsync(s.d_buf.p, s.h_buf.p, end, H2D, st) == hipSuccess;
+    if (!ok) return EMURX_EDEVICE;
+    if (emurx_launch_zmq_walk(s.d_buf.p, s.d_ctl.p, nmsg, s.d_desc.p, s.d_stat.p, st)) return EMURX_EDEVICE;
+    if (n) {
+        const emurx_dev_out o{s.d_rec.p, s.d_qlist.p, (uint32_t)qcap, s.d_tile_cnt.p, s.d_hist.p};
+        if (emurx_launch_batch(s.d_buf.p, s.d_desc.p, n, h->tables(), true, o, st, nullptr)) return EMURX_EDEVICE;
+    }
+    if (emurx_launch_queue_pack(s.d_qlist.p, (uint32_t)qcap, s.d_tile_cnt.p, n, s.d_seg_off.p, s.d_packed.p,
+                                s.d_qoff.p, s.d_hist.p, s.d_hist_out.p, st))
+        return EMURX_EDEVICE;
+    if (n)
+        ok = hipMemcpyAsync(s.h_rec.p, s.d_rec.p, (size_t)n * sizeof(emurx_rec), D2H, st) == hipSuccess &&
+             hipMemcpyAsync(s.h_desc.p, s.d_desc.p, (size_t)n * sizeof(emurx_desc), D2H, st) == hipSuccess &&
+             hipMemcpyAsync(s.h_qlist.p, s.d_packed.p, (size_t)n * 4, D2H, st) == hipSuccess;
+    if (nmsg) ok = ok && hipMemcpyAsync(s.h_stat.p, s.d_stat.p, (size_t)nmsg * 4, D2H, st) == hipSuccess;
+    ok = ok && hipMemcpyAsync(s.h_qoff.p, s.d_qoff.p, (EMURX_NUM_QUEUES + 1) * 4, D2H, st) == hipSuccess &&
+         hipMemcpyAsync(s.h_hist.p, s.d_hist_out.p, 2 * EMURX_HIST_BINS * 8, D2H, st) == hipSuccess &&
+         hipEventRecord(s.done, st) == hipSuccess;
+    if (!ok) return EMURX_EDEVICE;
+    s.pending = true;
+    s.nmsg = nmsg;
+    s.slots = n;
+    return EMURX_OK;
+}
+
+int ingest_wait(emurx_t* h, uint32_t slot, emurx_ingest_result* res) {
+    IngestSlot& s = h->ing[slot];
+    if (!s.pending) return EMURX_EINVAL;
+    int rc = bind(h);
+    if (rc) return rc;
+    s.pending = false;
+    if (hipEventSynchronize(s.done) != hipSuccess) return EMURX_EDEVICE;
+    memset(res, 0, sizeof(*res));
+    emurx_counters& d = res->delta;
+    d.rx_batch = s.nmsg;  // one OnRxStream per message, veth_zmq.go:278
+    uint64_t nf = 0;
+    for (uint32_t m = 0; m < s.nmsg; ++m) {
+        const uint32_t w = s.h_stat.p[m], f = w & 0xffffff, e = w >> 24;
+        s.h_mframes.p[m] = f;
+        s.h_mstatus.p[m] = (uint8_t)e;
+        nf += f;
+        if (e == EMURX_MSG_PARSE_ERR) d.rx_parse_err++;
+        if (e == EMURX_MSG_PANIC) d.ref_panic++;
+    }
+    if (nf > s.slots) return EMURX_EDEVICE;
+    if (nf < s.slots) {  // messages that announced more frames than they carried: close the holes
+        const uint32_t* base = s.h_ctl.p + 2 * (size_t)s.nmsg;
+        s.remap.assign(s.slots, EMURX_ID_NONE);
+        uint32_t c = 0;
+        for (uint32_t m = 0; m < s.nmsg; ++m) {
+            const uint32_t f = s.h_mframes.p[m];
+            if (c != base[m] && f) {
+                memmove(s.h_rec.p + c, s.h_rec.p + base[m], (size_t)f * sizeof(emurx_rec));
+                memmove(s.h_desc.p + c, s.h_desc.p + base[m], (size_t)f * sizeof(emurx_desc));
+            }
+            for (uint32_t k = 0; k < f; ++k) s.remap[base[m] + k] = c + k;
+            c += f;
+        }
+        for (uint64_t i = 0; i < nf; ++i) {
+            const uint32_t j = s.h_qlist.p[i];
+            if (j >= s.slots || s.remap[j] == EMURX_ID_NONE) return EMURX_EDEVICE;
+            s.h_qlist.p[i] = s.remap[j];
+        }
+    }
+    memcpy(res->qoff, s.h_qoff.p, sizeof(res->qoff));
+    if (res->qoff[EMURX_NUM_QUEUES] != nf) return EMURX_EDEVICE;
+    emurx_hist_to_counters(s.h_hist.p, &d);
+    d.rx_pkts = nf;  // VethIFZmq.OnRx veth_zmq.go:233-234
+    for (int b = 0; b < EMURX_HIST_BINS; ++b) d.rx_bytes += s.h_hist.p[2 * b + 1];
+    res->rec = s.h_rec.p;
+    res->desc = s.h_desc.p;
+    res->qlist = s.h_qlist.p;
+    res->msg_frames = s.h_mframes.p;
+    res->msg_status = s.h_mstatus.p;
+    res->n_frames = (uint32_t)nf;
+    res->n_msgs = s.nmsg;
+    return EMURX_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -335,12 +499,9 @@ void emurx_close(emurx_t* h) {
     if (!h) return;
     bind(h);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
+    for (auto& s : h->ing) s.release();
     h->d_ns.release(); h->d_nsinfo.release(); h->d_mac.release(); h->d_ip4.release();
     h->d_ip6.release(); h->d_client.release();
-    h->h_msg.release(); h->h_desc.release(); h->h_qlist.release(); h->h_tile_cnt.release();
-    h->h_hist.release();
-    h->d_msg.release(); h->d_desc.release(); h->d_rec.release(); h->d_qlist.release();
-    h->d_tile_cnt.release(); h->d_hist.release();
     h->d_route_cnt.release(); h->d_route_grp.release(); h->d_route_goff.release();
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
@@ -606,66 +767,40 @@ int emurx_rx_stream(emurx_t* h, const uint8_t* msg, size_t len, emurx_rec* out_r
     *n_out = 0;
     int rc = bind(h);
     if (rc) return rc;
-    const uint32_t cap = std::max<uint32_t>(std::min(out_cap, h->cfg.max_frames), 1);
-    const size_t qcap_max = queue_cap(cap), hist_words = (size_t)EMURX_HIST_SHARDS * 2 * EMURX_HIST_BINS;
-    if (h->h_desc.alloc(cap) || h->h_msg.alloc(len + 64) || h->h_qlist.alloc(EMURX_NUM_QUEUES * qcap_max) ||
-        h->h_tile_cnt.alloc(ntiles(cap) * 16) || h->h_hist.alloc(hist_words) || h->d_msg.alloc(len + 64) ||
-        h->d_desc.alloc(cap) || h->d_rec.alloc(cap) || h->d_qlist.alloc(EMURX_NUM_QUEUES * qcap_max) ||
-        h->d_tile_cnt.alloc(ntiles(cap) * 16) || h->d_hist.alloc(hist_words))
-        return EMURX_ENOMEM;
-    int perr = 0;
-    uint32_t n = 0;
-    rc = emurx_zmq_descriptors(msg, len, h->h_desc.p, cap, &n, &perr);
-    if (rc) return rc;
-    delta->rx_batch = 1;  // VethStats.RxBatch veth_zmq.go:278
-    if (perr == 1) delta->rx_parse_err = 1;
-    if (perr == 2) delta->ref_panic += 1;
-    for (uint32_t i = 0; i < n; ++i) {  // VethIFZmq.OnRx veth_zmq.go:233-234
-        delta->rx_pkts++;
-        delta->rx_bytes += h->h_desc.p[i].len;
+    // one message through the batched ingest (device framing walk), on the private slot
+    const uint32_t slot = EMURX_INGEST_SLOTS;
+    uint8_t* buf = nullptr;
+    if ((rc = ingest_buffer(h, slot, std::max<size_t>(len, 1), &buf))) return rc;
+    if (len) memcpy(buf, msg, len);
+    memset(buf + len, 0, 64);
+    const emurx_msg m{0, (uint32_t)len};
+    if ((rc = ingest_submit(h, slot, &m, 1))) return rc;
+    emurx_ingest_result r;
+    if ((rc = ingest_wait(h, slot, &r))) return rc;
+    if (r.n_frames > out_cap) return EMURX_ENOSPC;
+    if (r.n_frames && (!out_rec || !out_qlist)) return EMURX_EINVAL;
+    if (r.n_frames) {
+        memcpy(out_rec, r.rec, (size_t)r.n_frames * sizeof(emurx_rec));
+        memcpy(out_qlist, r.qlist, (size_t)r.n_frames * 4);
     }
-    *n_out = n;
-    hipStream_t st = h->stream;
-    if ((rc = rebuild_and_upload(h, st))) return rc;
-    if (n == 0) {
-        memset(out_qoff, 0, sizeof(uint32_t) * (EMURX_NUM_QUEUES + 1));
-        return EMURX_OK;
-    }
-    if (!out_rec || !out_qlist) return EMURX_EINVAL;
-    memcpy(h->h_msg.p, msg, len);
-    memset(h->h_msg.p + len, 0, 64);
-    // queue regions sized for this batch, so the whole qlist comes back in one copy
-    const uint32_t nt = ntiles(n);
-    const size_t qcap = queue_cap(n);
-    emurx_dev_out o{h->d_rec.p, h->d_qlist.p, (uint32_t)qcap, h->d_tile_cnt.p, h->d_hist.p};
-    bool ok = hipMemcpyAsync(h->d_msg.p, h->h_msg.p, len + 64, hipMemcpyHostToDevice, st) == hipSuccess &&
-              hipMemcpyAsync(h->d_desc.p, h->h_desc.p, (size_t)n * sizeof(emurx_desc), hipMemcpyHostToDevice, st) == hipSuccess &&
-              hipMemsetAsync(h->d_hist.p, 0, hist_words * sizeof(uint64_t), st) == hipSuccess;
-    if (!ok) return EMURX_EDEVICE;
-    if ((rc = run_dev(h, h->d_msg.p, h->d_desc.p, n, &o, st, true))) return rc;
-    ok = hipMemcpyAsync(out_rec, h->d_rec.p, (size_t)n * sizeof(emurx_rec), hipMemcpyDeviceToHost, st) == hipSuccess &&
-         hipMemcpyAsync(h->h_qlist.p, h->d_qlist.p, EMURX_NUM_QUEUES * qcap * 4, hipMemcpyDeviceToHost, st) == hipSuccess &&
-         hipMemcpyAsync(h->h_tile_cnt.p, h->d_tile_cnt.p, (size_t)nt * 16 * 4, hipMemcpyDeviceToHost, st) == hipSuccess &&
-         hipMemcpyAsync(h->h_hist.p, h->d_hist.p, hist_words * sizeof(uint64_t), hipMemcpyDeviceToHost, st) == hipSuccess &&
-         hipStreamSynchronize(st) == hipSuccess;
-    if (!ok) return EMURX_EDEVICE;
-    // concatenate each queue's per-tile segments (out_qoff[q] .. out_qoff[q+1])
-    uint32_t at = 0;
-    for (int q = 0; q < EMURX_NUM_QUEUES; ++q) {
-        out_qoff[q] = at;
-        for (uint32_t t = 0; t < nt; ++t) {
-            const uint32_t c = h->h_tile_cnt.p[t * 16 + q];
-            if (c > EMURX_QUEUE_TILE || at + c > n) return EMURX_EDEVICE;
-            memcpy(out_qlist + at, h->h_qlist.p + q * qcap + (size_t)t * EMURX_QUEUE_TILE, (size_t)c * 4);
-            at += c;
-        }
-    }
-    out_qoff[EMURX_NUM_QUEUES] = at;
-    if (at != n) return EMURX_EDEVICE;
-    uint64_t hist[2 * EMURX_HIST_BINS];
-    emurx_hist_fold(h->h_hist.p, hist);
-    emurx_hist_to_counters(hist, delta);
+    memcpy(out_qoff, r.qoff, sizeof(r.qoff));
+    *delta = r.delta;
+    *n_out = r.n_frames;
     return EMURX_OK;
+}
+
+int emurx_ingest_buffer(emurx_t* h, uint32_t slot, size_t bytes, uint8_t** buf) {
+    if (!h || !buf || slot >= EMURX_INGEST_SLOTS) return EMURX_EINVAL;
+    int rc = bind(h);
+    return rc ? rc : ingest_buffer(h, slot, bytes, buf);
+}
+int emurx_ingest_submit(emurx_t* h, uint32_t slot, const emurx_msg* msgs, uint32_t nmsg) {
+    if (!h || slot >= EMURX_INGEST_SLOTS) return EMURX_EINVAL;
+    return ingest_submit(h, slot, msgs, nmsg);
+}
+int emurx_ingest_wait(emurx_t* h, uint32_t slot, emurx_ingest_result* res) {
+    if (!h || !res || slot >= EMURX_INGEST_SLOTS) return EMURX_EINVAL;
+    return ingest_wait(h, slot, res);
 }
 
 void emurx_hist_fold(const uint64_t* shards, uint64_t out[2 * EMURX_HIST_BINS]) {

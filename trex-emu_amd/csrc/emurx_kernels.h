@@ -17,3 +17,15 @@ int emurx_launch_batch(const uint8_t* frames, const emurx_desc* desc, uint32_t n
 int emurx_launch_route(const emurx_rec* rec, uint32_t n, uint32_t n_parts, uint32_t my_rank, uint32_t cap,
                        emurx_route_rec* send, uint32_t* send_count, uint32_t* tile_cnt, uint32_t* grp,
                        uint32_t* grp_off, hipStream_t st);
+
+// Batched ZMQ ingest (emurx_ingest.hip).  zmq_walk: one lane per message; ctl = emurx_msg[nmsg]
+// then slot_base[nmsg + 1]; writes desc[slot_base[m] ..) (holes marked EMURX_DESC_HOLE) and
+// msg_stat[m] = frames | EMURX_MSG_* << 24.  The buffer must be readable 8 bytes past every message.
+int emurx_launch_zmq_walk(const uint8_t* buf, const uint32_t* ctl, uint32_t nmsg, emurx_desc* desc,
+                          uint32_t* msg_stat, hipStream_t st);
+// Concatenate k_rx's per-tile queue segments (queue-major, frame order) into `packed`, write
+// qoff[EMURX_NUM_QUEUES + 1], fold the histogram shards into hist_out[2 * EMURX_HIST_BINS] and
+// clear the shards.  Scratch seg_off: [ceil(n / 256) * 16].  Two launches.
+int emurx_launch_queue_pack(const uint32_t* qlist, uint32_t qcap, const uint32_t* tile_cnt, uint32_t n,
+                            uint32_t* seg_off, uint32_t* packed, uint32_t* qoff, uint64_t* hist,
+                            uint64_t* hist_out, hipStream_t st);

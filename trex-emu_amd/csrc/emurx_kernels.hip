@@ -42,11 +42,11 @@ __global__ __launch_bounds__(kBlock) void k_rx(const uint8_t* __restrict__ frame
     const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / kWave;
     const uint32_t tile = blockIdx.x;
     const uint32_t i = tile * EMURX_QUEUE_TILE + tid;
-    const bool valid = i < n;
     s_hist[wv][lane] = 0;  // each wave owns its copy: no cross-wave ordering needed
     if (lane < 16) s_wcnt[wv][lane] = 0;
 
-    const uint2 dd = valid ? *reinterpret_cast<const uint2*>(desc + i) : make_uint2(0, 0);
+    const uint2 dd = i < n ? *reinterpret_cast<const uint2*>(desc + i) : make_uint2(0, EMURX_DESC_HOLE << 24);
+    const bool valid = (dd.y >> 24) != EMURX_DESC_HOLE;  // an empty slot is no frame at all
     const uint32_t off = dd.x, len = dd.y & 0xffff, vport = (dd.y >> 16) & 0xff;
 
     // the wave's byte range [lo, hi) -> copied HBM -> LDS by LDS-DMA when it fits the slab

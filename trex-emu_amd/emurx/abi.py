@@ -74,6 +74,10 @@ assert ROUTE_REC_DTYPE.itemsize == 40
 MAX_PARTS = 8
 DESC_DTYPE = np.dtype([("off", "<u4"), ("len", "<u2"), ("vport", "u1"), ("pad", "u1")])
 assert DESC_DTYPE.itemsize == 8
+DESC_HOLE = 0xFF   # EMURX_DESC_HOLE: an empty descriptor slot
+INGEST_SLOTS = 2   # EMURX_INGEST_SLOTS
+MSG_OK, MSG_PARSE_ERR, MSG_PANIC = 0, 1, 2
+MSG_DTYPE = np.dtype([("off", "<u4"), ("len", "<u4")])
 
 
 class Cfg(C.Structure):
@@ -91,6 +95,12 @@ class Counters(C.Structure):
         for k in ("rx_pkts", "rx_bytes", "rx_batch", "rx_parse_err", "ref_panic"):
             d[k] = int(getattr(self, k))
         return d
+
+
+class IngestResult(C.Structure):
+    _fields_ = [("rec", C.c_void_p), ("desc", C.c_void_p), ("qlist", C.c_void_p),
+                ("msg_frames", C.c_void_p), ("msg_status", C.c_void_p), ("n_frames", C.c_uint32),
+                ("n_msgs", C.c_uint32), ("qoff", C.c_uint32 * (NUM_QUEUES + 1)), ("delta", Counters)]
 
 
 class DevOut(C.Structure):
@@ -141,6 +151,9 @@ SIGNATURES = [
     ("emurx_kernel_times", C.c_int, [_P, _P, C.c_uint32, C.POINTER(C.c_uint32)]),
     ("emurx_ns_owner", C.c_uint32, [_U8P, C.c_uint32]),
     ("emurx_route_dev", C.c_int, [_P, _P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P]),
+    ("emurx_ingest_buffer", C.c_int, [_P, C.c_uint32, C.c_size_t, C.POINTER(C.c_void_p)]),
+    ("emurx_ingest_submit", C.c_int, [_P, C.c_uint32, _P, C.c_uint32]),
+    ("emurx_ingest_wait", C.c_int, [_P, C.c_uint32, C.POINTER(IngestResult)]),
 ]
 
 _lib = None

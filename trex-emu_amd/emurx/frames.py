@@ -218,6 +218,39 @@ def zmq_pack(frames, vports=None) -> bytes:
     return bytes(out)
 
 
+def zmq_messages(buf, desc, per_msg: int = 64):
+    """A batch in the ZMQ layout (synth.pack_zmq_layout: each frame preceded by its 4-byte
+    frame header) -> (stream, msgs): consecutive groups of `per_msg` frames as ZMQ messages
+    (a 4-byte batch header each) laid back to back in `stream`, and msgs[i] = (off, len) of
+    message i in it (emurx.abi.MSG_DTYPE).  Frames must be in buffer order, contiguous."""
+    import numpy as np
+    from .abi import MSG_DTYPE
+    n = len(desc)
+    off = desc["off"].astype(np.int64)
+    end = off + desc["len"].astype(np.int64)
+    first = np.arange(0, n, per_msg)
+    last = np.minimum(first + per_msg, n) - 1
+    src_lo, src_hi = off[first] - 4, end[last]
+    cnt = last - first + 1
+    mlen = 4 + (src_hi - src_lo)
+    moff = np.zeros(len(first), np.int64)
+    moff[1:] = np.cumsum(mlen[:-1])
+    total = int(mlen.sum())
+    stream = np.empty(total, np.uint8)
+    hdr = ((0xBEEF << 16) | (cnt & 0xFFFF)).astype(">u4").view(np.uint8).reshape(-1, 4)
+    idx = moff[:, None] + np.arange(4)[None, :]
+    stream[idx] = hdr
+    # frame bytes (with their frame headers) are contiguous per message in the source
+    lens = src_hi - src_lo
+    body = int(lens.sum())
+    if body:
+        k = np.arange(body) - np.repeat(np.cumsum(lens) - lens, lens)  # byte index inside its message body
+        stream[np.repeat(moff + 4, lens) + k] = np.asarray(buf)[np.repeat(src_lo, lens) + k]
+    msgs = np.zeros(len(first), MSG_DTYPE)
+    msgs["off"], msgs["len"] = moff, mlen
+    return stream, msgs
+
+
 def pack_frames(frames, vports=None, header: int = 4):
     """Concatenate frames with a `header`-byte gap before each (ZMQ layout when 4) and
     return (buffer, desc) with desc a numpy structured array (see emurx.abi.DESC_DTYPE)."""

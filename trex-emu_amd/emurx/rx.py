@@ -149,6 +149,37 @@ class RxPath:
         return a[: n.value]
 
 
+    # ---- batched host ingest (many ZMQ messages per GPU round trip) -------------------------
+    def ingest_buffer(self, slot: int, nbytes: int) -> np.ndarray:
+        """The slot's pinned staging buffer as a writable uint8 view of `nbytes`."""
+        p = C.c_void_p()
+        abi.check(self.lib.emurx_ingest_buffer(self.h, slot, nbytes, C.byref(p)), "ingest_buffer")
+        return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(max(nbytes, 1),))[:nbytes]
+
+    def ingest_submit(self, slot: int, msgs) -> None:
+        """msgs: MSG_DTYPE array (or [(off, len), ...]) of messages in the slot buffer."""
+        m = np.ascontiguousarray(np.asarray(msgs, dtype=np.uint32).reshape(-1, 2))
+        abi.check(self.lib.emurx_ingest_submit(self.h, slot, _p(m) if len(m) else None, len(m)),
+                  "ingest_submit")
+
+    def ingest_wait(self, slot: int, copy: bool = True) -> dict:
+        """Results of the slot's batch: rec, desc, qlist, qoff, msg_frames, msg_status,
+        counters (views into library memory unless copy)."""
+        r = abi.IngestResult()
+        abi.check(self.lib.emurx_ingest_wait(self.h, slot, C.byref(r)), "ingest_wait")
+        n, m = int(r.n_frames), int(r.n_msgs)
+
+        def view(ptr, count, dt):
+            if not count:
+                return np.zeros(0, dt)
+            b = np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_uint8)), shape=(count * np.dtype(dt).itemsize,))
+            v = b.view(dt)
+            return v.copy() if copy else v
+        return dict(rec=view(r.rec, n, abi.REC_DTYPE), desc=view(r.desc, n, abi.DESC_DTYPE),
+                    qlist=view(r.qlist, n, np.uint32), qoff=np.array(r.qoff, np.uint32),
+                    msg_frames=view(r.msg_frames, m, np.uint32), msg_status=view(r.msg_status, m, np.uint8),
+                    counters=r.delta.as_dict(), n=n)
+
     # ---- Namespace-partitioned exchange ---------------------------------------------------
     def route_dev(self, rec, n: int, n_parts: int, my_rank: int, cap: int, send, send_count, stream=None):
         """Pack the batch's records with a Namespace into their owners' send regions
