@@ -350,6 +350,51 @@ int emurx_ingest_submit(emurx_t* h, uint32_t slot, const emurx_msg* msgs, uint32
 /* Wait for the slot's batch and point `res` at its results (library-owned pinned memory). */
 int emurx_ingest_wait(emurx_t* h, uint32_t slot, emurx_ingest_result* res);
 
+/* ---- tx-side checksum generation -----------------------------------
+   What the plugins' tx paths do to a frame before Veth.Send, for a batch of frames in
+   device memory, in place.  Per frame, `ops` selects:
+     EMURX_TX_IPV4_HDR   IPv4Header(p[l3:l3+IHL*4]).UpdateChecksum()         ip4.go:132-136
+                   (the callers' slice is the whole header: 20 B in transport, tcp_output.go:110-112;
+                   24 B with IGMP's router-alert option, igmp.go:1179-1186)
+   and one L4 kind (ops >> EMURX_TX_L4_SHIFT), the field zeroed first, the span p[l4:len]:
+     TCP4 / UDP4   p[l4+16 | l4+6] = PktChecksumTcpUdp(p[l4:], 0, IPv4Header(p[l3:l3+20]))
+                   tcpip.go:38-40 + ip4.go:49-58 (callers tcp_output.go:64-70, udp.go:143-150)
+     TCP6 / UDP6 / ICMP6   IPv6Header(p[l3:l3+40]).FixL4ChecksumOffset(p[l4:], osize, 16 | 6 | 2)
+                   ip6.go:40-56,127-134 (tcp_output.go:71-76, udp.go:151-156, ipv6/nd.go:1111);
+                   with EMURX_TX_V6_NH the pseudo header's next header is `nh` instead of
+                   o.NextHeader(): PktChecksumTcpUdpV6(p[l4:], 0, ipv6, osize, nh) tcpip.go:34-36
+                   (MLD reports behind a hop-by-hop header, ipv6/mld.go:1271)
+     ICMP4         ICMPv4Header(p[l4:]).UpdateChecksum()                      icmp4.go:252-256
+   A frame whose header or field would lie past `len` (the Go slices panic there) is left
+   untouched and gets status EMURX_TX_RANGE. */
+#define EMURX_TX_IPV4_HDR 0x01u
+#define EMURX_TX_V6_NH 0x02u
+#define EMURX_TX_L4_SHIFT 4
+enum emurx_tx_l4 {
+    EMURX_TX_L4_NONE = 0,
+    EMURX_TX_L4_TCP4 = 1,
+    EMURX_TX_L4_UDP4 = 2,
+    EMURX_TX_L4_TCP6 = 3,
+    EMURX_TX_L4_UDP6 = 4,
+    EMURX_TX_L4_ICMP6 = 5,
+    EMURX_TX_L4_ICMP4 = 6
+};
+#define EMURX_TX_OK 0u
+#define EMURX_TX_RANGE 1u
+typedef struct emurx_tx_desc {
+    uint32_t off;      /* frame start in the buffer                              */
+    uint16_t len;      /* frame length (the L4 span ends here)                   */
+    uint16_t l3, l4;   /* header offsets in the frame                            */
+    uint16_t osize;    /* IPv6 extension bytes given to FixL4ChecksumOffset      */
+    uint8_t ops;       /* EMURX_TX_IPV4_HDR | EMURX_TX_V6_NH | kind << EMURX_TX_L4_SHIFT */
+    uint8_t nh;        /* pseudo-header next header with EMURX_TX_V6_NH          */
+    uint8_t pad[2];
+} emurx_tx_desc;       /* 16 bytes */
+/* d_frames: device buffer, rewritten in place; d_status: [n] EMURX_TX_* (may be NULL).
+   One launch on `stream`, no host synchronisation. */
+int emurx_tx_checksum_dev(emurx_t* h, uint8_t* d_frames, const emurx_tx_desc* d_desc, uint32_t n,
+                          uint8_t* d_status, void* stream);
+
 /* ParserStats delta from an outcome histogram (pure host arithmetic). */
 void emurx_hist_to_counters(const uint64_t hist[2 * EMURX_HIST_BINS], emurx_counters* out);
 /* Sum the EMURX_HIST_SHARDS copies of a device histogram (after a D2H copy). */

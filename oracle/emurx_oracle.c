@@ -885,3 +885,47 @@ int orc_rx_stream(const orc_t* o, const uint8_t* msg, size_t len, emurx_rec* rec
     free(d);
     return EMURX_OK;
 }
+
+/* ===================================================================================== */
+/* Tx-side checksum generation (the plugins' send paths)                                   */
+/* ===================================================================================== */
+static void put16(uint8_t* p, uint16_t v) { p[0] = (uint8_t)(v >> 8); p[1] = (uint8_t)v; }
+
+/* One frame, in place.  IPv4Header.UpdateChecksum ip4.go:132-136; PktChecksumTcpUdp
+   tcpip.go:38-40 with IPv4Header.GetPhCs ip4.go:49-58 as tcp_output.go:64-70 / udp.go:143-150
+   call it; IPv6Header.FixL4ChecksumOffset ip6.go:40-44 (+ GetPhCs :127-134, nextH =
+   o.NextHeader()); ICMPv4Header.UpdateChecksum icmp4.go:252-256. */
+uint8_t orc_tx_frame(uint8_t* p, uint32_t len, uint16_t l3, uint16_t l4, uint16_t osize, uint8_t ops,
+                     uint8_t nh) {
+    const int kind = ops >> EMURX_TX_L4_SHIFT;
+    static const int field[7] = {0, 16, 6, 16, 6, 2, 2};
+    if (kind > EMURX_TX_L4_ICMP4) return EMURX_TX_RANGE;
+    /* every slice the Go code takes must lie inside the frame */
+    if ((ops & EMURX_TX_IPV4_HDR) && (uint32_t)l3 + 20 > len) return EMURX_TX_RANGE;
+    /* the header slice: IHL * 4 bytes (20, or 24 with IGMP's router-alert option) */
+    const uint32_t hlen = (ops & EMURX_TX_IPV4_HDR) && (p[l3] & 0xf) > 5 ? (uint32_t)(p[l3] & 0xf) << 2 : 20;
+    if ((ops & EMURX_TX_IPV4_HDR) && (uint32_t)l3 + hlen > len) return EMURX_TX_RANGE;
+    if ((kind == EMURX_TX_L4_TCP4 || kind == EMURX_TX_L4_UDP4) && (uint32_t)l3 + 20 > len) return EMURX_TX_RANGE;
+    if (kind >= EMURX_TX_L4_TCP6 && kind <= EMURX_TX_L4_ICMP6 && (uint32_t)l3 + 40 > len) return EMURX_TX_RANGE;
+    if (kind && (uint32_t)l4 + field[kind] + 2 > len) return EMURX_TX_RANGE;
+    if (ops & EMURX_TX_IPV4_HDR) {
+        put16(p + l3 + 10, 0);
+        put16(p + l3 + 10, orc_checksum(p + l3, hlen, 0));
+    }
+    if (kind) {
+        uint8_t* f = p + l4 + field[kind];
+        uint32_t ph = 0;
+        put16(f, 0);
+        if (kind == EMURX_TX_L4_TCP4 || kind == EMURX_TX_L4_UDP4) ph = ipv4_phcs(p + l3);
+        else if (kind != EMURX_TX_L4_ICMP4) ph = ipv6_phcs(p + l3, osize, (ops & EMURX_TX_V6_NH) ? nh : p[l3 + 6]);
+        put16(f, orc_checksum(p + l4, len - l4, ph));
+    }
+    return EMURX_TX_OK;
+}
+
+void orc_tx_checksum(uint8_t* frames, const emurx_tx_desc* d, uint32_t n, uint8_t* status) {
+    for (uint32_t i = 0; i < n; i++) {
+        uint8_t st = orc_tx_frame(frames + d[i].off, d[i].len, d[i].l3, d[i].l4, d[i].osize, d[i].ops, d[i].nh);
+        if (status) status[i] = st;
+    }
+}

@@ -65,6 +65,10 @@ int orc_rx_stream(const orc_t* o, const uint8_t* msg, size_t len, emurx_rec* rec
 int orc_zmq_descriptors(const uint8_t* msg, size_t len, emurx_desc* out, uint32_t cap,
                         uint32_t* n_out, int* parse_err);
 
+/* tx checksum generation over a batch, in place (see emu_rx.h emurx_tx_checksum_dev) */
+uint8_t orc_tx_frame(uint8_t* p, uint32_t len, uint16_t l3, uint16_t l4, uint16_t osize, uint8_t ops, uint8_t nh);
+void orc_tx_checksum(uint8_t* frames, const emurx_tx_desc* d, uint32_t n, uint8_t* status);
+
 #ifdef __cplusplus
 }
 #endif

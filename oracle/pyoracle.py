@@ -20,6 +20,8 @@ REC_DTYPE = np.dtype([
     ("vport", "<u2"), ("l3", "<u2"), ("l4", "<u2"), ("l7", "<u2"), ("l7_len", "<u2"),
     ("next_hdr", "u1"), ("proto", "u1"), ("status", "u1"), ("flags", "u1"), ("rsv", "<u2")])
 DESC_DTYPE = np.dtype([("off", "<u4"), ("len", "<u2"), ("vport", "u1"), ("pad", "u1")])
+TX_DESC_DTYPE = np.dtype([("off", "<u4"), ("len", "<u2"), ("l3", "<u2"), ("l4", "<u2"), ("osize", "<u2"),
+                          ("ops", "u1"), ("nh", "u1"), ("pad", "u1", 2)])
 NPC = 50
 NQ = 13
 
@@ -64,6 +66,7 @@ def lib():
                                         C.POINTER(C.c_uint32), P, C.POINTER(Counters)]),
             ("orc_zmq_descriptors", C.c_int, [P, C.c_size_t, P, C.c_uint32,
                                               C.POINTER(C.c_uint32), C.POINTER(C.c_int)]),
+            ("orc_tx_checksum", None, [P, P, C.c_uint32, P]),
         ]:
             f = getattr(L, name)
             f.restype = res
@@ -189,6 +192,15 @@ def zmq_descriptors(msg: bytes, cap=1 << 16):
     rc = lib().orc_zmq_descriptors(m.ctypes.data, len(msg), d.ctypes.data, cap, C.byref(n),
                                    C.byref(e))
     return rc, d[:n.value], e.value
+
+
+def tx_checksum(buf: np.ndarray, desc: np.ndarray):
+    """orc_tx_checksum on a copy of buf -> (new buffer, status[n])."""
+    out = np.ascontiguousarray(buf, dtype=np.uint8).copy()
+    d = np.ascontiguousarray(desc).view(TX_DESC_DTYPE)
+    st = np.zeros(max(len(d), 1), np.uint8)
+    lib().orc_tx_checksum(out.ctypes.data, d.ctypes.data, len(d), st.ctypes.data)
+    return out, st[: len(d)]
 
 
 def counters_dict(cnt: Counters):

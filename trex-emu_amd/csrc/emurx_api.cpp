@@ -847,6 +847,16 @@ int emurx_kernel_times(emurx_t* h, float* batch_ms, uint32_t cap, uint32_t* n_ou
     return EMURX_OK;
 }
 
+int emurx_tx_checksum_dev(emurx_t* h, uint8_t* d_frames, const emurx_tx_desc* d_desc, uint32_t n,
+                          uint8_t* d_status, void* stream) {
+    if (!h || (n && (!d_frames || !d_desc))) return EMURX_EINVAL;
+    if ((uintptr_t)d_desc & 15) return EMURX_EINVAL;  // one 16-byte load per descriptor
+    int rc = bind(h);
+    if (rc) return rc;
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    return emurx_launch_tx_csum(d_frames, d_desc, n, d_status, st) ? EMURX_EDEVICE : EMURX_OK;
+}
+
 uint32_t emurx_ns_owner(const uint8_t key[12], uint32_t n_parts) {
     if (!key || n_parts == 0) return 0;
     return emurx_owner(emurx_tk_hash(le32(key), le32(key + 4), le32(key + 8)), n_parts);

@@ -29,3 +29,7 @@ int emurx_launch_zmq_walk(const uint8_t* buf, const uint32_t* ctl, uint32_t nmsg
 int emurx_launch_queue_pack(const uint32_t* qlist, uint32_t qcap, const uint32_t* tile_cnt, uint32_t n,
                             uint32_t* seg_off, uint32_t* packed, uint32_t* qoff, uint64_t* hist,
                             uint64_t* hist_out, hipStream_t st);
+
+// Tx checksum generation (emurx_tx.hip): one launch, in place; status may be null.
+int emurx_launch_tx_csum(uint8_t* frames, const emurx_tx_desc* desc, uint32_t n, uint8_t* status,
+                         hipStream_t st);

@@ -57,7 +57,7 @@ __global__ __launch_bounds__(kBlock) void k_rx(const uint8_t* __restrict__ frame
     const bool staged = nvec > 0 && nvec <= kStage / 16;
     uint4* wslab = reinterpret_cast<uint4*>(slab) + wv * (kStage / 16);
     if (staged) {  // all copies in flight before the wait; clamped sources stay in bounds
-        static_assert(kStage / 16 / kWave == 8, "staging assumes 8 vectors per lane");
+        static_assert(kStage / 16 <= 8 * kWave, "staging issues at most 8 vectors per lane");
         const uint4* src = reinterpret_cast<const uint4*>(frames + start);
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k)
@@ -68,7 +68,7 @@ __global__ __launch_bounds__(kBlock) void k_rx(const uint8_t* __restrict__ frame
         const uint4* src = reinterpret_cast<const uint4*>(fa & ~(uintptr_t)15);
         const uint32_t nv = valid ? (uint32_t)(((fa & 15) + len + 15) >> 4) : 0;  // vectors of the frame
 #pragma unroll
-        for (uint32_t k = 0; k < 8; ++k)
+        for (uint32_t k = 0; k < kWinVec; ++k)
             if (k < nv) glds16(src + k, wslab + k * kWave);
         wait_vm0();
     }
@@ -88,7 +88,7 @@ __global__ __launch_bounds__(kBlock) void k_rx(const uint8_t* __restrict__ frame
     } else {
         const uint32_t head = (uint32_t)((uintptr_t)(frames + off) & 15);
         WinSrc s{reinterpret_cast<const uint8_t*>(slab), slab, wv * kStage + lane * 16, head,
-                 min(8 * 16 - head, len), frames + off};
+                 min(kWinVec * 16 - head, len), frames + off};
         if (valid) parse_packet(s, len, vport, T.cb_mask, r);
         coop_checksum(r, frames + off);  // the wave's long L4 spans, converged
         if (valid && kClassify && !(EMURX_ABL & 2)) classify(s, len, T, r);
@@ -141,6 +141,7 @@ __global__ __launch_bounds__(kBlock) void k_rx(const uint8_t* __restrict__ frame
         }
     }
 }
+
 
 }  // namespace emurx
 

@@ -17,7 +17,10 @@ namespace emurx {
 constexpr int kWave = 64;
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / kWave;
-constexpr uint32_t kStage = 8192;  // LDS bytes staged per wave (64 frames)
+// LDS bytes staged per wave (64 frames).  7 KiB keeps a workgroup's LDS under 32 KiB, so
+// five workgroups (20 waves) fit a CU; waves whose frames span more take the window path
+constexpr uint32_t kStage = 7168;
+constexpr uint32_t kWinVec = kStage / 16 / 64;  // window path: 16-byte vectors per lane (112 B)
 
 #ifndef EMURX_ABL
 #define EMURX_ABL 0  // experiment-only stage ablation (tools/ablate.sh); 0 in every real build
@@ -460,7 +463,7 @@ __device__ __forceinline__ void coop_checksum(Rec& r, const uint8_t* f) {
     const uintptr_t my = (uintptr_t)(f + r.dstart);
     uint64_t pend = __ballot(r.dlen != 0);
     while (pend) {
-        constexpr int kB = 8;  // frames in flight
+        constexpr int kB = 4;  // frames in flight
         uint32_t J[kB], nv[kB];
         int h[kB], t[kB];
         const uint8_t* base[kB];

@@ -78,6 +78,12 @@ DESC_HOLE = 0xFF   # EMURX_DESC_HOLE: an empty descriptor slot
 INGEST_SLOTS = 2   # EMURX_INGEST_SLOTS
 MSG_OK, MSG_PARSE_ERR, MSG_PANIC = 0, 1, 2
 MSG_DTYPE = np.dtype([("off", "<u4"), ("len", "<u4")])
+TX_IPV4_HDR, TX_V6_NH, TX_L4_SHIFT = 0x01, 0x02, 4
+TX_L4_NONE, TX_L4_TCP4, TX_L4_UDP4, TX_L4_TCP6, TX_L4_UDP6, TX_L4_ICMP6, TX_L4_ICMP4 = range(7)
+TX_OK, TX_RANGE = 0, 1
+TX_DESC_DTYPE = np.dtype([("off", "<u4"), ("len", "<u2"), ("l3", "<u2"), ("l4", "<u2"), ("osize", "<u2"),
+                          ("ops", "u1"), ("nh", "u1"), ("pad", "u1", 2)])
+assert TX_DESC_DTYPE.itemsize == 16
 
 
 class Cfg(C.Structure):
@@ -154,6 +160,7 @@ SIGNATURES = [
     ("emurx_ingest_buffer", C.c_int, [_P, C.c_uint32, C.c_size_t, C.POINTER(C.c_void_p)]),
     ("emurx_ingest_submit", C.c_int, [_P, C.c_uint32, _P, C.c_uint32]),
     ("emurx_ingest_wait", C.c_int, [_P, C.c_uint32, C.POINTER(IngestResult)]),
+    ("emurx_tx_checksum_dev", C.c_int, [_P, _P, _P, C.c_uint32, _P, _P]),
 ]
 
 _lib = None

@@ -158,7 +158,9 @@ class RxPath:
 
     def ingest_submit(self, slot: int, msgs) -> None:
         """msgs: MSG_DTYPE array (or [(off, len), ...]) of messages in the slot buffer."""
-        m = np.ascontiguousarray(np.asarray(msgs, dtype=np.uint32).reshape(-1, 2))
+        a = np.asarray(msgs)
+        a = np.ascontiguousarray(a).view(np.uint32) if a.dtype.names else np.asarray(msgs, dtype=np.uint32)
+        m = np.ascontiguousarray(a).reshape(-1, 2)
         abi.check(self.lib.emurx_ingest_submit(self.h, slot, _p(m) if len(m) else None, len(m)),
                   "ingest_submit")
 
@@ -179,6 +181,13 @@ class RxPath:
                     qlist=view(r.qlist, n, np.uint32), qoff=np.array(r.qoff, np.uint32),
                     msg_frames=view(r.msg_frames, m, np.uint32), msg_status=view(r.msg_status, m, np.uint8),
                     counters=r.delta.as_dict(), n=n)
+
+    # ---- tx-side checksum generation ------------------------------------------------------
+    def tx_checksum_dev(self, frames, desc, n: int, status=None, stream=None):
+        """Rewrite the checksums selected by each TX_DESC_DTYPE descriptor, in place on the
+        device buffer `frames` (include/emu_rx.h emurx_tx_checksum_dev)."""
+        return abi.check(self.lib.emurx_tx_checksum_dev(self.h, _addr(frames), _addr(desc), n, _addr(status),
+                                                        _stream(stream)), "tx_checksum_dev")
 
     # ---- Namespace-partitioned exchange ---------------------------------------------------
     def route_dev(self, rec, n: int, n_parts: int, my_rank: int, cap: int, send, send_count, stream=None):
