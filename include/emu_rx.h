@@ -236,7 +236,22 @@ typedef struct emurx_dev_out {
     uint32_t qcap;         /* per-queue region, >= ceil(n / TILE) * TILE                    */
     uint32_t* tile_cnt;    /* [ceil(n / TILE) * 16] frames per (tile, queue), 13 used of 16  */
     uint64_t* hist;        /* [EMURX_HIST_SHARDS * 2 * EMURX_HIST_BINS], ACCUMULATED         */
+    uint32_t* flow;        /* [n] transport flow outcome (EMURX_FLOW_* / flow id), or NULL   */
 } emurx_dev_out;
+
+/* Transport flow outcome per frame (emurx_dev_out.flow), the decision
+   TransportCtx.handleRxPacket (src/emu/plugins/transport/client_ctx.go:912-969) takes before
+   any socket code runs.  Only frames that reach a client's transport handler get one of these
+   (tcp / udp callback, lookup EMURX_LK_CLIENT); the key is the reference's c5tuplekey
+   (client_ctx.go:44-112): src, dst, src port, dst port, protocol (IPv4: the header's protocol
+   field; IPv6: ParserPacketState.NextHeader). */
+#define EMURX_FLOW_NONE 0xFFFFFFFFu      /* the transport handler is not reached              */
+#define EMURX_FLOW_NO_CTX 0xFFFFFFF0u    /* client without a TransportCtx: handler returns -1
+                                            (PluginTransClient.handleRxTransPacket :73-80)     */
+#define EMURX_FLOW_NO_SYN 0xFFFFFFF1u    /* new TCP flow without a bare SYN (ft_new_tcp_no_syn) :840-844 */
+#define EMURX_FLOW_NO_SERVER 0xFFFFFFF2u /* new flow, no listener on the port (ft_new_no_cb) :848-853,884-887 */
+#define EMURX_FLOW_NEW 0xFFFFFFF3u       /* new flow with a listener: OnAccept runs in Go :855-868,890-903 */
+#define EMURX_FLOW_ID_MAX 0xFFFFFFEFu    /* flow ids are 0 .. EMURX_FLOW_ID_MAX                */
 
 typedef struct emurx_ctx emurx_t;
 
@@ -268,6 +283,19 @@ int emurx_client_update_ipv6(emurx_t* h, uint32_t client_id, const uint8_t ipv6[
 int emurx_client_update_dipv6(emurx_t* h, uint32_t client_id, const uint8_t dhcpv6[16]);
 int emurx_client_set_ra(emurx_t* h, uint32_t client_id, const uint8_t prefix[16],
                         uint8_t prefix_len);
+/* Transport flow tables.  A flow key is the reference's tuple bytes: 13 for IPv4
+   (c5tuplekeyv4: src[4] dst[4] sport BE dport BE proto), 37 for IPv6 (c5tuplekeyv6: src[16]
+   dst[16] sport dport next header), as buildTuplev4/v6 (client_ctx.go:89-112) builds it from a
+   received frame.  flow_add / flow_remove mirror TransportCtx.addFlowv4/6 / removeFlowv4/6
+   (client_ctx.go:597-651); server_add / server_remove the listener map serverCb
+   (lookupServerPort :1142-1155, proto 6 or 17).  Adding either marks the client as having a
+   TransportCtx (created on first use, socketApi.go:174-193); client_set_transport sets or
+   clears that mark directly.  Removing a client drops its flows and listeners. */
+int emurx_flow_add(emurx_t* h, uint32_t client_id, const uint8_t* tuple, uint32_t tuple_len, uint32_t flow_id);
+int emurx_flow_remove(emurx_t* h, uint32_t client_id, const uint8_t* tuple, uint32_t tuple_len);
+int emurx_server_add(emurx_t* h, uint32_t client_id, uint16_t port, uint8_t proto);
+int emurx_server_remove(emurx_t* h, uint32_t client_id, uint16_t port, uint8_t proto);
+int emurx_client_set_transport(emurx_t* h, uint32_t client_id, int has_ctx);
 /* Upload pending table deltas to the device (enqueued on `stream`, or the handle's own
    stream when NULL).  Called implicitly by emurx_rx_stream. */
 int emurx_sync(emurx_t* h, void* stream);

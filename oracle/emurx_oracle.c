@@ -105,6 +105,7 @@ typedef struct {
     uint8_t dhcpv6[16];
     uint32_t plugins;
     int has_ra;              /* Ipv6Router != nil */
+    int has_ctx;             /* GetTransportCtx() != nil (socketApi.go:174-193) */
     uint8_t ra_prefix[16];   /* Ipv6Router.PrefixIpv6 */
     uint8_t ra_plen;         /* Ipv6Router.PrefixLen */
 } orc_client;
@@ -123,6 +124,9 @@ struct orc {
     bmap mac_map;    /* ns_id|MAC (10 B)  -> client  (MapClientMAC) */
     bmap ip4_map;    /* ns_id|IPv4 (8 B)  -> client  (MapClientIPv4) */
     bmap ip6_map;    /* ns_id|IPv6 (20 B) -> client  (MapClientIPv6) */
+    bmap ft4_map;    /* client|c5tuplekeyv4 (4+13 B) -> flow (TransportCtx.ftv4) */
+    bmap ft6_map;    /* client|c5tuplekeyv6 (4+37 B) -> flow (TransportCtx.ftv6) */
+    bmap srv_map;    /* client|port BE|proto (7 B) -> 1 (TransportCtx.serverCb)   */
     orc_ns* ns; uint32_t nns;
     orc_client* cl; uint32_t ncl;
 };
@@ -142,12 +146,16 @@ orc_t* orc_new(void) {
     bmap_init(&o->mac_map, 10);
     bmap_init(&o->ip4_map, 8);
     bmap_init(&o->ip6_map, 20);
+    bmap_init(&o->ft4_map, 17);
+    bmap_init(&o->ft6_map, 41);
+    bmap_init(&o->srv_map, 7);
     o->cb_mask = (1u << EMURX_NUM_CB) - 1u; /* production registers all 12 (trex-emu.go:47-67) */
     return o;
 }
 void orc_free(orc_t* o) {
     if (!o) return;
     bmap_free(&o->ns_map); bmap_free(&o->mac_map); bmap_free(&o->ip4_map); bmap_free(&o->ip6_map);
+    bmap_free(&o->ft4_map); bmap_free(&o->ft6_map); bmap_free(&o->srv_map);
     for (uint32_t i = 0; i < o->nns; i++) free(o->ns[i].order);
     free(o->ns); free(o->cl); free(o);
 }
@@ -253,6 +261,14 @@ int orc_client_remove(orc_t* o, uint32_t ns_id, const uint8_t mac[6]) {
     if (!is_zero(c->ipv4, 4)) { mk_key(k, ns_id, c->ipv4, 4); bmap_del(&o->ip4_map, k); }
     if (!is_zero(c->ipv6, 16)) { mk_key(k, ns_id, c->ipv6, 16); bmap_del(&o->ip6_map, k); }
     if (!is_zero(c->dhcpv6, 16)) { mk_key(k, ns_id, c->dhcpv6, 16); bmap_del(&o->ip6_map, k); }
+    /* TransportCtx.onRemove client_ctx.go:579-595: the client's sockets go with it */
+    bmap* tm[3] = {&o->ft4_map, &o->ft6_map, &o->srv_map};
+    for (int t = 0; t < 3; t++)
+        for (uint32_t i = 0; i < tm[t]->cap; i++)
+            if (tm[t]->state[i] == 1 && !memcmp(tm[t]->keys + (size_t)i * tm[t]->ksz, &cid, 4)) {
+                tm[t]->state[i] = 2; tm[t]->used--; tm[t]->tomb++;
+            }
+    c->has_ctx = 0;
     c->alive = 0;
     return EMURX_OK;
 }
@@ -928,4 +944,106 @@ void orc_tx_checksum(uint8_t* frames, const emurx_tx_desc* d, uint32_t n, uint8_
         uint8_t st = orc_tx_frame(frames + d[i].off, d[i].len, d[i].l3, d[i].l4, d[i].osize, d[i].ops, d[i].nh);
         if (status) status[i] = st;
     }
+}
+
+/* ===================================================================================== */
+/* Transport flow tables and TransportCtx.handleRxPacket's decision                       */
+/* ===================================================================================== */
+static int orc_client_ok(const orc_t* o, uint32_t cid) { return cid < o->ncl && o->cl[cid].alive; }
+
+/* TransportCtx.addFlowv4 / addFlowv6 client_ctx.go:629-651 (duplicate: ft_add_err_already_exits) */
+int orc_flow_add(orc_t* o, uint32_t cid, const uint8_t* tuple, uint32_t tlen, uint32_t flow) {
+    uint8_t k[41];
+    if (!tuple || (tlen != 13 && tlen != 37)) return EMURX_EINVAL;
+    if (!orc_client_ok(o, cid)) return EMURX_ENOENT;
+    if (flow > EMURX_FLOW_ID_MAX) return EMURX_EINVAL;
+    memcpy(k, &cid, 4);
+    memcpy(k + 4, tuple, tlen);
+    bmap* m = tlen == 13 ? &o->ft4_map : &o->ft6_map;
+    if (bmap_find(m, k, NULL)) return EMURX_EEXIST;
+    bmap_put(m, k, flow);
+    o->cl[cid].has_ctx = 1; /* the socket's TransportCtx (socketApi.go:174-193) */
+    return EMURX_OK;
+}
+/* TransportCtx.removeFlowv4 / removeFlowv6 client_ctx.go:597-627 */
+int orc_flow_remove(orc_t* o, uint32_t cid, const uint8_t* tuple, uint32_t tlen) {
+    uint8_t k[41];
+    if (!tuple || (tlen != 13 && tlen != 37)) return EMURX_EINVAL;
+    if (!orc_client_ok(o, cid)) return EMURX_ENOENT;
+    memcpy(k, &cid, 4);
+    memcpy(k + 4, tuple, tlen);
+    bmap* m = tlen == 13 ? &o->ft4_map : &o->ft6_map;
+    if (!bmap_find(m, k, NULL)) return EMURX_ENOENT;
+    bmap_del(m, k);
+    return EMURX_OK;
+}
+static void srv_key(uint8_t* k, uint32_t cid, uint16_t port, uint8_t proto) {
+    memcpy(k, &cid, 4);
+    k[4] = (uint8_t)(port >> 8); k[5] = (uint8_t)port; k[6] = proto;
+}
+/* serverCb[port][proto] (TransportCtx.serverCb, client_ctx.go:496; lookupServerPort :1142-1155) */
+int orc_server_add(orc_t* o, uint32_t cid, uint16_t port, uint8_t proto) {
+    uint8_t k[7];
+    if (proto != 6 && proto != 17) return EMURX_EINVAL;
+    if (!orc_client_ok(o, cid)) return EMURX_ENOENT;
+    srv_key(k, cid, port, proto);
+    if (bmap_find(&o->srv_map, k, NULL)) return EMURX_EEXIST;
+    bmap_put(&o->srv_map, k, 1);
+    o->cl[cid].has_ctx = 1;
+    return EMURX_OK;
+}
+int orc_server_remove(orc_t* o, uint32_t cid, uint16_t port, uint8_t proto) {
+    uint8_t k[7];
+    if (proto != 6 && proto != 17) return EMURX_EINVAL;
+    if (!orc_client_ok(o, cid)) return EMURX_ENOENT;
+    srv_key(k, cid, port, proto);
+    if (!bmap_find(&o->srv_map, k, NULL)) return EMURX_ENOENT;
+    bmap_del(&o->srv_map, k);
+    return EMURX_OK;
+}
+int orc_client_set_transport(orc_t* o, uint32_t cid, int has_ctx) {
+    if (!orc_client_ok(o, cid)) return EMURX_ENOENT;
+    o->cl[cid].has_ctx = has_ctx != 0;
+    return EMURX_OK;
+}
+
+/* The flow decision for one classified frame: HandleRxTransPacket plugin_transport.go:117-128
+   -> handleRxTransPacket :83-115 -> PluginTransClient.handleRxTransPacket :73-80 ->
+   TransportCtx.handleRxPacket client_ctx.go:912-969 (fillv4tuple / fillv6tuple :720-765),
+   handleRxTcpNewFlow :829-869, handleRxUdpNewFlow :871-904 up to OnAccept. */
+static uint32_t flow_of(const orc_t* o, const uint8_t* p, uint32_t len, const emurx_rec* r) {
+    if (r->status != EMURX_ST_OK || (r->proto != EMURX_CB_TCP && r->proto != EMURX_CB_UDP)) return EMURX_FLOW_NONE;
+    if (((r->flags & EMURX_FLAG_LK_MASK) >> EMURX_FLAG_LK_SHIFT) != EMURX_LK_CLIENT) return EMURX_FLOW_NONE;
+    const orc_client* c = &o->cl[r->client_id];
+    if (!c->has_ctx) return EMURX_FLOW_NO_CTX;
+    const uint8_t* ip = p + r->l3;
+    const uint8_t* udp = p + r->l4; /* layers.UDPHeader(p[ps.L4 : ps.L4+4]) */
+    uint8_t k[41];
+    uint32_t v, proto;
+    memcpy(k, &r->client_id, 4);
+    if ((ip[0] >> 4) == 4) { /* buildTuplev4 :89-99 */
+        memcpy(k + 4, ip + 12, 4);
+        memcpy(k + 8, ip + 16, 4);
+        memcpy(k + 12, udp, 4);
+        proto = k[16] = ip[9];
+        if (bmap_find(&o->ft4_map, k, &v)) return v;
+    } else { /* buildTuplev6 :101-112 */
+        memcpy(k + 4, ip + 8, 16);
+        memcpy(k + 20, ip + 24, 16);
+        memcpy(k + 36, udp, 4);
+        proto = k[40] = r->next_hdr;
+        if (bmap_find(&o->ft6_map, k, &v)) return v;
+    }
+    if (proto == 6) { /* TcpHeader(p[ps.L4:ps.L4+20]).GetFlags() & 0x3F != 0x2: ft_new_tcp_no_syn */
+        uint8_t flags = (uint32_t)r->l4 + 13 < len ? udp[13] : 0; /* past the frame: stale mbuf bytes in Go */
+        if ((flags & 0x3f) != 0x2) return EMURX_FLOW_NO_SYN;
+    }
+    uint8_t sk[7];
+    srv_key(sk, r->client_id, (uint16_t)((udp[2] << 8) | udp[3]), proto == 6 ? 6 : 17);
+    return bmap_find(&o->srv_map, sk, NULL) ? EMURX_FLOW_NEW : EMURX_FLOW_NO_SERVER;
+}
+
+void orc_flows(const orc_t* o, const uint8_t* frames, const emurx_desc* desc, const emurx_rec* rec,
+               uint32_t n, uint32_t* flow) {
+    for (uint32_t i = 0; i < n; i++) flow[i] = flow_of(o, frames + desc[i].off, desc[i].len, &rec[i]);
 }

@@ -65,6 +65,15 @@ int orc_rx_stream(const orc_t* o, const uint8_t* msg, size_t len, emurx_rec* rec
 int orc_zmq_descriptors(const uint8_t* msg, size_t len, emurx_desc* out, uint32_t cap,
                         uint32_t* n_out, int* parse_err);
 
+/* transport flow tables + the per-frame flow decision (see emu_rx.h emurx_flow_add) */
+int orc_flow_add(orc_t* o, uint32_t cid, const uint8_t* tuple, uint32_t tlen, uint32_t flow);
+int orc_flow_remove(orc_t* o, uint32_t cid, const uint8_t* tuple, uint32_t tlen);
+int orc_server_add(orc_t* o, uint32_t cid, uint16_t port, uint8_t proto);
+int orc_server_remove(orc_t* o, uint32_t cid, uint16_t port, uint8_t proto);
+int orc_client_set_transport(orc_t* o, uint32_t cid, int has_ctx);
+void orc_flows(const orc_t* o, const uint8_t* frames, const emurx_desc* desc, const emurx_rec* rec,
+               uint32_t n, uint32_t* flow);
+
 /* tx checksum generation over a batch, in place (see emu_rx.h emurx_tx_checksum_dev) */
 uint8_t orc_tx_frame(uint8_t* p, uint32_t len, uint16_t l3, uint16_t l4, uint16_t osize, uint8_t ops, uint8_t nh);
 void orc_tx_checksum(uint8_t* frames, const emurx_tx_desc* d, uint32_t n, uint8_t* status);

@@ -67,6 +67,12 @@ def lib():
             ("orc_zmq_descriptors", C.c_int, [P, C.c_size_t, P, C.c_uint32,
                                               C.POINTER(C.c_uint32), C.POINTER(C.c_int)]),
             ("orc_tx_checksum", None, [P, P, C.c_uint32, P]),
+            ("orc_flow_add", C.c_int, [P, C.c_uint32, P, C.c_uint32, C.c_uint32]),
+            ("orc_flow_remove", C.c_int, [P, C.c_uint32, P, C.c_uint32]),
+            ("orc_server_add", C.c_int, [P, C.c_uint32, C.c_uint16, C.c_uint8]),
+            ("orc_server_remove", C.c_int, [P, C.c_uint32, C.c_uint16, C.c_uint8]),
+            ("orc_client_set_transport", C.c_int, [P, C.c_uint32, C.c_int]),
+            ("orc_flows", None, [P, P, P, P, C.c_uint32, P]),
         ]:
             f = getattr(L, name)
             f.restype = res
@@ -138,6 +144,34 @@ class Oracle:
     def client_set_ra(self, cid, prefix, plen):
         a = _b(prefix, 16)
         return lib().orc_client_set_ra(self._h, cid, a.ctypes.data, plen)
+
+    # ---- transport flow tables --------------------------------------------------------
+    def flow_add(self, cid, tuple_bytes, flow_id):
+        t = _b(tuple_bytes)
+        return lib().orc_flow_add(self._h, cid, t.ctypes.data, len(t), flow_id)
+
+    def flow_remove(self, cid, tuple_bytes):
+        t = _b(tuple_bytes)
+        return lib().orc_flow_remove(self._h, cid, t.ctypes.data, len(t))
+
+    def server_add(self, cid, port, proto):
+        return lib().orc_server_add(self._h, cid, port, proto)
+
+    def server_remove(self, cid, port, proto):
+        return lib().orc_server_remove(self._h, cid, port, proto)
+
+    def client_set_transport(self, cid, has_ctx):
+        return lib().orc_client_set_transport(self._h, cid, int(has_ctx))
+
+    def flows(self, buf, desc, rec):
+        """TransportCtx.handleRxPacket's decision per classified frame (EMURX_FLOW_* / id)."""
+        n = len(desc)
+        out = np.zeros(max(n, 1), np.uint32)
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        d = np.ascontiguousarray(desc).view(DESC_DTYPE)
+        r = np.ascontiguousarray(rec).view(REC_DTYPE)
+        lib().orc_flows(self._h, buf.ctypes.data, d.ctypes.data, r.ctypes.data, n, out.ctypes.data)
+        return out[:n]
 
     # ---- data path ------------------------------------------------------------------
     def parse_frame(self, frame: bytes, vport: int = 0):

@@ -14,7 +14,7 @@ def to_dev(a: np.ndarray, pad: int = 64):
     return t
 
 
-def run_dev(rx, buf, desc, classify=True, qcap=None):
+def run_dev(rx, buf, desc, classify=True, qcap=None, flows=False):
     """-> rec, qlist (packed in queue order), qoff(14), hist(2*64) as numpy, via
     emurx_classify_dev / emurx_parse_dev (per-tile queue segments, sharded histogram)."""
     import torch
@@ -27,11 +27,15 @@ def run_dev(rx, buf, desc, classify=True, qcap=None):
     qlist = torch.full((abi.NUM_QUEUES * qcap,), -1, dtype=torch.int32, device="cuda")
     tile_cnt = torch.full((nt * 16,), -1, dtype=torch.int32, device="cuda")
     hist = torch.zeros(abi.HIST_SHARDS * 2 * abi.HIST_BINS, dtype=torch.int64, device="cuda")
-    rx.classify_dev(tb, td, n, rec, qlist, qcap, tile_cnt, hist, classify=classify)
+    flow = torch.full((max(n, 1),), 0x5A5A5A5A, dtype=torch.int32, device="cuda") if flows else None
+    rx.classify_dev(tb, td, n, rec, qlist, qcap, tile_cnt, hist, classify=classify, flow=flow)
     torch.cuda.synchronize()
     r = rec.cpu().numpy()[: n * 32].view(abi.REC_DTYPE)
     packed, qoff = pack_queues(qlist.cpu().numpy(), qcap, tile_cnt.cpu().numpy(), n)
-    return r, packed, qoff, hist_fold(hist.cpu().numpy().view(np.uint64))
+    out = (r, packed, qoff, hist_fold(hist.cpu().numpy().view(np.uint64)))
+    if flows:
+        out += (flow.cpu().numpy().view(np.uint32)[:n],)
+    return out
 
 
 def rec_diff(a, b, limit=5):
@@ -101,3 +105,20 @@ def load_frame_tables(targets, ns, clients, plug_ns=abi.PLUG_ALL, plug_cl=abi.PL
         for (nsid, mac), (cid, ip4, ip6) in clients.items():
             p = plug_cl if cid % 7 else plug_cl & ~(1 << 7)  # some clients without transport
             assert t.client_add(nsid, cid, mac, ip4, ip6, None, p) == 0
+
+
+def frame_tuples(buf, desc, rec):
+    """The reference's c5tuplekey bytes of every tcp/udp frame reaching a client (client_ctx.go:
+    89-112): 13 bytes for IPv4, 37 for IPv6; None elsewhere."""
+    out = []
+    for d, r in zip(desc, rec):
+        if r["status"] != 0 or r["proto"] not in (abi.CB_TCP, abi.CB_UDP) or (r["flags"] >> 4) & 7 != abi.LK["CLIENT"]:
+            out.append(None)
+            continue
+        p = buf[d["off"]:d["off"] + d["len"]].tobytes()
+        l3, l4 = int(r["l3"]), int(r["l4"])
+        if p[l3] >> 4 == 4:
+            out.append(p[l3 + 12:l3 + 20] + p[l4:l4 + 4] + bytes([p[l3 + 9]]))
+        else:
+            out.append(p[l3 + 8:l3 + 40] + p[l4:l4 + 4] + bytes([int(r["next_hdr"])]))
+    return out

@@ -494,3 +494,55 @@ def test_tx_checksum_fuzz_vs_oracle(rxmod):
     bad = np.nonzero(got != want)[0]
     assert len(bad) == 0, (len(bad), bad[:10])
     assert (wst == abi.TX_OK).sum() > n // 3 and (wst == abi.TX_RANGE).sum() > n // 10
+
+
+# ---- transport flow decision (TransportCtx.handleRxPacket) -------------------------------
+def test_transport_flows(rxmod):
+    """Per-frame flow outcome (flow id / no TransportCtx / no SYN / no listener / new) equals the
+    oracle's restatement over IPv4 and IPv6 TCP/UDP traffic with flows, listeners and
+    TransportCtx marks on a random subset; then after flow, listener and client removals."""
+    from gpu_util import frame_tuples
+    rng = np.random.default_rng(0xF10)
+    w = synth.config_c(30000, syn=0.3)
+    rx, o = new_pair(rxmod)
+    synth.load_tables(w, rx)
+    synth.load_tables(w, o)
+    buf, desc = w["buf"], w["desc"]
+    orec, _, _, _ = o.rx_batch(buf, desc)
+    tup = frame_tuples(buf, desc, orec)
+    idx = np.array([i for i, t in enumerate(tup) if t is not None])
+    assert len(idx) > 15000
+    for i in rng.choice(idx, len(idx) * 2 // 5, replace=False):
+        cid = int(orec[i]["client_id"])
+        assert rx.flow_add(cid, tup[i], int(i)) == o.flow_add(cid, tup[i], int(i))
+    for i in rng.choice(idx, len(idx) // 4, replace=False):
+        cid, t = int(orec[i]["client_id"]), tup[i]
+        dport = (t[10] << 8 | t[11]) if len(t) == 13 else (t[34] << 8 | t[35])
+        proto = 6 if orec[i]["proto"] == abi.CB_TCP else 17
+        assert rx.server_add(cid, dport, proto) == o.server_add(cid, dport, proto)
+    cids = np.unique(orec["client_id"][idx])
+    for c in rng.choice(cids, len(cids) // 5, replace=False):
+        v = int(rng.integers(0, 2))
+        assert rx.client_set_transport(int(c), v) == o.client_set_transport(int(c), v) == 0
+
+    def check():
+        rec, _, _, _, flow = run_dev(rx, buf, desc, flows=True)
+        orec2, _, _, _ = o.rx_batch(buf, desc)
+        assert rec.tobytes() == orec2.tobytes(), rec_diff(rec, orec2)
+        want = o.flows(buf, desc, orec2)
+        bad = np.nonzero(flow != want)[0]
+        assert len(bad) == 0, (len(bad), [(int(flow[b]), int(want[b])) for b in bad[:5]])
+        return want
+
+    want = check()
+    for code in (abi.FLOW_NONE, abi.FLOW_NO_CTX, abi.FLOW_NO_SYN, abi.FLOW_NO_SERVER, abi.FLOW_NEW):
+        assert (want == code).sum() > 50, hex(code)
+    assert (want <= abi.FLOW_ID_MAX).sum() > 5000
+    for i in rng.choice(idx, 2000, replace=False):
+        cid = int(orec[i]["client_id"])
+        assert rx.flow_remove(cid, tup[i]) == o.flow_remove(cid, tup[i])
+    c = w["clients"]
+    for k in rng.choice(len(c["cid"]), 200, replace=False):
+        assert rx.client_remove(int(c["ns"][k]), c["mac"][k].tobytes()) == \
+            o.client_remove(int(c["ns"][k]), c["mac"][k].tobytes())
+    check()

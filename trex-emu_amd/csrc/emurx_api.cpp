@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <string>
 #include <unordered_map>
 #include <vector>
 
@@ -70,6 +71,7 @@ struct ClientInfo {
     bool has_ra = false;
     uint8_t ra_prefix[16] = {0};
     uint8_t ra_plen = 0;
+    bool has_ctx = false;  // CClient.GetTransportCtx() != nil
 };
 
 template <class T>
@@ -159,6 +161,14 @@ struct emurx_ctx {
     std::vector<ClientInfo> cl;
     bool dirty = true;
 
+    // transport tables: (client id, tuple bytes) -> flow id; listeners (client id, port | proto << 16)
+    std::unordered_map<std::string, uint32_t> ft_map;
+    std::unordered_map<uint64_t, uint32_t> srv_map;
+    uint32_t ft4_buckets = 1, ft6_buckets = 1, srv_buckets = 1;
+    DevBuf<uint32_t> d_ft4, d_ft6, d_srv;
+    std::vector<uint32_t> h_ft4, h_ft6, h_srv;
+    bool ft_on = false;
+
     // device tables
     uint32_t ns_buckets = 0, mac_buckets = 0, ip4_buckets = 0, ip6_buckets = 0;
     DevBuf<uint32_t> d_ns, d_nsinfo, d_mac, d_ip4, d_ip6, d_client;
@@ -189,6 +199,13 @@ struct emurx_ctx {
         T.max_ns = cfg.max_ns;
         T.max_clients = cfg.max_clients;
         T.cb_mask = cb_mask;
+        T.ft_on = ft_on ? 1u : 0u;
+        T.ft4_tab = d_ft4.p;
+        T.ft6_tab = d_ft6.p;
+        T.srv_tab = d_srv.p;
+        T.ft4_mask = ft4_buckets - 1;
+        T.ft6_mask = ft6_buckets - 1;
+        T.srv_mask = srv_buckets - 1;
         return T;
     }
 };
@@ -213,6 +230,46 @@ void bucket_put(std::vector<uint32_t>& t, uint32_t bmask, uint32_t words, uint32
 void empty_table(std::vector<uint32_t>& t, uint32_t buckets, uint32_t words) {
     t.assign((size_t)buckets * EMURX_BUCKET_WORDS, 0);
     for (size_t i = words - 1; i < t.size(); i += words) t[i] = EMURX_EMPTY;
+}
+
+// transport tables, sized to their entries (load <= 1/2 in slots), device buffers grown on demand
+int build_transport(emurx_t* h) {
+    size_t n4 = 0, n6 = 0;
+    for (auto& kv : h->ft_map) (kv.first.size() == 4 + 13 ? n4 : n6)++;
+    h->ft4_buckets = pow2_at_least(2 * n4 + 2) / 2;
+    h->ft6_buckets = pow2_at_least(2 * n6 + 1);
+    h->srv_buckets = pow2_at_least(2 * h->srv_map.size() + 4) / 4;
+    empty_table(h->h_ft4, h->ft4_buckets, 8);
+    empty_table(h->h_ft6, h->ft6_buckets, 16);
+    empty_table(h->h_srv, h->srv_buckets, 4);
+    for (auto& kv : h->ft_map) {
+        const uint8_t* k = reinterpret_cast<const uint8_t*>(kv.first.data());
+        const uint32_t cid = le32(k);
+        const uint8_t* t = k + 4;
+        if (kv.first.size() == 4 + 13) {
+            uint32_t e[8] = {cid, le32(t), le32(t + 4), le32(t + 8), t[12], 0, 0, kv.second};
+            bucket_put(h->h_ft4, h->ft4_buckets - 1, 8, emurx_ft4_hash(cid, e[1], e[2], e[3], e[4]), e);
+        } else {
+            uint32_t e[16] = {cid};
+            for (int j = 0; j < 4; ++j) {
+                e[1 + j] = le32(t + 4 * j);
+                e[5 + j] = le32(t + 16 + 4 * j);
+            }
+            e[9] = le32(t + 32);
+            e[10] = t[36];
+            e[15] = kv.second;
+            bucket_put(h->h_ft6, h->ft6_buckets - 1, 16, emurx_ft6_hash(cid, e + 1, e + 5, e[9], e[10]), e);
+        }
+    }
+    for (auto& kv : h->srv_map) {
+        uint32_t e[4] = {(uint32_t)(kv.first >> 32), (uint32_t)kv.first, 0, 1};
+        bucket_put(h->h_srv, h->srv_buckets - 1, 4, emurx_srv_hash(e[0], e[1]), e);
+    }
+    h->ft_on = false;
+    for (auto& c : h->cl) h->ft_on = h->ft_on || (c.alive && c.has_ctx);
+    if (h->d_ft4.alloc(h->h_ft4.size()) || h->d_ft6.alloc(h->h_ft6.size()) || h->d_srv.alloc(h->h_srv.size()))
+        return -1;
+    return 0;
 }
 
 int rebuild_and_upload(emurx_t* h, hipStream_t st) {
@@ -270,12 +327,15 @@ int rebuild_and_upload(emurx_t* h, hipStream_t st) {
         o[3] = (c.has_ra ? 1u : 0u) | ((uint32_t)c.ra_plen << 8);
         o[4] = le32(c.ra_prefix);
         o[5] = le32(c.ra_prefix + 4);
+        o[6] = c.has_ctx ? 1u : 0u;
     }
+    if (build_transport(h)) return EMURX_ENOMEM;
     struct {
         uint32_t* d;
         std::vector<uint32_t>* h;
     } up[] = {{h->d_ns.p, &h->h_ns},   {h->d_nsinfo.p, &h->h_nsinfo}, {h->d_mac.p, &h->h_mac},
-              {h->d_ip4.p, &h->h_ip4}, {h->d_ip6.p, &h->h_ip6},       {h->d_client.p, &h->h_client}};
+              {h->d_ip4.p, &h->h_ip4}, {h->d_ip6.p, &h->h_ip6},       {h->d_client.p, &h->h_client},
+              {h->d_ft4.p, &h->h_ft4}, {h->d_ft6.p, &h->h_ft6},       {h->d_srv.p, &h->h_srv}};
     for (auto& u : up)
         if (hipMemcpyAsync(u.d, u.h->data(), u.h->size() * 4, hipMemcpyHostToDevice, st) != hipSuccess)
             return EMURX_EDEVICE;
@@ -502,6 +562,7 @@ void emurx_close(emurx_t* h) {
     for (auto& s : h->ing) s.release();
     h->d_ns.release(); h->d_nsinfo.release(); h->d_mac.release(); h->d_ip4.release();
     h->d_ip6.release(); h->d_client.release();
+    h->d_ft4.release(); h->d_ft6.release(); h->d_srv.release();
     h->d_route_cnt.release(); h->d_route_grp.release(); h->d_route_goff.release();
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
@@ -603,6 +664,14 @@ int emurx_client_add(emurx_t* h, uint32_t ns_id, uint32_t cid, const uint8_t mac
     return EMURX_OK;
 }
 
+static void drop_transport(emurx_t* h, uint32_t cid) {
+    for (auto it = h->ft_map.begin(); it != h->ft_map.end();)
+        it = le32(reinterpret_cast<const uint8_t*>(it->first.data())) == cid ? h->ft_map.erase(it) : std::next(it);
+    for (auto it = h->srv_map.begin(); it != h->srv_map.end();)
+        it = (uint32_t)(it->first >> 32) == cid ? h->srv_map.erase(it) : std::next(it);
+    h->cl[cid].has_ctx = false;
+}
+
 // CNSCtx.RemoveClient ns_ctx.go:392-440 (map entries are deleted by key)
 int emurx_client_remove(emurx_t* h, uint32_t ns_id, const uint8_t mac[6]) {
     if (!h || !mac) return EMURX_EINVAL;
@@ -618,6 +687,7 @@ int emurx_client_remove(emurx_t* h, uint32_t ns_id, const uint8_t mac[6]) {
     if (!zero(c.ipv4, 4)) h->ip4_map.erase(key_ip4(ns_id, c.ipv4));
     if (!zero(c.ipv6, 16)) h->ip6_map.erase(key_ip6(ns_id, c.ipv6));
     if (!zero(c.dhcpv6, 16)) h->ip6_map.erase(key_ip6(ns_id, c.dhcpv6));
+    drop_transport(h, cid);  // TransportCtx.onRemove: its sockets go with the client
     c.alive = false;
     h->dirty = true;
     return EMURX_OK;
@@ -665,6 +735,67 @@ int emurx_client_set_ra(emurx_t* h, uint32_t cid, const uint8_t prefix[16], uint
     c.has_ra = true;
     memcpy(c.ra_prefix, prefix, 16);
     c.ra_plen = plen;
+    h->dirty = true;
+    return EMURX_OK;
+}
+
+// ---- transport flow tables (TransportCtx.addFlowv4/6 / removeFlowv4/6 client_ctx.go:597-651,
+// serverCb / lookupServerPort :1142-1155, GetTransportCtx socketApi.go:174-193) -----------
+static int flow_key(emurx_t* h, uint32_t cid, const uint8_t* tuple, uint32_t tlen, std::string& k) {
+    if (!h || !tuple || (tlen != 13 && tlen != 37)) return EMURX_EINVAL;
+    if (cid >= h->cfg.max_clients || !h->cl[cid].alive) return EMURX_ENOENT;
+    k.assign(4 + tlen, '\0');
+    memcpy(&k[0], &cid, 4);
+    memcpy(&k[4], tuple, tlen);
+    return EMURX_OK;
+}
+int emurx_flow_add(emurx_t* h, uint32_t cid, const uint8_t* tuple, uint32_t tlen, uint32_t flow_id) {
+    std::string k;
+    int rc = flow_key(h, cid, tuple, tlen, k);
+    if (rc) return rc;
+    if (flow_id > EMURX_FLOW_ID_MAX) return EMURX_EINVAL;
+    if (h->ft_map.count(k)) return EMURX_EEXIST;  // ft_add_err_already_exits
+    h->ft_map[k] = flow_id;
+    h->cl[cid].has_ctx = true;
+    h->dirty = true;
+    return EMURX_OK;
+}
+int emurx_flow_remove(emurx_t* h, uint32_t cid, const uint8_t* tuple, uint32_t tlen) {
+    std::string k;
+    int rc = flow_key(h, cid, tuple, tlen, k);
+    if (rc) return rc;
+    if (!h->ft_map.erase(k)) return EMURX_ENOENT;  // ft_remove_err_not_exits
+    h->dirty = true;
+    return EMURX_OK;
+}
+static int srv_key(emurx_t* h, uint32_t cid, uint16_t port, uint8_t proto, uint64_t& k) {
+    if (!h || (proto != 6 && proto != 17)) return EMURX_EINVAL;
+    if (cid >= h->cfg.max_clients || !h->cl[cid].alive) return EMURX_ENOENT;
+    k = ((uint64_t)cid << 32) | port | ((uint32_t)proto << 16);
+    return EMURX_OK;
+}
+int emurx_server_add(emurx_t* h, uint32_t cid, uint16_t port, uint8_t proto) {
+    uint64_t k;
+    int rc = srv_key(h, cid, port, proto, k);
+    if (rc) return rc;
+    if (h->srv_map.count(k)) return EMURX_EEXIST;
+    h->srv_map[k] = 1;
+    h->cl[cid].has_ctx = true;
+    h->dirty = true;
+    return EMURX_OK;
+}
+int emurx_server_remove(emurx_t* h, uint32_t cid, uint16_t port, uint8_t proto) {
+    uint64_t k;
+    int rc = srv_key(h, cid, port, proto, k);
+    if (rc) return rc;
+    if (!h->srv_map.erase(k)) return EMURX_ENOENT;
+    h->dirty = true;
+    return EMURX_OK;
+}
+int emurx_client_set_transport(emurx_t* h, uint32_t cid, int has_ctx) {
+    if (!h) return EMURX_EINVAL;
+    if (cid >= h->cfg.max_clients || !h->cl[cid].alive) return EMURX_ENOENT;
+    h->cl[cid].has_ctx = has_ctx != 0;
     h->dirty = true;
     return EMURX_OK;
 }

@@ -34,7 +34,8 @@ __global__ __launch_bounds__(kBlock) void k_rx(const uint8_t* __restrict__ frame
                                                emurx_dev_tables T, emurx_rec* __restrict__ rec,
                                                uint32_t* __restrict__ qlist, uint32_t qcap,
                                                uint32_t* __restrict__ tile_cnt,
-                                               unsigned long long* __restrict__ hist) {
+                                               unsigned long long* __restrict__ hist,
+                                               uint32_t* __restrict__ flow) {
     __shared__ __attribute__((aligned(16))) uint32_t slab[kWaves * kStage / 4];
     __shared__ uint32_t s_wcnt[kWaves][16];
     __shared__ unsigned long long s_hist[kWaves][EMURX_HIST_BINS];  // {pkts << 40 | bytes}
@@ -100,6 +101,7 @@ __global__ __launch_bounds__(kBlock) void k_rx(const uint8_t* __restrict__ frame
             o[1] = make_uint4(r.vport | (r.l3 << 16), r.l4 | (r.l7 << 16),
                               r.l7len | (r.nh << 16) | (r.proto << 24), r.status | (r.flags << 8));
         }
+        if (flow) flow[i] = r.flow;
         // outcome histogram: one packed LDS add per frame into the wave's copy
         if (!(EMURX_ABL & 4))
             atomicAdd(&s_hist[wv][EMURX_HIST_BIN(r.status, r.proto)], (1ull << 40) | (unsigned long long)len);
@@ -158,10 +160,10 @@ int emurx_launch_batch(const uint8_t* frames, const emurx_desc* desc, uint32_t n
         unsigned long long* hist = reinterpret_cast<unsigned long long*>(out.hist);
         if (classify)
             hipLaunchKernelGGL(k_rx<true>, dim3(ntiles), dim3(kBlock), 0, st, frames, desc, n, T, out.rec,
-                               out.qlist, out.qcap, out.tile_cnt, hist);
+                               out.qlist, out.qcap, out.tile_cnt, hist, out.flow);
         else
             hipLaunchKernelGGL(k_rx<false>, dim3(ntiles), dim3(kBlock), 0, st, frames, desc, n, T, out.rec,
-                               out.qlist, out.qcap, out.tile_cnt, hist);
+                               out.qlist, out.qcap, out.tile_cnt, hist, out.flow);
     }
     if (ev) (void)hipEventRecord(ev[1], st);
     return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -221,6 +221,7 @@ struct Rec {
     // L4 checksum deferred to the wave-cooperative pass (WinSrc spans past the window):
     // bytes [dstart, dstart + dlen) with pseudo sum dpcs; on failure the outcome becomes dfail
     uint32_t dstart, dlen, dpcs, dfail;
+    uint32_t flow;  // EMURX_FLOW_* / flow id (transport handler decision)
 };
 
 __device__ __forceinline__ void invoke(Rec& r, uint32_t cb, uint32_t cb_mask) {
@@ -347,6 +348,7 @@ __device__ __forceinline__ void parse_packet(const S& s, uint32_t len, uint32_t 
     r.l3 = r.l4 = r.l7 = r.l7len = 0;
     r.nh = 0; r.proto = EMURX_CB_NONE; r.status = EMURX_ST_OK; r.flags = 0;
     r.dlen = 0;
+    r.flow = EMURX_FLOW_NONE;
     if (len < 14) { fail(r, EMURX_ST_PACKET_TOO_SHORT); return; }
     uint32_t offset = 14;
     uint32_t nextHdr = be16(s, 12);
@@ -647,6 +649,62 @@ __device__ bool dhcp_chaddr(const S& s, uint32_t len, const Rec& r, uint32_t& lo
     return true;
 }
 
+// TransportCtx.handleRxPacket src/emu/plugins/transport/client_ctx.go:912-969: the frame's
+// c5tuplekey (fillv4tuple / fillv6tuple :720-765) in the client's flow map, else the new-flow
+// checks of handleRxTcpNewFlow / handleRxUdpNewFlow (:829-904) up to OnAccept.
+template <class S>
+__device__ uint32_t flow_lookup(const S& s, uint32_t len, const emurx_dev_tables& T, const Rec& r, uint32_t cid) {
+    if (!(gld4(T.client + 8 * cid + 6) & 1u)) return EMURX_FLOW_NO_CTX;  // GetTransportCtx() == nil
+    const uint32_t L3 = r.l3, L4 = r.l4;
+    const uint32_t ports = le32(s, L4);  // UDPHeader(p[L4:L4+4]): sport, dport as on the wire
+    uint32_t proto;
+    if ((s.u8(L3) >> 4) == 4) {  // IPv4Header(p[L3:L3+20]).Version()
+        proto = s.u8(L3 + 9);
+        const uint32_t src = le32(s, L3 + 12), dst = le32(s, L3 + 16);
+        for (uint32_t b = emurx_ft4_hash(cid, src, dst, ports, proto) & T.ft4_mask, k = 0; k <= T.ft4_mask;
+             ++k, b = (b + 1) & T.ft4_mask) {
+            const Bucket e = ld_bucket(T.ft4_tab, b);
+            const uint4 x0 = e.s[0], x1 = e.s[1], y0 = e.s[2], y1 = e.s[3];
+            if (x0.x == cid && x0.y == src && x0.z == dst && x0.w == ports && x1.x == proto && x1.w != EMURX_EMPTY)
+                return x1.w;
+            if (x1.w == EMURX_EMPTY) break;
+            if (y0.x == cid && y0.y == src && y0.z == dst && y0.w == ports && y1.x == proto && y1.w != EMURX_EMPTY)
+                return y1.w;
+            if (y1.w == EMURX_EMPTY) break;
+        }
+    } else {
+        proto = r.nh;  // ps.NextHeader
+        uint32_t a[4], d[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            a[k] = le32(s, L3 + 8 + 4 * k);
+            d[k] = le32(s, L3 + 24 + 4 * k);
+        }
+        for (uint32_t b = emurx_ft6_hash(cid, a, d, ports, proto) & T.ft6_mask, k = 0; k <= T.ft6_mask;
+             ++k, b = (b + 1) & T.ft6_mask) {
+            const Bucket e = ld_bucket(T.ft6_tab, b);
+            if (e.s[3].w == EMURX_EMPTY) break;
+            if (e.s[0].x == cid && e.s[0].y == a[0] && e.s[0].z == a[1] && e.s[0].w == a[2] && e.s[1].x == a[3] &&
+                e.s[1].y == d[0] && e.s[1].z == d[1] && e.s[1].w == d[2] && e.s[2].x == d[3] && e.s[2].y == ports &&
+                e.s[2].z == proto)
+                return e.s[3].w;
+        }
+    }
+    // a new flow: handleRxTcpNewFlow needs a bare SYN (GetFlags() & 0x3F == 0x2; a flags byte
+    // past the frame is read as 0 here, stale mbuf bytes in Go)
+    if (proto == 6 && (((L4 + 13 < len) ? s.u8(L4 + 13) : 0u) & 0x3f) != 0x2) return EMURX_FLOW_NO_SYN;
+    const uint32_t key = be16(s, L4 + 2) | ((proto == 6 ? 6u : 17u) << 16);  // lookupServerPort(dst, TCP|UDP)
+    for (uint32_t b = emurx_srv_hash(cid, key) & T.srv_mask, k = 0; k <= T.srv_mask; ++k, b = (b + 1) & T.srv_mask) {
+        const Bucket e = ld_bucket(T.srv_tab, b);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (e.s[j].w == EMURX_EMPTY) return EMURX_FLOW_NO_SERVER;
+            if (e.s[j].x == cid && e.s[j].y == key) return EMURX_FLOW_NEW;
+        }
+    }
+    return EMURX_FLOW_NO_SERVER;
+}
+
 __constant__ uint8_t kCbPlugin[EMURX_NUM_CB] = {
     EMURX_PLUG_ARP, EMURX_PLUG_ICMP, EMURX_PLUG_IGMP, EMURX_PLUG_DHCP, EMURX_PLUG_DHCPSRV,
     EMURX_PLUG_DHCPV6, EMURX_PLUG_MDNS, EMURX_PLUG_TRANSPORT, EMURX_PLUG_TRANSPORT,
@@ -789,6 +847,10 @@ __device__ __forceinline__ void classify(const S& s, uint32_t len, const emurx_d
     default: {  // kMac
         const uint2 c = resolve_mac(T, cbk, ce, ns, mlo, mhi);
         client_result(r, c.x, c.y, plug, true);
+        // transport: the client's TransportCtx decides (plugin_transport.go:109-114, :73-80)
+        if (T.ft_on && (cb == EMURX_CB_TCP || cb == EMURX_CB_UDP) &&
+            ((r.flags & EMURX_FLAG_LK_MASK) >> EMURX_FLAG_LK_SHIFT) == EMURX_LK_CLIENT)
+            r.flow = flow_lookup(s, len, T, r, c.x);
         return;
     }
     }

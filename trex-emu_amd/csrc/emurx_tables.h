@@ -69,6 +69,22 @@ EMURX_HD uint32_t emurx_ip6_hash(uint32_t tk, uint32_t a, uint32_t b, uint32_t c
     return emurx_hash(tk, a ^ 0x697036u, b, c, d);
 }
 
+// Transport tables (TransportCtx.ftv4 / ftv6 / serverCb, src/emu/plugins/transport/
+// client_ctx.go:490-497), one global map per kind keyed by (client id, tuple):
+//  ft4  [8]: cid, src LE, dst LE, ports (4 wire bytes LE), proto, 0, 0, flow_id   (2 per bucket)
+//  ft6 [16]: cid, src[4], dst[4], ports, nh, 0 x 5, flow_id                       (1 per bucket)
+//  srv  [4]: cid, port | proto << 16, 0, 1                                        (4 per bucket)
+// client word 6 bit 0: the client has a TransportCtx.
+EMURX_HD uint32_t emurx_ft4_hash(uint32_t cid, uint32_t src, uint32_t dst, uint32_t ports, uint32_t proto) {
+    return emurx_hash(cid, src, dst, ports, proto ^ 0x667434u);
+}
+EMURX_HD uint32_t emurx_ft6_hash(uint32_t cid, const uint32_t s[4], const uint32_t d[4], uint32_t ports, uint32_t nh) {
+    return emurx_hash(emurx_hash(cid, s[0], s[1], s[2], s[3]), d[0], d[1], d[2], d[3] ^ (ports * 0x9E3779B1u) ^ nh);
+}
+EMURX_HD uint32_t emurx_srv_hash(uint32_t cid, uint32_t port_proto) {
+    return emurx_hash(cid, port_proto, 0x737276u, 0, 0);
+}
+
 struct emurx_dev_tables {
     const uint32_t* ns_tab;   // [ns_mask + 1] buckets of 4 slots
     const uint32_t* ns_info;  // 4 words per ns id
@@ -79,7 +95,11 @@ struct emurx_dev_tables {
     uint32_t ns_mask, mac_mask, ip4_mask, ip6_mask;  // bucket count - 1
     uint32_t max_ns, max_clients;
     uint32_t cb_mask;         // registered callbacks (Parser.Register)
-    uint32_t pad;
+    uint32_t ft_on;           // any client has a TransportCtx: resolve transport flows
+    const uint32_t* ft4_tab;  // [ft4_mask + 1] buckets of 2 slots
+    const uint32_t* ft6_tab;  // [ft6_mask + 1] buckets of 1 slot
+    const uint32_t* srv_tab;  // [srv_mask + 1] buckets of 4 slots
+    uint32_t ft4_mask, ft6_mask, srv_mask, pad;
 };
 
 // Namespace partition of a tunnel-key hash among n_parts GPUs (multiply-high: uniform for a

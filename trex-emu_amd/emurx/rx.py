@@ -108,6 +108,24 @@ class RxPath:
         a = _u8(prefix, 16)
         return self.lib.emurx_client_set_ra(self.h, cid, _p(a), plen)
 
+    # transport flow tables (TransportCtx.addFlowv4/6, serverCb; include/emu_rx.h)
+    def flow_add(self, cid, tuple_bytes, flow_id) -> int:
+        t = np.frombuffer(bytes(tuple_bytes), np.uint8).copy()
+        return self.lib.emurx_flow_add(self.h, cid, _p(t), len(t), flow_id)
+
+    def flow_remove(self, cid, tuple_bytes) -> int:
+        t = np.frombuffer(bytes(tuple_bytes), np.uint8).copy()
+        return self.lib.emurx_flow_remove(self.h, cid, _p(t), len(t))
+
+    def server_add(self, cid, port, proto) -> int:
+        return self.lib.emurx_server_add(self.h, cid, port, proto)
+
+    def server_remove(self, cid, port, proto) -> int:
+        return self.lib.emurx_server_remove(self.h, cid, port, proto)
+
+    def client_set_transport(self, cid, has_ctx) -> int:
+        return self.lib.emurx_client_set_transport(self.h, cid, int(has_ctx))
+
     def sync(self, stream=None):
         return abi.check(self.lib.emurx_sync(self.h, stream), "sync")
 
@@ -127,11 +145,11 @@ class RxPath:
 
     # ---- device-resident batch -----------------------------------------------------------
     def classify_dev(self, frames, desc, n: int, rec=None, qlist=None, qcap: int = 0, tile_cnt=None,
-                     hist=None, stream=None, classify: bool = True):
+                     hist=None, stream=None, classify: bool = True, flow=None):
         """frames/desc/rec/qlist/tile_cnt/hist: device tensors (or raw device addresses).
         Tile t's frames of queue q land in qlist[q*qcap + t*QUEUE_TILE :][:tile_cnt[t*16+q]]
         (see pack_queues); hist holds HIST_SHARDS accumulating copies (see hist_fold)."""
-        out = abi.DevOut(_addr(rec), _addr(qlist), qcap, _addr(tile_cnt), _addr(hist))
+        out = abi.DevOut(_addr(rec), _addr(qlist), qcap, _addr(tile_cnt), _addr(hist), _addr(flow))
         fn = self.lib.emurx_classify_dev if classify else self.lib.emurx_parse_dev
         return abi.check(fn(self.h, _addr(frames), _addr(desc), n, C.byref(out),
                             _stream(stream)), "classify_dev")

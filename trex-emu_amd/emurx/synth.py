@@ -138,7 +138,7 @@ def build_frames(rng, spec):
             _be16(F, rows, L4 + 2, spec["dport"][rows])
             _be32(F, rows, L4 + 4, rows.astype(np.uint64) * 1000 + 1)
             F[rows, L4 + 12] = 5 << 4
-            F[rows, L4 + 13] = 0x18
+            F[rows, L4 + 13] = spec["tcpflags"][rows] if "tcpflags" in spec else 0x18
             _be16(F, rows, L4 + 14, np.full(m, 8192))
             cso = 16
         else:
@@ -264,7 +264,7 @@ def config_b(n=1 << 20, seed=SEED_B):
                 ns=[(tunnel_key(0, 0, 0), 0)], clients=clients, seed=seed)
 
 
-def _mixed(n, seed, n_ns, clients_per_ns, vports, imix=False, name="C", rank=0):
+def _mixed(n, seed, n_ns, clients_per_ns, vports, imix=False, name="C", rank=0, syn=0.0):
     rng = np.random.default_rng([seed, rank])
     lay = _ns_layout(n_ns, n_ns // vports)
     ns_of = rng.integers(0, n_ns, n)
@@ -311,6 +311,8 @@ def _mixed(n, seed, n_ns, clients_per_ns, vports, imix=False, name="C", rank=0):
     spec = dict(ntag=ntag, tpid0=tpid0, vid0=vid0, vid1=vid1, ipver=ipver, ext=ext, l4=l4,
                 dmac=dmac, smac=smac, sip4=sip4, dip4=dip4, sip6=sip6, dip6=dip6, sport=sport,
                 dport=dport, plen=plen, bad=bad)
+    if syn:  # a share of bare SYNs (new TCP flows); the default keeps PSH|ACK
+        spec["tcpflags"] = np.where(rng.random(n) < syn, 0x02, 0x18)
     F, length = build_frames(rng, spec)
     buf, desc = pack_zmq_layout(F, length, vport)
     del F
@@ -322,8 +324,8 @@ def _mixed(n, seed, n_ns, clients_per_ns, vports, imix=False, name="C", rank=0):
                 clients=clients, seed=seed, layout=lay)
 
 
-def config_c(n=1 << 20, seed=SEED_C, rank=0):
-    return _mixed(n, seed, 4096, 16, 4, name="C", rank=rank)
+def config_c(n=1 << 20, seed=SEED_C, rank=0, syn=0.0):
+    return _mixed(n, seed, 4096, 16, 4, name="C", rank=rank, syn=syn)
 
 
 def config_d(n=1 << 24, seed=SEED_D, rank=0):
