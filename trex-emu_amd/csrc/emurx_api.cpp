@@ -258,7 +258,7 @@ int build_transport(emurx_t* h) {
             e[9] = le32(t + 32);
             e[10] = t[36];
             e[15] = kv.second;
-            bucket_put(h->h_ft6, h->ft6_buckets - 1, 16, emurx_ft6_hash(cid, e + 1, e + 5, e[9], e[10]), e);
+            bucket_put(h->h_ft6, h->ft6_buckets - 1, 16, emurx_ft6_hash(cid, e[1], e[2], e[3], e[4], e[5], e[6], e[7], e[8], e[9], e[10]), e);
         }
     }
     for (auto& kv : h->srv_map) {

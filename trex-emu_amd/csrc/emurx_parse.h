@@ -653,7 +653,7 @@ __device__ bool dhcp_chaddr(const S& s, uint32_t len, const Rec& r, uint32_t& lo
 // c5tuplekey (fillv4tuple / fillv6tuple :720-765) in the client's flow map, else the new-flow
 // checks of handleRxTcpNewFlow / handleRxUdpNewFlow (:829-904) up to OnAccept.
 template <class S>
-__device__ uint32_t flow_lookup(const S& s, uint32_t len, const emurx_dev_tables& T, const Rec& r, uint32_t cid) {
+__device__ __forceinline__ uint32_t flow_lookup(const S& s, uint32_t len, const emurx_dev_tables& T, const Rec& r, uint32_t cid) {
     if (!(gld4(T.client + 8 * cid + 6) & 1u)) return EMURX_FLOW_NO_CTX;  // GetTransportCtx() == nil
     const uint32_t L3 = r.l3, L4 = r.l4;
     const uint32_t ports = le32(s, L4);  // UDPHeader(p[L4:L4+4]): sport, dport as on the wire
@@ -674,18 +674,14 @@ __device__ uint32_t flow_lookup(const S& s, uint32_t len, const emurx_dev_tables
         }
     } else {
         proto = r.nh;  // ps.NextHeader
-        uint32_t a[4], d[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            a[k] = le32(s, L3 + 8 + 4 * k);
-            d[k] = le32(s, L3 + 24 + 4 * k);
-        }
-        for (uint32_t b = emurx_ft6_hash(cid, a, d, ports, proto) & T.ft6_mask, k = 0; k <= T.ft6_mask;
-             ++k, b = (b + 1) & T.ft6_mask) {
+        const uint32_t a0 = le32(s, L3 + 8), a1 = le32(s, L3 + 12), a2 = le32(s, L3 + 16), a3 = le32(s, L3 + 20);
+        const uint32_t d0 = le32(s, L3 + 24), d1 = le32(s, L3 + 28), d2 = le32(s, L3 + 32), d3 = le32(s, L3 + 36);
+        for (uint32_t b = emurx_ft6_hash(cid, a0, a1, a2, a3, d0, d1, d2, d3, ports, proto) & T.ft6_mask, k = 0;
+             k <= T.ft6_mask; ++k, b = (b + 1) & T.ft6_mask) {
             const Bucket e = ld_bucket(T.ft6_tab, b);
             if (e.s[3].w == EMURX_EMPTY) break;
-            if (e.s[0].x == cid && e.s[0].y == a[0] && e.s[0].z == a[1] && e.s[0].w == a[2] && e.s[1].x == a[3] &&
-                e.s[1].y == d[0] && e.s[1].z == d[1] && e.s[1].w == d[2] && e.s[2].x == d[3] && e.s[2].y == ports &&
+            if (e.s[0].x == cid && e.s[0].y == a0 && e.s[0].z == a1 && e.s[0].w == a2 && e.s[1].x == a3 &&
+                e.s[1].y == d0 && e.s[1].z == d1 && e.s[1].w == d2 && e.s[2].x == d3 && e.s[2].y == ports &&
                 e.s[2].z == proto)
                 return e.s[3].w;
         }

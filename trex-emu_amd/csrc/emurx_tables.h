@@ -78,8 +78,9 @@ EMURX_HD uint32_t emurx_ip6_hash(uint32_t tk, uint32_t a, uint32_t b, uint32_t c
 EMURX_HD uint32_t emurx_ft4_hash(uint32_t cid, uint32_t src, uint32_t dst, uint32_t ports, uint32_t proto) {
     return emurx_hash(cid, src, dst, ports, proto ^ 0x667434u);
 }
-EMURX_HD uint32_t emurx_ft6_hash(uint32_t cid, const uint32_t s[4], const uint32_t d[4], uint32_t ports, uint32_t nh) {
-    return emurx_hash(emurx_hash(cid, s[0], s[1], s[2], s[3]), d[0], d[1], d[2], d[3] ^ (ports * 0x9E3779B1u) ^ nh);
+EMURX_HD uint32_t emurx_ft6_hash(uint32_t cid, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, uint32_t d0,
+                                 uint32_t d1, uint32_t d2, uint32_t d3, uint32_t ports, uint32_t nh) {
+    return emurx_hash(emurx_hash(cid, s0, s1, s2, s3), d0, d1, d2, d3 ^ (ports * 0x9E3779B1u) ^ nh);
 }
 EMURX_HD uint32_t emurx_srv_hash(uint32_t cid, uint32_t port_proto) {
     return emurx_hash(cid, port_proto, 0x737276u, 0, 0);
