@@ -22,6 +22,7 @@ namespace emurx {
 
 static_assert(EMURX_QUEUE_TILE == kBlock, "one frame per lane per tile");
 
+
 // LDS-DMA (global_load_lds_dwordx4): lane l's 16 source bytes land at dst + 16 * l
 __device__ __forceinline__ void glds16(const uint4* src, uint4* dst_wave_base) {
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst_wave_base, 16, 0, 0);
@@ -94,13 +95,17 @@ __global__ __launch_bounds__(kBlock) void k_rx(const uint8_t* __restrict__ frame
         coop_checksum(r, frames + off);  // the wave's long L4 spans, converged
         if (valid && kClassify && !(EMURX_ABL & 2)) classify(s, len, T, r);
     }
-    if (valid) {
-        if (rec && !(EMURX_ABL & 16)) {
+    if (rec && !(EMURX_ABL & 16)) {
+        const uint4 h0 = make_uint4(r.ns, r.cl, r.vlan0, r.vlan1);
+        const uint4 h1 = make_uint4(r.vport | (r.l3 << 16), r.l4 | (r.l7 << 16),
+                                    r.l7len | (r.nh << 16) | (r.proto << 24), r.status | (r.flags << 8));
+        if (valid) {
             uint4* o = reinterpret_cast<uint4*>(rec + i);
-            o[0] = make_uint4(r.ns, r.cl, r.vlan0, r.vlan1);
-            o[1] = make_uint4(r.vport | (r.l3 << 16), r.l4 | (r.l7 << 16),
-                              r.l7len | (r.nh << 16) | (r.proto << 24), r.status | (r.flags << 8));
+            o[0] = h0;
+            o[1] = h1;
         }
+    }
+    if (valid) {
         if (flow) flow[i] = r.flow;
         // outcome histogram: one packed LDS add per frame into the wave's copy
         if (!(EMURX_ABL & 4))
