@@ -1,0 +1,32 @@
+#!/bin/bash
+# SQ counter passes over the config-B bench (k_rx only), one rocprofv3 run per pass.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+out=gpurun_out/pmc_sq; mkdir -p $out
+timeout -s KILL 60 rocprofv3 -L > $out/counters_list.txt 2>&1
+i=0
+while read -r set; do
+  [ -z "$set" ] && continue
+  i=$((i+1)); echo "== pass $i: $set"
+  timeout -s KILL 90 rocprofv3 --pmc $set -T --kernel-include-regex k_rx -d $out/p$i -o run --output-format csv \
+      -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-check "$@" > $out/p$i.log 2>&1
+  rc=$?; echo "rc=$rc"; [ $rc -eq 0 ] || { tail -3 $out/p$i.log; exit $rc; }
+done <<'SETS'
+SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA
+SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_SALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR
+SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH SQ_ACTIVE_INST_MISC SQ_INSTS_VALU_INT32 SQ_IFETCH GRBM_GUI_ACTIVE
+SETS
+python - <<'PY'
+import csv, glob, collections
+tot = collections.defaultdict(list)
+for f in glob.glob("gpurun_out/pmc_sq/p*/**/*counter_collection.csv", recursive=True):
+    per = collections.defaultdict(float)
+    for r in csv.DictReader(open(f)):
+        per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
+    for (d, c), v in per.items():
+        tot[c].append((int(d), v))
+for c, l in sorted(tot.items()):
+    l.sort(); v = [x[1] for x in l][3:] or [x[1] for x in l]
+    print(f"{c:28s} {sum(v)/len(v):14.1f}")
+PY

@@ -437,6 +437,168 @@ __device__ __forceinline__ void parse_packet(const S& s, uint32_t len, uint32_t 
 }
 
 // ---------------------------------------------------------------------------------------
+// The same ParsePacket, written for the staged (LDS) path with as little divergent control
+// flow as the Go semantics allow: every check of a layer is evaluated and the first failing
+// one (in Go's order) is picked by selects, every checksum of a frame is one dword-sum call
+// whose length is zero where Go would not reach it.  Reads past a frame stay inside the
+// workgroup's LDS (out-of-range LDS reads return 0 on CDNA), so evaluating a check Go would
+// not reach is harmless; only the loop bounds (checksum spans, IPv6 extension headers) must
+// be the ones Go would use.  Field values on every return path equal parse_packet's.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void first(uint32_t& st, bool cond, uint32_t code) {
+    st = (st == EMURX_ST_OK && cond) ? code : st;
+}
+
+// Parser.parsePacketL4 parser.go:583-724, flat
+__device__ __forceinline__ void parse_l4_flat(const LdsSrc& s, uint32_t len, Rec& r, uint32_t nextHdr, uint32_t pcs,
+                                              uint32_t l4len, bool v6, uint32_t cb_mask) {
+    r.nh = nextHdr;
+    const uint32_t L4 = r.l4;
+    const bool p1 = nextHdr == 1, p2 = nextHdr == 2, p6 = nextHdr == 6, p17 = nextHdr == 17, p58 = nextHdr == 58;
+    const uint32_t L4_8 = (L4 + 8) & 0xffff, L4_4 = (L4 + 4) & 0xffff, L4_12 = (L4 + 12) & 0xffff;
+    const bool sok = span_ok(L4, l4len);
+    const uint32_t tcplen = (s.u8(L4_12) >> 4) << 2;
+    const bool ucs = be16(s, L4 + 6) > 0;  // UDP checksum present
+    uint32_t st = EMURX_ST_OK;
+    bool tcp_hdr = false;  // TCP got past its length checks (L7 / L7Len are set)
+    if (p1) {
+        first(st, len < L4_8, EMURX_ST_ICMPV4_TOO_SHORT);
+        first(st, !sok, EMURX_ST_PANIC_L4LEN);
+    } else if (p2) {
+        first(st, len < L4_8, EMURX_ST_ICMPV4_TOO_SHORT);
+    } else if (p6) {
+        first(st, l4len < 20, EMURX_ST_TCP_TOO_SHORT);
+        first(st, L4_12 >= len, EMURX_ST_PANIC_L4LEN);
+        first(st, l4len < tcplen, EMURX_ST_TCP_TOO_SHORT);
+        tcp_hdr = st == EMURX_ST_OK;
+        first(st, !sok, EMURX_ST_PANIC_L4LEN);
+    } else if (p17) {
+        first(st, len < L4_8, EMURX_ST_UDP_TOO_SHORT);
+        first(st, ucs && !sok, EMURX_ST_PANIC_L4LEN);
+    } else if (p58) {
+        first(st, len < L4_4, EMURX_ST_ICMPV6_TOO_SHORT);
+        first(st, !sok, EMURX_ST_PANIC_L4LEN);
+    } else {
+        st = EMURX_ST_L4_UNSUPPORTED;
+    }
+    const bool need = st == EMURX_ST_OK && (p1 || p6 || p58 || (p17 && ucs));
+    const bool cs_ok = csum(s, L4, need ? l4len : 0u, p1 ? 0u : pcs);
+    first(st, need && !cs_ok, p1 ? EMURX_ST_ICMPV4_CS : p6 ? EMURX_ST_TCP_CS : p17 ? EMURX_ST_UDP_CS : EMURX_ST_ICMPV6_CS);
+    // L7 / L7Len as Go leaves them on each path (set before the checksum for TCP, L7Len
+    // before it for UDP, L7 only on success for ICMP and UDP)
+    r.l7len = tcp_hdr ? ((l4len - tcplen) & 0xffff) : (p17 && len >= L4_8) ? ((l4len - 8) & 0xffff) : 0u;
+    r.l7 = tcp_hdr ? ((L4 + tcplen) & 0xffff) : ((p1 || p17) && st == EMURX_ST_OK) ? L4_8 : 0u;
+    const uint32_t src = be16(s, L4), dst = be16(s, L4 + 2), t6 = s.u8(L4);
+    uint32_t cb = p1 ? EMURX_CB_ICMP : p2 ? EMURX_CB_IGMP : p6 ? EMURX_CB_TCP : p58 ? EMURX_CB_ICMPV6 : EMURX_CB_UDP;
+    if (p17) {
+        cb = dst == 5353 ? EMURX_CB_MDNS
+           : v6 ? ((src == 547 && dst == 546) ? EMURX_CB_DHCPV6 : EMURX_CB_UDP)
+           : (src == 67 && dst == 68) ? EMURX_CB_DHCP
+           : (dst == 67 && (src == 67 || src == 68)) ? EMURX_CB_DHCPSRV : EMURX_CB_UDP;
+    }
+    first(st, p58 && !((t6 >= 1 && t6 <= 4) || (t6 >= 128 && t6 <= 136)), EMURX_ST_ICMPV6_UNSUPPORTED);
+    if (st == EMURX_ST_OK) invoke(r, cb, cb_mask);
+    else fail(r, st);
+}
+
+// Parser.ParsePacket parser.go:756-959, flat (staged frames)
+__device__ __forceinline__ void parse_flat(const LdsSrc& s, uint32_t len, uint32_t vport, uint32_t cb_mask, Rec& r) {
+    r.ns = EMURX_ID_NONE; r.cl = EMURX_ID_NONE;
+    r.vlan0 = 0; r.vlan1 = 0; r.vport = vport;
+    r.l3 = r.l4 = r.l7 = r.l7len = 0;
+    r.nh = 0; r.proto = EMURX_CB_NONE; r.status = EMURX_ST_OK; r.flags = 0;
+    r.dlen = 0;
+    r.flow = EMURX_FLOW_NONE;
+    // ---- L2: at most two tags, a third is errToManyDot1q; PPPoE right after a tag ----
+    auto is_tag = [](uint32_t x) { return x == 0x8100 || x == 0x88A8; };
+    auto is_ppp = [](uint32_t x) { return x == 0x8863 || x == 0x8864; };
+    uint32_t st = EMURX_ST_OK;
+    first(st, len < 14, EMURX_ST_PACKET_TOO_SHORT);
+    const uint32_t e0 = be16(s, 12), e1 = be16(s, 16), e2 = be16(s, 20);
+    const bool t0 = st == EMURX_ST_OK && is_tag(e0);
+    first(st, t0 && len < 18, EMURX_ST_DOT1Q_TOO_SHORT);
+    const bool g0 = t0 && st == EMURX_ST_OK;  // tag 0 parsed
+    const bool ppp0 = g0 && is_ppp(e1);
+    const bool t1 = g0 && !ppp0 && is_tag(e1);
+    first(st, t1 && len < 22, EMURX_ST_DOT1Q_TOO_SHORT);
+    const bool g1 = t1 && st == EMURX_ST_OK;
+    const bool ppp1 = g1 && is_ppp(e2);
+    const bool t2 = g1 && !ppp1 && is_tag(e2);
+    first(st, t2 && len < 26, EMURX_ST_DOT1Q_TOO_SHORT);
+    first(st, t2, EMURX_ST_TOO_MANY_DOT1Q);
+    r.vlan0 = g0 ? (be32(s, 12) & 0xffff0fffu) : 0u;
+    r.vlan1 = g1 ? (be32(s, 16) & 0xffff0fffu) : 0u;
+    if (st != EMURX_ST_OK) { fail(r, st); return; }
+    if (ppp0 || ppp1) { invoke(r, EMURX_CB_PPP, cb_mask); return; }
+    const uint32_t offset = 14 + (g0 ? 4u : 0u) + (g1 ? 4u : 0u);
+    const uint32_t et = g1 ? e2 : g0 ? e1 : e0;
+
+    if (et == 0x0800) {  // IPv4
+        r.l3 = offset;
+        const uint32_t b0 = s.u8(offset), frag = be16(s, offset + 6), totlen = be16(s, offset + 2);
+        const uint32_t hdr = (b0 & 0xf) << 2;
+        first(st, len < offset + 20, EMURX_ST_IPV4_TOO_SHORT);
+        first(st, (b0 >> 4) != 4, EMURX_ST_IPV4_HDR_TOO_SHORT);
+        first(st, (frag & 0x3fff) != 0, EMURX_ST_IPV4_FRAGMENT);
+        first(st, hdr < 20, EMURX_ST_IPV4_HDR_TOO_SHORT);
+        first(st, len < offset + hdr, EMURX_ST_IPV4_HDR_TOO_SHORT);
+        first(st, len < ((offset + totlen) & 0xffff), EMURX_ST_IPV4_TOO_SHORT);
+        const bool hok = csum(s, offset, st == EMURX_ST_OK ? hdr : 0u, 0);
+        first(st, !hok, EMURX_ST_IPV4_CS);
+        if (st != EMURX_ST_OK) { fail(r, st); return; }
+        const uint32_t l4len = (totlen - hdr) & 0xffff;
+        r.l4 = offset + hdr;
+        const uint32_t proto = s.u8(offset + 9);
+        const uint32_t pcs = pseudo(s, offset + 12, 8) + proto + l4len;  // src, dst, 0|proto, len
+        parse_l4_flat(s, len, r, proto, pcs, l4len, false, cb_mask);
+        return;
+    }
+    if (et == 0x86DD) {  // IPv6
+        r.l3 = offset;
+        const uint32_t plen = be16(s, offset + 4);
+        first(st, len < offset + 40, EMURX_ST_IPV6_TOO_SHORT);
+        first(st, (s.u8(offset) >> 4) != 6, EMURX_ST_IPV6_TOO_SHORT);
+        first(st, len < ((offset + 40 + plen) & 0xffff), EMURX_ST_IPV6_TOO_SHORT);
+        first(st, s.u8(offset + 7) == 0, EMURX_ST_IPV6_HOPLIMIT);
+        if (st != EMURX_ST_OK) { fail(r, st); return; }
+        uint32_t l4 = offset + 40, l4len = plen, osize = 0;
+        uint32_t nh = s.u8(offset + 6);
+        for (;;) {  // extension headers (parser.go:886-931): rare, kept as Go's loop
+            const bool ext = nh == 0 || nh == 60 || nh == 43 || nh == 51 || nh == 50 || nh == 135 ||
+                             nh == 139 || nh == 140;
+            if (!ext) break;
+            if (l4len < 8) { fail(r, EMURX_ST_IPV6_TOO_SHORT); return; }
+            if (l4 + 2 > len) { fail(r, EMURX_ST_PANIC_L4LEN); return; }
+            const uint32_t hl = (s.u8(l4 + 1) << 3) + 8;
+            if (l4len < hl) { fail(r, EMURX_ST_IPV6_TOO_SHORT); return; }
+            if (l4 + hl > len) { fail(r, EMURX_ST_PANIC_L4LEN); return; }
+            const uint32_t nnh = s.u8(l4);
+            if (!ipv6_options(s, l4 + 2, (int)hl - 2, r.flags)) { fail(r, EMURX_ST_PANIC_IPV6_OPT); return; }
+            nh = nnh;
+            l4len -= hl;
+            osize += hl;
+            l4 += hl;
+        }
+        first(st, nh == 44, EMURX_ST_IPV6_FRAGMENT);
+        first(st, nh == 194, EMURX_ST_IPV6_JUMBO);
+        first(st, nh == 59, EMURX_ST_IPV6_EMPTY);
+        if (st != EMURX_ST_OK) { fail(r, st); return; }
+        r.l4 = l4;
+        const uint32_t pcs = pseudo(s, offset + 8, 32) + ((plen - osize) & 0xffff) + nh;
+        parse_l4_flat(s, len, r, nh, pcs, l4len, true, cb_mask);
+        return;
+    }
+    // EAPOL, ARP (ARPHeaderSize 28), PPPoE, anything else
+    const bool eap = et == 0x888E, arp = et == 0x0806;
+    first(st, eap && len < offset + 4, EMURX_ST_EAPOL_TOO_SHORT);
+    first(st, arp && len < offset + 28, EMURX_ST_ARP_TOO_SHORT);
+    first(st, !eap && !arp && !is_ppp(et), EMURX_ST_L3_UNSUPPORTED);
+    if (st != EMURX_ST_OK) { fail(r, st); return; }
+    if (eap || arp) r.l3 = offset;
+    invoke(r, eap ? EMURX_CB_EAPOL : arp ? EMURX_CB_ARP : EMURX_CB_PPP, cb_mask);
+}
+
+// ---------------------------------------------------------------------------------------
 // Wave-cooperative L4 checksums for the WinSrc path (long spans, IMIX / jumbo frames): the
 // 64 lanes stream one frame's span at a time with coalesced 16-byte loads, eight frames in
 // flight, and reduce it on the DPP network; the owner lane settles its outcome.  Replaces
