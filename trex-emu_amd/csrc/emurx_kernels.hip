@@ -40,6 +40,7 @@ __global__ __launch_bounds__(kBlock) void k_rx(const uint8_t* __restrict__ frame
     __shared__ __attribute__((aligned(16))) uint32_t slab[kWaves * kStage / 4];
     __shared__ uint32_t s_wcnt[kWaves][16];
     __shared__ unsigned long long s_hist[kWaves][EMURX_HIST_BINS];  // {pkts << 40 | bytes}
+    __shared__ uint32_t s_csum[kWaves][kWave];                      // window path: span sums
 
     const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / kWave;
     const uint32_t tile = blockIdx.x;
@@ -92,7 +93,7 @@ __global__ __launch_bounds__(kBlock) void k_rx(const uint8_t* __restrict__ frame
         WinSrc s{reinterpret_cast<const uint8_t*>(slab), slab, wv * kStage + lane * 16, head,
                  min(kWinVec * 16 - head, len), frames + off};
         if (valid) parse_packet(s, len, vport, T.cb_mask, r);
-        coop_checksum(r, frames + off);  // the wave's long L4 spans, converged
+        coop_checksum(r, frames + off, s_csum[wv]);  // the wave's long L4 spans, converged
         if (valid && kClassify && !(EMURX_ABL & 2)) classify(s, len, T, r);
     }
     if (rec && !(EMURX_ABL & 16)) {

@@ -622,55 +622,59 @@ __device__ __forceinline__ uint32_t span_sum(const uint4& x, uint32_t nv, int h,
     if (k >= nv) return 0;
     return sad_vec_masked(x, k == 0 ? h : 0, k == nv - 1 ? t : 16, 0);
 }
-__device__ __forceinline__ void coop_checksum(Rec& r, const uint8_t* f) {
+__device__ __forceinline__ void coop_checksum(Rec& r, const uint8_t* f, uint32_t* wsum) {
+    // The wave's deferred spans are laid end to end as one list of 16-byte vectors (an
+    // exclusive prefix over lanes); each pass covers 64 x kPV consecutive vectors of that
+    // list, all loads in flight together, every lane finding the span its vector belongs to
+    // by a binary search over the prefix.  Partial sums go to the owner's LDS word.  No slot
+    // is wasted on short spans and a wave needs ceil(total / (64 kPV)) memory round trips.
+    constexpr uint32_t kPV = 4;
     const uint32_t lane = lane_id();
-    const uintptr_t my = (uintptr_t)(f + r.dstart);
-    uint64_t pend = __ballot(r.dlen != 0);
-    while (pend) {
-        constexpr int kB = 4;  // frames in flight
-        uint32_t J[kB], nv[kB];
-        int h[kB], t[kB];
-        const uint8_t* base[kB];
-        uint4 xa[kB], xb[kB];
+    const bool mine = r.dlen != 0;
+    if (!__ballot(mine)) return;
+    const uintptr_t a = (uintptr_t)(f + r.dstart), e = a + r.dlen;
+    const uint32_t nv = mine ? (uint32_t)((((e + 15) & ~(uintptr_t)15) - (a & ~(uintptr_t)15)) >> 4) : 0u;
+    uint32_t incl = nv;
 #pragma unroll
-        for (int k = 0; k < kB; ++k) {  // wave-uniform: frame, span geometry (scalar registers)
-            J[k] = pend ? (uint32_t)__ffsll((long long)pend) - 1 : 64u;
-            if (pend) pend &= pend - 1;
-            nv[k] = 0;
-            base[k] = f;
-            h[k] = 0;
-            t[k] = 16;
-            if (J[k] < 64) {
-                const uint32_t alo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)my, (int)J[k]);
-                const uint32_t ahi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(my >> 32), (int)J[k]);
-                const uint32_t n = (uint32_t)__builtin_amdgcn_readlane((int)r.dlen, (int)J[k]);
-                const uintptr_t a = ((uintptr_t)ahi << 32) | alo, e = a + n;
-                base[k] = reinterpret_cast<const uint8_t*>(a & ~(uintptr_t)15);
-                nv[k] = (uint32_t)((((e + 15) & ~(uintptr_t)15) - (a & ~(uintptr_t)15)) >> 4);
-                h[k] = (int)(a & 15);
-                t[k] = 16 - (int)((0u - (uint32_t)e) & 15);
-            }
-        }
-        // every frame's first two vectors per lane in flight before the first use
+    for (uint32_t o = 1; o < kWave; o <<= 1) {
+        const uint32_t up = (uint32_t)__shfl_up((int)incl, o);
+        if (lane >= o) incl += up;
+    }
+    const uint32_t P = incl - nv;
+    const uint32_t V = (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
+    const uintptr_t a16 = a & ~(uintptr_t)15;
+    const uint32_t blo = (uint32_t)a16, bhi = (uint32_t)(a16 >> 32);
+    const uint32_t geo = nv | ((uint32_t)(a & 15) << 16) | ((16u - ((0u - (uint32_t)e) & 15)) << 24);
+    wsum[lane] = 0;  // the wave's own words; its later LDS atomics are ordered after this
+    for (uint32_t b = 0; b < V; b += kWave * kPV) {  // wave-uniform
+        uint4 x[kPV];
+        uint32_t own[kPV], kin[kPV];
 #pragma unroll
-        for (int k = 0; k < kB; ++k) {
-            if (nv[k]) {
-                xa[k] = span_load(base[k], nv[k], lane);
-                xb[k] = span_load(base[k], nv[k], lane + 64);
-            }
+        for (uint32_t k = 0; k < kPV; ++k) {  // converged: shuffles read every lane
+            const uint32_t v = b + k * kWave + lane;
+            uint32_t j = 0;
+#pragma unroll
+            for (uint32_t s2 = kWave / 2; s2 > 0; s2 >>= 1)
+                if ((uint32_t)__shfl((int)P, (int)(j + s2)) <= v) j += s2;
+            own[k] = j;
+            kin[k] = v - (uint32_t)__shfl((int)P, (int)j);
+            const uint32_t lo = (uint32_t)__shfl((int)blo, (int)j), hi = (uint32_t)__shfl((int)bhi, (int)j);
+            const uint8_t* src = reinterpret_cast<const uint8_t*>(((uintptr_t)hi << 32) | lo);
+            x[k] = v < V ? gld16(src + 16 * kin[k]) : make_uint4(0, 0, 0, 0);
         }
 #pragma unroll
-        for (int k = 0; k < kB; ++k) {
-            if (J[k] >= 64) continue;
-            uint32_t acc = span_sum(xa[k], nv[k], h[k], t[k], lane) + span_sum(xb[k], nv[k], h[k], t[k], lane + 64);
-            for (uint32_t v = 128; v < nv[k]; v += 64)  // spans past 2 KiB (jumbo frames)
-                acc += span_sum(span_load(base[k], nv[k], v + lane), nv[k], h[k], t[k], v + lane);
-            const uint32_t T = wave_sum_u32(acc);
-            if (lane == J[k]) {
-                settle_deferred(r, csum_ok(T, (uint32_t)my, r.dpcs));
-                r.dlen = 0;
-            }
+        for (uint32_t k = 0; k < kPV; ++k) {
+            const uint32_t g = (uint32_t)__shfl((int)geo, (int)own[k]);
+            const uint32_t part = span_sum(x[k], g & 0xffff, (int)((g >> 16) & 0xff), (int)(g >> 24), kin[k]);
+            if (b + k * kWave + lane < V) atomicAdd(&wsum[own[k]], part);
         }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (mine) {
+        settle_deferred(r, csum_ok(wsum[lane], (uint32_t)a, r.dpcs));
+        r.dlen = 0;
     }
 }
 
