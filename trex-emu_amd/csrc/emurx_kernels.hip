@@ -106,11 +106,23 @@ __global__ __launch_bounds__(kBlock) void k_rx(const uint8_t* __restrict__ frame
             o[1] = h1;
         }
     }
-    if (valid) {
-        if (flow) flow[i] = r.flow;
-        // outcome histogram: one packed LDS add per frame into the wave's copy
-        if (!(EMURX_ABL & 4))
-            atomicAdd(&s_hist[wv][EMURX_HIST_BIN(r.status, r.proto)], (1ull << 40) | (unsigned long long)len);
+    if (valid && flow) flow[i] = r.flow;
+    // outcome histogram into the wave's LDS copy: a wave whose frames all share one
+    // (status, proto) bin adds its count (ballot) and byte sum (DPP reduction) once, instead
+    // of 64 LDS atomics serialised on one address; mixed waves add per frame
+    if (!(EMURX_ABL & 4)) {
+        const uint32_t bin = valid ? EMURX_HIST_BIN(r.status, r.proto) : 0xffu;
+        const uint64_t vm = __ballot(valid);
+        if (vm) {
+            const uint32_t lead = (uint32_t)__ffsll((long long)vm) - 1;
+            const uint32_t bb = (uint32_t)__builtin_amdgcn_readlane((int)bin, (int)lead);
+            if (__ballot(bin == bb) == vm) {
+                const uint32_t bytes = wave_sum_u32(valid ? len : 0u);  // <= 64 x 65535
+                if (lane == lead) s_hist[wv][bb] += ((unsigned long long)__popcll(vm) << 40) | bytes;
+            } else if (valid) {
+                atomicAdd(&s_hist[wv][bin], (1ull << 40) | (unsigned long long)len);
+            }
+        }
     }
     const uint32_t q = valid ? (r.status == EMURX_ST_OK ? r.proto : EMURX_Q_DROP) : 0xffu;
 
