@@ -12,9 +12,8 @@ if [ "${1:-run}" = build ]; then
     H="/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -DEMURX_ABL=$v"
     $H -c trex-emu_amd/csrc/emurx_kernels.hip -o trex-emu_amd/build/abl/k$v.o &&
     $H -c trex-emu_amd/csrc/emurx_route.hip -o trex-emu_amd/build/abl/r$v.o &&
-    $H -x hip -c trex-emu_amd/csrc/emurx_api.cpp -o trex-emu_amd/build/abl/a$v.o &&
     $H -shared -o trex-emu_amd/lib/abl/libemurx_$v.so trex-emu_amd/build/abl/k$v.o trex-emu_amd/build/abl/r$v.o \
-       trex-emu_amd/build/abl/a$v.o || exit 1
+       trex-emu_amd/build/emurx_ingest.o trex-emu_amd/build/emurx_tx.o trex-emu_amd/build/emurx_api.o || exit 1
   done
   exit 0
 fi
