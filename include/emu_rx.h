@@ -438,6 +438,13 @@ void emurx_hist_fold(const uint64_t* shards, uint64_t out[2 * EMURX_HIST_BINS]);
 int emurx_set_timing(emurx_t* h, uint32_t slots, uint32_t stride);
 int emurx_kernel_times(emurx_t* h, float* batch_ms, uint32_t cap, uint32_t* n_out);
 
+/* LDS staging slab (bytes per wave) of the most recent k_rx launch: 7168 or 6144 (0 before
+   the first).  Chosen per launch from sampled feedback of earlier launches (a wave whose
+   frames span 6-7 KiB fits only the wider slab); EMURX_STAGE=wide|narrow in the environment
+   at emurx_open forces one.  Results never depend on it.  No ABI replacement: a tuning
+   observable of this implementation. */
+uint32_t emurx_last_stage(const emurx_t* h);
+
 /* ---- Namespace-partitioned exchange (multi-GPU, one process per GPU) -------------------
    Frames shard by input offset across the GPUs of a node; each Namespace is owned by one
    partition, emurx_ns_owner(key) = a hash of its CTunnelKey (thread_ctx.go:92-97) mapped

@@ -259,6 +259,49 @@ def test_configs(rxmod, cfg, n):
         assert (rec["ns_id"] == 0).all() and (rec["client_id"] == 0).all()
 
 
+# ---- the two LDS staging slabs (emurx_launch_batch) ----------------------------------------
+@pytest.mark.parametrize("mode", ["wide", "narrow"])
+def test_stage_sizes(rxmod, monkeypatch, mode):
+    monkeypatch.setenv("EMURX_STAGE", mode)
+    for cfg, n in (("config_c", 1 << 17), ("config_e", 1 << 15), ("config_b", 1 << 16)):
+        w = getattr(synth, cfg)(n)
+        rx, o = new_pair(rxmod)
+        synth.load_tables(w, rx)
+        synth.load_tables(w, o)
+        check_batch(rx, o, w["buf"], w["desc"])
+        assert rx.last_stage() == (7168 if mode == "wide" else 6144)
+
+
+def _spaced(w, stride):
+    """The same frames, `stride` bytes apart: every wave spans 64 * stride bytes."""
+    d = w["desc"]
+    buf = np.zeros(len(d) * stride + 64, np.uint8)
+    nd = d.copy()
+    for i in range(len(d)):
+        o, n = int(d["off"][i]), int(d["len"][i])
+        buf[i * stride:i * stride + n] = w["buf"][o:o + n]
+    nd["off"] = np.arange(len(d), dtype=np.uint32) * stride
+    return buf, nd
+
+
+def test_stage_auto_choice(rxmod, monkeypatch):
+    """Waves spanning 6-7 KiB keep the wide slab; 64-byte frames switch to the narrow one
+    after one launch of feedback.  Parity holds either way."""
+    monkeypatch.delenv("EMURX_STAGE", raising=False)
+    w = synth.config_b(1 << 16)
+    rx, o = new_pair(rxmod)
+    synth.load_tables(w, rx)
+    synth.load_tables(w, o)
+    sbuf, sdesc = _spaced(w, 100)  # 6,400 B per wave
+    seq = []
+    # decisions at launches 8, 16, 24, 32, each from the samples copied back by the launch
+    # at the previous decision point (launch 24 sees launch 16's dense frames)
+    for buf, desc in [(sbuf, sdesc)] * 8 + [(w["buf"], w["desc"])] * 8 + [(sbuf, sdesc)] * 16:
+        check_batch(rx, o, buf, desc)
+        seq.append(rx.last_stage())
+    assert seq == [7168] * 23 + [6144] * 8 + [7168], seq
+
+
 def test_kernel_timing_stride(rxmod):
     """emurx_set_timing(slots, stride): every stride-th batch carries an event pair."""
     rx, _ = new_pair(rxmod)

@@ -180,6 +180,20 @@ struct emurx_ctx {
     // Namespace-partition packing scratch (emurx_route_dev)
     DevBuf<uint32_t> d_route_cnt, d_route_grp, d_route_goff;  // grp: zero between batches
 
+    // k_rx staging slab per launch (emurx_launch_batch): the narrow 6 KiB slab runs 6
+    // workgroups per CU instead of 5, but a wave whose frames span 6-7 KiB then takes the
+    // slower window path.  Sampled tiles report how many of their waves fall in that band
+    // into device words; every 8th launch copies them to pinned memory behind itself (stream
+    // order, no synchronisation) and the next decision point reads that copy.  The kernel
+    // writing host memory directly was tried: host reads of lines the GPU keeps writing made
+    // some launches 5x slower.  EMURX_STAGE=wide|narrow forces one size (tests, A/B).
+    DevBuf<uint32_t> d_stage_fb;  // 64 sampled tiles x 4 waves: gen << 2 | has_frames << 1 | mid
+    PinBuf<uint32_t> stage_fb;    // its copy
+    uint32_t stage_gen = 0, stage_mode = 0;  // 0 auto, 1 wide, 2 narrow
+    bool stage_copy = false;
+    bool stage_narrow = false;
+    uint32_t last_stage = 0;
+
     // timing ring: 2 events per batch (around the k_rx launch)
     std::vector<hipEvent_t> ev;
     uint32_t slots = 0, ev_head = 0, ev_count = 0, stride = 1, batch_seq = 0;
@@ -347,6 +361,41 @@ int rebuild_and_upload(emurx_t* h, hipStream_t st) {
 uint32_t ntiles(uint32_t n) { return (n + EMURX_QUEUE_TILE - 1) / EMURX_QUEUE_TILE; }
 size_t queue_cap(uint32_t n) { return (size_t)ntiles(n) * EMURX_QUEUE_TILE; }
 
+// the staging slab of the next k_rx launch (see emurx_ctx::stage_fb); advances stage_gen
+bool choose_stage_(emurx_t* h) {
+    ++h->stage_gen;
+    h->stage_gen &= 0x3fffffffu;
+    if (h->stage_mode) return h->stage_mode == 2;
+    // re-decided every 8th launch from the copy the previous decision point's launch made
+    // (the samples of up to 16 launches back); this launch refreshes the copy
+    if (h->stage_gen & 7) return h->stage_narrow;
+    h->stage_copy = true;
+    uint32_t waves = 0, mid = 0;
+    for (int i = 0; i < 256; ++i) {
+        const uint32_t w = __atomic_load_n(h->stage_fb.p + i, __ATOMIC_RELAXED);
+        const uint32_t age = (h->stage_gen - (w >> 2)) & 0x3fffffffu;
+        if ((w >> 2) && age <= 24) {
+            waves += (w >> 1) & 1;
+            mid += w & 1;
+        }
+    }
+    // a wave in the 6-7 KiB band costs several staged waves on the window path; below 1% of
+    // the sampled waves the extra workgroup per CU wins (configs B, E), above it loses (C)
+    if (waves) h->stage_narrow = mid * 100 <= waves;
+    return h->stage_narrow;
+}
+int stage_copy_back(emurx_t* h, hipStream_t st) {
+    if (!h->stage_copy) return 0;
+    h->stage_copy = false;
+    return hipMemcpyAsync(h->stage_fb.p, h->d_stage_fb.p, 256 * sizeof(uint32_t), hipMemcpyDeviceToHost, st) ==
+                   hipSuccess ? 0 : -1;
+}
+bool choose_stage(emurx_t* h) {
+    const bool narrow = choose_stage_(h);
+    h->last_stage = narrow ? 6144u : 7168u;
+    return narrow;
+}
+
 int run_dev(emurx_t* h, const uint8_t* frames, const emurx_desc* desc, uint32_t n,
             const emurx_dev_out* out, void* stream, bool classify) {
     if (!h || !out || !out->hist || (n && (!frames || !desc))) return EMURX_EINVAL;
@@ -365,7 +414,9 @@ int run_dev(emurx_t* h, const uint8_t* frames, const emurx_desc* desc, uint32_t 
         h->ev_head = (s + 1) % h->slots;
         h->ev_count = std::min(h->ev_count + 1, h->slots);
     }
-    int r = emurx_launch_batch(frames, desc, n, T, classify, *out, st, ev);
+    const bool narrow = choose_stage(h);
+    int r = emurx_launch_batch(frames, desc, n, T, classify, *out, st, ev, narrow, h->d_stage_fb.p, h->stage_gen);
+    if (!r) r = stage_copy_back(h, st);
     return r ? EMURX_EDEVICE : EMURX_OK;
 }
 
@@ -433,7 +484,11 @@ int ingest_submit(emurx_t* h, uint32_t slot, const emurx_msg* msgs, uint32_t nms
     if (emurx_launch_zmq_walk(s.d_buf.p, s.d_ctl.p, nmsg, s.d_desc.p, s.d_stat.p, st)) return EMURX_EDEVICE;
     if (n) {
         const emurx_dev_out o{s.d_rec.p, s.d_qlist.p, (uint32_t)qcap, s.d_tile_cnt.p, s.d_hist.p};
-        if (emurx_launch_batch(s.d_buf.p, s.d_desc.p, n, h->tables(), true, o, st, nullptr)) return EMURX_EDEVICE;
+        const bool narrow = choose_stage(h);
+        if (emurx_launch_batch(s.d_buf.p, s.d_desc.p, n, h->tables(), true, o, st, nullptr, narrow,
+                               h->d_stage_fb.p, h->stage_gen) ||
+            stage_copy_back(h, st))
+            return EMURX_EDEVICE;
     }
     if (emurx_launch_queue_pack(s.d_qlist.p, (uint32_t)qcap, s.d_tile_cnt.p, n, s.d_seg_off.p, s.d_packed.p,
                                 s.d_qoff.p, s.d_hist.p, s.d_hist_out.p, st))
@@ -549,6 +604,13 @@ int emurx_open(const emurx_cfg* cfg, emurx_t** out) {
         emurx_close(h);
         return EMURX_ENOMEM;
     }
+    if (const char* e = getenv("EMURX_STAGE")) h->stage_mode = !strcmp(e, "wide") ? 1 : !strcmp(e, "narrow") ? 2 : 0;
+    if (h->stage_fb.alloc(256) || h->d_stage_fb.alloc(256) ||
+        hipMemset(h->d_stage_fb.p, 0, 256 * sizeof(uint32_t)) != hipSuccess) {
+        emurx_close(h);
+        return EMURX_ENOMEM;
+    }
+    memset(h->stage_fb.p, 0, 256 * sizeof(uint32_t));
     h->dirty = true;
     if ((rc = rebuild_and_upload(h, h->stream))) { emurx_close(h); return rc; }
     *out = h;
@@ -560,6 +622,8 @@ void emurx_close(emurx_t* h) {
     bind(h);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     for (auto& s : h->ing) s.release();
+    h->stage_fb.release();
+    h->d_stage_fb.release();
     h->d_ns.release(); h->d_nsinfo.release(); h->d_mac.release(); h->d_ip4.release();
     h->d_ip6.release(); h->d_client.release();
     h->d_ft4.release(); h->d_ft6.release(); h->d_srv.release();
@@ -957,6 +1021,8 @@ int emurx_set_timing(emurx_t* h, uint32_t slots, uint32_t stride) {
     h->ev_head = h->ev_count = h->batch_seq = 0;
     return EMURX_OK;
 }
+
+uint32_t emurx_last_stage(const emurx_t* h) { return h ? h->last_stage : 0; }
 
 int emurx_kernel_times(emurx_t* h, float* batch_ms, uint32_t cap, uint32_t* n_out) {
     if (!h || !n_out || (cap && !batch_ms)) return EMURX_EINVAL;

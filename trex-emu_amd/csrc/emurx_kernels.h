@@ -6,10 +6,12 @@
 #include "emurx_tables.h"
 
 // Enqueue one batch on `st`: a single k_rx launch, no host synchronisation (capturable in a
-// hipGraph).  ev[0..1] (optional) are recorded before and after it.  Returns 0 or -1.
+// hipGraph).  ev[0..1] (optional) are recorded before and after it.  narrow: the 6 KiB
+// staging slab (6 workgroups per CU) instead of 7 KiB (5).  fb (optional, host-visible,
+// 64 * 4 words): the sampled tiles' stage feedback, tagged with gen.  Returns 0 or -1.
 int emurx_launch_batch(const uint8_t* frames, const emurx_desc* desc, uint32_t n,
                        const emurx_dev_tables& T, bool classify, const emurx_dev_out& out,
-                       hipStream_t st, const hipEvent_t* ev);
+                       hipStream_t st, const hipEvent_t* ev, bool narrow, uint32_t* fb, uint32_t gen);
 
 // Enqueue the Namespace-partition packing of a classified batch (emurx_route.hip): three
 // launches on `st`.  Scratch: tile_cnt [ceil(n / 256) * 16]; grp, grp_off [groups * 16] with

@@ -29,17 +29,19 @@ __device__ __forceinline__ void glds16(const uint4* src, uint4* dst_wave_base) {
 }
 __device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0)
 
-template <bool kClassify>
+template <bool kClassify, uint32_t kStage>
 __global__ __launch_bounds__(kBlock) void k_rx(const uint8_t* __restrict__ frames,
                                                const emurx_desc* __restrict__ desc, uint32_t n,
                                                emurx_dev_tables T, emurx_rec* __restrict__ rec,
                                                uint32_t* __restrict__ qlist, uint32_t qcap,
                                                uint32_t* __restrict__ tile_cnt,
                                                unsigned long long* __restrict__ hist,
-                                               uint32_t* __restrict__ flow) {
+                                               uint32_t* __restrict__ flow, uint32_t* __restrict__ fb,
+                                               uint32_t gen) {
+    constexpr uint32_t kWinVec = kStage / 16 / kWave;  // window path: 16-byte vectors per lane
     __shared__ __attribute__((aligned(16))) uint32_t slab[kWaves * kStage / 4];
     __shared__ uint32_t s_wcnt[kWaves][16];
-    __shared__ unsigned long long s_hist[kWaves][EMURX_HIST_BINS];  // {pkts << 40 | bytes}
+    __shared__ uint32_t s_hist[kWaves][EMURX_HIST_BINS];  // {pkts << 23 | bytes}: <= 64 x 65535 B
     __shared__ uint32_t s_csum[kWaves][kWave];                      // window path: span sums
 
     const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / kWave;
@@ -59,6 +61,13 @@ __global__ __launch_bounds__(kBlock) void k_rx(const uint8_t* __restrict__ frame
     const uint32_t nvec = hi > lo ? (hi - start + 15) >> 4 : 0;
     const bool staged = nvec > 0 && nvec <= kStage / 16;
     uint4* wslab = reinterpret_cast<uint4*>(slab) + wv * (kStage / 16);
+    // stage-size feedback from every 64th tile (the launcher's choice, emurx_api.cpp): one
+    // word per wave {gen, the wave has frames, its range fits the wide slab only}
+    if (fb && (tile & 63) == 0 && lane == 0) {
+        const uint32_t bytes = nvec * 16;
+        const uint32_t mid = bytes > kStageNarrow && bytes <= kStageWide;
+        fb[((tile >> 6) & 63) * kWaves + wv] = (gen << 2) | ((nvec > 0) << 1) | mid;
+    }
     if (staged) {  // all copies in flight before the wait; clamped sources stay in bounds
         static_assert(kStage / 16 <= 8 * kWave, "staging issues at most 8 vectors per lane");
         const uint4* src = reinterpret_cast<const uint4*>(frames + start);
@@ -121,9 +130,9 @@ __global__ __launch_bounds__(kBlock) void k_rx(const uint8_t* __restrict__ frame
             const uint32_t bb = (uint32_t)__builtin_amdgcn_readlane((int)bin, (int)lead);
             if (__ballot(bin == bb) == vm) {
                 const uint32_t bytes = wave_sum_u32(valid ? len : 0u);  // <= 64 x 65535
-                if (lane == lead) s_hist[wv][bb] += ((unsigned long long)__popcll(vm) << 40) | bytes;
+                if (lane == lead) s_hist[wv][bb] += ((uint32_t)__popcll(vm) << 23) | bytes;
             } else if (valid) {
-                atomicAdd(&s_hist[wv][bin], (1ull << 40) | (unsigned long long)len);
+                atomicAdd(&s_hist[wv][bin], (1u << 23) | len);
             }
         }
     }
@@ -156,11 +165,16 @@ __global__ __launch_bounds__(kBlock) void k_rx(const uint8_t* __restrict__ frame
     // every workgroup would serialise; the shards are folded on the host
     if (tid >= 64 && tid < 64 + EMURX_HIST_BINS) {
         const uint32_t b = tid - 64;
-        const unsigned long long v = s_hist[0][b] + s_hist[1][b] + s_hist[2][b] + s_hist[3][b];
-        if (v) {
+        uint32_t pk = 0, by = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < kWaves; ++w) {
+            pk += s_hist[w][b] >> 23;
+            by += s_hist[w][b] & ((1u << 23) - 1);
+        }
+        if (pk) {
             unsigned long long* hs = hist + (size_t)(tile & (EMURX_HIST_SHARDS - 1)) * 2 * EMURX_HIST_BINS;
-            atomicAdd(&hs[2 * b], v >> 40);
-            atomicAdd(&hs[2 * b + 1], v & ((1ull << 40) - 1));
+            atomicAdd(&hs[2 * b], (unsigned long long)pk);
+            atomicAdd(&hs[2 * b + 1], (unsigned long long)by);
         }
     }
 }
@@ -173,18 +187,16 @@ __global__ __launch_bounds__(kBlock) void k_rx(const uint8_t* __restrict__ frame
 // ---------------------------------------------------------------------------------------
 int emurx_launch_batch(const uint8_t* frames, const emurx_desc* desc, uint32_t n,
                        const emurx_dev_tables& T, bool classify, const emurx_dev_out& out,
-                       hipStream_t st, const hipEvent_t* ev) {
+                       hipStream_t st, const hipEvent_t* ev, bool narrow, uint32_t* fb, uint32_t gen) {
     using namespace emurx;
     if (ev) (void)hipEventRecord(ev[0], st);
     if (n) {
-        const uint32_t ntiles = (n + EMURX_QUEUE_TILE - 1) / EMURX_QUEUE_TILE;
+        const dim3 g((n + EMURX_QUEUE_TILE - 1) / EMURX_QUEUE_TILE), b(kBlock);
         unsigned long long* hist = reinterpret_cast<unsigned long long*>(out.hist);
-        if (classify)
-            hipLaunchKernelGGL(k_rx<true>, dim3(ntiles), dim3(kBlock), 0, st, frames, desc, n, T, out.rec,
-                               out.qlist, out.qcap, out.tile_cnt, hist, out.flow);
-        else
-            hipLaunchKernelGGL(k_rx<false>, dim3(ntiles), dim3(kBlock), 0, st, frames, desc, n, T, out.rec,
-                               out.qlist, out.qcap, out.tile_cnt, hist, out.flow);
+        auto k = classify ? (narrow ? k_rx<true, kStageNarrow> : k_rx<true, kStageWide>)
+                          : (narrow ? k_rx<false, kStageNarrow> : k_rx<false, kStageWide>);
+        hipLaunchKernelGGL(k, g, b, 0, st, frames, desc, n, T, out.rec, out.qlist, out.qcap, out.tile_cnt, hist,
+                           out.flow, fb, gen);
     }
     if (ev) (void)hipEventRecord(ev[1], st);
     return hipGetLastError() == hipSuccess ? 0 : -1;

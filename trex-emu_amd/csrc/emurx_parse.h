@@ -19,8 +19,9 @@ constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / kWave;
 // LDS bytes staged per wave (64 frames).  7 KiB keeps a workgroup's LDS under 32 KiB, so
 // five workgroups (20 waves) fit a CU; waves whose frames span more take the window path
-constexpr uint32_t kStage = 7168;
-constexpr uint32_t kWinVec = kStage / 16 / 64;  // window path: 16-byte vectors per lane (112 B)
+// LDS staging slab per wave (emurx_kernels.hip): two sizes, chosen per launch (kStageNarrow
+// gives 6 workgroups per CU instead of 5; waves wider than it take the window path)
+constexpr uint32_t kStageWide = 7168, kStageNarrow = 6144;
 
 #ifndef EMURX_ABL
 #define EMURX_ABL 0  // experiment-only stage ablation (tools/ablate.sh); 0 in every real build

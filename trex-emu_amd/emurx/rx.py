@@ -166,6 +166,10 @@ class RxPath:
         abi.check(self.lib.emurx_kernel_times(self.h, _p(a), cap, C.byref(n)), "kernel_times")
         return a[: n.value]
 
+    def last_stage(self) -> int:
+        """LDS staging bytes per wave of the most recent k_rx launch (7168 or 6144)."""
+        return int(self.lib.emurx_last_stage(self.h))
+
 
     # ---- batched host ingest (many ZMQ messages per GPU round trip) -------------------------
     def ingest_buffer(self, slot: int, nbytes: int) -> np.ndarray:
