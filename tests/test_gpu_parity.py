@@ -294,12 +294,12 @@ def test_stage_auto_choice(rxmod, monkeypatch):
     synth.load_tables(w, o)
     sbuf, sdesc = _spaced(w, 100)  # 6,400 B per wave
     seq = []
-    # decisions at launches 8, 16, 24, 32, each from the samples copied back by the launch
-    # at the previous decision point (launch 24 sees launch 16's dense frames)
+    # launches 1, 9, 17, 25 copy their samples back; each batch here is synchronised, so
+    # launches 2, 10, 18, 26 decide from them (launch 10 from launch 9's dense frames)
     for buf, desc in [(sbuf, sdesc)] * 8 + [(w["buf"], w["desc"])] * 8 + [(sbuf, sdesc)] * 16:
         check_batch(rx, o, buf, desc)
         seq.append(rx.last_stage())
-    assert seq == [7168] * 23 + [6144] * 8 + [7168], seq
+    assert seq == [7168] * 9 + [6144] * 8 + [7168] * 15, seq
 
 
 def test_kernel_timing_stride(rxmod):

@@ -183,14 +183,17 @@ struct emurx_ctx {
     // k_rx staging slab per launch (emurx_launch_batch): the narrow 6 KiB slab runs 6
     // workgroups per CU instead of 5, but a wave whose frames span 6-7 KiB then takes the
     // slower window path.  Sampled tiles report how many of their waves fall in that band
-    // into device words; every 8th launch copies them to pinned memory behind itself (stream
-    // order, no synchronisation) and the next decision point reads that copy.  The kernel
+    // into device words; the first launch and then at most every 8th copies them to pinned
+    // memory behind itself (stream order, an event, no synchronisation), and the first
+    // launch after the copy has landed decides.  The kernel
     // writing host memory directly was tried: host reads of lines the GPU keeps writing made
     // some launches 5x slower.  EMURX_STAGE=wide|narrow forces one size (tests, A/B).
     DevBuf<uint32_t> d_stage_fb;  // 64 sampled tiles x 4 waves: gen << 2 | has_frames << 1 | mid
     PinBuf<uint32_t> stage_fb;    // its copy
     uint32_t stage_gen = 0, stage_mode = 0;  // 0 auto, 1 wide, 2 narrow
-    bool stage_copy = false;
+    bool stage_copy = false, stage_pending = false;
+    uint32_t stage_copy_gen = 0;
+    hipEvent_t stage_ev = nullptr;
     bool stage_narrow = false;
     uint32_t last_stage = 0;
 
@@ -366,29 +369,40 @@ bool choose_stage_(emurx_t* h) {
     ++h->stage_gen;
     h->stage_gen &= 0x3fffffffu;
     if (h->stage_mode) return h->stage_mode == 2;
-    // re-decided every 8th launch from the copy the previous decision point's launch made
-    // (the samples of up to 16 launches back); this launch refreshes the copy
-    if (h->stage_gen & 7) return h->stage_narrow;
-    h->stage_copy = true;
-    uint32_t waves = 0, mid = 0;
-    for (int i = 0; i < 256; ++i) {
-        const uint32_t w = __atomic_load_n(h->stage_fb.p + i, __ATOMIC_RELAXED);
-        const uint32_t age = (h->stage_gen - (w >> 2)) & 0x3fffffffu;
-        if ((w >> 2) && age <= 24) {
-            waves += (w >> 1) & 1;
-            mid += w & 1;
+    // decide as soon as the last copy-back has landed (an event query, no waiting)
+    if (h->stage_pending && hipEventQuery(h->stage_ev) == hipSuccess) {
+        h->stage_pending = false;
+        // the sampled waves of the 16 launches up to the copied one (a 1M-frame launch
+        // rewrites all 256 words, a small one only the first few)
+        uint32_t waves = 0, mid = 0;
+        for (int i = 0; i < 256; ++i) {
+            const uint32_t w = h->stage_fb.p[i];
+            const uint32_t age = (h->stage_copy_gen - (w >> 2)) & 0x3fffffffu;
+            if ((w >> 2) && age < 16) {
+                waves += (w >> 1) & 1;
+                mid += w & 1;
+            }
         }
+        // a wave in the 6-7 KiB band costs several staged waves on the window path; below
+        // 1% of the sampled waves the extra workgroup per CU wins (configs B, E), above it
+        // loses (C)
+        if (waves) h->stage_narrow = mid * 100 <= waves;
     }
-    // a wave in the 6-7 KiB band costs several staged waves on the window path; below 1% of
-    // the sampled waves the extra workgroup per CU wins (configs B, E), above it loses (C)
-    if (waves) h->stage_narrow = mid * 100 <= waves;
+    // the first launch and then at most every 8th copies its samples back
+    if (!h->stage_pending && (!h->stage_copy_gen || ((h->stage_gen - h->stage_copy_gen) & 0x3fffffffu) >= 8))
+        h->stage_copy = true;
     return h->stage_narrow;
 }
 int stage_copy_back(emurx_t* h, hipStream_t st) {
     if (!h->stage_copy) return 0;
     h->stage_copy = false;
-    return hipMemcpyAsync(h->stage_fb.p, h->d_stage_fb.p, 256 * sizeof(uint32_t), hipMemcpyDeviceToHost, st) ==
-                   hipSuccess ? 0 : -1;
+    if (hipMemcpyAsync(h->stage_fb.p, h->d_stage_fb.p, 256 * sizeof(uint32_t), hipMemcpyDeviceToHost, st) !=
+            hipSuccess ||
+        hipEventRecord(h->stage_ev, st) != hipSuccess)
+        return -1;
+    h->stage_pending = true;
+    h->stage_copy_gen = h->stage_gen;
+    return 0;
 }
 bool choose_stage(emurx_t* h) {
     const bool narrow = choose_stage_(h);
@@ -606,6 +620,7 @@ int emurx_open(const emurx_cfg* cfg, emurx_t** out) {
     }
     if (const char* e = getenv("EMURX_STAGE")) h->stage_mode = !strcmp(e, "wide") ? 1 : !strcmp(e, "narrow") ? 2 : 0;
     if (h->stage_fb.alloc(256) || h->d_stage_fb.alloc(256) ||
+        hipEventCreateWithFlags(&h->stage_ev, hipEventDisableTiming) != hipSuccess ||
         hipMemset(h->d_stage_fb.p, 0, 256 * sizeof(uint32_t)) != hipSuccess) {
         emurx_close(h);
         return EMURX_ENOMEM;
@@ -624,6 +639,7 @@ void emurx_close(emurx_t* h) {
     for (auto& s : h->ing) s.release();
     h->stage_fb.release();
     h->d_stage_fb.release();
+    if (h->stage_ev) (void)hipEventDestroy(h->stage_ev);
     h->d_ns.release(); h->d_nsinfo.release(); h->d_mac.release(); h->d_ip4.release();
     h->d_ip6.release(); h->d_client.release();
     h->d_ft4.release(); h->d_ft6.release(); h->d_srv.release();

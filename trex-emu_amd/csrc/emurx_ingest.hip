@@ -22,7 +22,7 @@
 
 namespace emurx {
 
-constexpr uint32_t kScanLanes = 1024;
+constexpr uint32_t kScanLanes = 512;  // 1024 capped VGPRs at 128 and spilled
 
 // 4 bytes at any address as a big-endian word (two aligned dword loads + funnel shift; the
 // staging buffer is padded, so the second dword is always readable)
