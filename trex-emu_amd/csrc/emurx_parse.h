@@ -693,17 +693,26 @@ __device__ __forceinline__ Bucket ld_bucket(const uint32_t* tab, uint32_t b) {
     return Bucket{{gld16(p), gld16(p + 4), gld16(p + 8), gld16(p + 12)}};
 }
 
+// Lookups stop at the first bucket holding an empty slot.  A key sits at most once in a
+// table and the host rebuilds the tables without holes (bucket_put, emurx_api.cpp), so "a
+// matching slot anywhere in the bucket" equals the in-order scan and slot order is free.
 // ns slot {vport | ns_plugins << 16, vlan0, vlan1, ns_id} -> (ns_id, ns plugin mask)
 __device__ __forceinline__ uint2 resolve_ns(const emurx_dev_tables& T, uint32_t b, Bucket e, uint32_t w0, uint32_t w1,
                             uint32_t w2) {
+    {  // the home bucket's first slot alone: the common hit, a uniform early exit
+        const uint4 x = e.s[0];
+        if (x.w != EMURX_EMPTY && (x.x & 0xffffu) == w0 && x.y == w1 && x.z == w2) return make_uint2(x.w, x.x >> 16);
+    }
     for (uint32_t n = 0;;) {
+        bool hole = false;
+        uint2 hit = make_uint2(EMURX_ID_NONE, 0);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint4 x = e.s[k];
-            if (x.w == EMURX_EMPTY) return make_uint2(EMURX_ID_NONE, 0);
-            if ((x.x & 0xffffu) == w0 && x.y == w1 && x.z == w2) return make_uint2(x.w, x.x >> 16);
+            hole |= x.w == EMURX_EMPTY;
+            if (x.w != EMURX_EMPTY && (x.x & 0xffffu) == w0 && x.y == w1 && x.z == w2) hit = make_uint2(x.w, x.x >> 16);
         }
-        if (++n > T.ns_mask) return make_uint2(EMURX_ID_NONE, 0);
+        if (hit.x != EMURX_ID_NONE || hole || ++n > T.ns_mask) return hit;
         b = (b + 1) & T.ns_mask;
         e = ld_bucket(T.ns_tab, b);
     }
@@ -711,28 +720,40 @@ __device__ __forceinline__ uint2 resolve_ns(const emurx_dev_tables& T, uint32_t 
 // mac slot {ns_id, mac[0..3], mac[4..5] | client_plugins << 16, client_id} -> (cid, plugins)
 __device__ __forceinline__ uint2 resolve_mac(const emurx_dev_tables& T, uint32_t b, Bucket e, uint32_t ns, uint32_t lo,
                              uint32_t hi) {
+    {
+        const uint4 x = e.s[0];
+        if (x.w != EMURX_EMPTY && x.x == ns && x.y == lo && (x.z & 0xffffu) == hi) return make_uint2(x.w, x.z >> 16);
+    }
     for (uint32_t n = 0;;) {
+        bool hole = false;
+        uint2 hit = make_uint2(EMURX_ID_NONE, 0);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint4 x = e.s[k];
-            if (x.w == EMURX_EMPTY) return make_uint2(EMURX_ID_NONE, 0);
-            if (x.x == ns && x.y == lo && (x.z & 0xffffu) == hi) return make_uint2(x.w, x.z >> 16);
+            hole |= x.w == EMURX_EMPTY;
+            if (x.w != EMURX_EMPTY && x.x == ns && x.y == lo && (x.z & 0xffffu) == hi) hit = make_uint2(x.w, x.z >> 16);
         }
-        if (++n > T.mac_mask) return make_uint2(EMURX_ID_NONE, 0);
+        if (hit.x != EMURX_ID_NONE || hole || ++n > T.mac_mask) return hit;
         b = (b + 1) & T.mac_mask;
         e = ld_bucket(T.mac_tab, b);
     }
 }
 // ip4 slot {ns_id, ip, 0, client_id}
 __device__ __forceinline__ uint32_t resolve_ip4(const emurx_dev_tables& T, uint32_t b, Bucket e, uint32_t ns, uint32_t ip) {
+    {
+        const uint4 x = e.s[0];
+        if (x.w != EMURX_EMPTY && x.x == ns && x.y == ip) return x.w;
+    }
     for (uint32_t n = 0;;) {
+        bool hole = false;
+        uint32_t hit = EMURX_ID_NONE;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint4 x = e.s[k];
-            if (x.w == EMURX_EMPTY) return EMURX_ID_NONE;
-            if (x.x == ns && x.y == ip) return x.w;
+            hole |= x.w == EMURX_EMPTY;
+            if (x.w != EMURX_EMPTY && x.x == ns && x.y == ip) hit = x.w;
         }
-        if (++n > T.ip4_mask) return EMURX_ID_NONE;
+        if (hit != EMURX_ID_NONE || hole || ++n > T.ip4_mask) return hit;
         b = (b + 1) & T.ip4_mask;
         e = ld_bucket(T.ip4_tab, b);
     }
@@ -740,13 +761,15 @@ __device__ __forceinline__ uint32_t resolve_ip4(const emurx_dev_tables& T, uint3
 // ip6 slot {ns_id, ip[0..3], ip[4..7], ip[8..11]} {ip[12..15], 0, 0, client_id}, 2 per bucket
 __device__ __forceinline__ uint32_t resolve_ip6(const emurx_dev_tables& T, uint32_t b, Bucket e, uint32_t ns, const uint32_t w[4]) {
     for (uint32_t n = 0;;) {
+        bool hole = false;
+        uint32_t hit = EMURX_ID_NONE;
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             const uint4 x = e.s[2 * k], y = e.s[2 * k + 1];
-            if (y.w == EMURX_EMPTY) return EMURX_ID_NONE;
-            if (x.x == ns && x.y == w[0] && x.z == w[1] && x.w == w[2] && y.x == w[3]) return y.w;
+            hole |= y.w == EMURX_EMPTY;
+            if (y.w != EMURX_EMPTY && x.x == ns && x.y == w[0] && x.z == w[1] && x.w == w[2] && y.x == w[3]) hit = y.w;
         }
-        if (++n > T.ip6_mask) return EMURX_ID_NONE;
+        if (hit != EMURX_ID_NONE || hole || ++n > T.ip6_mask) return hit;
         b = (b + 1) & T.ip6_mask;
         e = ld_bucket(T.ip6_tab, b);
     }
