@@ -30,7 +30,7 @@ __device__ __forceinline__ void glds16(const uint4* src, uint4* dst_wave_base) {
 __device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0)
 
 template <bool kClassify, uint32_t kStage>
-__global__ __launch_bounds__(kBlock) void k_rx(const uint8_t* __restrict__ frames,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage == kStageNarrow ? 6 : 5))) void k_rx(const uint8_t* __restrict__ frames,
                                                const emurx_desc* __restrict__ desc, uint32_t n,
                                                emurx_dev_tables T, emurx_rec* __restrict__ rec,
                                                uint32_t* __restrict__ qlist, uint32_t qcap,
