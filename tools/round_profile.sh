@@ -25,7 +25,7 @@ step prof_B 300 rocprofv3 --kernel-trace --stats -d $out/prof_B -o run --output-
   -- python bench.py --steps 50 --warmup 5 --no-cpu-baseline
 for c in FETCH_SIZE WRITE_SIZE; do
   step pmc_$c 120 rocprofv3 --pmc $c -T --kernel-include-regex k_rx -d $out/pmc_$c -o run --output-format csv \
-    -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-check
+    -- python bench.py --steps 40 --warmup 8 --no-cpu-baseline --no-check
 done
 python tools/pmc_summary.py $out > $out/pmc_summary.txt 2>&1; cat $out/pmc_summary.txt
 echo done
