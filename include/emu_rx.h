@@ -423,6 +423,25 @@ typedef struct emurx_tx_desc {
 int emurx_tx_checksum_dev(emurx_t* h, uint8_t* d_frames, const emurx_tx_desc* d_desc, uint32_t n,
                           uint8_t* d_status, void* stream);
 
+/* ---- tx framing: VethIFZmq.Send / FlushTx (src/emu/core/veth_zmq.go:149-200) ------------
+   The n frames desc[i] = {off, len, vport} of d_frames, in order, are packed into ZMQ
+   messages exactly as n consecutive Send calls followed by one FlushTx would pack them:
+     a frame whose length would bring the open message's frame bytes to
+     ZMQ_TX_MAX_BUFFER_SIZE or more first closes it (:186-188); a message closes at
+     ZMQ_TX_PKT_BURST_SIZE frames (:198-200);
+     message = BE32 EMURX_ZMQ_MAGIC << 16 | frames (:157-159), then per frame
+     BE32 0xAA << 24 | vport << 16 | len (:167-169) and the frame's bytes.
+   The messages land back to back in d_out.  d_msg_off[m] (u64) is message m's start and
+   d_msg_off[n_msgs] the total; capacity n + 1.  d_info = {n_msgs, total bytes}.  Nothing is
+   written at or past out_cap; out_cap >= 8 * n + sum(len) always suffices, and d_info
+   tells the size needed when it did not.  A stream-ordered sequence of launches, no host
+   synchronisation.  Replaces VethIFZmq.FlushTx's per-frame append loop. */
+#define EMURX_ZMQ_TX_BURST 64u            /* ZMQ_TX_PKT_BURST_SIZE  veth_zmq.go:36 */
+#define EMURX_ZMQ_TX_MAX_BUFFER 32768u    /* ZMQ_TX_MAX_BUFFER_SIZE veth_zmq.go:37 */
+#define EMURX_ZMQ_PKT_MAGIC 0xAAu         /* per-frame header tag   veth_zmq.go:167 */
+int emurx_tx_zmq_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_desc, uint32_t n,
+                     uint8_t* d_out, uint64_t out_cap, uint64_t* d_msg_off, uint64_t* d_info, void* stream);
+
 /* ParserStats delta from an outcome histogram (pure host arithmetic). */
 void emurx_hist_to_counters(const uint64_t hist[2 * EMURX_HIST_BINS], emurx_counters* out);
 /* Sum the EMURX_HIST_SHARDS copies of a device histogram (after a D2H copy). */

@@ -947,6 +947,58 @@ void orc_tx_checksum(uint8_t* frames, const emurx_tx_desc* d, uint32_t n, uint8_
 }
 
 /* ===================================================================================== */
+/* Tx framing: VethIFZmq.Send / FlushTx src/emu/core/veth_zmq.go:149-200, statement by     */
+/* statement (o.vec = the open message's frames, o.txVecSize = their bytes)               */
+/* ===================================================================================== */
+typedef struct {
+    const uint8_t* frames;
+    const emurx_desc* d;
+    uint32_t first, count;  /* o.vec */
+    uint32_t size;          /* o.txVecSize */
+    uint8_t* out;
+    uint64_t cap, at, nmsg;
+    uint64_t* msg_off;
+} orc_txz;
+
+static void txz_put(orc_txz* z, const uint8_t* b, uint32_t len) {
+    for (uint32_t k = 0; k < len; k++, z->at++)
+        if (z->at < z->cap) z->out[z->at] = b[k];
+}
+static void txz_be32(orc_txz* z, uint32_t v) {
+    const uint8_t b[4] = {(uint8_t)(v >> 24), (uint8_t)(v >> 16), (uint8_t)(v >> 8), (uint8_t)v};
+    txz_put(z, b, 4);
+}
+/* FlushTx :149-178 */
+static void txz_flush(orc_txz* z) {
+    if (z->count == 0) return;
+    z->msg_off[z->nmsg++] = z->at;
+    txz_be32(z, ((uint32_t)EMURX_ZMQ_MAGIC << 16) + z->count);
+    for (uint32_t k = 0; k < z->count; k++) {
+        const emurx_desc* e = &z->d[z->first + k];
+        txz_be32(z, ((uint32_t)EMURX_ZMQ_PKT_MAGIC << 24) + ((uint32_t)(e->vport & 0xff) << 16) + e->len);
+        txz_put(z, z->frames + e->off, e->len);
+    }
+    z->first += z->count;
+    z->count = 0;
+    z->size = 0;
+}
+uint64_t orc_tx_zmq(const uint8_t* frames, const emurx_desc* d, uint32_t n, uint8_t* out, uint64_t cap,
+                    uint64_t* msg_off, uint64_t* n_msgs) {
+    orc_txz z = {frames, d, 0, 0, 0, out, cap, 0, 0, msg_off};
+    for (uint32_t i = 0; i < n; i++) {  /* Send :180-200 */
+        const uint32_t pktlen = d[i].len;
+        if (z.size + pktlen >= EMURX_ZMQ_TX_MAX_BUFFER) txz_flush(&z);
+        z.count++;  /* o.vec = append(o.vec, m) (frames i.. are contiguous in order) */
+        z.size += pktlen;
+        if (z.count == EMURX_ZMQ_TX_BURST) txz_flush(&z);
+    }
+    txz_flush(&z);
+    msg_off[z.nmsg] = z.at;
+    *n_msgs = z.nmsg;
+    return z.at;
+}
+
+/* ===================================================================================== */
 /* Transport flow tables and TransportCtx.handleRxPacket's decision                       */
 /* ===================================================================================== */
 static int orc_client_ok(const orc_t* o, uint32_t cid) { return cid < o->ncl && o->cl[cid].alive; }

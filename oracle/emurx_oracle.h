@@ -77,6 +77,10 @@ void orc_flows(const orc_t* o, const uint8_t* frames, const emurx_desc* desc, co
 /* tx checksum generation over a batch, in place (see emu_rx.h emurx_tx_checksum_dev) */
 uint8_t orc_tx_frame(uint8_t* p, uint32_t len, uint16_t l3, uint16_t l4, uint16_t osize, uint8_t ops, uint8_t nh);
 void orc_tx_checksum(uint8_t* frames, const emurx_tx_desc* d, uint32_t n, uint8_t* status);
+/* VethIFZmq.Send x n + FlushTx (veth_zmq.go:149-200) into out; returns the total bytes
+   (written only below cap); msg_off[0..n_msgs] (capacity n + 1); *n_msgs */
+uint64_t orc_tx_zmq(const uint8_t* frames, const emurx_desc* d, uint32_t n, uint8_t* out, uint64_t cap,
+                    uint64_t* msg_off, uint64_t* n_msgs);
 
 #ifdef __cplusplus
 }

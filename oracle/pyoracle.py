@@ -67,6 +67,7 @@ def lib():
             ("orc_zmq_descriptors", C.c_int, [P, C.c_size_t, P, C.c_uint32,
                                               C.POINTER(C.c_uint32), C.POINTER(C.c_int)]),
             ("orc_tx_checksum", None, [P, P, C.c_uint32, P]),
+            ("orc_tx_zmq", C.c_uint64, [P, P, C.c_uint32, P, C.c_uint64, P, P]),
             ("orc_flow_add", C.c_int, [P, C.c_uint32, P, C.c_uint32, C.c_uint32]),
             ("orc_flow_remove", C.c_int, [P, C.c_uint32, P, C.c_uint32]),
             ("orc_server_add", C.c_int, [P, C.c_uint32, C.c_uint16, C.c_uint8]),
@@ -235,6 +236,21 @@ def tx_checksum(buf: np.ndarray, desc: np.ndarray):
     st = np.zeros(max(len(d), 1), np.uint8)
     lib().orc_tx_checksum(out.ctypes.data, d.ctypes.data, len(d), st.ctypes.data)
     return out, st[: len(d)]
+
+
+def tx_zmq(buf: np.ndarray, desc: np.ndarray, cap=None):
+    """orc_tx_zmq: VethIFZmq.Send per frame + FlushTx -> (bytes, msg_off[n_msgs + 1])."""
+    d = np.ascontiguousarray(desc)
+    n = len(d)
+    need = 8 * n + int(d["len"].astype(np.int64).sum())
+    cap = need if cap is None else cap
+    out = np.zeros(max(cap, 1), np.uint8)
+    off = np.zeros(n + 1, np.uint64)
+    nm = C.c_uint64()
+    b = np.ascontiguousarray(buf, dtype=np.uint8)
+    total = lib().orc_tx_zmq(b.ctypes.data, d.ctypes.data, n, out.ctypes.data, cap, off.ctypes.data,
+                             C.byref(nm))
+    return out[:min(total, cap)], off[: nm.value + 1], int(total)
 
 
 def counters_dict(cnt: Counters):

@@ -1,0 +1,69 @@
+"""GPU parity of the tx ZMQ framing (emurx_tx_zmq_dev) against the oracle's restatement of
+VethIFZmq.Send / FlushTx (veth_zmq.go:149-200): the message bytes, the message offsets and
+{n_msgs, total} bit-exact, for every length profile, the 32 KiB / 64-frame boundaries,
+1M-frame batches (three levels of the chain scan) and a capacity smaller than the output."""
+import numpy as np
+import pytest
+
+import txzmq_util as U
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rx(gpu_ok, oracle_built):
+    from emurx.rx import RxPath
+    return RxPath(0, max_ns=16, max_clients=16, max_frames=1 << 10)
+
+
+def run_dev(rx, buf, d, cap=None):
+    import torch
+    from gpu_util import to_dev
+    n = len(d)
+    need = 8 * n + int(d["len"].astype(np.int64).sum())
+    cap = need if cap is None else cap
+    tb, td = to_dev(buf), to_dev(d) if n else torch.zeros(8, dtype=torch.uint8, device="cuda")
+    out = torch.full((max(cap, 1),), 0xEE, dtype=torch.uint8, device="cuda")
+    off = torch.full((n + 1,), -1, dtype=torch.int64, device="cuda")
+    info = torch.full((2,), -1, dtype=torch.int64, device="cuda")
+    rx.tx_zmq_dev(tb, td, n, out, cap, off, info)
+    torch.cuda.synchronize()
+    nm, total = (int(x) for x in info.cpu().numpy())
+    return out.cpu().numpy()[: min(total, cap)], off.cpu().numpy()[: nm + 1].astype(np.uint64), total, \
+        out.cpu().numpy()
+
+
+def check(rx, buf, d, cap=None):
+    import pyoracle
+    want, woff, wtotal = pyoracle.tx_zmq(buf, d, cap)
+    got, off, total, raw = run_dev(rx, buf, d, cap)
+    assert total == wtotal
+    assert np.array_equal(off, woff)
+    assert got.tobytes() == want.tobytes(), np.nonzero(got != want)[0][:10]
+    if cap is not None:
+        assert (raw[min(total, cap):] == 0xEE).all()  # nothing past the data / the capacity
+    return len(woff) - 1
+
+
+@pytest.mark.parametrize("n,kind", [(0, 0), (1, 0), (63, 3), (64, 3), (65, 3), (129, 0), (1000, 0), (3000, 1),
+                                    (5000, 2), (4096 * 64 + 7, 0)])
+def test_tx_zmq_profiles(rx, n, kind):
+    buf, d = U.batch(n, kind, seed=11)
+    check(rx, buf, d)
+
+
+def test_tx_zmq_thresholds(rx):
+    buf, d = U.threshold_batch()
+    assert check(rx, buf, d) == 12
+
+
+def test_tx_zmq_million(rx):
+    """1M x 64 B: 16,384 tiles, chain levels of 256 and 4 units; 16,384 full bursts."""
+    buf, d = U.batch(1 << 20, 3, seed=2, gap=0)
+    assert check(rx, buf, d) == (1 << 20) // 64
+
+
+def test_tx_zmq_capacity(rx):
+    buf, d = U.batch(2000, 2, seed=4)
+    need = 8 * len(d) + int(d["len"].astype(np.int64).sum())
+    check(rx, buf, d, cap=need // 3)

@@ -13,7 +13,7 @@ if [ "${1:-run}" = build ]; then
     $H -c trex-emu_amd/csrc/emurx_kernels.hip -o trex-emu_amd/build/abl/k$v.o &&
     $H -c trex-emu_amd/csrc/emurx_route.hip -o trex-emu_amd/build/abl/r$v.o &&
     $H -shared -o trex-emu_amd/lib/abl/libemurx_$v.so trex-emu_amd/build/abl/k$v.o trex-emu_amd/build/abl/r$v.o \
-       trex-emu_amd/build/emurx_ingest.o trex-emu_amd/build/emurx_tx.o trex-emu_amd/build/emurx_api.o || exit 1
+       trex-emu_amd/build/emurx_ingest.o trex-emu_amd/build/emurx_tx.o trex-emu_amd/build/emurx_txzmq.o trex-emu_amd/build/emurx_api.o || exit 1
   done
   exit 0
 fi

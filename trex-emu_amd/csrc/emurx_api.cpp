@@ -177,6 +177,9 @@ struct emurx_ctx {
     // batched host ingest: EMURX_INGEST_SLOTS public slots + one private to emurx_rx_stream
     IngestSlot ing[EMURX_INGEST_SLOTS + 1];
 
+    // tx ZMQ framing scratch (emurx_tx_zmq_dev): per-level chain transfer tables
+    DevBuf<uint8_t> d_txz;
+
     // Namespace-partition packing scratch (emurx_route_dev)
     DevBuf<uint32_t> d_route_cnt, d_route_grp, d_route_goff;  // grp: zero between batches
 
@@ -644,6 +647,7 @@ void emurx_close(emurx_t* h) {
     h->d_ip6.release(); h->d_client.release();
     h->d_ft4.release(); h->d_ft6.release(); h->d_srv.release();
     h->d_route_cnt.release(); h->d_route_grp.release(); h->d_route_goff.release();
+    h->d_txz.release();
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
     h->ev.clear();
@@ -1068,6 +1072,24 @@ int emurx_tx_checksum_dev(emurx_t* h, uint8_t* d_frames, const emurx_tx_desc* d_
     if (rc) return rc;
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
     return emurx_launch_tx_csum(d_frames, d_desc, n, d_status, st) ? EMURX_EDEVICE : EMURX_OK;
+}
+
+int emurx_tx_zmq_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_desc, uint32_t n,
+                     uint8_t* d_out, uint64_t out_cap, uint64_t* d_msg_off, uint64_t* d_info, void* stream) {
+    if (!h || !d_msg_off || !d_info || (n && (!d_frames || !d_desc || (!d_out && out_cap))))
+        return EMURX_EINVAL;
+    if (n > (1u << 30)) return EMURX_EINVAL;
+    int rc = bind(h);
+    if (rc) return rc;
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    const size_t need = emurx_txz_scratch_bytes(n);
+    if (need > h->d_txz.n) {  // grows on demand; a launch in flight may still read the old one
+        (void)hipStreamSynchronize(st);
+        if (h->d_txz.alloc(need)) return EMURX_ENOMEM;
+    }
+    return emurx_launch_tx_zmq(d_frames, d_desc, n, d_out, out_cap, d_msg_off, d_info, h->d_txz.p, st)
+               ? EMURX_EDEVICE
+               : EMURX_OK;
 }
 
 uint32_t emurx_ns_owner(const uint8_t key[12], uint32_t n_parts) {

@@ -35,3 +35,8 @@ int emurx_launch_queue_pack(const uint32_t* qlist, uint32_t qcap, const uint32_t
 // Tx checksum generation (emurx_tx.hip): one launch, in place; status may be null.
 int emurx_launch_tx_csum(uint8_t* frames, const emurx_tx_desc* desc, uint32_t n, uint8_t* status,
                          hipStream_t st);
+
+// Tx ZMQ framing (emurx_txzmq.hip): see emurx_tx_zmq_dev.  scratch: emurx_txz_scratch_bytes(n).
+size_t emurx_txz_scratch_bytes(uint32_t n);
+int emurx_launch_tx_zmq(const uint8_t* frames, const emurx_desc* desc, uint32_t n, uint8_t* out, uint64_t cap,
+                        uint64_t* msg_off, uint64_t* info, void* scratch, hipStream_t st);

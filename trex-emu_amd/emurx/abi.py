@@ -81,6 +81,7 @@ MSG_DTYPE = np.dtype([("off", "<u4"), ("len", "<u4")])
 TX_IPV4_HDR, TX_V6_NH, TX_L4_SHIFT = 0x01, 0x02, 4
 TX_L4_NONE, TX_L4_TCP4, TX_L4_UDP4, TX_L4_TCP6, TX_L4_UDP6, TX_L4_ICMP6, TX_L4_ICMP4 = range(7)
 TX_OK, TX_RANGE = 0, 1
+ZMQ_TX_BURST, ZMQ_TX_MAX_BUFFER, ZMQ_PKT_MAGIC = 64, 32768, 0xAA  # veth_zmq.go:36-37, :167
 FLOW_NONE, FLOW_NO_CTX, FLOW_NO_SYN, FLOW_NO_SERVER, FLOW_NEW = (0xFFFFFFFF, 0xFFFFFFF0, 0xFFFFFFF1,
                                                                 0xFFFFFFF2, 0xFFFFFFF3)
 FLOW_ID_MAX = 0xFFFFFFEF
@@ -165,6 +166,7 @@ SIGNATURES = [
     ("emurx_ingest_submit", C.c_int, [_P, C.c_uint32, _P, C.c_uint32]),
     ("emurx_ingest_wait", C.c_int, [_P, C.c_uint32, C.POINTER(IngestResult)]),
     ("emurx_tx_checksum_dev", C.c_int, [_P, _P, _P, C.c_uint32, _P, _P]),
+    ("emurx_tx_zmq_dev", C.c_int, [_P, _P, _P, C.c_uint32, _P, C.c_uint64, _P, _P, _P]),
     ("emurx_flow_add", C.c_int, [_P, C.c_uint32, _U8P, C.c_uint32, C.c_uint32]),
     ("emurx_flow_remove", C.c_int, [_P, C.c_uint32, _U8P, C.c_uint32]),
     ("emurx_server_add", C.c_int, [_P, C.c_uint32, C.c_uint16, C.c_uint8]),

@@ -211,6 +211,13 @@ class RxPath:
         return abi.check(self.lib.emurx_tx_checksum_dev(self.h, _addr(frames), _addr(desc), n, _addr(status),
                                                         _stream(stream)), "tx_checksum_dev")
 
+    def tx_zmq_dev(self, frames, desc, n: int, out, cap: int, msg_off, info, stream=None):
+        """Pack the n frames into ZMQ messages as VethIFZmq.Send x n + FlushTx would
+        (include/emu_rx.h emurx_tx_zmq_dev): messages back to back in `out`, msg_off u64
+        [n + 1], info u64 {n_msgs, total bytes}."""
+        return abi.check(self.lib.emurx_tx_zmq_dev(self.h, _addr(frames), _addr(desc), n, _addr(out), cap,
+                                                   _addr(msg_off), _addr(info), _stream(stream)), "tx_zmq_dev")
+
     # ---- Namespace-partitioned exchange ---------------------------------------------------
     def route_dev(self, rec, n: int, n_parts: int, my_rank: int, cap: int, send, send_count, stream=None):
         """Pack the batch's records with a Namespace into their owners' send regions
