@@ -56,6 +56,8 @@ def parse_args():
                     help="record HIP events around every N-th launch of the timed region")
     ap.add_argument("--no-check", action="store_true",
                     help="skip the output sanity check (stage-ablation builds, tools/ablate.sh)")
+    ap.add_argument("--tx-path", action="store_true",
+                    help="also time the device tx ZMQ framing (emurx_tx_zmq_dev) over the same frames")
     ap.add_argument("--host-path", action="store_true",
                     help="also time the host-inclusive path (pinned H2D + kernels + D2H)")
     return ap.parse_args()
@@ -132,6 +134,8 @@ def main():
             out["namespace_exchange"] = {"error": repr(e)[:300]}
     if a.host_path:
         out["host_inclusive"] = host_path_rate(rx, w)
+    if a.tx_path:
+        out["tx_zmq"] = tx_zmq_rate(rx, w, torch)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(w, a.cpu_seconds)
     if rank == 0:
@@ -359,6 +363,41 @@ def host_path_rate(rx, w, per_msg=64, budget_s=3.0):
         rx.on_rx_stream(m, cap=per_msg)
     out["mpkts_one_msg_per_call"] = round(len(one) * per_msg / (time.perf_counter() - t0) / 1e6, 4)
     return out
+
+
+def tx_zmq_rate(rx, w, torch, reps=50):
+    """Device tx framing (VethIFZmq.Send x n + FlushTx as emurx_tx_zmq_dev) of the batch's
+    frames, device-resident in and out; CUDA events on torch's stream around `reps` calls.
+    Bytes moved per call: the frames read + the messages written (+ descriptors)."""
+    import numpy as np
+
+    def to_dev(a):
+        b = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
+        t = torch.zeros(b.size + 64, dtype=torch.uint8, device="cuda")
+        t[: b.size] = torch.from_numpy(b.copy()).to("cuda")
+        return t
+    n = len(w["desc"])
+    fb = int(w["desc"]["len"].astype(np.int64).sum())
+    need = 8 * n + fb
+    tb, td = to_dev(w["buf"]), to_dev(w["desc"])
+    out = torch.empty(need, dtype=torch.uint8, device="cuda")
+    off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    info = torch.empty(2, dtype=torch.int64, device="cuda")
+    st = torch.cuda.current_stream()
+    for _ in range(3):
+        rx.tx_zmq_dev(tb, td, n, out, need, off, info, stream=st.cuda_stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        rx.tx_zmq_dev(tb, td, n, out, need, off, info, stream=st.cuda_stream)
+    e1.record(st)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    nm, total = (int(x) for x in info.cpu().numpy())
+    moved = fb + total + 8 * n
+    return {"frames": n, "msgs": nm, "bytes_out": total, "ms_per_call": round(ms, 4),
+            "mpkts": round(n / ms / 1e3, 1), "gbs_moved": round(moved / ms / 1e6, 1),
+            "note": "launch sequence: leaf + compose/descend per level + finish + write"}
 
 
 if __name__ == "__main__":

@@ -434,8 +434,9 @@ int emurx_tx_checksum_dev(emurx_t* h, uint8_t* d_frames, const emurx_tx_desc* d_
    The messages land back to back in d_out.  d_msg_off[m] (u64) is message m's start and
    d_msg_off[n_msgs] the total; capacity n + 1.  d_info = {n_msgs, total bytes}.  Nothing is
    written at or past out_cap; out_cap >= 8 * n + sum(len) always suffices, and d_info
-   tells the size needed when it did not.  A stream-ordered sequence of launches, no host
-   synchronisation.  Replaces VethIFZmq.FlushTx's per-frame append loop. */
+   tells the size needed when it did not.  d_out 16-byte aligned; the frames are read as
+   the aligned 16-byte blocks that hold them.  A stream-ordered sequence of launches, no
+   host synchronisation.  Replaces VethIFZmq.FlushTx's per-frame append loop. */
 #define EMURX_ZMQ_TX_BURST 64u            /* ZMQ_TX_PKT_BURST_SIZE  veth_zmq.go:36 */
 #define EMURX_ZMQ_TX_MAX_BUFFER 32768u    /* ZMQ_TX_MAX_BUFFER_SIZE veth_zmq.go:37 */
 #define EMURX_ZMQ_PKT_MAGIC 0xAAu         /* per-frame header tag   veth_zmq.go:167 */

@@ -1078,7 +1078,7 @@ int emurx_tx_zmq_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_de
                      uint8_t* d_out, uint64_t out_cap, uint64_t* d_msg_off, uint64_t* d_info, void* stream) {
     if (!h || !d_msg_off || !d_info || (n && (!d_frames || !d_desc || (!d_out && out_cap))))
         return EMURX_EINVAL;
-    if (n > (1u << 30)) return EMURX_EINVAL;
+    if (n > (1u << 30) || ((uintptr_t)d_out & 15) || ((uintptr_t)d_desc & 7)) return EMURX_EINVAL;
     int rc = bind(h);
     if (rc) return rc;
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;

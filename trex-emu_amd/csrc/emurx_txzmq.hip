@@ -213,15 +213,47 @@ __global__ __launch_bounds__(256) void k_txz_write(const uint8_t* __restrict__ f
         }
         put_be32(out, fo, cap, ((uint32_t)EMURX_ZMQ_PKT_MAGIC << 24) + ((uint32_t)dl.vport << 16) + dl.len);
     }
-    // the bytes, one frame at a time by the whole wave (byte lanes, coalesced)
+    // the bytes, one frame at a time by the whole wave (coalesced).  Short frames: one byte
+    // per lane.  Longer ones: aligned 16-byte output stores, each funnel-shifted out of two
+    // aligned 16-byte source vectors, with the head and tail bytes (up to the 16-byte
+    // boundaries) stored singly by lanes 0-15 and 16-31.
     for (uint32_t f = 0; f < lim; ++f) {
         const uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)len, (int)f);
-        const uint32_t src = (uint32_t)__builtin_amdgcn_readlane((int)dl.off, (int)f);
-        const unsigned long long dst =
+        const uint8_t* s = frames + (uint32_t)__builtin_amdgcn_readlane((int)dl.off, (int)f);
+        const unsigned long long D =
             ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(fo >> 32), (int)f) << 32 |
              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)fo, (int)f)) + 4;
-        for (uint32_t k = lane; k < fl; k += kWave)
-            if (dst + k < cap) out[dst + k] = frames[(size_t)src + k];
+        if (fl < 128) {
+            for (uint32_t k = lane; k < fl; k += kWave)
+                if (D + k < cap) out[D + k] = s[k];
+            continue;
+        }
+        const unsigned long long Ee = D + fl, a0 = (D + 15) & ~15ull, a1 = Ee & ~15ull;  // a0 < a1
+        const unsigned long long hb = lane < 16 ? D + lane : a1 + (lane - 16);
+        if (lane < 32 && hb < (lane < 16 ? a0 : Ee) && hb < cap) out[hb] = s[hb - D];
+        const uintptr_t sa = (uintptr_t)(s + (a0 - D));
+        const uint4* sv = reinterpret_cast<const uint4*>(sa & ~(uintptr_t)15);
+        const uint32_t r = (uint32_t)(sa & 15), q = r >> 2, b = r & 3;
+        const uint32_t nch = (uint32_t)((a1 - a0) >> 4);
+        for (uint32_t c = lane; c < nch; c += kWave) {
+            const uint4 cur = sv[c];
+            const uint4 nxt = r ? sv[c + 1] : make_uint4(0, 0, 0, 0);  // r > 0: this chunk's tail
+            const uint32_t w[8] = {cur.x, cur.y, cur.z, cur.w, nxt.x, nxt.y, nxt.z, nxt.w};
+            uint32_t o[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t lo = q == 0 ? w[i] : q == 1 ? w[i + 1] : q == 2 ? w[i + 2] : w[i + 3];
+                const uint32_t hi = q == 0 ? w[i + 1] : q == 1 ? w[i + 2] : q == 2 ? w[i + 3] : w[i + 4];
+                o[i] = __builtin_amdgcn_alignbyte(hi, lo, b);
+            }
+            const unsigned long long x = a0 + 16ull * c;
+            if (x + 16 <= cap) {
+                *reinterpret_cast<uint4*>(out + x) = make_uint4(o[0], o[1], o[2], o[3]);
+            } else {
+                for (uint32_t j = 0; j < 16; ++j)
+                    if (x + j < cap) out[x + j] = (uint8_t)(o[j >> 2] >> (8 * (j & 3)));
+            }
+        }
     }
 }
 
