@@ -316,24 +316,32 @@ int rebuild_and_upload(emurx_t* h, hipStream_t st) {
         const uint8_t* k = h->ns[ns].key;
         return emurx_tk_hash(le32(k), le32(k + 4), le32(k + 8));
     };
-    auto fill4 = [&](std::vector<uint32_t>& t, uint32_t buckets, const Map& m, int kind) {
-        empty_table(t, buckets, 4);
-        for (auto& kv : m) {
-            uint32_t e[4] = {kv.first.w[0], kv.first.w[1], kv.first.w[2], kv.second};
-            const uint32_t tk = tk_of(e[0]);
-            uint32_t hh = kind == 0 ? emurx_mac_hash(tk, e[1], e[2]) : emurx_ip4_hash(tk, e[1]);
-            if (kind == 1) e[2] = 0;
-            // MAC slots carry the client's plugin mask in the free upper half of mac[4..5]
-            if (kind == 0) e[2] |= (h->cl[kv.second].plugins & 0xffffu) << 16;
-            bucket_put(t, buckets - 1, 4, hh, e);
-        }
+    // the client's MAC and plugin mask ride in the MAC slot's free upper half and in the IPv4 /
+    // IPv6 slots' spare words: the rules that check them (PluginCtx.Get, IsUnicastToMe) need
+    // no second read of the client record
+    auto mac_words = [&](uint32_t cid, uint32_t& lo, uint32_t& hip) {
+        const ClientInfo& c = h->cl[cid];
+        lo = le32(c.mac);
+        hip = (uint32_t)(c.mac[4] | (c.mac[5] << 8)) | ((c.plugins & 0xffffu) << 16);
     };
-    fill4(h->h_mac, h->mac_buckets, h->mac_map, 0);
-    fill4(h->h_ip4, h->ip4_buckets, h->ip4_map, 1);
+    empty_table(h->h_mac, h->mac_buckets, 4);
+    for (auto& kv : h->mac_map) {
+        uint32_t e[4] = {kv.first.w[0], kv.first.w[1], kv.first.w[2], kv.second};
+        const uint32_t hh = emurx_mac_hash(tk_of(e[0]), e[1], e[2]);
+        e[2] |= (h->cl[kv.second].plugins & 0xffffu) << 16;
+        bucket_put(h->h_mac, h->mac_buckets - 1, 4, hh, e);
+    }
+    empty_table(h->h_ip4, h->ip4_buckets, 8);
+    for (auto& kv : h->ip4_map) {
+        uint32_t e[8] = {kv.first.w[0], kv.first.w[1], 0, 0, 0, 0, 0, kv.second};
+        mac_words(kv.second, e[2], e[3]);
+        bucket_put(h->h_ip4, h->ip4_buckets - 1, 8, emurx_ip4_hash(tk_of(e[0]), e[1]), e);
+    }
     empty_table(h->h_ip6, h->ip6_buckets, 8);
     for (auto& kv : h->ip6_map) {
         const uint32_t* w = kv.first.w;
         uint32_t e[8] = {w[0], w[1], w[2], w[3], w[4], 0, 0, kv.second};
+        mac_words(kv.second, e[5], e[6]);
         bucket_put(h->h_ip6, h->ip6_buckets - 1, 8, emurx_ip6_hash(tk_of(w[0]), w[1], w[2], w[3], w[4]), e);
     }
     h->h_client.assign((size_t)h->cfg.max_clients * 8, 0);
@@ -610,7 +618,7 @@ int emurx_open(const emurx_cfg* cfg, emurx_t** out) {
     // load factor <= 1/2 in slots: 4 slots (IPv6: 2) per 64-byte bucket
     h->ns_buckets = pow2_at_least(2ull * cfg->max_ns) / 4;
     h->mac_buckets = pow2_at_least(2ull * cfg->max_clients) / 4;
-    h->ip4_buckets = pow2_at_least(2ull * cfg->max_clients) / 4;
+    h->ip4_buckets = pow2_at_least(4ull * cfg->max_clients) / 2;
     h->ip6_buckets = pow2_at_least(4ull * cfg->max_clients) / 2;
     h->ns.resize(cfg->max_ns);
     h->cl.resize(cfg->max_clients);

@@ -738,38 +738,44 @@ __device__ __forceinline__ uint2 resolve_mac(const emurx_dev_tables& T, uint32_t
         e = ld_bucket(T.mac_tab, b);
     }
 }
-// ip4 slot {ns_id, ip, 0, client_id}
-__device__ __forceinline__ uint32_t resolve_ip4(const emurx_dev_tables& T, uint32_t b, Bucket e, uint32_t ns, uint32_t ip) {
+// IP slots carry the client's MAC and plugin mask: {cid, mac_lo, mac_hi | plugins << 16}
+struct IpHit {
+    uint32_t cid, mlo, mhip;
+};
+// ip4 slot {ns_id, ip, mac_lo, mac_hi | plugins << 16} {0, 0, 0, client_id}, 2 per bucket
+__device__ __forceinline__ IpHit resolve_ip4(const emurx_dev_tables& T, uint32_t b, Bucket e, uint32_t ns, uint32_t ip) {
     {
-        const uint4 x = e.s[0];
-        if (x.w != EMURX_EMPTY && x.x == ns && x.y == ip) return x.w;
+        const uint4 x = e.s[0], y = e.s[1];
+        if (y.w != EMURX_EMPTY && x.x == ns && x.y == ip) return IpHit{y.w, x.z, x.w};
     }
     for (uint32_t n = 0;;) {
         bool hole = false;
-        uint32_t hit = EMURX_ID_NONE;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint4 x = e.s[k];
-            hole |= x.w == EMURX_EMPTY;
-            if (x.w != EMURX_EMPTY && x.x == ns && x.y == ip) hit = x.w;
-        }
-        if (hit != EMURX_ID_NONE || hole || ++n > T.ip4_mask) return hit;
-        b = (b + 1) & T.ip4_mask;
-        e = ld_bucket(T.ip4_tab, b);
-    }
-}
-// ip6 slot {ns_id, ip[0..3], ip[4..7], ip[8..11]} {ip[12..15], 0, 0, client_id}, 2 per bucket
-__device__ __forceinline__ uint32_t resolve_ip6(const emurx_dev_tables& T, uint32_t b, Bucket e, uint32_t ns, const uint32_t w[4]) {
-    for (uint32_t n = 0;;) {
-        bool hole = false;
-        uint32_t hit = EMURX_ID_NONE;
+        IpHit hit{EMURX_ID_NONE, 0, 0};
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             const uint4 x = e.s[2 * k], y = e.s[2 * k + 1];
             hole |= y.w == EMURX_EMPTY;
-            if (y.w != EMURX_EMPTY && x.x == ns && x.y == w[0] && x.z == w[1] && x.w == w[2] && y.x == w[3]) hit = y.w;
+            if (y.w != EMURX_EMPTY && x.x == ns && x.y == ip) hit = IpHit{y.w, x.z, x.w};
         }
-        if (hit != EMURX_ID_NONE || hole || ++n > T.ip6_mask) return hit;
+        if (hit.cid != EMURX_ID_NONE || hole || ++n > T.ip4_mask) return hit;
+        b = (b + 1) & T.ip4_mask;
+        e = ld_bucket(T.ip4_tab, b);
+    }
+}
+// ip6 slot {ns_id, ip[0..3], ip[4..7], ip[8..11]} {ip[12..15], mac_lo, mac_hi | plugins << 16,
+// client_id}, 2 per bucket
+__device__ __forceinline__ IpHit resolve_ip6(const emurx_dev_tables& T, uint32_t b, Bucket e, uint32_t ns, const uint32_t w[4]) {
+    for (uint32_t n = 0;;) {
+        bool hole = false;
+        IpHit hit{EMURX_ID_NONE, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const uint4 x = e.s[2 * k], y = e.s[2 * k + 1];
+            hole |= y.w == EMURX_EMPTY;
+            if (y.w != EMURX_EMPTY && x.x == ns && x.y == w[0] && x.z == w[1] && x.w == w[2] && y.x == w[3])
+                hit = IpHit{y.w, y.y, y.z};
+        }
+        if (hit.cid != EMURX_ID_NONE || hole || ++n > T.ip6_mask) return hit;
         b = (b + 1) & T.ip6_mask;
         e = ld_bucket(T.ip6_tab, b);
     }
@@ -789,11 +795,8 @@ __device__ __forceinline__ void client_result(Rec& r, uint32_t cid, uint32_t cpl
 __device__ __forceinline__ uint32_t client_plugins(const emurx_dev_tables& T, uint32_t cid) {
     return cid == EMURX_ID_NONE ? 0u : gld4(T.client + 8 * cid + 2);
 }
-// CClient.IsUnicastToMe client_ctx.go:389-398 (frames here are always > 6 bytes)
-__device__ __forceinline__ bool unicast_to_me(const emurx_dev_tables& T, uint32_t cid,
-                                              uint32_t dlo, uint32_t dhi) {
-    return gld4(T.client + 8 * cid + 0) == dlo && gld4(T.client + 8 * cid + 1) == dhi;
-}
+// CClient.IsUnicastToMe client_ctx.go:389-398 (frames here are always > 6 bytes) compares the
+// frame's destination with the client's MAC, which the IP slots carry (IpHit)
 
 // Go 1.18 net.IP.IsLinkLocalUnicast / IsGlobalUnicast for a 16-byte address (words LE)
 __device__ __forceinline__ bool ip6_local_or_global(const uint32_t w[4]) {
@@ -1002,20 +1005,22 @@ __device__ __forceinline__ void classify(const S& s, uint32_t len, const emurx_d
         return;
     }
     case kIp4: {
-        uint32_t cid = resolve_ip4(T, cbk, ce, ns, kw[0]);
+        const IpHit h = resolve_ip4(T, cbk, ce, ns, kw[0]);
         if (cb == EMURX_CB_ARP) {
-            client_result(r, cid, client_plugins(T, cid), plug, true);
-        } else {  // icmp
-            if (cid != EMURX_ID_NONE && !unicast_to_me(T, cid, dlo, dhi)) cid = EMURX_ID_NONE;
-            client_result(r, cid, 0, plug, false);
+            client_result(r, h.cid, h.mhip >> 16, plug, true);
+        } else {  // icmp: IsUnicastToMe against the MAC in the slot
+            const bool me = h.mlo == dlo && (h.mhip & 0xffffu) == dhi;
+            client_result(r, me ? h.cid : EMURX_ID_NONE, 0, plug, false);
         }
         return;
     }
     case kEui:
     case kIp6: {  // icmpv6 echo request
-        uint32_t cid;
+        uint32_t cid, clo, chi;  // the client and its MAC (IsUnicastToMe)
         if (key == kEui) {
             cid = resolve_mac(T, cbk, ce, ns, mlo, mhi).x;
+            clo = mlo;  // the MAC table's key is the client's MAC
+            chi = mhi;
             // CClient.IsValidPrefix client_ctx.go:279-295
             if (cid != EMURX_ID_NONE && !(kw[0] == 0x000080feu && kw[1] == 0)) {
                 const uint32_t* c = T.client + 8 * cid;
@@ -1023,9 +1028,12 @@ __device__ __forceinline__ void classify(const S& s, uint32_t len, const emurx_d
                 if (!((ra & 1u) && ((ra >> 8) & 0xff) == 64 && c[4] == kw[0] && c[5] == kw[1])) cid = EMURX_ID_NONE;
             }
         } else {
-            cid = resolve_ip6(T, cbk, ce, ns, kw);
+            const IpHit h = resolve_ip6(T, cbk, ce, ns, kw);
+            cid = h.cid;
+            clo = h.mlo;
+            chi = h.mhip & 0xffffu;
         }
-        if (cid != EMURX_ID_NONE && !unicast_to_me(T, cid, dlo, dhi)) cid = EMURX_ID_NONE;
+        if (cid != EMURX_ID_NONE && !(clo == dlo && chi == dhi)) cid = EMURX_ID_NONE;
         if (cid != EMURX_ID_NONE && s.u8(r.l3 + 8) == 0xff) cid = EMURX_ID_NONE;
         client_result(r, cid, 0, plug, false);
         return;

@@ -6,8 +6,8 @@
 //   MapClientMAC  map[MACKey]*CClient      src/emu/core/ns_ctx.go:110-112  (per Namespace)
 //   MapClientIPv4 map[Ipv4Key]*CClient
 //   MapClientIPv6 map[Ipv6Key]*CClient     (static Ipv6 and Dhcpv6 addresses, ns_ctx.go:377-383)
-// as flat open-addressing arrays of 64-byte BUCKETS (one cache line; 4 slots of 16 B, IPv6:
-// 2 slots of 32 B), load factor <= 1/2, power-of-two bucket counts, linear probing over
+// as flat open-addressing arrays of 64-byte BUCKETS (one cache line; 4 slots of 16 B, IPv4 and
+// IPv6: 2 slots of 32 B), load factor <= 1/2, power-of-two bucket counts, linear probing over
 // buckets.  A lookup reads its home bucket with four 16-byte loads of one line and ends at
 // the first bucket that holds an empty slot.  Only exact-match semantics matter for parity
 // with the Go maps; the hash function is ours.
@@ -49,8 +49,10 @@ EMURX_HD uint32_t emurx_hash(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uin
 // Slot layouts (uint32 words; the last word of a slot is the value, EMURX_EMPTY = free):
 //  ns   [4]: vport | ns_plugins << 16, vlan0, vlan1, ns_id   (key = CTunnelKey as 3 LE words)
 //  mac  [4]: ns_id, mac[0..3] LE, mac[4..5] LE | client_plugins << 16, client_id
-//  ip4  [4]: ns_id, ipv4 bytes LE, 0, client_id
-//  ip6  [8]: ns_id, ip[0..3], ip[4..7], ip[8..11], ip[12..15], 0, 0, client_id
+//  ip4  [8]: ns_id, ipv4 bytes LE, mac[0..3], mac[4..5] | client_plugins << 16, 0, 0, 0, client_id
+//  ip6  [8]: ns_id, ip[0..3], ip[4..7], ip[8..11], ip[12..15], mac[0..3], mac[4..5] | client_plugins << 16,
+//            client_id
+//  (the client's MAC and plugin mask in the IP slots answer IsUnicastToMe / PluginCtx.Get)
 //  ns_info   [4]: plugin_mask, first_client, 0, 0
 //  client    [8]: mac_lo, mac_hi, plugin_mask, ra (bit0 has_ra, bits 8..15 prefix_len),
 //                 ra_prefix[0..3], ra_prefix[4..7], 0, 0
@@ -90,7 +92,7 @@ struct emurx_dev_tables {
     const uint32_t* ns_tab;   // [ns_mask + 1] buckets of 4 slots
     const uint32_t* ns_info;  // 4 words per ns id
     const uint32_t* mac_tab;  // [mac_mask + 1] buckets of 4 slots
-    const uint32_t* ip4_tab;  // [ip4_mask + 1] buckets of 4 slots
+    const uint32_t* ip4_tab;  // [ip4_mask + 1] buckets of 2 slots
     const uint32_t* ip6_tab;  // [ip6_mask + 1] buckets of 2 slots
     const uint32_t* client;   // 8 words per client id
     uint32_t ns_mask, mac_mask, ip4_mask, ip6_mask;  // bucket count - 1
