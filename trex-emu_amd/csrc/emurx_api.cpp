@@ -618,7 +618,7 @@ int emurx_open(const emurx_cfg* cfg, emurx_t** out) {
     // load factor <= 1/2 in slots: 4 slots (IPv6: 2) per 64-byte bucket
     h->ns_buckets = pow2_at_least(2ull * cfg->max_ns) / 4;
     h->mac_buckets = pow2_at_least(2ull * cfg->max_clients) / 4;
-    h->ip4_buckets = pow2_at_least(4ull * cfg->max_clients) / 2;
+    h->ip4_buckets = pow2_at_least(2ull * cfg->max_clients) / 2;  // one address per client, 2 slots per bucket
     h->ip6_buckets = pow2_at_least(4ull * cfg->max_clients) / 2;
     h->ns.resize(cfg->max_ns);
     h->cl.resize(cfg->max_clients);
