@@ -176,6 +176,7 @@ def measure(a, cfg, n, exchange, steps, warmup, rank, world, local, dist, torch)
         send = torch.empty(world * cap * X.REC_BYTES, dtype=torch.uint8, device=dev)
         send_count = torch.zeros(world, dtype=torch.int32, device=dev)
         xch = dict(cap=cap, recv=None, recv_count=None, ev=[], timing=False, k=0)
+        rx.set_route_parts(world)  # the route's counting pass rides in k_rx (emurx_set_route_parts)
 
     def step():
         rx.classify_dev(buf, desc, n, rec, qlist, qcap, tile_cnt, hist, stream=stream)

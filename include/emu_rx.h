@@ -488,6 +488,12 @@ uint32_t emurx_ns_owner(const uint8_t key[12], uint32_t n_parts);
    d_send_count: [n_parts] (device).  Three kernel launches on `stream`, no host sync. */
 int emurx_route_dev(emurx_t* h, const emurx_rec* d_rec, uint32_t n, uint32_t n_parts, uint32_t my_rank,
                     uint32_t cap, emurx_route_rec* d_send, uint32_t* d_send_count, void* stream);
+/* With n_parts > 0, every later classify launch of this handle (emurx_classify_dev) also
+   counts its records per Namespace owner (the first of emurx_route_dev's three passes), and
+   emurx_route_dev of that same batch (the same d_rec, n and n_parts, stream-ordered after
+   it) skips that pass.  Counts no route consumed are cleared by the next classify launch.
+   0 turns it off.  Results are identical either way. */
+int emurx_set_route_parts(emurx_t* h, uint32_t n_parts);
 
 #ifdef __cplusplus
 }

@@ -345,6 +345,66 @@ def test_route_dev(rxmod, n_parts, my_rank):
     assert sum(got_cnt) == int((orec["ns_id"] != abi.ID_NONE).sum())
 
 
+def _classify_to(rx, w, rec, n):
+    import torch
+    from emurx import abi as A
+    buf = torch.from_numpy(w["buf"]).cuda()
+    desc = torch.from_numpy(w["desc"].view(np.uint8).copy()).cuda()
+    qcap = A.queue_cap(n)
+    qlist = torch.empty(A.NUM_QUEUES * qcap, dtype=torch.int32, device="cuda")
+    tile_cnt = torch.empty(A.ntiles(n) * 16, dtype=torch.int32, device="cuda")
+    hist = torch.zeros(A.HIST_SHARDS * 2 * A.HIST_BINS, dtype=torch.int64, device="cuda")
+    rx.classify_dev(buf, desc, n, rec, qlist, qcap, tile_cnt, hist)
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("n_parts,my_rank", [(1, 0), (2, 1), (8, 3)])
+def test_route_fused_counts(rxmod, n_parts, my_rank):
+    """emurx_set_route_parts: the owners counted inside k_rx give the same send regions; a
+    batch classified but never routed, a route of other records and a route with another
+    n_parts all fall back to the counting pass correctly."""
+    import torch
+    import route_ref
+    from emurx import exchange as X
+    n = 30000 + 5
+    wa = synth.config_c(n, rank=my_rank)
+    wb = synth.config_c(n, rank=my_rank + 10)
+    rx, o = new_pair(rxmod)
+    synth.load_tables(wa, rx)
+    synth.load_tables(wa, o)
+    rx.set_route_parts(n_parts)
+    orec_b, _, _, _ = o.rx_batch(wb["buf"], wb["desc"])
+    orec_a, _, _, _ = o.rx_batch(wa["buf"], wa["desc"])
+    def route(rec, parts):
+        cap = X.capacity(n, parts)
+        send = torch.full((parts * cap * X.REC_BYTES,), 0xEE, dtype=torch.uint8, device="cuda")
+        cnt = torch.full((parts,), -1, dtype=torch.int32, device="cuda")
+        rx.route_dev(rec, n, parts, my_rank % parts, cap, send, cnt)
+        torch.cuda.synchronize()
+        c = cnt.cpu().numpy()
+        return c, send.cpu().numpy().view(abi.ROUTE_REC_DTYPE).reshape(parts, cap)
+
+    def check(got, orec, parts):
+        c, sreg = got
+        want = route_ref.route(orec, parts, my_rank % parts)
+        assert list(c) == [len(x) for x in want]
+        for d in range(parts):
+            assert sreg[d, : c[d]].tobytes() == want[d].tobytes(), d
+
+    rec = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    _classify_to(rx, wb, rec, n)  # counted, never routed
+    _classify_to(rx, wa, rec, n)  # clears b's counts first
+    assert rec.cpu().numpy().view(abi.REC_DTYPE).tobytes() == orec_a.tobytes()
+    check(route(rec, n_parts), orec_a, n_parts)  # fused counts
+    check(route(rec, n_parts), orec_a, n_parts)  # nothing pending: counting pass
+    other = torch.from_numpy(orec_b.view(np.uint8).copy()).cuda()
+    _classify_to(rx, wa, rec, n)
+    check(route(other, n_parts), orec_b, n_parts)  # other records: counting pass
+    _classify_to(rx, wa, rec, n)
+    check(route(rec, 2 if n_parts != 2 else 3), orec_a, 2 if n_parts != 2 else 3)  # other n_parts
+    rx.set_route_parts(0)
+
+
 def test_route_dev_overflow(rxmod):
     """A region smaller than its records: the count reports the true total, nothing is
     written past the region."""

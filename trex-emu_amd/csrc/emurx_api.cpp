@@ -180,6 +180,12 @@ struct emurx_ctx {
     // tx ZMQ framing scratch (emurx_tx_zmq_dev): per-level chain transfer tables
     DevBuf<uint8_t> d_txz;
 
+    // route count pass fused into classify launches (emurx_set_route_parts): the counts of
+    // the last such launch wait in d_route_cnt / d_route_grp for emurx_route_dev
+    uint32_t route_parts = 0, route_n = 0;
+    const emurx_rec* route_rec = nullptr;
+    bool route_pending = false;
+
     // Namespace-partition packing scratch (emurx_route_dev)
     DevBuf<uint32_t> d_route_cnt, d_route_grp, d_route_goff;  // grp: zero between batches
 
@@ -440,7 +446,18 @@ int run_dev(emurx_t* h, const uint8_t* frames, const emurx_desc* desc, uint32_t 
         h->ev_count = std::min(h->ev_count + 1, h->slots);
     }
     const bool narrow = choose_stage(h);
-    int r = emurx_launch_batch(frames, desc, n, T, classify, *out, st, ev, narrow, h->d_stage_fb.p, h->stage_gen);
+    emurx_route_counts rt{h->route_parts, h->d_route_cnt.p, h->d_route_grp.p};
+    const bool fuse = classify && h->route_parts && out->rec && n;
+    if (fuse && h->route_pending &&  // counts nobody routed: clear them
+        hipMemsetAsync(h->d_route_grp.p, 0, 1024 * 16 * sizeof(uint32_t), st) != hipSuccess)
+        return EMURX_EDEVICE;
+    int r = emurx_launch_batch(frames, desc, n, T, classify, *out, st, ev, narrow, h->d_stage_fb.p, h->stage_gen,
+                               fuse ? &rt : nullptr);
+    if (fuse) {
+        h->route_pending = true;
+        h->route_rec = out->rec;
+        h->route_n = n;
+    }
     if (!r) r = stage_copy_back(h, st);
     return r ? EMURX_EDEVICE : EMURX_OK;
 }
@@ -1122,10 +1139,38 @@ int emurx_route_dev(emurx_t* h, const emurx_rec* d_rec, uint32_t n, uint32_t n_p
     }
     if (h->d_route_cnt.alloc(std::max<size_t>(tiles, 1) * 16) || h->d_route_goff.alloc(gw)) return EMURX_ENOMEM;
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    // the owners of exactly this batch were counted by its classify launch: skip that pass
+    const bool counted = h->route_pending && d_rec == h->route_rec && n == h->route_n && n_parts == h->route_parts;
+    if (h->route_pending && !counted &&
+        hipMemsetAsync(h->d_route_grp.p, 0, gw * sizeof(uint32_t), st) != hipSuccess)
+        return EMURX_EDEVICE;
+    h->route_pending = false;
     return emurx_launch_route(d_rec, n, n_parts, my_rank, cap, d_send, d_send_count, h->d_route_cnt.p,
-                              h->d_route_grp.p, h->d_route_goff.p, st)
+                              h->d_route_grp.p, h->d_route_goff.p, st, counted)
                ? EMURX_EDEVICE
                : EMURX_OK;
+}
+
+int emurx_set_route_parts(emurx_t* h, uint32_t n_parts) {
+    if (!h || n_parts > EMURX_MAX_PARTS) return EMURX_EINVAL;
+    int rc = bind(h);
+    if (rc) return rc;
+    (void)hipStreamSynchronize(h->stream);
+    const size_t gw = 1024 * 16, tiles = ((size_t)h->cfg.max_frames + EMURX_QUEUE_TILE - 1) / EMURX_QUEUE_TILE;
+    if (n_parts) {
+        if (tiles > 1024u * 64u) return EMURX_EINVAL;
+        if (!h->d_route_grp.p) {
+            if (h->d_route_grp.alloc(gw) || hipMemset(h->d_route_grp.p, 0, gw * sizeof(uint32_t)) != hipSuccess)
+                return EMURX_ENOMEM;
+        }
+        if (h->d_route_cnt.alloc(std::max<size_t>(tiles, 1) * 16) || h->d_route_goff.alloc(gw)) return EMURX_ENOMEM;
+    }
+    if (h->route_pending && h->d_route_grp.p &&
+        hipMemset(h->d_route_grp.p, 0, gw * sizeof(uint32_t)) != hipSuccess)
+        return EMURX_EDEVICE;
+    h->route_pending = false;
+    h->route_parts = n_parts;
+    return EMURX_OK;
 }
 
 }  // extern "C"

@@ -9,16 +9,24 @@
 // hipGraph).  ev[0..1] (optional) are recorded before and after it.  narrow: the 6 KiB
 // staging slab (6 workgroups per CU) instead of 7 KiB (5).  fb (optional, host-visible,
 // 64 * 4 words): the sampled tiles' stage feedback, tagged with gen.  Returns 0 or -1.
+// rt (optional, classify only): the route count pass fused into k_rx: per-(tile, owner) counts
+// into cnt[ntiles * 16] and per-group sums added into grp (as emurx_launch_route's first pass).
+struct emurx_route_counts {
+    uint32_t parts;
+    uint32_t* cnt;
+    uint32_t* grp;
+};
 int emurx_launch_batch(const uint8_t* frames, const emurx_desc* desc, uint32_t n,
                        const emurx_dev_tables& T, bool classify, const emurx_dev_out& out,
-                       hipStream_t st, const hipEvent_t* ev, bool narrow, uint32_t* fb, uint32_t gen);
+                       hipStream_t st, const hipEvent_t* ev, bool narrow, uint32_t* fb, uint32_t gen,
+                       const emurx_route_counts* rt = nullptr);
 
 // Enqueue the Namespace-partition packing of a classified batch (emurx_route.hip): three
 // launches on `st`.  Scratch: tile_cnt [ceil(n / 256) * 16]; grp, grp_off [groups * 16] with
 // groups = ceil(n / 16384) <= 1024 (n <= 16M); grp must be zero (the launches leave it zero).
 int emurx_launch_route(const emurx_rec* rec, uint32_t n, uint32_t n_parts, uint32_t my_rank, uint32_t cap,
                        emurx_route_rec* send, uint32_t* send_count, uint32_t* tile_cnt, uint32_t* grp,
-                       uint32_t* grp_off, hipStream_t st);
+                       uint32_t* grp_off, hipStream_t st, bool counted = false);
 
 // Batched ZMQ ingest (emurx_ingest.hip).  zmq_walk: one lane per message; ctl = emurx_msg[nmsg]
 // then slot_base[nmsg + 1]; writes desc[slot_base[m] ..) (holes marked EMURX_DESC_HOLE) and

@@ -37,18 +37,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
                                                uint32_t* __restrict__ tile_cnt,
                                                unsigned long long* __restrict__ hist,
                                                uint32_t* __restrict__ flow, uint32_t* __restrict__ fb,
-                                               uint32_t gen) {
+                                               uint32_t gen, uint32_t rt_parts, uint32_t* __restrict__ rt_cnt,
+                                               uint32_t* __restrict__ rt_grp) {
     constexpr uint32_t kWinVec = kStage / 16 / kWave;  // window path: 16-byte vectors per lane
     __shared__ __attribute__((aligned(16))) uint32_t slab[kWaves * kStage / 4];
     __shared__ uint32_t s_wcnt[kWaves][16];
     __shared__ uint32_t s_hist[kWaves][EMURX_HIST_BINS];  // {pkts << 23 | bytes}: <= 64 x 65535 B
     __shared__ uint32_t s_csum[kWaves][kWave];                      // window path: span sums
+    __shared__ uint32_t s_rcnt[kWaves][EMURX_MAX_PARTS];            // Namespace owners (rt_cnt)
 
     const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / kWave;
     const uint32_t tile = blockIdx.x;
     const uint32_t i = tile * EMURX_QUEUE_TILE + tid;
     s_hist[wv][lane] = 0;  // each wave owns its copy: no cross-wave ordering needed
     if (lane < 16) s_wcnt[wv][lane] = 0;
+    if (lane < EMURX_MAX_PARTS) s_rcnt[wv][lane] = 0;
 
     const uint2 dd = i < n ? *reinterpret_cast<const uint2*>(desc + i) : make_uint2(0, EMURX_DESC_HOLE << 24);
     const bool valid = (dd.y >> 24) != EMURX_DESC_HOLE;  // an empty slot is no frame at all
@@ -149,7 +152,27 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
         if (lane == lead) s_wcnt[wv][qq] = (uint32_t)__popcll(m);
         left &= ~m;
     }
+    // the route count pass fused in (emurx_set_route_parts): the owner GPU of every record
+    // with a Namespace, counted per (tile, owner) and per group of 64 tiles as k_route<false>
+    // counts them (emurx_route.hip)
+    if (rt_cnt) {
+        const uint32_t d = valid && r.ns != EMURX_ID_NONE
+                               ? emurx_owner(emurx_tk_hash(r.vport, r.vlan0, r.vlan1), rt_parts) : 0xffu;
+        uint64_t rl = __ballot(d != 0xffu);
+        while (rl) {
+            const uint32_t lead = (uint32_t)__ffsll((long long)rl) - 1;
+            const uint32_t dd = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)lead);
+            const uint64_t m = __ballot(d == dd);
+            if (lane == lead) s_rcnt[wv][dd] = (uint32_t)__popcll(m);
+            rl &= ~m;
+        }
+    }
     __syncthreads();
+    if (rt_cnt && tid < 16) {
+        const uint32_t c = tid < rt_parts ? s_rcnt[0][tid] + s_rcnt[1][tid] + s_rcnt[2][tid] + s_rcnt[3][tid] : 0u;
+        rt_cnt[(size_t)tile * 16 + tid] = c;
+        if (c) atomicAdd(&rt_grp[(tile / 64) * 16 + tid], c);
+    }
 
     // this tile's segment of every queue: frames in (wave, lane) order == frame order
     if (qlist && q < EMURX_NUM_QUEUES && !(EMURX_ABL & 8)) {
@@ -187,7 +210,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
 // ---------------------------------------------------------------------------------------
 int emurx_launch_batch(const uint8_t* frames, const emurx_desc* desc, uint32_t n,
                        const emurx_dev_tables& T, bool classify, const emurx_dev_out& out,
-                       hipStream_t st, const hipEvent_t* ev, bool narrow, uint32_t* fb, uint32_t gen) {
+                       hipStream_t st, const hipEvent_t* ev, bool narrow, uint32_t* fb, uint32_t gen,
+                       const emurx_route_counts* rt) {
     using namespace emurx;
     if (ev) (void)hipEventRecord(ev[0], st);
     if (n) {
@@ -196,7 +220,7 @@ int emurx_launch_batch(const uint8_t* frames, const emurx_desc* desc, uint32_t n
         auto k = classify ? (narrow ? k_rx<true, kStageNarrow> : k_rx<true, kStageWide>)
                           : (narrow ? k_rx<false, kStageNarrow> : k_rx<false, kStageWide>);
         hipLaunchKernelGGL(k, g, b, 0, st, frames, desc, n, T, out.rec, out.qlist, out.qcap, out.tile_cnt, hist,
-                           out.flow, fb, gen);
+                           out.flow, fb, gen, rt ? rt->parts : 0u, rt ? rt->cnt : nullptr, rt ? rt->grp : nullptr);
     }
     if (ev) (void)hipEventRecord(ev[1], st);
     return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -135,13 +135,14 @@ __global__ __launch_bounds__(kScanThreads) void k_route_scan(uint32_t* __restric
 
 int emurx_launch_route(const emurx_rec* rec, uint32_t n, uint32_t n_parts, uint32_t my_rank, uint32_t cap,
                        emurx_route_rec* send, uint32_t* send_count, uint32_t* tile_cnt, uint32_t* grp,
-                       uint32_t* grp_off, hipStream_t st) {
+                       uint32_t* grp_off, hipStream_t st, bool counted) {
     using namespace emurx;
     const uint32_t ntiles = (n + kBlock - 1) / kBlock, ngroups = (ntiles + kGroup - 1) / kGroup;
     if (n == 0) return hipMemsetAsync(send_count, 0, n_parts * sizeof(uint32_t), st) == hipSuccess ? 0 : -1;
     if (ngroups > kScanThreads) return -1;
-    hipLaunchKernelGGL(k_route<false>, dim3(ntiles), dim3(kBlock), 0, st, rec, n, n_parts, my_rank, tile_cnt, grp,
-                       (const uint32_t*)nullptr, send, cap);
+    if (!counted)  // else k_rx counted the owners of this batch (emurx_set_route_parts)
+        hipLaunchKernelGGL(k_route<false>, dim3(ntiles), dim3(kBlock), 0, st, rec, n, n_parts, my_rank, tile_cnt,
+                           grp, (const uint32_t*)nullptr, send, cap);
     hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(kScanThreads), 0, st, grp, ngroups, n_parts, grp_off, send_count);
     hipLaunchKernelGGL(k_route<true>, dim3(ntiles), dim3(kBlock), 0, st, rec, n, n_parts, my_rank, tile_cnt, grp,
                        grp_off, send, cap);

@@ -162,6 +162,7 @@ SIGNATURES = [
     ("emurx_last_stage", C.c_uint32, [_P]),
     ("emurx_ns_owner", C.c_uint32, [_U8P, C.c_uint32]),
     ("emurx_route_dev", C.c_int, [_P, _P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P]),
+    ("emurx_set_route_parts", C.c_int, [_P, C.c_uint32]),
     ("emurx_ingest_buffer", C.c_int, [_P, C.c_uint32, C.c_size_t, C.POINTER(C.c_void_p)]),
     ("emurx_ingest_submit", C.c_int, [_P, C.c_uint32, _P, C.c_uint32]),
     ("emurx_ingest_wait", C.c_int, [_P, C.c_uint32, C.POINTER(IngestResult)]),

@@ -219,6 +219,11 @@ class RxPath:
                                                    _addr(msg_off), _addr(info), _stream(stream)), "tx_zmq_dev")
 
     # ---- Namespace-partitioned exchange ---------------------------------------------------
+    def set_route_parts(self, n_parts: int):
+        """Fuse route_dev's counting pass into the following classify launches
+        (include/emu_rx.h emurx_set_route_parts); 0 turns it off."""
+        return abi.check(self.lib.emurx_set_route_parts(self.h, n_parts), "set_route_parts")
+
     def route_dev(self, rec, n: int, n_parts: int, my_rank: int, cap: int, send, send_count, stream=None):
         """Pack the batch's records with a Namespace into their owners' send regions
         (send[d*cap:][:send_count[d]], frame order; include/emu_rx.h emurx_route_dev)."""
