@@ -58,6 +58,8 @@ def parse_args():
                     help="skip the output sanity check (stage-ablation builds, tools/ablate.sh)")
     ap.add_argument("--tx-path", action="store_true",
                     help="also time the device tx ZMQ framing (emurx_tx_zmq_dev) over the same frames")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="rendezvous + max-over-ranks reduction only, no GPU (CPU test of the launch path)")
     ap.add_argument("--host-path", action="store_true",
                     help="also time the host-inclusive path (pinned H2D + kernels + D2H)")
     return ap.parse_args()
@@ -74,10 +76,31 @@ def workload(cfg, n, rank):
     return synth.config_e(n, rank=rank)
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def host_cores():
+    """CPU threads this process may use: the affinity mask, capped by OMP_NUM_THREADS (the GPU
+    box exports the share of the machine a job gets; os.cpu_count() there is the whole host)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(cap))) if cap and cap.isdigit() else n
+
+
 def cpu_baseline(w, budget_s):
-    """Oracle (C restatement of the Go path) on 1 host core over repeated passes of a
-    bounded sample of the same frames.  Test infrastructure: imported only here."""
+    """Oracle (C restatement of the Go path: per-frame parse, byte-pair checksum, hash-map
+    lookups) over repeated passes of a bounded sample of the same frames, on 1 host core and
+    then on every core this job may use (frames split by offset, one thread per core; ctypes
+    drops the GIL, the tables are shared read-only).  Test infrastructure: imported only here."""
     sys.path.insert(0, str(ROOT / "oracle"))
+    import threading
     import numpy as np
     import pyoracle
     from emurx import synth
@@ -87,28 +110,84 @@ def cpu_baseline(w, budget_s):
     sample = min(len(w["desc"]), 1 << 18)
     desc = np.ascontiguousarray(w["desc"][:sample])
     o.rx_batch(w["buf"], desc[:1024])  # warm
-    frames, t0 = 0, time.perf_counter()
-    while True:
-        o.rx_batch(w["buf"], desc)
-        frames += sample
-        el = time.perf_counter() - t0
-        if el >= budget_s:
-            break
-    return {"value": round(frames / el / 1e6, 3), "unit": "Mpkt/s", "cores": 1, "kind": "port",
-            "sample": f"{sample} frames of config {w['name']} x {frames // sample} passes "
-                      f"({el:.1f} s), oracle/emurx_oracle.c rx_batch (parse + classify + queues + counters)"}
+
+    def run(d, stop, out, k):
+        frames = 0
+        while time.perf_counter() < stop:
+            o.rx_batch(w["buf"], d)
+            frames += len(d)
+        out[k] = frames
+
+    one = [0]
+    t0 = time.perf_counter()
+    run(desc, t0 + budget_s, one, 0)
+    el1 = time.perf_counter() - t0
+    cores = host_cores()
+    parts = np.array_split(desc, cores)
+    outs = [0] * cores
+    t0 = time.perf_counter()
+    th = [threading.Thread(target=run, args=(parts[k], t0 + budget_s * 0.75, outs, k)) for k in range(cores)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    eln = time.perf_counter() - t0
+    return {"value": round(one[0] / el1 / 1e6, 3), "unit": "Mpkt/s", "cores": 1, "kind": "port",
+            "sample": f"{sample} frames of config {w['name']} x {one[0] // sample} passes ({el1:.1f} s), "
+                      "oracle/emurx_oracle.c rx_batch (parse + classify + queues + counters)",
+            "cpu_model": cpu_model(),
+            "all_cores": {"value": round(sum(outs) / eln / 1e6, 3), "cores": cores,
+                          "seconds": round(eln, 1), "split": "frames by offset, one thread per core"}}
+
+
+def spawn_ranks(a):
+    """`bench.py --gpus N` without torchrun: start N fresh worker processes (one per GPU,
+    before any GPU call in this one), rendezvous on 127.0.0.1, forward rank 0's JSON line."""
+    import signal
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus),
+                   LOCAL_WORLD_SIZE=str(a.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] + sys.argv[1:], env=env,
+                                      start_new_session=True))
+    rc = 0
+    live = list(procs)
+    while live:
+        time.sleep(0.2)
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                for q in live:  # a failed rank leaves the others waiting in a collective
+                    try:
+                        os.killpg(q.pid, signal.SIGTERM)
+                    except OSError:
+                        pass
+    return rc
 
 
 def main():
     a = parse_args()
+    if a.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(spawn_ranks(a))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", str(a.gpus)))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus and "RANK" in os.environ:
+    if world != a.gpus:
         print(f"warning: WORLD_SIZE={world} != --gpus {a.gpus}", file=sys.stderr)
-    import numpy as np
     import torch
     import torch.distributed as dist
+    if a.launch_check:
+        sys.exit(launch_check(a, rank, world, dist, torch))
     if a.frames is None:
         a.frames = (1 << 21) if a.config == "D" else (1 << 20)
     a.exchange = a.exchange or a.config == "D"
@@ -145,6 +224,25 @@ def main():
         dist.destroy_process_group()
 
 
+def launch_check(a, rank, world, dist, torch):
+    """The multi-rank skeleton of a bench run without the GPU: rendezvous on MASTER_ADDR,
+    barrier, the max-over-ranks time reduction, rank 0's JSON line."""
+    if os.environ.get("EMURX_BENCH_FAIL_RANK") == str(rank):
+        return 3  # test hook: a rank that dies before the rendezvous completes
+    if world > 1:
+        dist.init_process_group("gloo")
+        dist.barrier()
+    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"launch_check": "ok", "n_gpus": world, "max_over_ranks": float(t.item()),
+                          "master": os.environ.get("MASTER_ADDR")}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
 def measure(a, cfg, n, exchange, steps, warmup, rank, world, local, dist, torch):
     """Run `steps` timed batches of workload `cfg` (n frames per rank) -> (JSON dict, rx, w)."""
     import numpy as np
@@ -168,36 +266,46 @@ def measure(a, cfg, n, exchange, steps, warmup, rank, world, local, dist, torch)
     hist = torch.zeros(abi.HIST_SHARDS * 2 * abi.HIST_BINS, dtype=torch.int64, device=dev)  # accumulates
     stream = torch.cuda.current_stream(dev)
     rx.sync(stream.cuda_stream)
+    classify = rx.classify_call(buf, desc, n, rec, qlist, qcap, tile_cnt, hist, stream=stream)
 
     xch = None
     if exchange:
         from emurx import exchange as X
-        cap = X.capacity(n, world)
-        send = torch.empty(world * cap * X.REC_BYTES, dtype=torch.uint8, device=dev)
-        send_count = torch.zeros(world, dtype=torch.int32, device=dev)
-        xch = dict(cap=cap, recv=None, recv_count=None, ev=[], timing=False, k=0)
+        xch = dict(cap=X.capacity(n, world), ev=[], timing=False, k=0)
+
+        def alloc_regions():
+            xch["send"] = torch.empty(world * xch["cap"] * X.REC_BYTES, dtype=torch.uint8, device=dev)
+            xch["send_count"] = torch.zeros(world, dtype=torch.int32, device=dev)
+        alloc_regions()
         rx.set_route_parts(world)  # the route's counting pass rides in k_rx (emurx_set_route_parts)
 
     def step():
-        rx.classify_dev(buf, desc, n, rec, qlist, qcap, tile_cnt, hist, stream=stream)
+        classify()
         if xch is not None:
             ev = None
             if xch["timing"] and xch["k"] % a.time_stride == 0:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 ev[0].record(stream)
             xch["k"] += 1
-            rx.route_dev(rec, n, world, rank, xch["cap"], send, send_count, stream=stream)
+            rx.route_dev(rec, n, world, rank, xch["cap"], xch["send"], xch["send_count"], stream=stream)
             if world > 1:
-                xch["recv"], xch["recv_count"] = X.exchange(send, send_count, xch["cap"])
+                xch["recv"], xch["recv_count"] = X.exchange(xch["send"], xch["send_count"], xch["cap"])
             else:
-                xch["recv"], xch["recv_count"] = send, send_count
+                xch["recv"], xch["recv_count"] = xch["send"], xch["send_count"]
             if ev is not None:
                 ev[1].record(stream)
                 xch["ev"].append(ev)
 
-    for _ in range(warmup):
-        step()
-    torch.cuda.synchronize()
+    for attempt in range(4):
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        if xch is None or not exchange_overflow(xch, world, dist, torch, dev):
+            break
+        # a region overflowed (send_count > cap): grow every rank's regions and redo
+        xch["cap"] = grow_cap(xch, world, dist, torch, dev)
+        alloc_regions()
+        hist.zero_()
     # sanity of the outcome on this rank (counts only; parity lives in tests/)
     if not a.no_check:
         from emurx.rx import hist_fold, pack_queues
@@ -217,12 +325,15 @@ def measure(a, cfg, n, exchange, steps, warmup, rank, world, local, dist, torch)
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
+    t_submit = time.perf_counter() - t0
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
     pk = rx.kernel_times()
     rx.set_timing(0)
+    if xch is not None and exchange_overflow(xch, world, dist, torch, dev):
+        raise RuntimeError("exchange region overflow in the timed region")
 
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev if a.backend == "nccl" else "cpu")
@@ -236,14 +347,18 @@ def measure(a, cfg, n, exchange, steps, warmup, rank, world, local, dist, torch)
     alg_bytes = w["nbytes"] + 8 * n + 32 * n + 4 * n
     parse_s = float(np.mean(pk)) * 1e-3 if len(pk) else float("nan")
     achieved = alg_bytes / parse_s / 1e9
-    traffic = None
+    traffic, pmc_src = None, None
     pmc = ROOT / "profiles" / f"pmc_config{cfg}.json"
     if pmc.exists():
         try:
             traffic = json.loads(pmc.read_text()).get("k_rx_hbm_bytes_per_launch")
+            pmc_src = str(pmc.relative_to(ROOT))
         except Exception:  # noqa: BLE001
             traffic = None
-
+    # the Namespace + Client bucket reads of every frame that reaches a callback (two 64-B
+    # buckets, issued together): outside the algorithmic bytes, served by L2 / MALL / HBM
+    r = rec.cpu().numpy().view(abi.REC_DTYPE)
+    probed = int((r["status"] == 0).sum())
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -275,13 +390,17 @@ def measure(a, cfg, n, exchange, steps, warmup, rank, world, local, dist, torch)
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
+            "traffic_source": pmc_src,
             "kernel": "k_rx",
             "alg_bytes_per_launch": alg_bytes,
+            "alg_bytes_per_frame": round(alg_bytes / n, 2),
+            "table_probe_bytes_per_launch": probed * 128,
             "kernel_ms_mean": round(parse_s * 1e3, 5),
             "kernel_launches_timed": int(len(pk)),
             "kernel_time_source": f"HIP events on the launch stream around every {a.time_stride}-th "
                                   "launch of the timed region",
         },
+        "host_submit_ms_per_step": round(t_submit / steps * 1e3, 5),
     }
     if xch is not None:
         xm = [e0.elapsed_time(e1) for e0, e1 in xch["ev"]]
@@ -293,6 +412,25 @@ def measure(a, cfg, n, exchange, steps, warmup, rank, world, local, dist, torch)
             "collective": f"all_to_all_single x2 ({a.backend})" if world > 1 else "none (1 rank)",
         }
     return out, rx, w
+
+
+def exchange_overflow(xch, world, dist, torch, dev):
+    """Did any rank's region overflow (send_count > cap) in the last step? (every step routes
+    the same batch, so the last step's counts are every step's)"""
+    over = torch.tensor([int((xch["send_count"].cpu() > xch["cap"]).any())], dtype=torch.int64)
+    if world > 1:
+        over = over.to(dev) if dist.get_backend() == "nccl" else over
+        dist.all_reduce(over, op=dist.ReduceOp.MAX)
+    return bool(over.cpu().item())
+
+
+def grow_cap(xch, world, dist, torch, dev):
+    from emurx import exchange as X
+    m = torch.tensor([int(xch["send_count"].cpu().max())], dtype=torch.int64)
+    if world > 1:
+        m = m.to(dev) if dist.get_backend() == "nccl" else m
+        dist.all_reduce(m, op=dist.ReduceOp.MAX)
+    return X.grow(xch["cap"], [int(m.cpu().item())])
 
 
 def xcheck(xch, rec, n, world, rank, dist, torch, dev):

@@ -276,6 +276,15 @@ int emurx_ns_set_plugins(emurx_t* h, uint32_t ns_id, uint32_t plugin_mask);
 int emurx_client_add(emurx_t* h, uint32_t ns_id, uint32_t client_id, const uint8_t mac[6],
                      const uint8_t ipv4[4], const uint8_t ipv6[16], const uint8_t dhcpv6[16],
                      uint32_t plugin_mask);
+/* ctx_client_add (ApiClientAddHandler rpc_base_cmds.go:350-406): a list of clients, each
+   through CNSCtx.AddClient in order; stops at the first error and returns it, *n_added =
+   clients added before it.  Zero address fields mean absent. */
+typedef struct emurx_client_spec {
+    uint32_t ns_id, client_id, plugin_mask;
+    uint8_t mac[6], ipv4[4], ipv6[16], dhcpv6[16];
+    uint8_t pad[2];
+} emurx_client_spec; /* 56 bytes */
+int emurx_clients_add(emurx_t* h, const emurx_client_spec* clients, uint32_t n, uint32_t* n_added);
 int emurx_client_remove(emurx_t* h, uint32_t ns_id, const uint8_t mac[6]);
 int emurx_client_set_plugins(emurx_t* h, uint32_t client_id, uint32_t plugin_mask);
 int emurx_client_update_ipv4(emurx_t* h, uint32_t client_id, const uint8_t ipv4[4]);

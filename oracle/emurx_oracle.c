@@ -240,6 +240,18 @@ int orc_client_add(orc_t* o, uint32_t ns_id, uint32_t cid, const uint8_t mac[6],
     return EMURX_OK;
 }
 
+/* ctx_client_add rpc_base_cmds.go:371-380: AddClient per listed client, stop at the first error */
+int orc_clients_add(orc_t* o, const emurx_client_spec* c, uint32_t n, uint32_t* n_added) {
+    uint32_t k = 0;
+    int rc = EMURX_OK;
+    for (; k < n; k++)
+        if ((rc = orc_client_add(o, c[k].ns_id, c[k].client_id, c[k].mac, c[k].ipv4, c[k].ipv6, c[k].dhcpv6,
+                                 c[k].plugin_mask)))
+            break;
+    if (n_added) *n_added = k;
+    return rc;
+}
+
 /* CNSCtx.RemoveClient ns_ctx.go:392-440 */
 int orc_client_remove(orc_t* o, uint32_t ns_id, const uint8_t mac[6]) {
     if (ns_id >= o->nns || !o->ns[ns_id].alive) return EMURX_ENOENT;

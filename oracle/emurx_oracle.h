@@ -32,6 +32,7 @@ int orc_ns_set_plugins(orc_t* o, uint32_t ns_id, uint32_t plugin_mask);
 int orc_client_add(orc_t* o, uint32_t ns_id, uint32_t client_id, const uint8_t mac[6],
                    const uint8_t ipv4[4], const uint8_t ipv6[16], const uint8_t dhcpv6[16],
                    uint32_t plugin_mask);
+int orc_clients_add(orc_t* o, const emurx_client_spec* c, uint32_t n, uint32_t* n_added);
 int orc_client_remove(orc_t* o, uint32_t ns_id, const uint8_t mac[6]);
 int orc_client_set_plugins(orc_t* o, uint32_t client_id, uint32_t plugin_mask);
 int orc_client_update_ipv4(orc_t* o, uint32_t client_id, const uint8_t ipv4[4]);

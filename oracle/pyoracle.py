@@ -52,6 +52,7 @@ def lib():
             ("orc_ns_remove", C.c_int, [P, P]),
             ("orc_ns_set_plugins", C.c_int, [P, C.c_uint32, C.c_uint32]),
             ("orc_client_add", C.c_int, [P, C.c_uint32, C.c_uint32, P, P, P, P, C.c_uint32]),
+            ("orc_clients_add", C.c_int, [P, P, C.c_uint32, C.POINTER(C.c_uint32)]),
             ("orc_client_remove", C.c_int, [P, C.c_uint32, P]),
             ("orc_client_set_plugins", C.c_int, [P, C.c_uint32, C.c_uint32]),
             ("orc_client_update_ipv4", C.c_int, [P, C.c_uint32, P]),
@@ -122,6 +123,14 @@ class Oracle:
         a = [_b(mac, 6), _b(ipv4, 4), _b(ipv6, 16), _b(dhcpv6, 16)]
         p = [x.ctypes.data if x is not None else None for x in a]
         return lib().orc_client_add(self._h, ns_id, cid, p[0], p[1], p[2], p[3], plugins)
+
+    def clients_add(self, spec):
+        """orc_clients_add over emurx_client_spec rows (56 B each) -> (rc, added)."""
+        a = np.ascontiguousarray(spec)
+        assert a.dtype.itemsize == 56
+        k = C.c_uint32()
+        rc = lib().orc_clients_add(self._h, a.ctypes.data if len(a) else None, len(a), C.byref(k))
+        return rc, k.value
 
     def client_remove(self, ns_id, mac):
         m = _b(mac, 6)

@@ -11,15 +11,16 @@ from emurx.rx import ns_owner
 
 
 def owners(rec, n_parts):
-    keys = {}
+    """emurx_ns_owner of every record's CTunnelKey (0xFF for records without a Namespace)."""
     out = np.full(len(rec), 0xFF, np.uint32)
-    for i, r in enumerate(rec):
-        if int(r["ns_id"]) == abi.ID_NONE:
-            continue
-        k = (int(r["vport"]), int(r["vlan0"]), int(r["vlan1"]))
-        if k not in keys:
-            keys[k] = ns_owner(F.tunnel_key(*k), n_parts)
-        out[i] = keys[k]
+    has = np.nonzero(rec["ns_id"] != abi.ID_NONE)[0]
+    if not len(has):
+        return out
+    k = np.stack([rec["vport"][has].astype(np.uint64), rec["vlan0"][has].astype(np.uint64),
+                  rec["vlan1"][has].astype(np.uint64)], 1)
+    uk, inv = np.unique(k, axis=0, return_inverse=True)
+    own = np.array([ns_owner(F.tunnel_key(int(a), int(b), int(c)), n_parts) for a, b, c in uk], np.uint32)
+    out[has] = own[inv.reshape(-1)]
     return out
 
 

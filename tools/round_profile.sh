@@ -1,12 +1,17 @@
 #!/bin/bash
-# Round evidence on the GPU box: benches (B with CPU baseline + host path, C, E, D), the
-# rocprofv3 kernel-trace summary of the config-B bench, and the HBM-traffic PMC passes
-# (FETCH_SIZE, WRITE_SIZE: one rocprofv3 run each, as the microarch guide prescribes).
-#   tools/round_profile.sh <tag>      -> gpurun_out/round_<tag>/
+# Round evidence on the GPU box, per BASELINE config:
+#   bench    bench.py lines (B with the CPU baseline and the host path)
+#   prof     rocprofv3 --kernel-trace --stats of the bench command
+#   pmc      HBM traffic of k_rx: FETCH_SIZE and WRITE_SIZE, one rocprofv3 run each (the
+#            microarch guide's recipe), folded by tools/pmc_summary.py
+#   tools/round_profile.sh <tag> "<configs>" "<phases>"   -> gpurun_out/round_<tag>/
+#   e.g. tools/round_profile.sh r02a "B C D E" "bench"
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 tag=${1:-v}
+configs=${2:-"B C D E"}
+phases=${3:-"bench prof pmc"}
 out=gpurun_out/round_$tag
 mkdir -p $out
 step() {  # name seconds cmd...
@@ -14,18 +19,34 @@ step() {  # name seconds cmd...
   echo "== $name ($(date +%T))"
   timeout -k 10 "$to" "$@" > "$out/$name.log" 2>&1
   local rc=$?
-  echo "$name rc=$rc"; tail -n 2 "$out/$name.log" | cut -c1-400
+  echo "$name rc=$rc"; tail -n 2 "$out/$name.log" | cut -c1-600
   [ $rc -eq 0 ] || exit $rc
 }
-step bench_B 600 python bench.py --host-path
-step bench_C 300 python bench.py --config C --steps 100 --warmup 10 --no-cpu-baseline
-step bench_E 300 python bench.py --config E --steps 50 --warmup 5 --no-cpu-baseline
-step bench_D 300 python bench.py --config D --steps 50 --warmup 5 --no-cpu-baseline
-step prof_B 300 rocprofv3 --kernel-trace --stats -d $out/prof_B -o run --output-format csv \
-  -- python bench.py --steps 50 --warmup 5 --no-cpu-baseline
-for c in FETCH_SIZE WRITE_SIZE; do
-  step pmc_$c 120 rocprofv3 --pmc $c -T --kernel-include-regex k_rx -d $out/pmc_$c -o run --output-format csv \
-    -- python bench.py --steps 40 --warmup 8 --no-cpu-baseline --no-check
+args() {  # bench arguments per config
+  case $1 in
+    B) echo "--steps 200 --warmup 20" ;;
+    C) echo "--config C --steps 100 --warmup 10" ;;
+    D) echo "--config D --steps 50 --warmup 5" ;;
+    E) echo "--config E --steps 50 --warmup 5" ;;
+  esac
+}
+for ph in $phases; do
+  for c in $configs; do
+    case $ph in
+      bench)
+        extra="--no-cpu-baseline"
+        [ "$c" = B ] && extra="--host-path"
+        step bench_$c 600 python bench.py $(args $c) $extra ;;
+      prof)
+        step prof_$c 300 rocprofv3 --kernel-trace --stats -d $out/prof_$c -o run --output-format csv \
+          -- python bench.py $(args $c) --no-cpu-baseline ;;
+      pmc)
+        for k in FETCH_SIZE WRITE_SIZE; do
+          step pmc_${c}_$k 180 rocprofv3 --pmc $k -T --kernel-include-regex k_rx -d $out/pmc_${c}/pmc_$k -o run \
+            --output-format csv -- python bench.py $(args $c) --steps 40 --warmup 8 --no-cpu-baseline --no-check
+        done
+        python tools/pmc_summary.py $out/pmc_${c} > $out/pmc_config$c.json 2>&1; cat $out/pmc_config$c.json ;;
+    esac
+  done
 done
-python tools/pmc_summary.py $out > $out/pmc_summary.txt 2>&1; cat $out/pmc_summary.txt
 echo done

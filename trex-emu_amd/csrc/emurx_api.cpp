@@ -238,7 +238,13 @@ struct emurx_ctx {
 
 namespace {
 
-int bind(emurx_t* h) { return hipSetDevice(h->cfg.device) == hipSuccess ? EMURX_OK : EMURX_EDEVICE; }
+// every entry point re-binds the handle's device (goroutines migrate between OS threads);
+// hipGetDevice is a thread-local read, hipSetDevice only when the thread is elsewhere
+int bind(emurx_t* h) {
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && cur == h->cfg.device) return EMURX_OK;
+    return hipSetDevice(h->cfg.device) == hipSuccess ? EMURX_OK : EMURX_EDEVICE;
+}
 
 // open-addressing insert into a bucketed table (emurx_tables.h): first free slot of the
 // first bucket, in linear bucket order from the home bucket, that has one
@@ -771,6 +777,18 @@ int emurx_client_add(emurx_t* h, uint32_t ns_id, uint32_t cid, const uint8_t mac
     h->ns[ns_id].order.push_back(cid);
     h->dirty = true;
     return EMURX_OK;
+}
+
+int emurx_clients_add(emurx_t* h, const emurx_client_spec* c, uint32_t n, uint32_t* n_added) {
+    if (!h || (n && !c)) return EMURX_EINVAL;
+    uint32_t k = 0;
+    int rc = EMURX_OK;
+    for (; k < n; ++k)
+        if ((rc = emurx_client_add(h, c[k].ns_id, c[k].client_id, c[k].mac, c[k].ipv4, c[k].ipv6, c[k].dhcpv6,
+                                   c[k].plugin_mask)))
+            break;
+    if (n_added) *n_added = k;
+    return rc;
 }
 
 static void drop_transport(emurx_t* h, uint32_t cid) {

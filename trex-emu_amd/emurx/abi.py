@@ -85,6 +85,10 @@ ZMQ_TX_BURST, ZMQ_TX_MAX_BUFFER, ZMQ_PKT_MAGIC = 64, 32768, 0xAA  # veth_zmq.go:
 FLOW_NONE, FLOW_NO_CTX, FLOW_NO_SYN, FLOW_NO_SERVER, FLOW_NEW = (0xFFFFFFFF, 0xFFFFFFF0, 0xFFFFFFF1,
                                                                 0xFFFFFFF2, 0xFFFFFFF3)
 FLOW_ID_MAX = 0xFFFFFFEF
+# emurx_client_spec (ctx_client_add list entry)
+CLIENT_SPEC_DTYPE = np.dtype([("ns_id", "<u4"), ("client_id", "<u4"), ("plugin_mask", "<u4"), ("mac", "u1", 6),
+                              ("ipv4", "u1", 4), ("ipv6", "u1", 16), ("dhcpv6", "u1", 16), ("pad", "u1", 2)])
+assert CLIENT_SPEC_DTYPE.itemsize == 56
 TX_DESC_DTYPE = np.dtype([("off", "<u4"), ("len", "<u2"), ("l3", "<u2"), ("l4", "<u2"), ("osize", "<u2"),
                           ("ops", "u1"), ("nh", "u1"), ("pad", "u1", 2)])
 assert TX_DESC_DTYPE.itemsize == 16
@@ -142,6 +146,7 @@ SIGNATURES = [
     ("emurx_ns_remove", C.c_int, [_P, _U8P]),
     ("emurx_ns_set_plugins", C.c_int, [_P, C.c_uint32, C.c_uint32]),
     ("emurx_client_add", C.c_int, [_P, C.c_uint32, C.c_uint32, _U8P, _U8P, _U8P, _U8P, C.c_uint32]),
+    ("emurx_clients_add", C.c_int, [_P, _P, C.c_uint32, C.POINTER(C.c_uint32)]),
     ("emurx_client_remove", C.c_int, [_P, C.c_uint32, _U8P]),
     ("emurx_client_set_plugins", C.c_int, [_P, C.c_uint32, C.c_uint32]),
     ("emurx_client_update_ipv4", C.c_int, [_P, C.c_uint32, _U8P]),

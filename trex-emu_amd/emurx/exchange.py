@@ -19,11 +19,20 @@ from . import abi
 REC_BYTES = abi.ROUTE_REC_DTYPE.itemsize
 
 
-def capacity(n_frames: int, n_parts: int, slack: float = 1.25) -> int:
-    """Records per destination region: the fair share plus slack for hash imbalance."""
+def capacity(n_frames: int, n_parts: int, slack: float = 1.06) -> int:
+    """Records per destination region: the fair share plus slack for the owner hash's
+    imbalance (config D: the fullest of 8 partitions holds 1.030x the fair share).  A
+    region that overflows anyway is reported by its count (> cap); the caller grows the
+    capacity (grow()) and routes the batch again."""
     if n_parts == 1:
         return max(n_frames, 1)
-    return int(n_frames / n_parts * slack) + 256
+    return int(n_frames / n_parts * slack) + 1024
+
+
+def grow(cap: int, counts) -> int:
+    """Capacity after an overflow: the largest region count seen plus 1/16 more."""
+    m = int(max(int(c) for c in counts))
+    return max(cap, m + m // 16 + 1024)
 
 
 def exchange(send, send_count, cap: int, group=None):

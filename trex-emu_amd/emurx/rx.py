@@ -85,6 +85,14 @@ class RxPath:
         a = [_u8(mac, 6), _u8(ipv4, 4), _u8(ipv6, 16), _u8(dhcpv6, 16)]
         return self.lib.emurx_client_add(self.h, ns_id, cid, *[_p(x) for x in a], plugins)
 
+    def clients_add(self, spec: np.ndarray) -> tuple[int, int]:
+        """ctx_client_add: CLIENT_SPEC_DTYPE rows in order -> (rc of the first failure or 0,
+        clients added)."""
+        a = np.ascontiguousarray(spec, dtype=abi.CLIENT_SPEC_DTYPE)
+        k = C.c_uint32()
+        rc = self.lib.emurx_clients_add(self.h, _p(a) if len(a) else None, len(a), C.byref(k))
+        return rc, k.value
+
     def client_remove(self, ns_id, mac) -> int:
         m = _u8(mac, 6)
         return self.lib.emurx_client_remove(self.h, ns_id, _p(m))
@@ -153,6 +161,21 @@ class RxPath:
         fn = self.lib.emurx_classify_dev if classify else self.lib.emurx_parse_dev
         return abi.check(fn(self.h, _addr(frames), _addr(desc), n, C.byref(out),
                             _stream(stream)), "classify_dev")
+
+    def classify_call(self, frames, desc, n: int, rec=None, qlist=None, qcap: int = 0, tile_cnt=None,
+                      hist=None, stream=None, classify: bool = True, flow=None):
+        """classify_dev with every argument resolved once: returns a zero-argument callable
+        that enqueues the same batch again (one C call, no Python-side argument work)."""
+        out = abi.DevOut(_addr(rec), _addr(qlist), qcap, _addr(tile_cnt), _addr(hist), _addr(flow))
+        fn = self.lib.emurx_classify_dev if classify else self.lib.emurx_parse_dev
+        args = (self.h, _addr(frames), _addr(desc), n, C.byref(out), _stream(stream))
+
+        def call():
+            rc = fn(*args)
+            if rc:
+                abi.check(rc, "classify_dev")
+        call.keep = out
+        return call
 
     def set_timing(self, slots: int = 1024, stride: int = 1):
         """Time every `stride`-th batch with HIP events (0 slots disables)."""

@@ -341,8 +341,15 @@ def load_tables(w, target):
     for key, ns_id in w["ns"]:
         rc = target.ns_add(key, ns_id, 0x7FF)
         assert rc == 0, rc
+    rc, k = target.clients_add(client_specs(w))
+    assert rc == 0 and k == len(w["clients"]["cid"]), (rc, k)
+
+
+def client_specs(w, plugins=0x7FF):
+    """The workload's clients as one ctx_client_add list (CLIENT_SPEC_DTYPE rows)."""
+    from .abi import CLIENT_SPEC_DTYPE
     c = w["clients"]
-    for i in range(len(c["cid"])):
-        rc = target.client_add(int(c["ns"][i]), int(c["cid"][i]), c["mac"][i].tobytes(),
-                               c["ipv4"][i].tobytes(), c["ipv6"][i].tobytes(), None, 0x7FF)
-        assert rc == 0, rc
+    s = np.zeros(len(c["cid"]), CLIENT_SPEC_DTYPE)
+    s["ns_id"], s["client_id"], s["plugin_mask"] = c["ns"], c["cid"], plugins
+    s["mac"], s["ipv4"], s["ipv6"] = c["mac"], c["ipv4"], c["ipv6"]
+    return s
