@@ -45,7 +45,12 @@ def parse_args():
     ap.add_argument("--frames", type=int, default=None,
                     help="frames per GPU per step (default 1M; config D: 2M = 16M over 8 GPUs)")
     ap.add_argument("--exchange", action="store_true",
-                    help="route records to their Namespace owners each step (default for D)")
+                    help="route to the Namespace owners each step (= --tables partitioned)")
+    ap.add_argument("--tables", choices=["none", "replicated", "partitioned"], default=None,
+                    help="none: classify only; replicated / partitioned: Namespace-owner exchange each step "
+                         "(default for D: partitioned, with the replicated alternative measured too)")
+    ap.add_argument("--table-updates", action="store_true",
+                    help="also time batches with 1 / 64 / 4096 table mutations between them")
     ap.add_argument("--no-exchange-run", action="store_true",
                     help="at N > 1, skip the extra config-D Namespace-exchange measurement")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -190,7 +195,7 @@ def main():
         sys.exit(launch_check(a, rank, world, dist, torch))
     if a.frames is None:
         a.frames = (1 << 21) if a.config == "D" else (1 << 20)
-    a.exchange = a.exchange or a.config == "D"
+    mode = a.tables or ("partitioned" if a.config == "D" or a.exchange else "none")
     local = local % max(torch.cuda.device_count(), 1)  # gloo rehearsal: ranks may share a GPU
     torch.cuda.set_device(local)
     if world > 1:
@@ -198,13 +203,25 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group("gloo")
-    out, rx, w = measure(a, a.config, a.frames, a.exchange, a.steps, a.warmup, rank, world, local, dist, torch)
-    if world > 1 and a.config == "B" and not a.no_exchange_run:
-        # evidence for the Namespace-owner all-to-all at N > 1 (SURVEY.md §8e): config D
-        # shards with the exchange in every step; the headline value stays config B's
+    out, rx, w = measure(a, a.config, a.frames, mode, a.steps, a.warmup, rank, world, local, dist, torch)
+    if a.config == "D" and not a.no_exchange_run:
+        # SURVEY.md §8e asks for both: the Namespace-partitioned lookups (the headline of D)
+        # and the "replicas only" alternative (every GPU holds every table)
+        other = "replicated" if mode == "partitioned" else "partitioned"
         try:
             rx.close()
-            xo, rx, _ = measure(a, "D", 1 << 21, True, max(10, a.steps // 4), max(2, a.warmup // 4),
+            xo, rx, _ = measure(a, "D", a.frames, other, max(10, a.steps // 2), max(2, a.warmup // 2),
+                                rank, world, local, dist, torch)
+            out["alternative"] = {k: xo[k] for k in ("value", "unit", "ms_per_step", "steps", "exchange")}
+            out["alternative"]["k_rx_ms_mean"] = xo["roofline"]["kernel_ms_mean"]
+        except Exception as e:  # noqa: BLE001 - report, keep the headline line
+            out["alternative"] = {"error": repr(e)[:300]}
+    if world > 1 and a.config == "B" and not a.no_exchange_run:
+        # evidence for the Namespace-owner all-to-all at N > 1 (SURVEY.md §8e): config D
+        # shards with the partitioned lookups in every step; the headline value stays config B's
+        try:
+            rx.close()
+            xo, rx, _ = measure(a, "D", 1 << 21, "partitioned", max(10, a.steps // 4), max(2, a.warmup // 4),
                                 rank, world, local, dist, torch)
             out["namespace_exchange"] = {k: xo[k] for k in ("value", "unit", "ms_per_step", "steps", "config",
                                                               "exchange")}
@@ -215,6 +232,8 @@ def main():
         out["host_inclusive"] = host_path_rate(rx, w)
     if a.tx_path:
         out["tx_zmq"] = tx_zmq_rate(rx, w, torch)
+    if a.table_updates and rank == 0:
+        out["table_updates"] = table_update_cost(a, rx, w, torch)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(w, a.cpu_seconds)
     if rank == 0:
@@ -243,16 +262,22 @@ def launch_check(a, rank, world, dist, torch):
     return 0
 
 
-def measure(a, cfg, n, exchange, steps, warmup, rank, world, local, dist, torch):
-    """Run `steps` timed batches of workload `cfg` (n frames per rank) -> (JSON dict, rx, w)."""
+def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
+    """Run `steps` timed batches of workload `cfg` (n frames per rank) -> (JSON dict, rx, w).
+    mode: "none" (classify, no collective), "replicated" (every GPU holds every table:
+    classify + route the found records to their Namespace owners + all-to-all), or
+    "partitioned" (each GPU holds its Namespace partition: parse + lookup keys, all-to-all of
+    the lookup records to the owners, lookups at the owner)."""
     import numpy as np
     from emurx import abi
     from emurx.rx import RxPath
     w = workload(cfg, n, rank)
     max_ns = max(4096, len(w["ns"]))
-    max_cl = max(65536, len(w["clients"]["cid"]))
+    max_cl = max(65536, len(w["clients"]["cid"]) + 8192)  # spare ids for --table-updates
     rx = RxPath(local, max_ns=max_ns, max_clients=max_cl, max_frames=n)
     rx.register_all()
+    if mode == "partitioned":
+        rx.set_partition(world, rank)  # device tables: this rank's Namespaces only
     from emurx import synth
     synth.load_tables(w, rx)
 
@@ -269,32 +294,43 @@ def measure(a, cfg, n, exchange, steps, warmup, rank, world, local, dist, torch)
     classify = rx.classify_call(buf, desc, n, rec, qlist, qcap, tile_cnt, hist, stream=stream)
 
     xch = None
-    if exchange:
+    if mode != "none":
         from emurx import exchange as X
-        xch = dict(cap=X.capacity(n, world), ev=[], timing=False, k=0)
+        rb = X.LOOKUP_BYTES if mode == "partitioned" else X.REC_BYTES
+        xch = dict(cap=X.capacity(n, world), ev=[], timing=False, k=0, rb=rb)
 
         def alloc_regions():
-            xch["send"] = torch.empty(world * xch["cap"] * X.REC_BYTES, dtype=torch.uint8, device=dev)
+            xch["send"] = torch.empty(world * xch["cap"] * rb, dtype=torch.uint8, device=dev)
             xch["send_count"] = torch.zeros(world, dtype=torch.int32, device=dev)
+            if mode == "partitioned":
+                xch["out"] = torch.empty(world * xch["cap"] * X.REC_BYTES, dtype=torch.uint8, device=dev)
         alloc_regions()
-        rx.set_route_parts(world)  # the route's counting pass rides in k_rx (emurx_set_route_parts)
 
     def step():
-        classify()
-        if xch is not None:
-            ev = None
-            if xch["timing"] and xch["k"] % a.time_stride == 0:
-                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                ev[0].record(stream)
-            xch["k"] += 1
-            rx.route_dev(rec, n, world, rank, xch["cap"], xch["send"], xch["send_count"], stream=stream)
-            if world > 1:
-                xch["recv"], xch["recv_count"] = X.exchange(xch["send"], xch["send_count"], xch["cap"])
-            else:
-                xch["recv"], xch["recv_count"] = xch["send"], xch["send_count"]
-            if ev is not None:
-                ev[1].record(stream)
-                xch["ev"].append(ev)
+        if xch is None:
+            classify()
+            return
+        ev = None
+        if xch["timing"] and xch["k"] % a.time_stride == 0:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record(stream)
+        xch["k"] += 1
+        if mode == "replicated":
+            # classify + route in one call: the route's owner counts are taken inside k_rx
+            rx.classify_route_dev(buf, desc, n, rec, qlist, qcap, tile_cnt, hist, world, rank, xch["cap"],
+                                  xch["send"], xch["send_count"], stream=stream)
+        else:
+            rx.parse_route_dev(buf, desc, n, rec, qlist, qcap, tile_cnt, hist, world, rank, xch["cap"],
+                               xch["send"], xch["send_count"], stream=stream)
+        if world > 1:
+            xch["recv"], xch["recv_count"] = X.exchange(xch["send"], xch["send_count"], xch["cap"], rec_bytes=rb)
+        else:
+            xch["recv"], xch["recv_count"] = xch["send"], xch["send_count"]
+        if mode == "partitioned":
+            rx.lookup_dev(xch["recv"], xch["recv_count"], world, xch["cap"], xch["out"], stream=stream)
+        if ev is not None:
+            ev[1].record(stream)
+            xch["ev"].append(ev)
 
     for attempt in range(4):
         for _ in range(warmup):
@@ -310,15 +346,16 @@ def measure(a, cfg, n, exchange, steps, warmup, rank, world, local, dist, torch)
     if not a.no_check:
         from emurx.rx import hist_fold, pack_queues
         h = hist_fold(hist.cpu().numpy().view(np.uint64))
-        assert int(h[0::2].sum()) == n * warmup, "histogram does not cover the batches"
+        assert int(h[0::2].sum()) % n == 0, "histogram does not cover the batches"
         _, qoff = pack_queues(qlist.cpu().numpy(), qcap, tile_cnt.cpu().numpy(), n)
         assert int(qoff[-1]) == n, "queues do not cover the batch"
         if xch is not None:
-            xcheck(xch, rec, n, world, rank, dist, torch, dev)
+            xcheck(xch, rec, n, world, rank, dist, torch, dev, mode)
 
     rx.set_timing(steps + 8, a.time_stride)
     if xch is not None:
         xch["timing"] = True
+        xch["ev"] = []
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -343,13 +380,16 @@ def measure(a, cfg, n, exchange, steps, warmup, rank, world, local, dist, torch)
     value = total_frames / el / 1e6
     ms_per_step = el / steps * 1e3
 
-    # roofline of the dominant kernel (k_rx): algorithmic bytes / its mean HIP-event duration
-    alg_bytes = w["nbytes"] + 8 * n + 32 * n + 4 * n
+    # roofline of the dominant kernel (k_rx): algorithmic bytes / its mean HIP-event duration.
+    # Per frame: the frame, its 8-B descriptor, the 32-B record, the 4-B queue entry (+ the
+    # 80-B lookup record in the partitioned mode's k_rx)
+    per_frame = 8 + 32 + 4 + (80 if mode == "partitioned" else 0)
+    alg_bytes = w["nbytes"] + per_frame * n
     parse_s = float(np.mean(pk)) * 1e-3 if len(pk) else float("nan")
     achieved = alg_bytes / parse_s / 1e9
     traffic, pmc_src = None, None
     pmc = ROOT / "profiles" / f"pmc_config{cfg}.json"
-    if pmc.exists():
+    if pmc.exists() and mode in ("none", "replicated"):
         try:
             traffic = json.loads(pmc.read_text()).get("k_rx_hbm_bytes_per_launch")
             pmc_src = str(pmc.relative_to(ROOT))
@@ -359,6 +399,12 @@ def measure(a, cfg, n, exchange, steps, warmup, rank, world, local, dist, torch)
     # buckets, issued together): outside the algorithmic bytes, served by L2 / MALL / HBM
     r = rec.cpu().numpy().view(abi.REC_DTYPE)
     probed = int((r["status"] == 0).sum())
+    ts = rx.table_stats()
+    par = {"none": f"frame shards x{world}, replicated tables, no collective",
+           "replicated": f"frame shards x{world}, replicated tables, classified records to the Namespace "
+                         f"owners (all-to-all, {a.backend})",
+           "partitioned": f"frame shards x{world}, Namespace-partitioned tables, lookup records to the "
+                          f"Namespace owners (all-to-all, {a.backend}), lookups at the owner"}[mode]
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -379,9 +425,9 @@ def measure(a, cfg, n, exchange, steps, warmup, rank, world, local, dist, torch)
                          "E": "E: IMIX 64/594/1518 TCP/UDP, 4K ns / 64K clients"}[cfg],
             "frames_per_gpu": n,
             "frame_bytes_per_gpu": w["nbytes"],
-            "parallelism": (f"frame shards x{world}, replicated tables, Namespace-owner all-to-all "
-                            f"({a.backend})" if exchange else
-                            f"frame shards x{world}, replicated tables, no collective"),
+            "parallelism": par,
+            "tables": mode if mode != "none" else "replicated",
+            "table_bytes_per_gpu": ts["table_bytes"],
         },
         "roofline": {
             "bound": "hbm",
@@ -391,10 +437,10 @@ def measure(a, cfg, n, exchange, steps, warmup, rank, world, local, dist, torch)
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
             "traffic_source": pmc_src,
-            "kernel": "k_rx",
+            "kernel": "k_rx" + (" (parse + lookup keys)" if mode == "partitioned" else ""),
             "alg_bytes_per_launch": alg_bytes,
             "alg_bytes_per_frame": round(alg_bytes / n, 2),
-            "table_probe_bytes_per_launch": probed * 128,
+            "table_probe_bytes_per_launch": probed * 128 if mode != "partitioned" else 0,
             "kernel_ms_mean": round(parse_s * 1e3, 5),
             "kernel_launches_timed": int(len(pk)),
             "kernel_time_source": f"HIP events on the launch stream around every {a.time_stride}-th "
@@ -404,14 +450,89 @@ def measure(a, cfg, n, exchange, steps, warmup, rank, world, local, dist, torch)
     }
     if xch is not None:
         xm = [e0.elapsed_time(e1) for e0, e1 in xch["ev"]]
+        step_ms = float(np.mean(xm)) if xm else float("nan")
         out["exchange"] = {
-            "route_plus_all_to_all_ms_mean": round(float(np.mean(xm)), 5) if xm else None,
+            "mode": mode,
+            "step_device_ms_mean": round(step_ms, 5),
+            "beyond_k_rx_ms_mean": round(step_ms - parse_s * 1e3, 5),
             "steps_timed": len(xm),
             "records_per_region_cap": xch["cap"],
-            "record_bytes": 40,
+            "record_bytes": xch["rb"],
             "collective": f"all_to_all_single x2 ({a.backend})" if world > 1 else "none (1 rank)",
+            "includes": ("k_rx + group scan + pack" + (" + all-to-all" if world > 1 else "") +
+                         (" + owner lookups (k_lookup)" if mode == "partitioned" else "")),
         }
     return out, rx, w
+
+
+def table_update_cost(a, rx, w, torch, rounds=8):
+    """Cost of table mutations between batches (the incremental shipment, include/emu_rx.h
+    emurx_sync): before every batch, K calls of a mix of CNSCtx.UpdateClientIpv4, AddClient and
+    RemoveClient (ns_ctx.go:332-471) on the workload's tables, then one classify_dev.  Device
+    time per batch from CUDA events around the call (the delta copy and k_apply run on the
+    batch's stream ahead of k_rx), host time of the call itself (gathering the edited blocks);
+    the mutation calls are not timed.  Last: the cost of a full rebuild + upload of every
+    table, what any mutation cost before the incremental path."""
+    import numpy as np
+    from emurx import abi
+    n = len(w["desc"])
+    dev = torch.device("cuda", torch.cuda.current_device())
+    buf = torch.from_numpy(w["buf"]).to(dev)
+    desc = torch.from_numpy(w["desc"].view(np.uint8).copy()).to(dev)
+    d_rec = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    qcap = abi.queue_cap(n)
+    qlist = torch.empty(abi.NUM_QUEUES * qcap, dtype=torch.int32, device=dev)
+    tile_cnt = torch.empty(abi.ntiles(n) * 16, dtype=torch.int32, device=dev)
+    hist = torch.zeros(abi.HIST_SHARDS * 2 * abi.HIST_BINS, dtype=torch.int64, device=dev)
+    st = torch.cuda.current_stream(dev)
+    call = rx.classify_call(buf, desc, n, d_rec, qlist, qcap, tile_cnt, hist, stream=st)
+    c = w["clients"]
+    ncl = len(c["cid"])
+    spare = int(rx.cfg.max_clients) - ncl
+    out = {"frames": n, "clients": ncl, "rounds": rounds}
+
+    def one(k, r):
+        # k mutations: a third IPv4 updates, a third AddClient of spare ids, a third RemoveClient
+        # of the spare clients added by the previous round
+        for j in range(k):
+            op, idx = j % 3, j // 3
+            if op == 0:
+                cid = int(c["cid"][(idx * 7919 + r) % ncl])
+                rx.client_update_ipv4(cid, bytes([172, 16 + (r & 7), (idx >> 8) & 0xFF, idx & 0xFF]))
+            elif spare > idx:
+                ns = int(c["ns"][idx % ncl])
+                mac = bytes([6, 0xEE, (idx >> 16) & 0xFF, (idx >> 8) & 0xFF, idx & 0xFF, 1])
+                if op == 1 and r % 2 == 0:
+                    rx.client_add(ns, ncl + idx, mac, None, None, None, 0x7FF)
+                elif op == 2 and r % 2 == 1:
+                    rx.client_remove(ns, mac)
+
+    for k in (0, 1, 64, 4096):
+        dev_ms, host_ms = [], []
+        for r in range(rounds + 2):
+            one(k, r)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            t0 = time.perf_counter()
+            call()
+            t1 = time.perf_counter()
+            e1.record(st)
+            torch.cuda.synchronize()
+            if r >= 2:
+                dev_ms.append(e0.elapsed_time(e1))
+                host_ms.append((t1 - t0) * 1e3)
+        out[f"k{k}"] = {"device_ms_per_batch": round(float(np.median(dev_ms)), 4),
+                        "host_ms_in_call": round(float(np.median(host_ms)), 4)}
+    blocks, whole, nbytes = (rx.table_stats()[x] for x in ("delta_blocks", "whole_tables", "table_bytes"))
+    out["delta_blocks_total"], out["table_bytes"] = blocks, nbytes
+    # a full rebuild + whole upload (set_partition(1, 0) rebuilds every table)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rx.set_partition(1, 0)
+    call()
+    torch.cuda.synchronize()
+    out["full_rebuild_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
+    return out
 
 
 def exchange_overflow(xch, world, dist, torch, dev):
@@ -433,14 +554,17 @@ def grow_cap(xch, world, dist, torch, dev):
     return X.grow(xch["cap"], [int(m.cpu().item())])
 
 
-def xcheck(xch, rec, n, world, rank, dist, torch, dev):
+def xcheck(xch, rec, n, world, rank, dist, torch, dev, mode):
     """Exchange sanity (counts only; the packing is parity-tested in tests/): every routed
-    record arrives once, within capacity."""
+    record arrives once, within capacity (replicated: records with a Namespace; partitioned:
+    every record that reached a callback)."""
     import numpy as np
+    from emurx import abi
     cnt = xch["recv_count"].cpu().numpy().astype(np.int64)
     assert (cnt <= xch["cap"]).all(), f"exchange overflow {cnt} > {xch['cap']}"
-    r = rec.cpu().numpy().view(np.dtype([("ns", "<u4"), ("rest", "V28")]))
-    routed = torch.tensor([int((r["ns"] != 0xFFFFFFFF).sum()), int(cnt.sum())], dtype=torch.int64)
+    r = rec.cpu().numpy().view(abi.REC_DTYPE)
+    sent = (r["ns_id"] != abi.ID_NONE).sum() if mode == "replicated" else (r["status"] == 0).sum()
+    routed = torch.tensor([int(sent), int(cnt.sum())], dtype=torch.int64)
     if world > 1:
         routed = routed.to(dev) if dist.get_backend() == "nccl" else routed
         dist.all_reduce(routed)

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define EMURX_ABI_VERSION 3
+#define EMURX_ABI_VERSION 4
 
 /* ---- return codes -------------------------------------------------------------------- */
 #define EMURX_OK 0
@@ -125,6 +125,9 @@ enum emurx_status {
     EMURX_ST_PANIC_MBUF = 30,        /* ZMQ frame > 9216 B: MbufPoll.Alloc panics, mbuf.go:106 */
     EMURX_NUM_STATUS = 31
 };
+/* status of the record written for an empty descriptor slot (EMURX_DESC_HOLE): no frame, no
+   Namespace (ns_id = client_id = EMURX_ID_NONE), proto EMURX_CB_NONE, not counted */
+#define EMURX_ST_HOLE 0xFFu
 
 /* ---- lookup outcome of the callback's Namespace/Client rule (record.flags bits 4..6) -- */
 enum emurx_lookup {
@@ -213,7 +216,9 @@ typedef struct emurx_counters {
 } emurx_counters;
 
 typedef struct emurx_cfg {
-    int device;            /* HIP device ordinal */
+    int device;            /* HIP device ordinal; < 0: a host-only handle (the table mirror,
+                              generations and image queries, no device: data-path calls
+                              return EMURX_EDEVICE) */
     uint32_t max_ns;       /* ns ids must be < max_ns */
     uint32_t max_clients;  /* client ids must be < max_clients */
     uint32_t max_frames;   /* frames per batch (device scratch is sized for it) */
@@ -305,9 +310,50 @@ int emurx_flow_remove(emurx_t* h, uint32_t client_id, const uint8_t* tuple, uint
 int emurx_server_add(emurx_t* h, uint32_t client_id, uint16_t port, uint8_t proto);
 int emurx_server_remove(emurx_t* h, uint32_t client_id, uint16_t port, uint8_t proto);
 int emurx_client_set_transport(emurx_t* h, uint32_t client_id, int has_ctx);
-/* Upload pending table deltas to the device (enqueued on `stream`, or the handle's own
-   stream when NULL).  Called implicitly by emurx_rx_stream. */
+/* Table edits reach the device incrementally: every call above edits the slots of the
+   device table image it changes (deleted slots become tombstones) and marks the 64-byte
+   blocks it touched.  Before the next launch that reads the tables, the edited blocks are
+   copied to the device and scattered by one kernel on that launch's stream, ordered after
+   every launch on any stream that read the tables since the previous shipment (stream
+   events, no host synchronisation) and before every later reader.  A table that outgrows
+   its load factor is rebuilt larger and shipped whole (then the host waits for the device
+   once).  Streams given to the library must outlive the handle.
+   emurx_sync ships pending edits now, on `stream` (NULL = the handle's stream). */
 int emurx_sync(emurx_t* h, void* stream);
+/* diagnostics: 64-byte blocks shipped as deltas and whole tables uploaded since emurx_open,
+   and the bytes of this handle's device tables (any pointer may be NULL) */
+int emurx_table_stats(const emurx_t* h, uint64_t* delta_blocks, uint64_t* whole_tables, uint64_t* image_bytes);
+
+/* Partitioned tables (multi-GPU, one handle per GPU): with n_parts > 1 this handle's device
+   tables hold only the Namespaces with emurx_ns_owner(key, n_parts) == part and their
+   clients, flows and listeners; the host maps stay complete, so every table call keeps Go's
+   semantics and return codes.  Device memory per handle ~ 1/n_parts of the tables.
+   Rebuilds and ships every table.  (1, 0) = replicated (the default). */
+int emurx_set_partition(emurx_t* h, uint32_t n_parts, uint32_t part);
+
+/* ---- mid-batch table mutations ---------------------------------------
+   A batch is classified against the tables as they stand when it is launched (a snapshot);
+   the Go loop dispatches its records in frame order, and a callback may mutate the maps
+   (DHCP's UpdateClientIpv4 dhcp.go:718, a TCP accept adding a flow) before later frames of
+   the same batch are dispatched, which Go would classify against the mutated maps.
+   emurx_table_gen() is the generation of the tables (it advances on every mutation); read it
+   when launching a batch.  While dispatching, a record whose emurx_recs_stale flag is set
+   may differ from what the live maps give (its Namespace was added, removed or mutated --
+   any of its clients, addresses, plugins, RA prefix, flows -- after that generation): the
+   caller re-probes it in its own maps.  Unflagged records equal the live classification. */
+uint64_t emurx_table_gen(const emurx_t* h);
+int emurx_recs_stale(const emurx_t* h, const emurx_rec* rec, uint32_t n, uint64_t gen, uint8_t* stale);
+
+/* The device tables' answer for a key, computed on the host image by the kernels' bucket walk
+   (tests of the incremental maintenance).  table: 0 ns {vport, vlan0, vlan1} -> ns id,
+   1 mac {ns, mac lo, mac hi} -> client, 2 ipv4 {ns, ip} -> client, 3 ipv6 {ns, ip[4]} -> client,
+   4 client info {client} -> plugin mask, 5 flow4 {client, src, dst, ports, proto} -> flow,
+   6 flow6 {client, src[4], dst[4], ports, nh} -> flow, 7 listener {client, port | proto << 16} -> 1
+   (words little-endian as in the tables).  EMURX_ENOENT when absent. */
+int emurx_image_lookup(emurx_t* h, uint32_t table, const uint32_t* key, uint32_t* value);
+/* Compare the device tables with the host image after a shipment (synchronises the handle's
+   stream): *mismatched = 32-bit words that differ. */
+int emurx_image_check(emurx_t* h, uint64_t* mismatched);
 
 /* ---- data path ---------------------------------------------------------------------- */
 /* Host batch, ZMQ wire format (veth_zmq.go:8-22).  Decodes the stream exactly like
@@ -497,12 +543,43 @@ uint32_t emurx_ns_owner(const uint8_t key[12], uint32_t n_parts);
    d_send_count: [n_parts] (device).  Three kernel launches on `stream`, no host sync. */
 int emurx_route_dev(emurx_t* h, const emurx_rec* d_rec, uint32_t n, uint32_t n_parts, uint32_t my_rank,
                     uint32_t cap, emurx_route_rec* d_send, uint32_t* d_send_count, void* stream);
-/* With n_parts > 0, every later classify launch of this handle (emurx_classify_dev) also
-   counts its records per Namespace owner (the first of emurx_route_dev's three passes), and
-   emurx_route_dev of that same batch (the same d_rec, n and n_parts, stream-ordered after
-   it) skips that pass.  Counts no route consumed are cleared by the next classify launch.
-   0 turns it off.  Results are identical either way. */
-int emurx_set_route_parts(emurx_t* h, uint32_t n_parts);
+/* Classify + route in one call: emurx_classify_dev of the batch (out->rec required) with the
+   route's per-owner counts taken inside the k_rx launch, then the group scan and the packing
+   of emurx_route_dev into d_send / d_send_count.  Equal to the two calls in sequence.  One
+   route at a time per handle (the route scratch is the handle's). */
+int emurx_classify_route_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_desc, uint32_t n,
+                             const emurx_dev_out* out, uint32_t n_parts, uint32_t my_rank, uint32_t cap,
+                             emurx_route_rec* d_send, uint32_t* d_send_count, void* stream);
+
+/* ---- owner-partitioned classification ---------------------------------
+   With partitioned tables (emurx_set_partition) the lookups run on the GPU that owns the
+   frame's Namespace.  The receiving GPU parses its shard and derives each frame's lookup key
+   (emurx_parse_route_dev); every frame that reached a callback travels, as an 80-byte
+   emurx_lookup_rec, to the owner of its CTunnelKey (an equal-split all-to-all, as for
+   emurx_route_rec); the owner resolves Namespace, Client and flow against its partition
+   (emurx_lookup_dev).  The owner's output for a frame equals emurx_classify_dev's record for
+   it on replicated tables, bit for bit (frames whose Namespace is unknown come back with
+   ns_id EMURX_ID_NONE and lookup EMURX_LK_NO_NS instead of staying on the receiving GPU). */
+typedef struct emurx_lookup_rec {
+    emurx_rec rec;     /* the parsed record, with ns_id = source frame index and
+                          client_id = source rank (the lookups fill them at the owner)    */
+    uint32_t key[12];  /* the callback rule's key: destination MAC, client key (MAC / IPv4 /
+                          IPv6 / EUI-64 / chaddr / first client), or for tcp/udp the
+                          c5tuplekey + TCP flags of the flow decision (emurx_parse.h)     */
+} emurx_lookup_rec;    /* 80 bytes */
+/* Parse the batch (records without lookups into out->rec when non-NULL, queues, histogram as
+   emurx_parse_dev) and pack the lookup record of every frame that reached a callback into
+   the region of its Namespace's owner: d_send[d * cap ..  + d_send_count[d]), frame order.
+   Reads no table.  Counts > cap: overflow as in emurx_route_dev. */
+int emurx_parse_route_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_desc, uint32_t n,
+                          const emurx_dev_out* out, uint32_t n_parts, uint32_t my_rank, uint32_t cap,
+                          emurx_lookup_rec* d_send, uint32_t* d_send_count, void* stream);
+/* The owner's half: d_recv holds n_parts regions of cap lookup records (the all-to-all's
+   receive buffer), d_recv_count[s] of them valid in region s.  Writes d_out[s * cap + j] (the
+   classified record + source index / rank, emurx_route_rec) and d_flow (optional, the
+   transport flow decision) for every valid slot.  One launch, no host synchronisation. */
+int emurx_lookup_dev(emurx_t* h, const emurx_lookup_rec* d_recv, const uint32_t* d_recv_count,
+                     uint32_t n_parts, uint32_t cap, emurx_route_rec* d_out, uint32_t* d_flow, void* stream);
 
 #ifdef __cplusplus
 }

@@ -31,7 +31,7 @@ def test_exports_every_declared_symbol(lib):
 
 
 def test_abi_version(lib):
-    assert lib.emurx_abi_version() == 3
+    assert lib.emurx_abi_version() == 4
 
 
 def test_layouts():

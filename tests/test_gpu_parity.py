@@ -392,51 +392,100 @@ def _classify_to(rx, w, rec, n):
     torch.cuda.synchronize()
 
 
+def _dev_out(n):
+    import torch
+    from emurx import abi as A
+    qcap = A.queue_cap(n)
+    return dict(rec=torch.zeros(max(n, 1) * 32, dtype=torch.uint8, device="cuda"),
+                qlist=torch.empty(A.NUM_QUEUES * qcap, dtype=torch.int32, device="cuda"), qcap=qcap,
+                tile_cnt=torch.empty(max(A.ntiles(n), 1) * 16, dtype=torch.int32, device="cuda"),
+                hist=torch.zeros(A.HIST_SHARDS * 2 * A.HIST_BINS, dtype=torch.int64, device="cuda"))
+
+
 @pytest.mark.parametrize("n_parts,my_rank", [(1, 0), (2, 1), (8, 3)])
-def test_route_fused_counts(rxmod, n_parts, my_rank):
-    """emurx_set_route_parts: the owners counted inside k_rx give the same send regions; a
-    batch classified but never routed, a route of other records and a route with another
-    n_parts all fall back to the counting pass correctly."""
+def test_classify_route_dev(rxmod, n_parts, my_rank):
+    """emurx_classify_route_dev (the owner counts taken inside k_rx) gives the oracle's
+    records and the send regions of the host restatement, the same as classify_dev followed
+    by route_dev; back-to-back batches of different sizes reuse the route scratch."""
     import torch
     import route_ref
     from emurx import exchange as X
-    n = 30000 + 5
-    wa = synth.config_c(n, rank=my_rank)
-    wb = synth.config_c(n, rank=my_rank + 10)
     rx, o = new_pair(rxmod)
-    synth.load_tables(wa, rx)
-    synth.load_tables(wa, o)
-    rx.set_route_parts(n_parts)
-    orec_b, _, _, _ = o.rx_batch(wb["buf"], wb["desc"])
-    orec_a, _, _, _ = o.rx_batch(wa["buf"], wa["desc"])
-    def route(rec, parts):
-        cap = X.capacity(n, parts)
-        send = torch.full((parts * cap * X.REC_BYTES,), 0xEE, dtype=torch.uint8, device="cuda")
-        cnt = torch.full((parts,), -1, dtype=torch.int32, device="cuda")
-        rx.route_dev(rec, n, parts, my_rank % parts, cap, send, cnt)
+    for n, seed in ((30000 + 5, 0), (777, 1), (30000 + 5, 2)):
+        w = synth.config_c(n, rank=my_rank + 10 * seed)
+        if seed == 0:
+            synth.load_tables(w, rx)
+            synth.load_tables(w, o)
+        orec, _, _, _ = o.rx_batch(w["buf"], w["desc"])
+        buf = torch.from_numpy(w["buf"]).cuda()
+        desc = torch.from_numpy(w["desc"].view(np.uint8).copy()).cuda()
+        cap = X.capacity(n, n_parts)
+        d = _dev_out(n)
+        send = torch.full((n_parts * cap * X.REC_BYTES,), 0xEE, dtype=torch.uint8, device="cuda")
+        cnt = torch.full((n_parts,), -1, dtype=torch.int32, device="cuda")
+        rx.classify_route_dev(buf, desc, n, d["rec"], d["qlist"], d["qcap"], d["tile_cnt"], d["hist"], n_parts,
+                              my_rank, cap, send, cnt)
+        torch.cuda.synchronize()
+        assert d["rec"].cpu().numpy()[: n * 32].view(abi.REC_DTYPE).tobytes() == orec.tobytes()
+        want = route_ref.route(orec, n_parts, my_rank)
+        c = cnt.cpu().numpy()
+        assert list(c) == [len(x) for x in want]
+        sreg = send.cpu().numpy().view(abi.ROUTE_REC_DTYPE).reshape(n_parts, cap)
+        for k in range(n_parts):
+            assert sreg[k, : c[k]].tobytes() == want[k].tobytes(), k
+
+
+def _hole_rec():
+    h = np.zeros(1, abi.REC_DTYPE)
+    h["ns_id"] = h["client_id"] = abi.ID_NONE
+    h["proto"], h["status"] = abi.CB_NONE, abi.ST_HOLE
+    return h[0]
+
+
+def test_holes_records_and_route(rxmod):
+    """Empty descriptor slots (EMURX_DESC_HOLE) get a hole record (no Namespace, status
+    EMURX_ST_HOLE), no queue entry and no count; the route, standalone and fused, skips them."""
+    import torch
+    import route_ref
+    from emurx import exchange as X
+    n = 20000
+    w = synth.config_c(n)
+    rx, o = new_pair(rxmod)
+    synth.load_tables(w, rx)
+    synth.load_tables(w, o)
+    rng = np.random.default_rng(44)
+    holes = np.sort(rng.choice(n, n // 20, replace=False))
+    keep = np.setdiff1d(np.arange(n), holes)
+    desc = w["desc"].copy()
+    desc["pad"][holes] = abi.DESC_HOLE
+    orec, oq, oqoff, ocnt = o.rx_batch(w["buf"], w["desc"][keep])
+    want = np.zeros(n, abi.REC_DTYPE)
+    want[keep] = orec
+    want[holes] = _hole_rec()
+    rec, qlist, qoff, hist = run_dev(rx, w["buf"], desc)
+    assert rec.tobytes() == want.tobytes(), rec_diff(rec, want)
+    assert np.array_equal(qlist, keep[oq].astype(np.uint32)) and np.array_equal(qoff, oqoff)
+    assert int(hist[0::2].sum()) == len(keep)
+    buf = torch.from_numpy(w["buf"]).cuda()
+    ddesc = torch.from_numpy(desc.view(np.uint8).copy()).cuda()
+    drec = torch.from_numpy(want.view(np.uint8).copy()).cuda()
+    wroute = route_ref.route(want, 4, 1)
+    for fused in (False, True):
+        cap = X.capacity(n, 4)
+        send = torch.full((4 * cap * X.REC_BYTES,), 0xEE, dtype=torch.uint8, device="cuda")
+        cnt = torch.full((4,), -1, dtype=torch.int32, device="cuda")
+        if fused:
+            d = _dev_out(n)
+            rx.classify_route_dev(buf, ddesc, n, d["rec"], d["qlist"], d["qcap"], d["tile_cnt"], d["hist"], 4, 1, cap,
+                                  send, cnt)
+        else:
+            rx.route_dev(drec, n, 4, 1, cap, send, cnt)
         torch.cuda.synchronize()
         c = cnt.cpu().numpy()
-        return c, send.cpu().numpy().view(abi.ROUTE_REC_DTYPE).reshape(parts, cap)
-
-    def check(got, orec, parts):
-        c, sreg = got
-        want = route_ref.route(orec, parts, my_rank % parts)
-        assert list(c) == [len(x) for x in want]
-        for d in range(parts):
-            assert sreg[d, : c[d]].tobytes() == want[d].tobytes(), d
-
-    rec = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
-    _classify_to(rx, wb, rec, n)  # counted, never routed
-    _classify_to(rx, wa, rec, n)  # clears b's counts first
-    assert rec.cpu().numpy().view(abi.REC_DTYPE).tobytes() == orec_a.tobytes()
-    check(route(rec, n_parts), orec_a, n_parts)  # fused counts
-    check(route(rec, n_parts), orec_a, n_parts)  # nothing pending: counting pass
-    other = torch.from_numpy(orec_b.view(np.uint8).copy()).cuda()
-    _classify_to(rx, wa, rec, n)
-    check(route(other, n_parts), orec_b, n_parts)  # other records: counting pass
-    _classify_to(rx, wa, rec, n)
-    check(route(rec, 2 if n_parts != 2 else 3), orec_a, 2 if n_parts != 2 else 3)  # other n_parts
-    rx.set_route_parts(0)
+        assert list(c) == [len(x) for x in wroute], fused
+        sreg = send.cpu().numpy().view(abi.ROUTE_REC_DTYPE).reshape(4, cap)
+        for k in range(4):
+            assert sreg[k, : c[k]].tobytes() == wroute[k].tobytes(), (fused, k)
 
 
 def test_route_dev_overflow(rxmod):

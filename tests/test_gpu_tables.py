@@ -1,0 +1,256 @@
+"""GPU: incremental table shipment, cross-stream ordering, and the owner-partitioned
+classification, all bit-exact against the oracle.
+
+* Mutations between batches reach the device as edited 64-byte blocks (no whole-table
+  upload): every batch equals the oracle with the same mutations applied, and the device
+  tables equal the host image (emurx_image_check).
+* A batch in flight on one stream keeps the tables it was launched against while the next
+  mutations ship on another stream (no half-old, half-new tables).
+* Partitioned: G handles, each holding one Namespace partition; every shard is parsed and
+  its lookup records packed per owner (emurx_parse_route_dev), the all-to-all is played on
+  the device, and each owner resolves its records (emurx_lookup_dev).  The owners' output
+  equals the oracle's records of every frame that reached a callback, grouped by owner, and
+  the records with a Namespace equal the replicated path's routed records byte for byte;
+  the transport flow decisions equal the oracle's.
+"""
+import numpy as np
+import pytest
+
+from emurx import abi, synth
+from emurx import frames as F
+from gpu_util import frame_tuples, rec_diff, run_dev
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rxmod(gpu_ok, oracle_built):
+    from emurx.rx import RxPath
+    return RxPath
+
+
+def _check(rx, o, w):
+    import pyoracle
+    rec, qlist, qoff, hist = run_dev(rx, w["buf"], w["desc"])
+    orec, oq, oqoff, ocnt = o.rx_batch(w["buf"], w["desc"])
+    assert rec.tobytes() == orec.tobytes(), rec_diff(rec, orec)
+    assert np.array_equal(qlist, oq) and np.array_equal(qoff, oqoff)
+    from emurx.rx import hist_to_counters
+    got, want = hist_to_counters(hist), pyoracle.counters_dict(ocnt)
+    assert all(got[k] == want[k] for k in abi.PARSER_COUNTER_NAMES)
+    return rec
+
+
+def test_incremental_deltas(rxmod):
+    """Rounds of 1 / 64 / 4096 mixed mutations (UpdateClientIpv4 / Ipv6 / DIpv6, AddClient,
+    RemoveClient, plugin masks, RA prefixes, AddNs / RemoveNs) between batches; each batch
+    bit-exact, the device tables equal to the image, and only deltas shipped."""
+    import pyoracle
+    n = 1 << 16
+    w = synth.config_c(n, seed=0xDE17A)
+    rx = rxmod(0, max_ns=4096 + 256, max_clients=65536 + 8192, max_frames=n)
+    o = pyoracle.Oracle()
+    rx.register_all()
+    for t in (rx, o):
+        synth.load_tables(w, t)
+    _check(rx, o, w)
+    base = rx.table_stats()
+    c = w["clients"]
+    rng = np.random.default_rng(17)
+    spare = list(range(65536, 65536 + 8192))
+    added = []
+    for k in (1, 64, 4096, 64, 1):
+        for j in range(k):
+            op = int(rng.integers(0, 8))
+            i = int(rng.integers(0, len(c["cid"])))
+            cid, ns = int(c["cid"][i]), int(c["ns"][i])
+            if op == 0:
+                ip = bytes([172, 16, int(rng.integers(0, 256)), int(rng.integers(1, 255))])
+                assert rx.client_update_ipv4(cid, ip) == o.client_update_ipv4(cid, ip)
+            elif op == 1:
+                ip = bytes([0x20, 1, 0xd, 0xb8, 9, 9] + [0] * 8 + [int(rng.integers(0, 256)), 1])
+                assert rx.client_update_ipv6(cid, ip) == o.client_update_ipv6(cid, ip)
+            elif op == 2:
+                ip = bytes([0xfe, 0x80] + [0] * 8 + list(rng.integers(0, 256, 6, dtype=np.uint8)))
+                assert rx.client_update_dipv6(cid, ip) == o.client_update_dipv6(cid, ip)
+            elif op == 3 and spare:
+                nc = spare.pop()
+                mac = bytes([6, 1, nc >> 16 & 255, nc >> 8 & 255, nc & 255, 7])
+                ip4 = bytes([11, nc >> 16 & 255, nc >> 8 & 255, nc & 255])
+                assert rx.client_add(ns, nc, mac, ip4, None, None, 0x7FF) == o.client_add(ns, nc, mac, ip4, None, None, 0x7FF)
+                added.append((ns, mac, nc))
+            elif op == 4 and added:
+                ns2, mac, nc = added.pop(int(rng.integers(0, len(added))))
+                assert rx.client_remove(ns2, mac) == o.client_remove(ns2, mac) == 0
+                spare.append(nc)
+            elif op == 5:
+                p = int(rng.integers(0, 1 << 11))
+                assert rx.client_set_plugins(cid, p) == o.client_set_plugins(cid, p)
+            elif op == 6:
+                pre = bytes([0x20, 1, 0xd, 0xb8, 0, 0, 0, 0]) + bytes(8)
+                assert rx.client_set_ra(cid, pre, 64) == o.client_set_ra(cid, pre, 64)
+            else:
+                key = F.tunnel_key(int(rng.integers(0, 4)), 0x81000000 | int(rng.integers(4090, 4095)), 0)
+                nsid = 4096 + int(rng.integers(0, 256))
+                r1, r2 = rx.ns_add(key, nsid, 0x7FF), o.ns_add(key, nsid, 0x7FF)
+                assert r1 == r2
+                if r1 != 0:
+                    assert rx.ns_remove(key) == o.ns_remove(key)
+        _check(rx, o, w)
+        assert rx.image_check() == 0
+    st = rx.table_stats()
+    assert st["delta_blocks"] > base["delta_blocks"] + 1000
+    assert st["whole_tables"] == base["whole_tables"]  # nothing outgrew its table
+
+
+def test_mutation_while_batch_in_flight(rxmod):
+    """An ingest batch runs on its slot stream while the tables change and the next batch is
+    classified on another stream: the in-flight batch sees the old tables, the new one the
+    new tables (the shipment waits for the in-flight reader by an event)."""
+    import pyoracle
+    n = 1 << 17
+    w = synth.config_c(n)
+    rx = rxmod(0, max_ns=4096, max_clients=65536, max_frames=n)
+    rx.register_all()
+    o_old, o_new = pyoracle.Oracle(), pyoracle.Oracle()
+    for t in (rx, o_old, o_new):
+        synth.load_tables(w, t)
+    fr = [w["buf"][d["off"]:d["off"] + d["len"]].tobytes() for d in w["desc"]]
+    vp = [int(v) for v in w["desc"]["vport"]]
+    msgs = [F.zmq_pack(fr[i:i + 64], vp[i:i + 64]) for i in range(0, n, 64)]
+    total = sum(len(m) for m in msgs)
+    buf = rx.ingest_buffer(0, total)
+    tab = np.zeros(len(msgs), abi.MSG_DTYPE)
+    at = 0
+    for i, m in enumerate(msgs):
+        buf[at:at + len(m)] = np.frombuffer(m, np.uint8)
+        tab[i] = (at, len(m))
+        at += len(m)
+    rx.ingest_submit(0, tab)
+    # mutate every client's IPv4 and half the MACs' plugins while the batch is in flight
+    c = w["clients"]
+    for i in range(0, len(c["cid"]), 2):
+        cid = int(c["cid"][i])
+        ip = bytes([172, 20, cid >> 8 & 255, cid & 255])
+        assert rx.client_update_ipv4(cid, ip) == o_new.client_update_ipv4(cid, ip) == 0
+        assert rx.client_set_plugins(cid, 0x0FF) == o_new.client_set_plugins(cid, 0x0FF) == 0
+    rec_new = _check(rx, o_new, w)  # its own stream: the shipment orders after the ingest
+    res = rx.ingest_wait(0)
+    orec_old, _, _, _ = o_old.rx_batch(w["buf"], w["desc"])
+    assert res["rec"].tobytes() == orec_old.tobytes(), rec_diff(res["rec"], orec_old)
+    assert rec_new.tobytes() != orec_old.tobytes()
+
+
+def _owners_by_key(rec, parts):
+    """Owner of every record that reached a callback (its CTunnelKey), 0xFF elsewhere."""
+    from emurx.rx import ns_owner
+    out = np.full(len(rec), 0xFF, np.uint32)
+    ok = np.nonzero(rec["status"] == 0)[0]
+    k = np.stack([rec["vport"][ok].astype(np.uint64), rec["vlan0"][ok].astype(np.uint64),
+                  rec["vlan1"][ok].astype(np.uint64)], 1)
+    if len(ok):
+        uk, inv = np.unique(k, axis=0, return_inverse=True)
+        own = np.array([ns_owner(F.tunnel_key(int(a), int(b), int(c)), parts) for a, b, c in uk], np.uint32)
+        out[ok] = own[inv.reshape(-1)]
+    return out
+
+
+@pytest.mark.parametrize("parts", [2, 4])
+def test_partitioned_lookups_equal_replicated(rxmod, parts):
+    import pyoracle
+    import torch
+    import route_ref
+    from emurx import exchange as X
+    n = 40000
+    shards = [synth.config_c(n, rank=s, syn=0.3) for s in range(parts)]
+    w0 = shards[0]
+    o = pyoracle.Oracle()
+    synth.load_tables(w0, o)
+    full = rxmod(0, max_ns=4096, max_clients=65536, max_frames=n)
+    full.register_all()
+    synth.load_tables(w0, full)
+    owners = []
+    for p in range(parts):
+        h = rxmod(0, max_ns=4096, max_clients=65536, max_frames=n)
+        h.register_all()
+        h.set_partition(parts, p)
+        synth.load_tables(w0, h)
+        owners.append(h)
+    # transport state on every handle and the oracle: flows of shard 0's frames, listeners
+    orecs = [o.rx_batch(w["buf"], w["desc"])[0] for w in shards]
+    tup = frame_tuples(shards[0]["buf"], shards[0]["desc"], orecs[0])
+    rng = np.random.default_rng(0xAB)
+    idx = [i for i, t in enumerate(tup) if t is not None]
+    for i in rng.choice(idx, len(idx) // 3, replace=False):
+        cid = int(orecs[0][i]["client_id"])
+        rcs = {t.flow_add(cid, tup[i], int(i)) for t in [o, full] + owners}
+        assert len(rcs) == 1
+    for i in rng.choice(idx, len(idx) // 5, replace=False):
+        cid, t = int(orecs[0][i]["client_id"]), tup[i]
+        dport = (t[10] << 8 | t[11]) if len(t) == 13 else (t[34] << 8 | t[35])
+        proto = 6 if orecs[0][i]["proto"] == abi.CB_TCP else 17
+        rcs = {x.server_add(cid, dport, proto) for x in [o, full] + owners}
+        assert len(rcs) == 1
+    orecs = [o.rx_batch(w["buf"], w["desc"])[0] for w in shards]
+    ts_full = full.table_stats()["table_bytes"]
+    assert max(h.table_stats()["table_bytes"] for h in owners) < 1.25 * ts_full / parts + (1 << 16)
+
+    cap = X.capacity(n, parts)
+    send, cnt, rep_send, rep_cnt = [], [], [], []
+    from gpu_util import to_dev
+    for s, w in enumerate(shards):
+        buf, desc = to_dev(w["buf"]), to_dev(w["desc"])
+        qcap = abi.queue_cap(n)
+        mk = lambda: (torch.zeros(n * 32, dtype=torch.uint8, device="cuda"),  # noqa: E731
+                      torch.empty(abi.NUM_QUEUES * qcap, dtype=torch.int32, device="cuda"),
+                      torch.empty(abi.ntiles(n) * 16, dtype=torch.int32, device="cuda"),
+                      torch.zeros(abi.HIST_SHARDS * 2 * abi.HIST_BINS, dtype=torch.int64, device="cuda"))
+        rec, ql, tc, hi = mk()
+        sd = torch.full((parts * cap * X.LOOKUP_BYTES,), 0xEE, dtype=torch.uint8, device="cuda")
+        sc = torch.full((parts,), -1, dtype=torch.int32, device="cuda")
+        owners[s].parse_route_dev(buf, desc, n, rec, ql, qcap, tc, hi, parts, s, cap, sd, sc)
+        rrec, rql, rtc, rhi = mk()
+        rsd = torch.full((parts * cap * X.REC_BYTES,), 0xEE, dtype=torch.uint8, device="cuda")
+        rsc = torch.full((parts,), -1, dtype=torch.int32, device="cuda")
+        full.classify_route_dev(buf, desc, n, rrec, rql, qcap, rtc, rhi, parts, s, cap, rsd, rsc)
+        torch.cuda.synchronize()
+        # the source's parse-only records equal the oracle's parse (no lookups)
+        pr = rec.cpu().numpy().view(abi.REC_DTYPE)
+        assert (pr["ns_id"] == abi.ID_NONE).all()
+        assert np.array_equal(pr["status"], orecs[s]["status"]) and np.array_equal(pr["l4"], orecs[s]["l4"])
+        send.append(sd)
+        cnt.append(sc.cpu().numpy())
+        rep_send.append(rsd)
+        rep_cnt.append(rsc.cpu().numpy())
+    for p in range(parts):
+        # the all-to-all, played on the device: region s of owner p's receive buffer = region p of s
+        recv = torch.empty(parts * cap * X.LOOKUP_BYTES, dtype=torch.uint8, device="cuda")
+        rc = torch.tensor([int(cnt[s][p]) for s in range(parts)], dtype=torch.int32, device="cuda")
+        for s in range(parts):
+            recv[s * cap * X.LOOKUP_BYTES:(s + 1) * cap * X.LOOKUP_BYTES] = \
+                send[s][p * cap * X.LOOKUP_BYTES:(p + 1) * cap * X.LOOKUP_BYTES]
+        out = torch.full((parts * cap * X.REC_BYTES,), 0xEE, dtype=torch.uint8, device="cuda")
+        flow = torch.full((parts * cap,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+        owners[p].lookup_dev(recv, rc, parts, cap, out, flow)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().view(abi.ROUTE_REC_DTYPE).reshape(parts, cap)
+        fl = flow.cpu().numpy().view(np.uint32).reshape(parts, cap)
+        rep = [rep_send[s].cpu().numpy().view(abi.ROUTE_REC_DTYPE).reshape(parts, cap)[p, : rep_cnt[s][p]]
+               for s in range(parts)]
+        for s in range(parts):
+            own = _owners_by_key(orecs[s], parts)
+            sel = np.nonzero(own == p)[0]
+            assert cnt[s][p] == len(sel)
+            want = np.zeros(len(sel), abi.ROUTE_REC_DTYPE)
+            want["rec"], want["src_index"], want["src_rank"] = orecs[s][sel], sel, s
+            g = got[s, : len(sel)]
+            assert g.tobytes() == want.tobytes(), rec_diff(g["rec"], want["rec"])
+            # the records with a Namespace = the replicated path's routed records
+            hasns = g[g["rec"]["ns_id"] != abi.ID_NONE]
+            assert hasns.tobytes() == rep[s].tobytes()
+            assert hasns.tobytes() == route_ref.route(orecs[s], parts, s)[p].tobytes()
+            wf = o.flows(shards[s]["buf"], shards[s]["desc"][sel], orecs[s][sel])
+            assert np.array_equal(fl[s, : len(sel)], wf), (s, p)
+    # the flow decisions were exercised
+    allf = o.flows(shards[0]["buf"], shards[0]["desc"], orecs[0])
+    assert (allf <= abi.FLOW_ID_MAX).sum() > 1000 and (allf == abi.FLOW_NEW).sum() > 100

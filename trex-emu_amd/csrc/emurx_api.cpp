@@ -1,8 +1,10 @@
 // emurx_api.cpp — C-ABI of the MI355X receive path (include/emu_rx.h).
 //
-// Owns the Namespace / Client tables (host copies with the Go maps' semantics, flattened
-// into the device layout of emurx_tables.h on emurx_sync), the device scratch of a batch,
-// and the host batch entry point that replaces VethIFZmq.OnRxStream's per-frame loop
+// Owns the Namespace / Client tables (emurx_mirror.*: the Go maps plus the image of every
+// device table, edited slot by slot), ships the edited 64-byte blocks to the device before
+// the next batch that reads them (one H2D copy + one k_apply launch, stream-ordered against
+// every stream that read the tables, no host synchronisation), the device scratch of a batch,
+// and the host batch entry points that replace VethIFZmq.OnRxStream's per-frame loop
 // (src/emu/core/veth_zmq.go:277-320).  No exception or abort crosses the ABI.
 #include <hip/hip_runtime.h>
 
@@ -13,66 +15,24 @@
 #include <cstring>
 #include <new>
 #include <string>
-#include <unordered_map>
 #include <vector>
 
 #include "../../include/emu_rx.h"
 #include "emurx_kernels.h"
+#include "emurx_mirror.h"
 #include "emurx_tables.h"
+
+using emurx_host::Blocks;
+using emurx_host::Hash;
+using emurx_host::Mirror;
 
 namespace {
 
-uint32_t pow2_at_least(uint64_t v) {
-    uint64_t p = 16;
-    while (p < v) p <<= 1;
-    return (uint32_t)p;
-}
-uint32_t le32(const uint8_t* p) { return p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24); }
 uint16_t be16(const uint8_t* p) { return (uint16_t)((p[0] << 8) | p[1]); }
 uint32_t be32(const uint8_t* p) {
     return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
 }
-bool zero(const uint8_t* p, int n) {
-    for (int i = 0; i < n; ++i)
-        if (p[i]) return false;
-    return true;
-}
-
-// table keys: (ns_id, address words) — the per-Namespace Go maps flattened into one
-struct K5 {
-    uint32_t w[5];
-    bool operator==(const K5& o) const { return !memcmp(w, o.w, sizeof(w)); }
-};
-struct K5Hash {
-    size_t operator()(const K5& k) const { return emurx_hash(k.w[0], k.w[1], k.w[2], k.w[3], k.w[4]); }
-};
-using Map = std::unordered_map<K5, uint32_t, K5Hash>;
-
-K5 key_ns(const uint8_t* k12) { return K5{{le32(k12), le32(k12 + 4), le32(k12 + 8), 0, 0}}; }
-K5 key_mac(uint32_t ns, const uint8_t* m) {
-    return K5{{ns, le32(m), (uint32_t)(m[4] | (m[5] << 8)), 0, 0}};
-}
-K5 key_ip4(uint32_t ns, const uint8_t* ip) { return K5{{ns, le32(ip), 0, 0, 0}}; }
-K5 key_ip6(uint32_t ns, const uint8_t* ip) {
-    return K5{{ns, le32(ip), le32(ip + 4), le32(ip + 8), le32(ip + 12)}};
-}
-
-struct NsInfo {
-    bool alive = false;
-    uint8_t key[12] = {0};
-    uint32_t plugins = 0;
-    std::vector<uint32_t> order;  // clientHead dlist (insertion order)
-};
-struct ClientInfo {
-    bool alive = false;
-    uint32_t ns = 0;
-    uint8_t mac[6] = {0}, ipv4[4] = {0}, ipv6[16] = {0}, dhcpv6[16] = {0};
-    uint32_t plugins = 0;
-    bool has_ra = false;
-    uint8_t ra_prefix[16] = {0};
-    uint8_t ra_plen = 0;
-    bool has_ctx = false;  // CClient.GetTransportCtx() != nil
-};
+uint32_t le32(const uint8_t* p) { return p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24); }
 
 template <class T>
 struct DevBuf {
@@ -148,31 +108,39 @@ struct IngestSlot {
     }
 };
 
+// one staging slot of the table-delta ring: pinned entries -> device entries -> k_apply
+struct DeltaSlot {
+    PinBuf<emurx_delta> h;
+    DevBuf<emurx_delta> d;
+    hipEvent_t ev = nullptr;  // recorded after the k_apply that read d
+    bool used = false;
+};
+constexpr int kDeltaRing = 4;
+constexpr size_t kMaxReaders = 16;
+
 }  // namespace
 
 struct emurx_ctx {
     emurx_cfg cfg{};
+    bool host_only = false;  // cfg.device < 0: the table mirror alone, no HIP calls
     hipStream_t stream = nullptr;
     uint32_t cb_mask = 0;  // Parser.Init: every callback parserNotSupported (eapol nil)
 
-    // authoritative tables (Go map semantics)
-    Map ns_map, mac_map, ip4_map, ip6_map;
-    std::vector<NsInfo> ns;
-    std::vector<ClientInfo> cl;
-    bool dirty = true;
+    Mirror m;  // Go maps + device table images (emurx_mirror.h)
 
-    // transport tables: (client id, tuple bytes) -> flow id; listeners (client id, port | proto << 16)
-    std::unordered_map<std::string, uint32_t> ft_map;
-    std::unordered_map<uint64_t, uint32_t> srv_map;
-    uint32_t ft4_buckets = 1, ft6_buckets = 1, srv_buckets = 1;
-    DevBuf<uint32_t> d_ft4, d_ft6, d_srv;
-    std::vector<uint32_t> h_ft4, h_ft6, h_srv;
-    bool ft_on = false;
-
-    // device tables
-    uint32_t ns_buckets = 0, mac_buckets = 0, ip4_buckets = 0, ip6_buckets = 0;
-    DevBuf<uint32_t> d_ns, d_nsinfo, d_mac, d_ip4, d_ip6, d_client;
-    std::vector<uint32_t> h_ns, h_nsinfo, h_mac, h_ip4, h_ip6, h_client;
+    // device tables: the 8 hash images (emurx_host::kTab*) and the dense ns info
+    DevBuf<uint32_t> d_tab[emurx_host::kNumTabs];
+    DevBuf<uint32_t> d_nsinfo;
+    // table shipment: delta ring, the streams that read the tables since the last shipment,
+    // and which shipment every stream has waited for
+    DeltaSlot ring[kDeltaRing];
+    uint32_t ring_i = 0;
+    hipEvent_t ship_ev = nullptr;
+    uint64_t ship_gen = 0;
+    std::vector<hipStream_t> readers;
+    std::vector<hipEvent_t> reader_ev;
+    std::vector<std::pair<hipStream_t, uint64_t>> waited;
+    uint64_t shipped_blocks = 0, shipped_whole = 0;  // counters (emurx_table_stats)
 
     // batched host ingest: EMURX_INGEST_SLOTS public slots + one private to emurx_rx_stream
     IngestSlot ing[EMURX_INGEST_SLOTS + 1];
@@ -180,14 +148,10 @@ struct emurx_ctx {
     // tx ZMQ framing scratch (emurx_tx_zmq_dev): per-level chain transfer tables
     DevBuf<uint8_t> d_txz;
 
-    // route count pass fused into classify launches (emurx_set_route_parts): the counts of
-    // the last such launch wait in d_route_cnt / d_route_grp for emurx_route_dev
-    uint32_t route_parts = 0, route_n = 0;
-    const emurx_rec* route_rec = nullptr;
-    bool route_pending = false;
-
-    // Namespace-partition packing scratch (emurx_route_dev)
+    // Namespace-partition packing scratch (emurx_route_dev / emurx_classify_route_dev /
+    // emurx_parse_route_dev; one route at a time per handle, stream-ordered)
     DevBuf<uint32_t> d_route_cnt, d_route_grp, d_route_goff;  // grp: zero between batches
+    DevBuf<emurx_lookup_rec> d_lk;  // emurx_parse_route_dev: lookup records in frame order
 
     // k_rx staging slab per launch (emurx_launch_batch): the narrow 6 KiB slab runs 6
     // workgroups per CU instead of 5, but a wave whose frames span 6-7 KiB then takes the
@@ -211,27 +175,28 @@ struct emurx_ctx {
     uint32_t slots = 0, ev_head = 0, ev_count = 0, stride = 1, batch_seq = 0;
 
     emurx_dev_tables tables() const {
+        using namespace emurx_host;
         emurx_dev_tables T{};
-        T.ns_tab = d_ns.p;
+        T.ns_tab = d_tab[kTabNs].p;
         T.ns_info = d_nsinfo.p;
-        T.mac_tab = d_mac.p;
-        T.ip4_tab = d_ip4.p;
-        T.ip6_tab = d_ip6.p;
-        T.client = d_client.p;
-        T.ns_mask = ns_buckets - 1;
-        T.mac_mask = mac_buckets - 1;
-        T.ip4_mask = ip4_buckets - 1;
-        T.ip6_mask = ip6_buckets - 1;
+        T.mac_tab = d_tab[kTabMac].p;
+        T.ip4_tab = d_tab[kTabIp4].p;
+        T.ip6_tab = d_tab[kTabIp6].p;
+        T.ci_tab = d_tab[kTabCi].p;
+        T.ns_mask = m.ns_t.mask();
+        T.mac_mask = m.mac_t.mask();
+        T.ip4_mask = m.ip4_t.mask();
+        T.ip6_mask = m.ip6_t.mask();
+        T.ci_mask = m.ci_t.mask();
         T.max_ns = cfg.max_ns;
-        T.max_clients = cfg.max_clients;
         T.cb_mask = cb_mask;
-        T.ft_on = ft_on ? 1u : 0u;
-        T.ft4_tab = d_ft4.p;
-        T.ft6_tab = d_ft6.p;
-        T.srv_tab = d_srv.p;
-        T.ft4_mask = ft4_buckets - 1;
-        T.ft6_mask = ft6_buckets - 1;
-        T.srv_mask = srv_buckets - 1;
+        T.ft_on = m.n_ctx ? 1u : 0u;
+        T.ft4_tab = d_tab[kTabFt4].p;
+        T.ft6_tab = d_tab[kTabFt6].p;
+        T.srv_tab = d_tab[kTabSrv].p;
+        T.ft4_mask = m.ft4_t.mask();
+        T.ft6_mask = m.ft6_t.mask();
+        T.srv_mask = m.srv_t.mask();
         return T;
     }
 };
@@ -241,146 +206,115 @@ namespace {
 // every entry point re-binds the handle's device (goroutines migrate between OS threads);
 // hipGetDevice is a thread-local read, hipSetDevice only when the thread is elsewhere
 int bind(emurx_t* h) {
+    if (h->host_only) return EMURX_EDEVICE;
     int cur = -1;
     if (hipGetDevice(&cur) == hipSuccess && cur == h->cfg.device) return EMURX_OK;
     return hipSetDevice(h->cfg.device) == hipSuccess ? EMURX_OK : EMURX_EDEVICE;
 }
 
-// open-addressing insert into a bucketed table (emurx_tables.h): first free slot of the
-// first bucket, in linear bucket order from the home bucket, that has one
-void bucket_put(std::vector<uint32_t>& t, uint32_t bmask, uint32_t words, uint32_t h, const uint32_t* e) {
-    const uint32_t per = EMURX_BUCKET_WORDS / words;
-    for (uint32_t b = h & bmask;; b = (b + 1) & bmask)
-        for (uint32_t k = 0; k < per; ++k) {
-            uint32_t* slot = &t[(size_t)b * EMURX_BUCKET_WORDS + k * words];
-            if (slot[words - 1] == EMURX_EMPTY) {
-                memcpy(slot, e, words * sizeof(uint32_t));
-                return;
-            }
-        }
-}
-void empty_table(std::vector<uint32_t>& t, uint32_t buckets, uint32_t words) {
-    t.assign((size_t)buckets * EMURX_BUCKET_WORDS, 0);
-    for (size_t i = words - 1; i < t.size(); i += words) t[i] = EMURX_EMPTY;
+uint64_t& waited_gen(emurx_t* h, hipStream_t s) {
+    for (auto& w : h->waited)
+        if (w.first == s) return w.second;
+    h->waited.emplace_back(s, 0);
+    return h->waited.back().second;
 }
 
-// transport tables, sized to their entries (load <= 1/2 in slots), device buffers grown on demand
-int build_transport(emurx_t* h) {
-    size_t n4 = 0, n6 = 0;
-    for (auto& kv : h->ft_map) (kv.first.size() == 4 + 13 ? n4 : n6)++;
-    h->ft4_buckets = pow2_at_least(2 * n4 + 2) / 2;
-    h->ft6_buckets = pow2_at_least(2 * n6 + 1);
-    h->srv_buckets = pow2_at_least(2 * h->srv_map.size() + 4) / 4;
-    empty_table(h->h_ft4, h->ft4_buckets, 8);
-    empty_table(h->h_ft6, h->ft6_buckets, 16);
-    empty_table(h->h_srv, h->srv_buckets, 4);
-    for (auto& kv : h->ft_map) {
-        const uint8_t* k = reinterpret_cast<const uint8_t*>(kv.first.data());
-        const uint32_t cid = le32(k);
-        const uint8_t* t = k + 4;
-        if (kv.first.size() == 4 + 13) {
-            uint32_t e[8] = {cid, le32(t), le32(t + 4), le32(t + 8), t[12], 0, 0, kv.second};
-            bucket_put(h->h_ft4, h->ft4_buckets - 1, 8, emurx_ft4_hash(cid, e[1], e[2], e[3], e[4]), e);
-        } else {
-            uint32_t e[16] = {cid};
-            for (int j = 0; j < 4; ++j) {
-                e[1 + j] = le32(t + 4 * j);
-                e[5 + j] = le32(t + 16 + 4 * j);
-            }
-            e[9] = le32(t + 32);
-            e[10] = t[36];
-            e[15] = kv.second;
-            bucket_put(h->h_ft6, h->ft6_buckets - 1, 16, emurx_ft6_hash(cid, e[1], e[2], e[3], e[4], e[5], e[6], e[7], e[8], e[9], e[10]), e);
+// Ship the edited table blocks on `st`: after every stream that read the tables since the
+// last shipment (an event recorded on it now, waited on by st), before every later reader
+// (ship_ev, waited on by each reader stream once).  Edited blocks travel as emurx_delta
+// entries through a ring of pinned + device staging buffers (one H2D copy + one k_apply).
+// Whole images (first upload, a rebuilt or grown table, or a quarter of a table edited)
+// are copied synchronously; growing a device table waits for the device first, since
+// batches in flight may still read the old buffer.
+int ship_tables(emurx_t* h, hipStream_t st) {
+    using namespace emurx_host;
+    Mirror& m = h->m;
+    for (size_t k = 0; k < h->readers.size(); ++k) {
+        const hipStream_t r = h->readers[k];
+        if (r == st) continue;
+        if (k >= h->reader_ev.size()) {
+            hipEvent_t e;
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return EMURX_EDEVICE;
+            h->reader_ev.push_back(e);
         }
-    }
-    for (auto& kv : h->srv_map) {
-        uint32_t e[4] = {(uint32_t)(kv.first >> 32), (uint32_t)kv.first, 0, 1};
-        bucket_put(h->h_srv, h->srv_buckets - 1, 4, emurx_srv_hash(e[0], e[1]), e);
-    }
-    h->ft_on = false;
-    for (auto& c : h->cl) h->ft_on = h->ft_on || (c.alive && c.has_ctx);
-    if (h->d_ft4.alloc(h->h_ft4.size()) || h->d_ft6.alloc(h->h_ft6.size()) || h->d_srv.alloc(h->h_srv.size()))
-        return -1;
-    return 0;
-}
-
-int rebuild_and_upload(emurx_t* h, hipStream_t st) {
-    if (!h->dirty) return EMURX_OK;
-    (void)hipStreamSynchronize(st);  // previous upload may still read the staging vectors
-    empty_table(h->h_ns, h->ns_buckets, 4);
-    for (auto& kv : h->ns_map) {
-        // a key with non-zero bytes [2:4] can never equal a parsed CTunnelKey (Set writes 0
-        // there, thread_ctx.go:93): it has no device slot.  The free upper half of the vport
-        // word carries the Namespace's plugin mask, so one probe answers GetNs + PluginCtx.Get.
-        if (kv.first.w[0] >> 16) continue;
-        uint32_t e[4] = {kv.first.w[0] | (h->ns[kv.second].plugins << 16), kv.first.w[1], kv.first.w[2],
-                         kv.second};
-        bucket_put(h->h_ns, h->ns_buckets - 1, 4, emurx_tk_hash(kv.first.w[0], e[1], e[2]), e);
-    }
-    h->h_nsinfo.assign((size_t)h->cfg.max_ns * 4, 0);
-    for (uint32_t i = 0; i < h->ns.size(); ++i) {
-        const NsInfo& n = h->ns[i];
-        h->h_nsinfo[i * 4 + 0] = n.alive ? n.plugins : 0;
-        h->h_nsinfo[i * 4 + 1] = (n.alive && !n.order.empty()) ? n.order.front() : EMURX_ID_NONE;
-    }
-    // client entries hash from their Namespace's tunnel key (emurx_tables.h)
-    auto tk_of = [&](uint32_t ns) {
-        const uint8_t* k = h->ns[ns].key;
-        return emurx_tk_hash(le32(k), le32(k + 4), le32(k + 8));
-    };
-    // the client's MAC and plugin mask ride in the MAC slot's free upper half and in the IPv4 /
-    // IPv6 slots' spare words: the rules that check them (PluginCtx.Get, IsUnicastToMe) need
-    // no second read of the client record
-    auto mac_words = [&](uint32_t cid, uint32_t& lo, uint32_t& hip) {
-        const ClientInfo& c = h->cl[cid];
-        lo = le32(c.mac);
-        hip = (uint32_t)(c.mac[4] | (c.mac[5] << 8)) | ((c.plugins & 0xffffu) << 16);
-    };
-    empty_table(h->h_mac, h->mac_buckets, 4);
-    for (auto& kv : h->mac_map) {
-        uint32_t e[4] = {kv.first.w[0], kv.first.w[1], kv.first.w[2], kv.second};
-        const uint32_t hh = emurx_mac_hash(tk_of(e[0]), e[1], e[2]);
-        e[2] |= (h->cl[kv.second].plugins & 0xffffu) << 16;
-        bucket_put(h->h_mac, h->mac_buckets - 1, 4, hh, e);
-    }
-    empty_table(h->h_ip4, h->ip4_buckets, 8);
-    for (auto& kv : h->ip4_map) {
-        uint32_t e[8] = {kv.first.w[0], kv.first.w[1], 0, 0, 0, 0, 0, kv.second};
-        mac_words(kv.second, e[2], e[3]);
-        bucket_put(h->h_ip4, h->ip4_buckets - 1, 8, emurx_ip4_hash(tk_of(e[0]), e[1]), e);
-    }
-    empty_table(h->h_ip6, h->ip6_buckets, 8);
-    for (auto& kv : h->ip6_map) {
-        const uint32_t* w = kv.first.w;
-        uint32_t e[8] = {w[0], w[1], w[2], w[3], w[4], 0, 0, kv.second};
-        mac_words(kv.second, e[5], e[6]);
-        bucket_put(h->h_ip6, h->ip6_buckets - 1, 8, emurx_ip6_hash(tk_of(w[0]), w[1], w[2], w[3], w[4]), e);
-    }
-    h->h_client.assign((size_t)h->cfg.max_clients * 8, 0);
-    for (uint32_t i = 0; i < h->cl.size(); ++i) {
-        const ClientInfo& c = h->cl[i];
-        if (!c.alive) continue;
-        uint32_t* o = &h->h_client[(size_t)i * 8];
-        o[0] = le32(c.mac);
-        o[1] = (uint32_t)(c.mac[4] | (c.mac[5] << 8));
-        o[2] = c.plugins;
-        o[3] = (c.has_ra ? 1u : 0u) | ((uint32_t)c.ra_plen << 8);
-        o[4] = le32(c.ra_prefix);
-        o[5] = le32(c.ra_prefix + 4);
-        o[6] = c.has_ctx ? 1u : 0u;
-    }
-    if (build_transport(h)) return EMURX_ENOMEM;
-    struct {
-        uint32_t* d;
-        std::vector<uint32_t>* h;
-    } up[] = {{h->d_ns.p, &h->h_ns},   {h->d_nsinfo.p, &h->h_nsinfo}, {h->d_mac.p, &h->h_mac},
-              {h->d_ip4.p, &h->h_ip4}, {h->d_ip6.p, &h->h_ip6},       {h->d_client.p, &h->h_client},
-              {h->d_ft4.p, &h->h_ft4}, {h->d_ft6.p, &h->h_ft6},       {h->d_srv.p, &h->h_srv}};
-    for (auto& u : up)
-        if (hipMemcpyAsync(u.d, u.h->data(), u.h->size() * 4, hipMemcpyHostToDevice, st) != hipSuccess)
+        if (hipEventRecord(h->reader_ev[k], r) != hipSuccess || hipStreamWaitEvent(st, h->reader_ev[k], 0) != hipSuccess)
             return EMURX_EDEVICE;
-    if (hipStreamSynchronize(st) != hipSuccess) return EMURX_EDEVICE;
-    h->dirty = false;
+    }
+    Blocks* img[kNumTabs + 1];
+    DevBuf<uint32_t>* dev[kNumTabs + 1];
+    for (int k = 0; k < kNumTabs; ++k) {
+        img[k] = m.hashes(k);
+        dev[k] = &h->d_tab[k];
+    }
+    img[kNumTabs] = &m.nsinfo;
+    dev[kNumTabs] = &h->d_nsinfo;
+    bool whole = false, grow = false;
+    size_t nd = 0;
+    for (int k = 0; k <= kNumTabs; ++k) {
+        if (!img[k]->all && img[k]->dirty.size() * 4 > img[k]->nblocks()) img[k]->all = true;
+        whole = whole || img[k]->all;
+        grow = grow || (img[k]->all && img[k]->img.size() > dev[k]->n);
+        if (!img[k]->all) nd += img[k]->dirty.size();
+    }
+    if (grow && hipDeviceSynchronize() != hipSuccess) return EMURX_EDEVICE;
+    if (whole) {
+        if (hipStreamSynchronize(st) != hipSuccess) return EMURX_EDEVICE;
+        for (int k = 0; k <= kNumTabs; ++k) {
+            if (!img[k]->all) continue;
+            if (dev[k]->alloc(img[k]->img.size())) return EMURX_ENOMEM;
+            if (hipMemcpy(dev[k]->p, img[k]->img.data(), img[k]->img.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+                return EMURX_EDEVICE;
+            h->shipped_whole++;
+        }
+    }
+    if (nd) {
+        DeltaSlot& s = h->ring[h->ring_i++ % kDeltaRing];
+        if (s.used && hipEventSynchronize(s.ev) != hipSuccess) return EMURX_EDEVICE;
+        if (s.h.alloc(nd) || s.d.alloc(nd)) return EMURX_ENOMEM;
+        size_t j = 0;
+        for (int k = 0; k <= kNumTabs; ++k) {
+            if (img[k]->all) continue;
+            for (uint32_t b : img[k]->dirty) {
+                emurx_delta& e = s.h.p[j++];
+                e.dst = (uint64_t)(uintptr_t)(dev[k]->p + (size_t)b * EMURX_BUCKET_WORDS);
+                e.pad = 0;
+                memcpy(e.w, &img[k]->img[(size_t)b * EMURX_BUCKET_WORDS], sizeof(e.w));
+            }
+        }
+        if (hipMemcpyAsync(s.d.p, s.h.p, nd * sizeof(emurx_delta), hipMemcpyHostToDevice, st) != hipSuccess ||
+            emurx_launch_apply(s.d.p, (uint32_t)nd, st) || hipEventRecord(s.ev, st) != hipSuccess)
+            return EMURX_EDEVICE;
+        s.used = true;
+        h->shipped_blocks += nd;
+    }
+    m.clean_all();
+    if (hipEventRecord(h->ship_ev, st) != hipSuccess) return EMURX_EDEVICE;
+    waited_gen(h, st) = ++h->ship_gen;
+    h->readers.clear();
+    return EMURX_OK;
+}
+
+// Before a launch on `st` that reads the tables: ship pending edits, or wait for the last
+// shipment if this stream has not yet; remember st as a reader for the next shipment.
+int prepare_read(emurx_t* h, hipStream_t st) {
+    int rc;
+    if (h->m.pending()) {
+        if ((rc = ship_tables(h, st))) return rc;
+    } else {
+        uint64_t& w = waited_gen(h, st);
+        if (w < h->ship_gen) {
+            if (hipStreamWaitEvent(st, h->ship_ev, 0) != hipSuccess) return EMURX_EDEVICE;
+            w = h->ship_gen;
+        }
+    }
+    if (std::find(h->readers.begin(), h->readers.end(), st) == h->readers.end()) {
+        if (h->readers.size() >= kMaxReaders) {  // many distinct streams: drain them all once
+            if (hipDeviceSynchronize() != hipSuccess) return EMURX_EDEVICE;
+            h->readers.clear();
+        }
+        h->readers.push_back(st);
+    }
+    if (h->waited.size() > 4 * kMaxReaders) h->waited.clear();  // forgotten streams wait again: harmless
     return EMURX_OK;
 }
 
@@ -433,16 +367,25 @@ bool choose_stage(emurx_t* h) {
     return narrow;
 }
 
-int run_dev(emurx_t* h, const uint8_t* frames, const emurx_desc* desc, uint32_t n,
-            const emurx_dev_out* out, void* stream, bool classify) {
-    if (!h || !out || !out->hist || (n && (!frames || !desc))) return EMURX_EINVAL;
-    if (((uintptr_t)frames & 15) || ((uintptr_t)desc & 7)) return EMURX_EINVAL;  // 16-B staging loads
-    if (n > h->cfg.max_frames) return EMURX_ENOMEM;
-    if (out->qlist && out->qcap < queue_cap(n)) return EMURX_EINVAL;
-    int rc = bind(h);
-    if (rc) return rc;
-    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
-    if (classify && (rc = rebuild_and_upload(h, st))) return rc;
+// route scratch for batches of up to max_frames: per-tile counts, per-group sums (kept zero
+// between routes) and group offsets
+int route_scratch(emurx_t* h, uint32_t n) {
+    const size_t gw = 1024 * 16, tiles = std::max<size_t>(ntiles(std::max(n, h->cfg.max_frames)), 1);
+    if (tiles > 1024u * 64u) return EMURX_EINVAL;  // 16M frames per batch
+    if (!h->d_route_grp.p) {
+        if (h->d_route_grp.alloc(gw) || hipMemset(h->d_route_grp.p, 0, gw * sizeof(uint32_t)) != hipSuccess)
+            return EMURX_ENOMEM;
+    }
+    if (h->d_route_cnt.alloc(tiles * 16) || h->d_route_goff.alloc(gw)) return EMURX_ENOMEM;
+    return EMURX_OK;
+}
+
+// one k_rx launch; kind: 0 parse only, 1 classify, 2 parse + lookup keys (partitioned source);
+// rt: the route count pass fused in (emurx_classify_route_dev / emurx_parse_route_dev)
+int run_dev(emurx_t* h, const uint8_t* frames, const emurx_desc* desc, uint32_t n, const emurx_dev_out* out,
+            hipStream_t st, int kind, const emurx_route_counts* rt, emurx_lookup_rec* keys) {
+    int rc;
+    if (kind == 1 && (rc = prepare_read(h, st))) return rc;
     emurx_dev_tables T = h->tables();
     const hipEvent_t* ev = nullptr;
     if (h->slots && (h->batch_seq++ % h->stride) == 0) {
@@ -452,20 +395,19 @@ int run_dev(emurx_t* h, const uint8_t* frames, const emurx_desc* desc, uint32_t 
         h->ev_count = std::min(h->ev_count + 1, h->slots);
     }
     const bool narrow = choose_stage(h);
-    emurx_route_counts rt{h->route_parts, h->d_route_cnt.p, h->d_route_grp.p};
-    const bool fuse = classify && h->route_parts && out->rec && n;
-    if (fuse && h->route_pending &&  // counts nobody routed: clear them
-        hipMemsetAsync(h->d_route_grp.p, 0, 1024 * 16 * sizeof(uint32_t), st) != hipSuccess)
-        return EMURX_EDEVICE;
-    int r = emurx_launch_batch(frames, desc, n, T, classify, *out, st, ev, narrow, h->d_stage_fb.p, h->stage_gen,
-                               fuse ? &rt : nullptr);
-    if (fuse) {
-        h->route_pending = true;
-        h->route_rec = out->rec;
-        h->route_n = n;
-    }
+    int r = emurx_launch_batch(frames, desc, n, T, kind, *out, st, ev, narrow, h->d_stage_fb.p, h->stage_gen, rt,
+                               keys);
     if (!r) r = stage_copy_back(h, st);
     return r ? EMURX_EDEVICE : EMURX_OK;
+}
+
+int check_batch_args(emurx_t* h, const uint8_t* frames, const emurx_desc* desc, uint32_t n,
+                     const emurx_dev_out* out) {
+    if (!h || !out || !out->hist || (n && (!frames || !desc))) return EMURX_EINVAL;
+    if (((uintptr_t)frames & 15) || ((uintptr_t)desc & 7)) return EMURX_EINVAL;  // 16-B staging loads
+    if (n > h->cfg.max_frames) return EMURX_ENOMEM;
+    if (out->qlist && out->qcap < queue_cap(n)) return EMURX_EINVAL;
+    return bind(h);
 }
 
 // ---- batched ZMQ ingest (emurx_ingest_*; emurx_rx_stream uses the private last slot) ----
@@ -517,12 +459,8 @@ int ingest_submit(emurx_t* h, uint32_t slot, const emurx_msg* msgs, uint32_t nms
         s.h_rec.alloc(n) || s.h_desc.alloc(n) || s.h_qlist.alloc(n) || s.h_qoff.alloc(16) ||
         s.h_hist.alloc(2 * EMURX_HIST_BINS) || s.h_mframes.alloc(nmsg) || s.h_mstatus.alloc(nmsg))
         return EMURX_ENOMEM;
-    if (h->dirty) {  // batches in flight read the device tables: let them finish first
-        for (auto& o : h->ing)
-            if (o.st) (void)hipStreamSynchronize(o.st);
-        if ((rc = rebuild_and_upload(h, h->stream))) return rc;
-    }
     hipStream_t st = s.st;
+    if ((rc = prepare_read(h, st))) return rc;  // table deltas ordered against every reader
     const auto H2D = hipMemcpyHostToDevice, D2H = hipMemcpyDeviceToHost;
     bool ok = true;
     if (fresh_hist) ok = ok && hipMemsetAsync(s.d_hist.p, 0, hw * sizeof(uint64_t), st) == hipSuccess;
@@ -635,49 +573,64 @@ int emurx_open(const emurx_cfg* cfg, emurx_t** out) {
     if (!h) return EMURX_ENOMEM;
     h->cfg = *cfg;
     if (h->cfg.max_bytes == 0) h->cfg.max_bytes = 1u << 20;
+    h->host_only = cfg->device < 0;
+    try {
+        h->m.open(cfg->max_ns, cfg->max_clients);
+    } catch (...) {
+        delete h;
+        return EMURX_ENOMEM;
+    }
+    if (h->host_only) {
+        *out = h;
+        return EMURX_OK;
+    }
     int rc = bind(h);
     if (rc) { delete h; return rc; }
     if (hipStreamCreate(&h->stream) != hipSuccess) { delete h; return EMURX_EDEVICE; }
-    // load factor <= 1/2 in slots: 4 slots (IPv6: 2) per 64-byte bucket
-    h->ns_buckets = pow2_at_least(2ull * cfg->max_ns) / 4;
-    h->mac_buckets = pow2_at_least(2ull * cfg->max_clients) / 4;
-    h->ip4_buckets = pow2_at_least(2ull * cfg->max_clients) / 2;  // one address per client, 2 slots per bucket
-    h->ip6_buckets = pow2_at_least(4ull * cfg->max_clients) / 2;
-    h->ns.resize(cfg->max_ns);
-    h->cl.resize(cfg->max_clients);
-    const size_t BW = EMURX_BUCKET_WORDS;
-    if (h->d_ns.alloc(h->ns_buckets * BW) || h->d_nsinfo.alloc((size_t)cfg->max_ns * 4) ||
-        h->d_mac.alloc(h->mac_buckets * BW) || h->d_ip4.alloc(h->ip4_buckets * BW) ||
-        h->d_ip6.alloc(h->ip6_buckets * BW) || h->d_client.alloc((size_t)cfg->max_clients * 8)) {
-        emurx_close(h);
-        return EMURX_ENOMEM;
-    }
     if (const char* e = getenv("EMURX_STAGE")) h->stage_mode = !strcmp(e, "wide") ? 1 : !strcmp(e, "narrow") ? 2 : 0;
     if (h->stage_fb.alloc(256) || h->d_stage_fb.alloc(256) ||
         hipEventCreateWithFlags(&h->stage_ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ship_ev, hipEventDisableTiming) != hipSuccess ||
         hipMemset(h->d_stage_fb.p, 0, 256 * sizeof(uint32_t)) != hipSuccess) {
         emurx_close(h);
         return EMURX_ENOMEM;
     }
+    for (auto& s : h->ring)
+        if (hipEventCreateWithFlags(&s.ev, hipEventDisableTiming) != hipSuccess) {
+            emurx_close(h);
+            return EMURX_EDEVICE;
+        }
     memset(h->stage_fb.p, 0, 256 * sizeof(uint32_t));
-    h->dirty = true;
-    if ((rc = rebuild_and_upload(h, h->stream))) { emurx_close(h); return rc; }
+    if ((rc = ship_tables(h, h->stream)) || (rc = route_scratch(h, cfg->max_frames)) == EMURX_ENOMEM) {
+        emurx_close(h);
+        return rc ? rc : EMURX_ENOMEM;
+    }
     *out = h;
     return EMURX_OK;
 }
 
 void emurx_close(emurx_t* h) {
     if (!h) return;
+    if (h->host_only) {
+        delete h;
+        return;
+    }
     bind(h);
-    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    (void)hipDeviceSynchronize();
     for (auto& s : h->ing) s.release();
     h->stage_fb.release();
     h->d_stage_fb.release();
     if (h->stage_ev) (void)hipEventDestroy(h->stage_ev);
-    h->d_ns.release(); h->d_nsinfo.release(); h->d_mac.release(); h->d_ip4.release();
-    h->d_ip6.release(); h->d_client.release();
-    h->d_ft4.release(); h->d_ft6.release(); h->d_srv.release();
-    h->d_route_cnt.release(); h->d_route_grp.release(); h->d_route_goff.release();
+    if (h->ship_ev) (void)hipEventDestroy(h->ship_ev);
+    for (auto& s : h->ring) {
+        s.h.release();
+        s.d.release();
+        if (s.ev) (void)hipEventDestroy(s.ev);
+    }
+    for (auto e : h->reader_ev) (void)hipEventDestroy(e);
+    for (auto& t : h->d_tab) t.release();
+    h->d_nsinfo.release();
+    h->d_route_cnt.release(); h->d_route_grp.release(); h->d_route_goff.release(); h->d_lk.release();
     h->d_txz.release();
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
@@ -707,231 +660,132 @@ int emurx_set_callbacks_mask(emurx_t* h, uint32_t mask) {
 }
 uint32_t emurx_get_callbacks_mask(const emurx_t* h) { return h ? h->cb_mask : 0; }
 
-// ---- tables ------------------------------------------------------------------------------
-// CThreadCtx.AddNs thread_ctx.go:786-795
+// ---- tables (emurx_mirror.cpp: Go map semantics + device image edits) ----------------------
+// CThreadCtx.AddNs / RemoveNs thread_ctx.go:786-812
 int emurx_ns_add(emurx_t* h, const uint8_t key[12], uint32_t ns_id, uint32_t plugin_mask) {
     if (!h || !key) return EMURX_EINVAL;
-    if (ns_id >= h->cfg.max_ns) return EMURX_ENOMEM;
-    K5 k = key_ns(key);
-    if (h->ns_map.count(k) || h->ns[ns_id].alive) return EMURX_EEXIST;
-    NsInfo& n = h->ns[ns_id];
-    n.alive = true;
-    memcpy(n.key, key, 12);
-    n.plugins = plugin_mask;
-    n.order.clear();
-    h->ns_map[k] = ns_id;
-    h->dirty = true;
-    return EMURX_OK;
+    return h->m.ns_add(key, ns_id, plugin_mask);
 }
-// CThreadCtx.RemoveNs thread_ctx.go:797-812 (refused while clients are active)
 int emurx_ns_remove(emurx_t* h, const uint8_t key[12]) {
     if (!h || !key) return EMURX_EINVAL;
-    auto it = h->ns_map.find(key_ns(key));
-    if (it == h->ns_map.end()) return EMURX_ENOENT;
-    NsInfo& n = h->ns[it->second];
-    if (!n.order.empty()) return EMURX_EEXIST;
-    n.alive = false;
-    h->ns_map.erase(it);
-    h->dirty = true;
-    return EMURX_OK;
+    return h->m.ns_remove(key);
 }
 int emurx_ns_set_plugins(emurx_t* h, uint32_t ns_id, uint32_t plugin_mask) {
     if (!h) return EMURX_EINVAL;
-    if (ns_id >= h->cfg.max_ns || !h->ns[ns_id].alive) return EMURX_ENOENT;
-    h->ns[ns_id].plugins = plugin_mask;
-    h->dirty = true;
-    return EMURX_OK;
+    return h->m.ns_set_plugins(ns_id, plugin_mask);
 }
-
 // CNSCtx.AddClient ns_ctx.go:332-389
-int emurx_client_add(emurx_t* h, uint32_t ns_id, uint32_t cid, const uint8_t mac[6],
-                     const uint8_t ipv4[4], const uint8_t ipv6[16], const uint8_t dhcpv6[16],
-                     uint32_t plugin_mask) {
-    static const uint8_t z[16] = {0};
+int emurx_client_add(emurx_t* h, uint32_t ns_id, uint32_t cid, const uint8_t mac[6], const uint8_t ipv4[4],
+                     const uint8_t ipv6[16], const uint8_t dhcpv6[16], uint32_t plugin_mask) {
     if (!h || !mac) return EMURX_EINVAL;
-    if (ns_id >= h->cfg.max_ns || !h->ns[ns_id].alive) return EMURX_ENOENT;
-    if (cid >= h->cfg.max_clients) return EMURX_ENOMEM;
-    if (!ipv4) ipv4 = z;
-    if (!ipv6) ipv6 = z;
-    if (!dhcpv6) dhcpv6 = z;
-    if (zero(mac, 6)) return EMURX_EINVAL;
-    if (h->mac_map.count(key_mac(ns_id, mac))) return EMURX_EEXIST;
-    bool has4 = !zero(ipv4, 4), has6 = !zero(ipv6, 16), has6d = !zero(dhcpv6, 16);
-    if (has4 && h->ip4_map.count(key_ip4(ns_id, ipv4))) return EMURX_EEXIST;
-    if (has6 && h->ip6_map.count(key_ip6(ns_id, ipv6))) return EMURX_EEXIST;
-    if (has6d && h->ip6_map.count(key_ip6(ns_id, dhcpv6))) return EMURX_EEXIST;
-    if (h->cl[cid].alive) return EMURX_EEXIST;
-    ClientInfo& c = h->cl[cid];
-    c = ClientInfo();
-    c.alive = true;
-    c.ns = ns_id;
-    c.plugins = plugin_mask;
-    memcpy(c.mac, mac, 6);
-    memcpy(c.ipv4, ipv4, 4);
-    memcpy(c.ipv6, ipv6, 16);
-    memcpy(c.dhcpv6, dhcpv6, 16);
-    h->mac_map[key_mac(ns_id, mac)] = cid;
-    if (has4) h->ip4_map[key_ip4(ns_id, ipv4)] = cid;
-    if (has6) h->ip6_map[key_ip6(ns_id, ipv6)] = cid;
-    if (has6d) h->ip6_map[key_ip6(ns_id, dhcpv6)] = cid;
-    h->ns[ns_id].order.push_back(cid);
-    h->dirty = true;
-    return EMURX_OK;
+    return h->m.client_add(ns_id, cid, mac, ipv4, ipv6, dhcpv6, plugin_mask);
 }
-
+// ctx_client_add rpc_base_cmds.go:350-406: the listed clients in order, stop at the first error
 int emurx_clients_add(emurx_t* h, const emurx_client_spec* c, uint32_t n, uint32_t* n_added) {
     if (!h || (n && !c)) return EMURX_EINVAL;
     uint32_t k = 0;
     int rc = EMURX_OK;
     for (; k < n; ++k)
-        if ((rc = emurx_client_add(h, c[k].ns_id, c[k].client_id, c[k].mac, c[k].ipv4, c[k].ipv6, c[k].dhcpv6,
-                                   c[k].plugin_mask)))
+        if ((rc = h->m.client_add(c[k].ns_id, c[k].client_id, c[k].mac, c[k].ipv4, c[k].ipv6, c[k].dhcpv6,
+                                  c[k].plugin_mask)))
             break;
     if (n_added) *n_added = k;
     return rc;
 }
-
-static void drop_transport(emurx_t* h, uint32_t cid) {
-    for (auto it = h->ft_map.begin(); it != h->ft_map.end();)
-        it = le32(reinterpret_cast<const uint8_t*>(it->first.data())) == cid ? h->ft_map.erase(it) : std::next(it);
-    for (auto it = h->srv_map.begin(); it != h->srv_map.end();)
-        it = (uint32_t)(it->first >> 32) == cid ? h->srv_map.erase(it) : std::next(it);
-    h->cl[cid].has_ctx = false;
-}
-
-// CNSCtx.RemoveClient ns_ctx.go:392-440 (map entries are deleted by key)
+// CNSCtx.RemoveClient ns_ctx.go:392-440
 int emurx_client_remove(emurx_t* h, uint32_t ns_id, const uint8_t mac[6]) {
     if (!h || !mac) return EMURX_EINVAL;
-    if (ns_id >= h->cfg.max_ns || !h->ns[ns_id].alive) return EMURX_ENOENT;
-    if (zero(mac, 6)) return EMURX_EINVAL;
-    auto it = h->mac_map.find(key_mac(ns_id, mac));
-    if (it == h->mac_map.end()) return EMURX_ENOENT;
-    uint32_t cid = it->second;
-    ClientInfo& c = h->cl[cid];
-    h->mac_map.erase(it);
-    auto& ord = h->ns[ns_id].order;
-    ord.erase(std::remove(ord.begin(), ord.end(), cid), ord.end());
-    if (!zero(c.ipv4, 4)) h->ip4_map.erase(key_ip4(ns_id, c.ipv4));
-    if (!zero(c.ipv6, 16)) h->ip6_map.erase(key_ip6(ns_id, c.ipv6));
-    if (!zero(c.dhcpv6, 16)) h->ip6_map.erase(key_ip6(ns_id, c.dhcpv6));
-    drop_transport(h, cid);  // TransportCtx.onRemove: its sockets go with the client
-    c.alive = false;
-    h->dirty = true;
-    return EMURX_OK;
+    return h->m.client_remove(ns_id, mac);
 }
-
 int emurx_client_set_plugins(emurx_t* h, uint32_t cid, uint32_t plugin_mask) {
     if (!h) return EMURX_EINVAL;
-    if (cid >= h->cfg.max_clients || !h->cl[cid].alive) return EMURX_ENOENT;
-    h->cl[cid].plugins = plugin_mask;
-    h->dirty = true;
-    return EMURX_OK;
+    return h->m.client_set_plugins(cid, plugin_mask);
 }
-
 // CNSCtx.UpdateClientIpv4 / Ipv6 / DIpv6 ns_ctx.go:442-533
-static int update_addr(emurx_t* h, uint32_t cid, int which, const uint8_t* nw) {
-    if (!h || !nw) return EMURX_EINVAL;
-    if (cid >= h->cfg.max_clients || !h->cl[cid].alive) return EMURX_ENOENT;
-    ClientInfo& c = h->cl[cid];
-    const int n = which == 4 ? 4 : 16;
-    uint8_t* cur = which == 4 ? c.ipv4 : (which == 6 ? c.ipv6 : c.dhcpv6);
-    Map& m = which == 4 ? h->ip4_map : h->ip6_map;
-    auto key = [&](const uint8_t* a) { return which == 4 ? key_ip4(c.ns, a) : key_ip6(c.ns, a); };
-    if (!memcmp(cur, nw, n)) return EMURX_OK;
-    h->dirty = true;
-    if (!zero(cur, n)) {
-        auto it = m.find(key(cur));
-        if (it == m.end()) { memset(cur, 0, n); return EMURX_ENOENT; }
-        m.erase(it);
-    }
-    if (!zero(nw, n)) {
-        if (m.count(key(nw))) { memset(cur, 0, n); return EMURX_EEXIST; }
-        m[key(nw)] = cid;
-    }
-    memcpy(cur, nw, n);
-    return EMURX_OK;
+int emurx_client_update_ipv4(emurx_t* h, uint32_t cid, const uint8_t ipv4[4]) {
+    return h && ipv4 ? h->m.update_addr(cid, 4, ipv4) : EMURX_EINVAL;
 }
-int emurx_client_update_ipv4(emurx_t* h, uint32_t cid, const uint8_t ipv4[4]) { return update_addr(h, cid, 4, ipv4); }
-int emurx_client_update_ipv6(emurx_t* h, uint32_t cid, const uint8_t ipv6[16]) { return update_addr(h, cid, 6, ipv6); }
-int emurx_client_update_dipv6(emurx_t* h, uint32_t cid, const uint8_t d[16]) { return update_addr(h, cid, 7, d); }
-
+int emurx_client_update_ipv6(emurx_t* h, uint32_t cid, const uint8_t ipv6[16]) {
+    return h && ipv6 ? h->m.update_addr(cid, 6, ipv6) : EMURX_EINVAL;
+}
+int emurx_client_update_dipv6(emurx_t* h, uint32_t cid, const uint8_t d[16]) {
+    return h && d ? h->m.update_addr(cid, 7, d) : EMURX_EINVAL;
+}
 int emurx_client_set_ra(emurx_t* h, uint32_t cid, const uint8_t prefix[16], uint8_t plen) {
     if (!h || !prefix) return EMURX_EINVAL;
-    if (cid >= h->cfg.max_clients || !h->cl[cid].alive) return EMURX_ENOENT;
-    ClientInfo& c = h->cl[cid];
-    c.has_ra = true;
-    memcpy(c.ra_prefix, prefix, 16);
-    c.ra_plen = plen;
-    h->dirty = true;
-    return EMURX_OK;
+    return h->m.client_set_ra(cid, prefix, plen);
 }
-
-// ---- transport flow tables (TransportCtx.addFlowv4/6 / removeFlowv4/6 client_ctx.go:597-651,
-// serverCb / lookupServerPort :1142-1155, GetTransportCtx socketApi.go:174-193) -----------
-static int flow_key(emurx_t* h, uint32_t cid, const uint8_t* tuple, uint32_t tlen, std::string& k) {
-    if (!h || !tuple || (tlen != 13 && tlen != 37)) return EMURX_EINVAL;
-    if (cid >= h->cfg.max_clients || !h->cl[cid].alive) return EMURX_ENOENT;
-    k.assign(4 + tlen, '\0');
-    memcpy(&k[0], &cid, 4);
-    memcpy(&k[4], tuple, tlen);
-    return EMURX_OK;
-}
+// transport flow tables (TransportCtx.addFlowv4/6 / removeFlowv4/6 client_ctx.go:597-651,
+// serverCb / lookupServerPort :1142-1155, GetTransportCtx socketApi.go:174-193)
 int emurx_flow_add(emurx_t* h, uint32_t cid, const uint8_t* tuple, uint32_t tlen, uint32_t flow_id) {
-    std::string k;
-    int rc = flow_key(h, cid, tuple, tlen, k);
-    if (rc) return rc;
-    if (flow_id > EMURX_FLOW_ID_MAX) return EMURX_EINVAL;
-    if (h->ft_map.count(k)) return EMURX_EEXIST;  // ft_add_err_already_exits
-    h->ft_map[k] = flow_id;
-    h->cl[cid].has_ctx = true;
-    h->dirty = true;
-    return EMURX_OK;
+    return h ? h->m.flow_add(cid, tuple, tlen, flow_id) : EMURX_EINVAL;
 }
 int emurx_flow_remove(emurx_t* h, uint32_t cid, const uint8_t* tuple, uint32_t tlen) {
-    std::string k;
-    int rc = flow_key(h, cid, tuple, tlen, k);
-    if (rc) return rc;
-    if (!h->ft_map.erase(k)) return EMURX_ENOENT;  // ft_remove_err_not_exits
-    h->dirty = true;
-    return EMURX_OK;
-}
-static int srv_key(emurx_t* h, uint32_t cid, uint16_t port, uint8_t proto, uint64_t& k) {
-    if (!h || (proto != 6 && proto != 17)) return EMURX_EINVAL;
-    if (cid >= h->cfg.max_clients || !h->cl[cid].alive) return EMURX_ENOENT;
-    k = ((uint64_t)cid << 32) | port | ((uint32_t)proto << 16);
-    return EMURX_OK;
+    return h ? h->m.flow_remove(cid, tuple, tlen) : EMURX_EINVAL;
 }
 int emurx_server_add(emurx_t* h, uint32_t cid, uint16_t port, uint8_t proto) {
-    uint64_t k;
-    int rc = srv_key(h, cid, port, proto, k);
-    if (rc) return rc;
-    if (h->srv_map.count(k)) return EMURX_EEXIST;
-    h->srv_map[k] = 1;
-    h->cl[cid].has_ctx = true;
-    h->dirty = true;
-    return EMURX_OK;
+    return h ? h->m.server_add(cid, port, proto) : EMURX_EINVAL;
 }
 int emurx_server_remove(emurx_t* h, uint32_t cid, uint16_t port, uint8_t proto) {
-    uint64_t k;
-    int rc = srv_key(h, cid, port, proto, k);
-    if (rc) return rc;
-    if (!h->srv_map.erase(k)) return EMURX_ENOENT;
-    h->dirty = true;
-    return EMURX_OK;
+    return h ? h->m.server_remove(cid, port, proto) : EMURX_EINVAL;
 }
 int emurx_client_set_transport(emurx_t* h, uint32_t cid, int has_ctx) {
-    if (!h) return EMURX_EINVAL;
-    if (cid >= h->cfg.max_clients || !h->cl[cid].alive) return EMURX_ENOENT;
-    h->cl[cid].has_ctx = has_ctx != 0;
-    h->dirty = true;
-    return EMURX_OK;
+    return h ? h->m.client_set_transport(cid, has_ctx != 0) : EMURX_EINVAL;
 }
 
 int emurx_sync(emurx_t* h, void* stream) {
     if (!h) return EMURX_EINVAL;
+    if (h->host_only) return EMURX_OK;  // nothing to ship to
     int rc = bind(h);
     if (rc) return rc;
-    return rebuild_and_upload(h, stream ? (hipStream_t)stream : h->stream);
+    return prepare_read(h, stream ? (hipStream_t)stream : h->stream);
+}
+int emurx_table_stats(const emurx_t* h, uint64_t* delta_blocks, uint64_t* whole_tables, uint64_t* image_bytes) {
+    if (!h) return EMURX_EINVAL;
+    if (delta_blocks) *delta_blocks = h->shipped_blocks;
+    if (whole_tables) *whole_tables = h->shipped_whole;
+    if (image_bytes) {
+        uint64_t b = h->m.nsinfo.img.size() * 4;
+        for (int k = 0; k < emurx_host::kNumTabs; ++k) b += h->m.hashes(k)->img.size() * 4;
+        *image_bytes = b;
+    }
+    return EMURX_OK;
+}
+int emurx_set_partition(emurx_t* h, uint32_t n_parts, uint32_t part) {
+    if (!h || n_parts == 0 || n_parts > EMURX_MAX_PARTS || part >= n_parts) return EMURX_EINVAL;
+    h->m.set_partition(n_parts, part);
+    return EMURX_OK;
+}
+uint64_t emurx_table_gen(const emurx_t* h) { return h ? h->m.gen : 0; }
+int emurx_recs_stale(const emurx_t* h, const emurx_rec* rec, uint32_t n, uint64_t gen, uint8_t* stale) {
+    if (!h || (n && (!rec || !stale))) return EMURX_EINVAL;
+    for (uint32_t i = 0; i < n; ++i) stale[i] = h->m.stale(rec[i], gen) ? 1 : 0;
+    return EMURX_OK;
+}
+int emurx_image_lookup(emurx_t* h, uint32_t table, const uint32_t* key, uint32_t* value) {
+    if (!h) return EMURX_EINVAL;
+    return h->m.image_lookup(table, key, value);
+}
+int emurx_image_check(emurx_t* h, uint64_t* mismatched) {
+    using namespace emurx_host;
+    if (!h || !mismatched) return EMURX_EINVAL;
+    int rc = bind(h);
+    if (rc) return rc;
+    if ((rc = prepare_read(h, h->stream))) return rc;
+    if (hipStreamSynchronize(h->stream) != hipSuccess) return EMURX_EDEVICE;
+    uint64_t bad = 0;
+    std::vector<uint32_t> buf;
+    for (int k = 0; k <= kNumTabs; ++k) {
+        const Blocks& b = k < kNumTabs ? *h->m.hashes(k) : h->m.nsinfo;
+        const DevBuf<uint32_t>& d = k < kNumTabs ? h->d_tab[k] : h->d_nsinfo;
+        buf.resize(b.img.size());
+        if (b.img.size() > d.n) return EMURX_EDEVICE;
+        if (!buf.empty() && hipMemcpy(buf.data(), d.p, buf.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
+            return EMURX_EDEVICE;
+        for (size_t i = 0; i < buf.size(); ++i) bad += buf[i] != b.img[i];
+    }
+    *mismatched = bad;
+    return EMURX_OK;
 }
 
 // ---- data path ---------------------------------------------------------------------------
@@ -1010,11 +864,65 @@ void emurx_hist_to_counters(const uint64_t hist[2 * EMURX_HIST_BINS], emurx_coun
 
 int emurx_classify_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_desc, uint32_t n,
                        const emurx_dev_out* out, void* stream) {
-    return run_dev(h, d_frames, d_desc, n, out, stream, true);
+    int rc = check_batch_args(h, d_frames, d_desc, n, out);
+    if (rc) return rc;
+    return run_dev(h, d_frames, d_desc, n, out, stream ? (hipStream_t)stream : h->stream, 1, nullptr, nullptr);
 }
 int emurx_parse_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_desc, uint32_t n,
                     const emurx_dev_out* out, void* stream) {
-    return run_dev(h, d_frames, d_desc, n, out, stream, false);
+    int rc = check_batch_args(h, d_frames, d_desc, n, out);
+    if (rc) return rc;
+    return run_dev(h, d_frames, d_desc, n, out, stream ? (hipStream_t)stream : h->stream, 0, nullptr, nullptr);
+}
+
+int emurx_classify_route_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_desc, uint32_t n,
+                             const emurx_dev_out* out, uint32_t n_parts, uint32_t my_rank, uint32_t cap,
+                             emurx_route_rec* d_send, uint32_t* d_send_count, void* stream) {
+    int rc = check_batch_args(h, d_frames, d_desc, n, out);
+    if (rc) return rc;
+    if (!out->rec || !d_send_count || n_parts == 0 || n_parts > EMURX_MAX_PARTS || my_rank >= n_parts ||
+        (n && (!d_send || cap == 0)) || ((uintptr_t)d_send & 7))
+        return EMURX_EINVAL;
+    if ((rc = route_scratch(h, n))) return rc;
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    const emurx_route_counts rt{n_parts, h->d_route_cnt.p, h->d_route_grp.p, my_rank};
+    if (n && (rc = run_dev(h, d_frames, d_desc, n, out, st, 1, &rt, nullptr))) return rc;
+    return emurx_launch_route(out->rec, n, n_parts, my_rank, cap, d_send, d_send_count, h->d_route_cnt.p,
+                              h->d_route_grp.p, h->d_route_goff.p, st, true)
+               ? EMURX_EDEVICE
+               : EMURX_OK;
+}
+
+int emurx_parse_route_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_desc, uint32_t n,
+                          const emurx_dev_out* out, uint32_t n_parts, uint32_t my_rank, uint32_t cap,
+                          emurx_lookup_rec* d_send, uint32_t* d_send_count, void* stream) {
+    int rc = check_batch_args(h, d_frames, d_desc, n, out);
+    if (rc) return rc;
+    if (!d_send_count || n_parts == 0 || n_parts > EMURX_MAX_PARTS || my_rank >= n_parts ||
+        (n && (!d_send || cap == 0)) || ((uintptr_t)d_send & 15))
+        return EMURX_EINVAL;
+    if ((rc = route_scratch(h, n))) return rc;
+    if (h->d_lk.alloc(std::max<size_t>(n, 1))) return EMURX_ENOMEM;
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    const emurx_route_counts rt{n_parts, h->d_route_cnt.p, h->d_route_grp.p, my_rank};
+    if (n && (rc = run_dev(h, d_frames, d_desc, n, out, st, 2, &rt, h->d_lk.p))) return rc;
+    return emurx_launch_route_lk(h->d_lk.p, n, n_parts, cap, d_send, d_send_count, h->d_route_cnt.p,
+                                 h->d_route_grp.p, h->d_route_goff.p, st)
+               ? EMURX_EDEVICE
+               : EMURX_OK;
+}
+
+int emurx_lookup_dev(emurx_t* h, const emurx_lookup_rec* d_recv, const uint32_t* d_recv_count, uint32_t n_parts,
+                     uint32_t cap, emurx_route_rec* d_out, uint32_t* d_flow, void* stream) {
+    if (!h || !d_recv_count || n_parts == 0 || n_parts > EMURX_MAX_PARTS || (cap && (!d_recv || !d_out)) ||
+        ((uintptr_t)d_recv & 15) || ((uintptr_t)d_out & 7))
+        return EMURX_EINVAL;
+    int rc = bind(h);
+    if (rc) return rc;
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    if ((rc = prepare_read(h, st))) return rc;
+    return emurx_launch_lookup(d_recv, d_recv_count, n_parts, cap, h->tables(), d_out, d_flow, st) ? EMURX_EDEVICE
+                                                                                                    : EMURX_OK;
 }
 
 int emurx_rx_stream(emurx_t* h, const uint8_t* msg, size_t len, emurx_rec* out_rec,
@@ -1072,7 +980,6 @@ int emurx_set_timing(emurx_t* h, uint32_t slots, uint32_t stride) {
     if (!h) return EMURX_EINVAL;
     int rc = bind(h);
     if (rc) return rc;
-    (void)hipStreamSynchronize(h->stream);
     (void)hipDeviceSynchronize();
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
@@ -1148,47 +1055,12 @@ int emurx_route_dev(emurx_t* h, const emurx_rec* d_rec, uint32_t n, uint32_t n_p
     if (((uintptr_t)d_rec & 15) || ((uintptr_t)d_send & 7)) return EMURX_EINVAL;
     int rc = bind(h);
     if (rc) return rc;
-    const size_t tiles = ((size_t)n + EMURX_QUEUE_TILE - 1) / EMURX_QUEUE_TILE;
-    if (tiles > 1024u * 64u) return EMURX_EINVAL;  // 16M frames per batch
-    const size_t gw = 1024 * 16;
-    if (!h->d_route_grp.p) {
-        if (h->d_route_grp.alloc(gw) || hipMemset(h->d_route_grp.p, 0, gw * sizeof(uint32_t)) != hipSuccess)
-            return EMURX_ENOMEM;
-    }
-    if (h->d_route_cnt.alloc(std::max<size_t>(tiles, 1) * 16) || h->d_route_goff.alloc(gw)) return EMURX_ENOMEM;
+    if ((rc = route_scratch(h, n))) return rc;
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
-    // the owners of exactly this batch were counted by its classify launch: skip that pass
-    const bool counted = h->route_pending && d_rec == h->route_rec && n == h->route_n && n_parts == h->route_parts;
-    if (h->route_pending && !counted &&
-        hipMemsetAsync(h->d_route_grp.p, 0, gw * sizeof(uint32_t), st) != hipSuccess)
-        return EMURX_EDEVICE;
-    h->route_pending = false;
     return emurx_launch_route(d_rec, n, n_parts, my_rank, cap, d_send, d_send_count, h->d_route_cnt.p,
-                              h->d_route_grp.p, h->d_route_goff.p, st, counted)
+                              h->d_route_grp.p, h->d_route_goff.p, st, false)
                ? EMURX_EDEVICE
                : EMURX_OK;
-}
-
-int emurx_set_route_parts(emurx_t* h, uint32_t n_parts) {
-    if (!h || n_parts > EMURX_MAX_PARTS) return EMURX_EINVAL;
-    int rc = bind(h);
-    if (rc) return rc;
-    (void)hipStreamSynchronize(h->stream);
-    const size_t gw = 1024 * 16, tiles = ((size_t)h->cfg.max_frames + EMURX_QUEUE_TILE - 1) / EMURX_QUEUE_TILE;
-    if (n_parts) {
-        if (tiles > 1024u * 64u) return EMURX_EINVAL;
-        if (!h->d_route_grp.p) {
-            if (h->d_route_grp.alloc(gw) || hipMemset(h->d_route_grp.p, 0, gw * sizeof(uint32_t)) != hipSuccess)
-                return EMURX_ENOMEM;
-        }
-        if (h->d_route_cnt.alloc(std::max<size_t>(tiles, 1) * 16) || h->d_route_goff.alloc(gw)) return EMURX_ENOMEM;
-    }
-    if (h->route_pending && h->d_route_grp.p &&
-        hipMemset(h->d_route_grp.p, 0, gw * sizeof(uint32_t)) != hipSuccess)
-        return EMURX_EDEVICE;
-    h->route_pending = false;
-    h->route_parts = n_parts;
-    return EMURX_OK;
 }
 
 }  // extern "C"

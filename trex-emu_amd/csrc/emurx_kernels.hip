@@ -29,7 +29,9 @@ __device__ __forceinline__ void glds16(const uint4* src, uint4* dst_wave_base) {
 }
 __device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0)
 
-template <bool kClassify, uint32_t kStage>
+// kKind: 0 parse only, 1 parse + classify, 2 parse + lookup keys (the partitioned source:
+// an emurx_lookup_rec per frame into lk, no table reads)
+template <int kKind, uint32_t kStage>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage == kStageNarrow ? 6 : 5))) void k_rx(const uint8_t* __restrict__ frames,
                                                const emurx_desc* __restrict__ desc, uint32_t n,
                                                emurx_dev_tables T, emurx_rec* __restrict__ rec,
@@ -38,7 +40,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
                                                unsigned long long* __restrict__ hist,
                                                uint32_t* __restrict__ flow, uint32_t* __restrict__ fb,
                                                uint32_t gen, uint32_t rt_parts, uint32_t* __restrict__ rt_cnt,
-                                               uint32_t* __restrict__ rt_grp) {
+                                               uint32_t* __restrict__ rt_grp, uint32_t rt_rank,
+                                               emurx_lookup_rec* __restrict__ lk) {
+    constexpr bool kClassify = kKind == 1;
     constexpr uint32_t kWinVec = kStage / 16 / kWave;  // window path: 16-byte vectors per lane
     __shared__ __attribute__((aligned(16))) uint32_t slab[kWaves * kStage / 4];
     __shared__ uint32_t s_wcnt[kWaves][16];
@@ -94,11 +98,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
 
     Rec r;
     r.dlen = 0;
+    uint32_t kwd[12];  // kKind 2: the lookup key words of the frame
     if (staged) {  // wave-uniform branch
         if (valid) {
             LdsSrc s{reinterpret_cast<const uint8_t*>(slab), slab, wv * kStage + (off - start)};
             parse_flat(s, len, vport, T.cb_mask, r);
             if (kClassify && !(EMURX_ABL & 2)) classify(s, len, T, r);
+            if (kKind == 2 && r.status == EMURX_ST_OK) pack_key(s, len, r, make_key(s, len, r), kwd);
         }
     } else {
         const uint32_t head = (uint32_t)((uintptr_t)(frames + off) & 15);
@@ -107,21 +113,37 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
         if (valid) parse_packet(s, len, vport, T.cb_mask, r);
         coop_checksum(r, frames + off, s_csum[wv]);  // the wave's long L4 spans, converged
         if (valid && kClassify && !(EMURX_ABL & 2)) classify(s, len, T, r);
+        if (kKind == 2 && valid && r.status == EMURX_ST_OK) pack_key(s, len, r, make_key(s, len, r), kwd);
     }
-    if (rec && !(EMURX_ABL & 16)) {
-        const uint4 h0 = make_uint4(r.ns, r.cl, r.vlan0, r.vlan1);
-        const uint4 h1 = make_uint4(r.vport | (r.l3 << 16), r.l4 | (r.l7 << 16),
-                                    r.l7len | (r.nh << 16) | (r.proto << 24), r.status | (r.flags << 8));
-        if (valid) {
-            uint4* o = reinterpret_cast<uint4*>(rec + i);
-            // streaming stores: the records are read once, by the host copy or the route kernel
-            // (measured +2.6% on config B, neutral on C)
-            typedef unsigned v4u __attribute__((ext_vector_type(4)));
-            __builtin_nontemporal_store(v4u{h0.x, h0.y, h0.z, h0.w}, reinterpret_cast<v4u*>(o));
-            __builtin_nontemporal_store(v4u{h1.x, h1.y, h1.z, h1.w}, reinterpret_cast<v4u*>(o + 1));
+    typedef unsigned v4u __attribute__((ext_vector_type(4)));
+    if (rec && i < n && !(EMURX_ABL & 16)) {
+        // an empty descriptor slot gets a record too (no Namespace, status EMURX_ST_HOLE), so
+        // every consumer of rec[0, n) sees defined bytes
+        const uint4 h0 = valid ? make_uint4(r.ns, r.cl, r.vlan0, r.vlan1)
+                               : make_uint4(EMURX_ID_NONE, EMURX_ID_NONE, 0, 0);
+        const uint4 h1 = valid ? make_uint4(r.vport | (r.l3 << 16), r.l4 | (r.l7 << 16),
+                                            r.l7len | (r.nh << 16) | (r.proto << 24), r.status | (r.flags << 8))
+                               : make_uint4(0, 0, (uint32_t)EMURX_CB_NONE << 24, EMURX_ST_HOLE);
+        uint4* o = reinterpret_cast<uint4*>(rec + i);
+        // streaming stores: the records are read once, by the host copy or the route kernel
+        // (measured +2.6% on config B, neutral on C)
+        __builtin_nontemporal_store(v4u{h0.x, h0.y, h0.z, h0.w}, reinterpret_cast<v4u*>(o));
+        __builtin_nontemporal_store(v4u{h1.x, h1.y, h1.z, h1.w}, reinterpret_cast<v4u*>(o + 1));
+    }
+    if (kKind == 2 && i < n) {  // the lookup record: ns_id = frame index, client_id = source rank
+        const bool ok = valid && r.status == EMURX_ST_OK;
+        v4u* o = reinterpret_cast<v4u*>(lk + i);
+        o[0] = valid ? v4u{i, rt_rank, r.vlan0, r.vlan1} : v4u{i, rt_rank, 0, 0};
+        o[1] = valid ? v4u{r.vport | (r.l3 << 16), r.l4 | (r.l7 << 16), r.l7len | (r.nh << 16) | (r.proto << 24),
+                           r.status | (r.flags << 8)}
+                     : v4u{0, 0, (uint32_t)EMURX_CB_NONE << 24, EMURX_ST_HOLE};
+        if (ok) {
+            o[2] = v4u{kwd[0], kwd[1], kwd[2], kwd[3]};
+            o[3] = v4u{kwd[4], kwd[5], kwd[6], kwd[7]};
+            o[4] = v4u{kwd[8], kwd[9], kwd[10], kwd[11]};
         }
     }
-    if (valid && flow) flow[i] = r.flow;
+    if (flow && i < n) flow[i] = valid ? r.flow : EMURX_FLOW_NONE;
     // outcome histogram into the wave's LDS copy: a wave whose frames all share one
     // (status, proto) bin adds its count (ballot) and byte sum (DPP reduction) once, instead
     // of 64 LDS atomics serialised on one address; mixed waves add per frame
@@ -156,8 +178,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
     // with a Namespace, counted per (tile, owner) and per group of 64 tiles as k_route<false>
     // counts them (emurx_route.hip)
     if (rt_cnt) {
-        const uint32_t d = valid && r.ns != EMURX_ID_NONE
-                               ? emurx_owner(emurx_tk_hash(r.vport, r.vlan0, r.vlan1), rt_parts) : 0xffu;
+        // classify: records whose Namespace was found; lookup keys: every frame that reached
+        // a callback (its Namespace is resolved by the owner)
+        const bool routed = valid && (kKind == 2 ? r.status == EMURX_ST_OK : r.ns != EMURX_ID_NONE);
+        const uint32_t d = routed ? emurx_owner(emurx_tk_hash(r.vport, r.vlan0, r.vlan1), rt_parts) : 0xffu;
         uint64_t rl = __ballot(d != 0xffu);
         while (rl) {
             const uint32_t lead = (uint32_t)__ffsll((long long)rl) - 1;
@@ -203,24 +227,40 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
 }
 
 
+// table deltas (emurx_api.cpp ship_tables): 4 lanes per 64-byte block, 16 bytes each
+__global__ __launch_bounds__(kBlock) void k_apply(const emurx_delta* __restrict__ d, uint32_t n) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x, e = i >> 2, q = i & 3;
+    if (e >= n) return;
+    const uint4 v = reinterpret_cast<const uint4*>(d[e].w)[q];
+    reinterpret_cast<uint4*>((uintptr_t)d[e].dst)[q] = v;
+}
+
 }  // namespace emurx
+
+int emurx_launch_apply(const emurx_delta* d, uint32_t n, hipStream_t st) {
+    using namespace emurx;
+    if (n) hipLaunchKernelGGL(k_apply, dim3((n * 4 + kBlock - 1) / kBlock), dim3(kBlock), 0, st, d, n);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 // ---------------------------------------------------------------------------------------
 // launcher (called by emurx_api.cpp)
 // ---------------------------------------------------------------------------------------
 int emurx_launch_batch(const uint8_t* frames, const emurx_desc* desc, uint32_t n,
-                       const emurx_dev_tables& T, bool classify, const emurx_dev_out& out,
+                       const emurx_dev_tables& T, int kind, const emurx_dev_out& out,
                        hipStream_t st, const hipEvent_t* ev, bool narrow, uint32_t* fb, uint32_t gen,
-                       const emurx_route_counts* rt) {
+                       const emurx_route_counts* rt, emurx_lookup_rec* lk) {
     using namespace emurx;
     if (ev) (void)hipEventRecord(ev[0], st);
     if (n) {
         const dim3 g((n + EMURX_QUEUE_TILE - 1) / EMURX_QUEUE_TILE), b(kBlock);
         unsigned long long* hist = reinterpret_cast<unsigned long long*>(out.hist);
-        auto k = classify ? (narrow ? k_rx<true, kStageNarrow> : k_rx<true, kStageWide>)
-                          : (narrow ? k_rx<false, kStageNarrow> : k_rx<false, kStageWide>);
+        auto k = kind == 1 ? (narrow ? k_rx<1, kStageNarrow> : k_rx<1, kStageWide>)
+               : kind == 2 ? (narrow ? k_rx<2, kStageNarrow> : k_rx<2, kStageWide>)
+                           : (narrow ? k_rx<0, kStageNarrow> : k_rx<0, kStageWide>);
         hipLaunchKernelGGL(k, g, b, 0, st, frames, desc, n, T, out.rec, out.qlist, out.qcap, out.tile_cnt, hist,
-                           out.flow, fb, gen, rt ? rt->parts : 0u, rt ? rt->cnt : nullptr, rt ? rt->grp : nullptr);
+                           out.flow, fb, gen, rt ? rt->parts : 0u, rt ? rt->cnt : nullptr, rt ? rt->grp : nullptr,
+                           rt ? rt->rank : 0u, lk);
     }
     if (ev) (void)hipEventRecord(ev[1], st);
     return hipGetLastError() == hipSuccess ? 0 : -1;

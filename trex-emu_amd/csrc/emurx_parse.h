@@ -792,8 +792,26 @@ __device__ __forceinline__ void client_result(Rec& r, uint32_t cid, uint32_t cpl
     if (check && !(cplugins & (1u << plug))) { set_lk(r, EMURX_LK_CLIENT_NO_PLUGIN); return; }
     set_lk(r, EMURX_LK_CLIENT);
 }
-__device__ __forceinline__ uint32_t client_plugins(const emurx_dev_tables& T, uint32_t cid) {
-    return cid == EMURX_ID_NONE ? 0u : gld4(T.client + 8 * cid + 2);
+// client info slot {cid, plugins, ra, ra_prefix[0..3], ra_prefix[4..7], has_ctx, 0, 0} of a
+// client id (emurx_tables.h ci table, 2 per bucket); zeros when absent
+struct CInfo {
+    uint32_t plugins, ra, ra0, ra1, ctx;
+};
+__device__ __forceinline__ CInfo client_info(const emurx_dev_tables& T, uint32_t cid) {
+    CInfo c{0, 0, 0, 0, 0};
+    if (cid == EMURX_ID_NONE) return c;
+    for (uint32_t b = emurx_ci_hash(cid) & T.ci_mask, n = 0; n <= T.ci_mask; b = (b + 1) & T.ci_mask, ++n) {
+        const Bucket e = ld_bucket(T.ci_tab, b);
+        bool hole = false;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const uint4 x = e.s[2 * k], y = e.s[2 * k + 1];
+            hole |= y.w == EMURX_EMPTY;
+            if (y.w != EMURX_EMPTY && x.x == cid) return CInfo{x.y, x.z, x.w, y.x, y.y};
+        }
+        if (hole) break;
+    }
+    return c;
 }
 // CClient.IsUnicastToMe client_ctx.go:389-398 (frames here are always > 6 bytes) compares the
 // frame's destination with the client's MAC, which the IP slots carry (IpHit)
@@ -842,54 +860,75 @@ __device__ bool dhcp_chaddr(const S& s, uint32_t len, const Rec& r, uint32_t& lo
     return true;
 }
 
-// TransportCtx.handleRxPacket src/emu/plugins/transport/client_ctx.go:912-969: the frame's
-// c5tuplekey (fillv4tuple / fillv6tuple :720-765) in the client's flow map, else the new-flow
-// checks of handleRxTcpNewFlow / handleRxUdpNewFlow (:829-904) up to OnAccept.
+// The frame's c5tuplekey (fillv4tuple / fillv6tuple src/emu/plugins/transport/
+// client_ctx.go:720-765) and the TCP flags byte the new-flow check reads.
+struct Tuple {
+    uint32_t v6, proto, ports, flags;  // ports: sport, dport as on the wire (4 bytes LE)
+    uint32_t a[4], d[4];               // src / dst words LE (IPv4: a[0], d[0])
+};
 template <class S>
-__device__ __forceinline__ uint32_t flow_lookup(const S& s, uint32_t len, const emurx_dev_tables& T, const Rec& r, uint32_t cid) {
-    if (!(gld4(T.client + 8 * cid + 6) & 1u)) return EMURX_FLOW_NO_CTX;  // GetTransportCtx() == nil
+__device__ __forceinline__ Tuple get_tuple(const S& s, uint32_t len, const Rec& r) {
+    Tuple t{};
     const uint32_t L3 = r.l3, L4 = r.l4;
-    const uint32_t ports = le32(s, L4);  // UDPHeader(p[L4:L4+4]): sport, dport as on the wire
-    uint32_t proto;
+    t.ports = le32(s, L4);  // UDPHeader(p[L4:L4+4])
     if ((s.u8(L3) >> 4) == 4) {  // IPv4Header(p[L3:L3+20]).Version()
-        proto = s.u8(L3 + 9);
-        const uint32_t src = le32(s, L3 + 12), dst = le32(s, L3 + 16);
+        t.proto = s.u8(L3 + 9);
+        t.a[0] = le32(s, L3 + 12);
+        t.d[0] = le32(s, L3 + 16);
+    } else {
+        t.v6 = 1;
+        t.proto = r.nh;  // ps.NextHeader
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            t.a[k] = le32(s, L3 + 8 + 4 * k);
+            t.d[k] = le32(s, L3 + 24 + 4 * k);
+        }
+    }
+    // a flags byte past the frame is read as 0 here (stale mbuf bytes in Go)
+    t.flags = (L4 + 13 < len) ? s.u8(L4 + 13) : 0u;
+    return t;
+}
+// TransportCtx.handleRxPacket client_ctx.go:912-969: the tuple in the client's flow map,
+// else the new-flow checks of handleRxTcpNewFlow / handleRxUdpNewFlow (:829-904) up to OnAccept
+__device__ __forceinline__ uint32_t flow_probe(const emurx_dev_tables& T, const Tuple& t, uint32_t cid) {
+    const uint32_t proto = t.proto, ports = t.ports;
+    if (!t.v6) {
+        const uint32_t src = t.a[0], dst = t.d[0];
         for (uint32_t b = emurx_ft4_hash(cid, src, dst, ports, proto) & T.ft4_mask, k = 0; k <= T.ft4_mask;
              ++k, b = (b + 1) & T.ft4_mask) {
             const Bucket e = ld_bucket(T.ft4_tab, b);
             const uint4 x0 = e.s[0], x1 = e.s[1], y0 = e.s[2], y1 = e.s[3];
             if (x0.x == cid && x0.y == src && x0.z == dst && x0.w == ports && x1.x == proto && x1.w != EMURX_EMPTY)
                 return x1.w;
-            if (x1.w == EMURX_EMPTY) break;
             if (y0.x == cid && y0.y == src && y0.z == dst && y0.w == ports && y1.x == proto && y1.w != EMURX_EMPTY)
                 return y1.w;
-            if (y1.w == EMURX_EMPTY) break;
+            if (x1.w == EMURX_EMPTY || y1.w == EMURX_EMPTY) break;
         }
     } else {
-        proto = r.nh;  // ps.NextHeader
-        const uint32_t a0 = le32(s, L3 + 8), a1 = le32(s, L3 + 12), a2 = le32(s, L3 + 16), a3 = le32(s, L3 + 20);
-        const uint32_t d0 = le32(s, L3 + 24), d1 = le32(s, L3 + 28), d2 = le32(s, L3 + 32), d3 = le32(s, L3 + 36);
-        for (uint32_t b = emurx_ft6_hash(cid, a0, a1, a2, a3, d0, d1, d2, d3, ports, proto) & T.ft6_mask, k = 0;
+        for (uint32_t b = emurx_ft6_hash(cid, t.a[0], t.a[1], t.a[2], t.a[3], t.d[0], t.d[1], t.d[2], t.d[3], ports,
+                                         proto) & T.ft6_mask, k = 0;
              k <= T.ft6_mask; ++k, b = (b + 1) & T.ft6_mask) {
             const Bucket e = ld_bucket(T.ft6_tab, b);
             if (e.s[3].w == EMURX_EMPTY) break;
-            if (e.s[0].x == cid && e.s[0].y == a0 && e.s[0].z == a1 && e.s[0].w == a2 && e.s[1].x == a3 &&
-                e.s[1].y == d0 && e.s[1].z == d1 && e.s[1].w == d2 && e.s[2].x == d3 && e.s[2].y == ports &&
-                e.s[2].z == proto)
+            if (e.s[0].x == cid && e.s[0].y == t.a[0] && e.s[0].z == t.a[1] && e.s[0].w == t.a[2] &&
+                e.s[1].x == t.a[3] && e.s[1].y == t.d[0] && e.s[1].z == t.d[1] && e.s[1].w == t.d[2] &&
+                e.s[2].x == t.d[3] && e.s[2].y == ports && e.s[2].z == proto)
                 return e.s[3].w;
         }
     }
-    // a new flow: handleRxTcpNewFlow needs a bare SYN (GetFlags() & 0x3F == 0x2; a flags byte
-    // past the frame is read as 0 here, stale mbuf bytes in Go)
-    if (proto == 6 && (((L4 + 13 < len) ? s.u8(L4 + 13) : 0u) & 0x3f) != 0x2) return EMURX_FLOW_NO_SYN;
-    const uint32_t key = be16(s, L4 + 2) | ((proto == 6 ? 6u : 17u) << 16);  // lookupServerPort(dst, TCP|UDP)
+    // a new flow: handleRxTcpNewFlow needs a bare SYN (GetFlags() & 0x3F == 0x2)
+    if (proto == 6 && (t.flags & 0x3f) != 0x2) return EMURX_FLOW_NO_SYN;
+    const uint32_t dport = ((ports >> 16) & 0xff) << 8 | (ports >> 24);
+    const uint32_t key = dport | ((proto == 6 ? 6u : 17u) << 16);  // lookupServerPort(dst, TCP|UDP)
     for (uint32_t b = emurx_srv_hash(cid, key) & T.srv_mask, k = 0; k <= T.srv_mask; ++k, b = (b + 1) & T.srv_mask) {
         const Bucket e = ld_bucket(T.srv_tab, b);
+        bool hole = false;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            if (e.s[j].w == EMURX_EMPTY) return EMURX_FLOW_NO_SERVER;
-            if (e.s[j].x == cid && e.s[j].y == key) return EMURX_FLOW_NEW;
+            hole |= e.s[j].w == EMURX_EMPTY;
+            if (e.s[j].w != EMURX_EMPTY && e.s[j].x == cid && e.s[j].y == key) return EMURX_FLOW_NEW;
         }
+        if (hole) break;
     }
     return EMURX_FLOW_NO_SERVER;
 }
@@ -911,62 +950,84 @@ enum Key : uint32_t {
     kIp6,          // CLookupByIPv6(kw[0..3])
 };
 
+// The lookup key of a frame's callback rule, decided from the frame alone (before the
+// Namespace is known, so both probes can be issued together; and, in the partitioned path,
+// on the GPU that received the frame, with the probes on the Namespace's owner).
+struct LKey {
+    uint32_t key;    // enum Key
+    uint32_t kw[4];  // kMac: MAC lo, hi; kIp4: address; kIp6 / kEui: the IPv6 destination
+    uint32_t dlo, dhi;  // destination MAC (IsUnicastToMe)
+    uint32_t mc6;    // icmpv6: the IPv6 source starts with 0xff
+};
 template <class S>
-__device__ __forceinline__ void classify(const S& s, uint32_t len, const emurx_dev_tables& T, Rec& r) {
-    if (r.status != EMURX_ST_OK) return;
-    const uint32_t cb = r.proto, plug = kCbPlugin[cb];
-    const uint32_t dlo = le32(s, 0), dhi = s.u8(4) | (s.u8(5) << 8);  // p[0:6]
-    const bool bcast = dlo == 0xffffffffu && dhi == 0xffffu;
-
-    // ---- the client key of this callback's rule ----
-    uint32_t key = kMac, kw[4] = {dlo, dhi, 0, 0};
+__device__ __forceinline__ LKey make_key(const S& s, uint32_t len, const Rec& r) {
+    const uint32_t cb = r.proto;
+    LKey k;
+    k.dlo = le32(s, 0);
+    k.dhi = s.u8(4) | (s.u8(5) << 8);  // p[0:6]
+    k.mc6 = 0;
+    const bool bcast = k.dlo == 0xffffffffu && k.dhi == 0xffffu;
+    k.key = kMac;
+    k.kw[0] = k.dlo; k.kw[1] = k.dhi; k.kw[2] = 0; k.kw[3] = 0;
     switch (cb) {
     case EMURX_CB_ARP:  // arp.go:904-949: request -> IPv4 of the ARP target
-        if (be16(s, r.l3 + 6) == 1) { key = kIp4; kw[0] = le32(s, r.l3 + 24); }
-        else key = kNsLevel;
+        if (be16(s, r.l3 + 6) == 1) { k.key = kIp4; k.kw[0] = le32(s, r.l3 + 24); }
+        else k.key = kNsLevel;
         break;
     case EMURX_CB_ICMP:  // icmp.go:396-427: IPv4 destination, then IsUnicastToMe
-        key = kIp4; kw[0] = le32(s, r.l3 + 16);
+        k.key = kIp4; k.kw[0] = le32(s, r.l3 + 16);
         break;
     case EMURX_CB_IGMP:
     case EMURX_CB_MDNS:
-        key = kNsLevel;
+        k.key = kNsLevel;
         break;
     case EMURX_CB_DHCP:  // dhcp.go:893-917: broadcast -> chaddr
-        if (bcast && !dhcp_chaddr(s, len, r, kw[0], kw[1])) key = kNoClient;
+        if (bcast && !dhcp_chaddr(s, len, r, k.kw[0], k.kw[1])) k.key = kNoClient;
         break;
     case EMURX_CB_DHCPSRV:  // dhcpsrv.go:1798-1826: broadcast -> GetFirstClient
-        if (bcast) key = kFirst;
+        if (bcast) k.key = kFirst;
         break;
     case EMURX_CB_EAPOL:  // dot1x.go:624-650: 01:80:c2:00:00:03 -> GetFirstClient
-        if (dlo == 0x00c28001u && dhi == 0x0300u) key = kFirst;
+        if (k.dlo == 0x00c28001u && k.dhi == 0x0300u) k.key = kFirst;
         break;
     case EMURX_CB_ICMPV6: {  // ipv6.go:465-540: echo request -> CLookupByIPv6LocalGlobal(dst)
-        if (be16(s, r.l4) != 0x8000u) { key = kNsLevel; break; }
-        if (r.l3 + 40 > len) { key = kNoClient; break; }
-        for (int k = 0; k < 4; ++k) kw[k] = le32(s, r.l3 + 24 + 4 * k);
-        if (!ip6_local_or_global(kw)) { key = kNoClient; break; }
-        if (((kw[2] >> 24) & 0xff) == 0xff && (kw[3] & 0xff) == 0xfe) {  // ExtractOnlyMac client_ctx.go:314-329
-            key = kEui;
-        } else {
-            key = kIp6;
-        }
+        if (be16(s, r.l4) != 0x8000u) { k.key = kNsLevel; break; }
+        if (r.l3 + 40 > len) { k.key = kNoClient; break; }
+        for (int j = 0; j < 4; ++j) k.kw[j] = le32(s, r.l3 + 24 + 4 * j);
+        if (!ip6_local_or_global(k.kw)) { k.key = kNoClient; break; }
+        // ExtractOnlyMac client_ctx.go:314-329
+        k.key = (((k.kw[2] >> 24) & 0xff) == 0xff && (k.kw[3] & 0xff) == 0xfe) ? kEui : kIp6;
+        k.mc6 = s.u8(r.l3 + 8) == 0xff;
         break;
     }
     default:  // dhcpv6, ppp, tcp, udp: MAC[dst] (plugin_transport.go:83-115, ...)
         break;
     }
-    uint32_t mlo = kw[0], mhi = kw[1];  // the MAC probed for kMac / kEui
-    if (key == kEui) {
-        mlo = ((kw[2] & 0xff) ^ 2) | (((kw[2] >> 8) & 0xff) << 8) | (((kw[2] >> 16) & 0xff) << 16) |
-              (((kw[3] >> 8) & 0xff) << 24);
-        mhi = ((kw[3] >> 16) & 0xff) | ((kw[3] >> 24) << 8);
-    }
     // zero keys never match (MACKey / Ipv4Key / Ipv6Key IsZero, ns_ctx.go:262-329)
-    if ((key == kMac || key == kEui) && mlo == 0 && mhi == 0) key = kNoClient;
-    if (key == kIp4 && kw[0] == 0) key = kNoClient;
-    if (key == kIp6 && (kw[0] | kw[1] | kw[2] | kw[3]) == 0) key = kNoClient;
+    if (k.key == kMac && k.kw[0] == 0 && k.kw[1] == 0) k.key = kNoClient;
+    if (k.key == kIp4 && k.kw[0] == 0) k.key = kNoClient;
+    if (k.key == kIp6 && (k.kw[0] | k.kw[1] | k.kw[2] | k.kw[3]) == 0) k.key = kNoClient;
+    if (k.key == kEui) {  // the MAC of an EUI-64 address; a zero MAC never matches
+        const uint32_t lo = ((k.kw[2] & 0xff) ^ 2) | (((k.kw[2] >> 8) & 0xff) << 8) | (((k.kw[2] >> 16) & 0xff) << 16) |
+                            (((k.kw[3] >> 8) & 0xff) << 24);
+        const uint32_t hi = ((k.kw[3] >> 16) & 0xff) | ((k.kw[3] >> 24) << 8);
+        if (lo == 0 && hi == 0) k.key = kNoClient;
+    }
+    return k;
+}
 
+// GetNs + the callback's client rule against the tables.  `flow(cid)` gives the transport
+// flow decision of a tcp/udp frame whose client was found with the transport plugin.
+template <class Flow>
+__device__ __forceinline__ void resolve(const emurx_dev_tables& T, Rec& r, const LKey& k, Flow flow) {
+    const uint32_t cb = r.proto, plug = kCbPlugin[cb];
+    const uint32_t key = k.key;
+    uint32_t mlo = k.kw[0], mhi = k.kw[1];  // the MAC probed for kMac / kEui
+    if (key == kEui) {
+        mlo = ((k.kw[2] & 0xff) ^ 2) | (((k.kw[2] >> 8) & 0xff) << 8) | (((k.kw[2] >> 16) & 0xff) << 16) |
+              (((k.kw[3] >> 8) & 0xff) << 24);
+        mhi = ((k.kw[3] >> 16) & 0xff) | ((k.kw[3] >> 24) << 8);
+    }
     // ---- issue the Namespace and client bucket reads together ----
     const uint32_t tk = emurx_tk_hash(r.vport, r.vlan0, r.vlan1);  // CTunnelKey words
     const uint32_t nb = tk & T.ns_mask;
@@ -977,10 +1038,10 @@ __device__ __forceinline__ void classify(const S& s, uint32_t len, const emurx_d
         cbk = emurx_mac_hash(tk, mlo, mhi) & T.mac_mask;
         ce = ld_bucket(T.mac_tab, cbk);
     } else if (key == kIp4) {
-        cbk = emurx_ip4_hash(tk, kw[0]) & T.ip4_mask;
+        cbk = emurx_ip4_hash(tk, k.kw[0]) & T.ip4_mask;
         ce = ld_bucket(T.ip4_tab, cbk);
     } else if (key == kIp6) {
-        cbk = emurx_ip6_hash(tk, kw[0], kw[1], kw[2], kw[3]) & T.ip6_mask;
+        cbk = emurx_ip6_hash(tk, k.kw[0], k.kw[1], k.kw[2], k.kw[3]) & T.ip6_mask;
         ce = ld_bucket(T.ip6_tab, cbk);
     }
 
@@ -1001,15 +1062,15 @@ __device__ __forceinline__ void classify(const S& s, uint32_t len, const emurx_d
         return;
     case kFirst: {
         const uint32_t cid = gld4(T.ns_info + 4 * ns + 1);
-        client_result(r, cid, client_plugins(T, cid), plug, true);
+        client_result(r, cid, client_info(T, cid).plugins, plug, true);
         return;
     }
     case kIp4: {
-        const IpHit h = resolve_ip4(T, cbk, ce, ns, kw[0]);
+        const IpHit h = resolve_ip4(T, cbk, ce, ns, k.kw[0]);
         if (cb == EMURX_CB_ARP) {
             client_result(r, h.cid, h.mhip >> 16, plug, true);
         } else {  // icmp: IsUnicastToMe against the MAC in the slot
-            const bool me = h.mlo == dlo && (h.mhip & 0xffffu) == dhi;
+            const bool me = h.mlo == k.dlo && (h.mhip & 0xffffu) == k.dhi;
             client_result(r, me ? h.cid : EMURX_ID_NONE, 0, plug, false);
         }
         return;
@@ -1022,19 +1083,19 @@ __device__ __forceinline__ void classify(const S& s, uint32_t len, const emurx_d
             clo = mlo;  // the MAC table's key is the client's MAC
             chi = mhi;
             // CClient.IsValidPrefix client_ctx.go:279-295
-            if (cid != EMURX_ID_NONE && !(kw[0] == 0x000080feu && kw[1] == 0)) {
-                const uint32_t* c = T.client + 8 * cid;
-                const uint32_t ra = c[3];
-                if (!((ra & 1u) && ((ra >> 8) & 0xff) == 64 && c[4] == kw[0] && c[5] == kw[1])) cid = EMURX_ID_NONE;
+            if (cid != EMURX_ID_NONE && !(k.kw[0] == 0x000080feu && k.kw[1] == 0)) {
+                const CInfo c = client_info(T, cid);
+                if (!((c.ra & 1u) && ((c.ra >> 8) & 0xff) == 64 && c.ra0 == k.kw[0] && c.ra1 == k.kw[1]))
+                    cid = EMURX_ID_NONE;
             }
         } else {
-            const IpHit h = resolve_ip6(T, cbk, ce, ns, kw);
+            const IpHit h = resolve_ip6(T, cbk, ce, ns, k.kw);
             cid = h.cid;
             clo = h.mlo;
             chi = h.mhip & 0xffffu;
         }
-        if (cid != EMURX_ID_NONE && !(clo == dlo && chi == dhi)) cid = EMURX_ID_NONE;
-        if (cid != EMURX_ID_NONE && s.u8(r.l3 + 8) == 0xff) cid = EMURX_ID_NONE;
+        if (cid != EMURX_ID_NONE && !(clo == k.dlo && chi == k.dhi)) cid = EMURX_ID_NONE;
+        if (cid != EMURX_ID_NONE && k.mc6) cid = EMURX_ID_NONE;
         client_result(r, cid, 0, plug, false);
         return;
     }
@@ -1043,11 +1104,72 @@ __device__ __forceinline__ void classify(const S& s, uint32_t len, const emurx_d
         client_result(r, c.x, c.y, plug, true);
         // transport: the client's TransportCtx decides (plugin_transport.go:109-114, :73-80)
         if (T.ft_on && (cb == EMURX_CB_TCP || cb == EMURX_CB_UDP) &&
-            ((r.flags & EMURX_FLAG_LK_MASK) >> EMURX_FLAG_LK_SHIFT) == EMURX_LK_CLIENT)
-            r.flow = flow_lookup(s, len, T, r, c.x);
+            ((r.flags & EMURX_FLAG_LK_MASK) >> EMURX_FLAG_LK_SHIFT) == EMURX_LK_CLIENT) {
+            // GetTransportCtx() == nil -> the handler returns -1 (PluginTransClient :73-80)
+            r.flow = client_info(T, c.x).ctx & 1u ? flow(c.x) : EMURX_FLOW_NO_CTX;
+        }
         return;
     }
     }
+}
+
+// parse state -> Namespace / Client ids, lookup outcome, flow decision (replicated tables:
+// the frame's bytes are at hand, the flow tuple is read only when a flow probe runs)
+template <class S>
+__device__ __forceinline__ void classify(const S& s, uint32_t len, const emurx_dev_tables& T, Rec& r) {
+    if (r.status != EMURX_ST_OK) return;
+    const LKey k = make_key(s, len, r);
+    resolve(T, r, k, [&](uint32_t cid) { return flow_probe(T, get_tuple(s, len, r), cid); });
+}
+
+// ---- partitioned path: the lookup record (include/emu_rx.h emurx_lookup_rec) -------------
+// words 0..7: the parsed record with ns_id = source frame index, client_id = source rank;
+// key[12]: {dlo, dhi | key << 16 | mc6 << 20 | v6 << 21, kw[4] or the flow tuple ...}
+//   tcp / udp (MAC[dst] rule): the MAC key is dlo / dhi and key[2..11] carry the c5tuplekey:
+//     IPv4 {src, dst, ports, proto | flags << 8, 0 ...}; IPv6 {src[4], dst[4], ports, nh | flags << 8}
+//   other callbacks: key[2..5] = kw[0..3]
+__device__ __forceinline__ bool lk_transport(uint32_t cb) { return cb == EMURX_CB_TCP || cb == EMURX_CB_UDP; }
+template <class S>
+__device__ __forceinline__ void pack_key(const S& s, uint32_t len, const Rec& r, const LKey& k, uint32_t w[12]) {
+    const bool tr = lk_transport(r.proto) && k.key == kMac;
+    Tuple t{};
+    if (tr) t = get_tuple(s, len, r);
+    w[0] = k.dlo;
+    w[1] = k.dhi | (k.key << 16) | (k.mc6 << 20) | (t.v6 << 21);
+    if (!tr) {
+        w[2] = k.kw[0]; w[3] = k.kw[1]; w[4] = k.kw[2]; w[5] = k.kw[3];
+        w[6] = w[7] = w[8] = w[9] = w[10] = w[11] = 0;
+    } else if (!t.v6) {
+        w[2] = t.a[0]; w[3] = t.d[0]; w[4] = t.ports; w[5] = t.proto | (t.flags << 8);
+        w[6] = w[7] = w[8] = w[9] = w[10] = w[11] = 0;
+    } else {
+        w[2] = t.a[0]; w[3] = t.a[1]; w[4] = t.a[2]; w[5] = t.a[3];
+        w[6] = t.d[0]; w[7] = t.d[1]; w[8] = t.d[2]; w[9] = t.d[3];
+        w[10] = t.ports; w[11] = t.proto | (t.flags << 8);
+    }
+}
+__device__ __forceinline__ LKey unpack_key(const Rec& r, const uint32_t w[12], Tuple& t) {
+    LKey k;
+    k.dlo = w[0];
+    k.dhi = w[1] & 0xffffu;
+    k.key = (w[1] >> 16) & 0xf;
+    k.mc6 = (w[1] >> 20) & 1;
+    const bool tr = lk_transport(r.proto) && k.key == kMac;
+    t = Tuple{};
+    if (!tr) {
+        k.kw[0] = w[2]; k.kw[1] = w[3]; k.kw[2] = w[4]; k.kw[3] = w[5];
+    } else {
+        k.kw[0] = k.dlo; k.kw[1] = k.dhi; k.kw[2] = 0; k.kw[3] = 0;
+        t.v6 = (w[1] >> 21) & 1;
+        if (!t.v6) {
+            t.a[0] = w[2]; t.d[0] = w[3]; t.ports = w[4]; t.proto = w[5] & 0xff; t.flags = (w[5] >> 8) & 0xff;
+        } else {
+            t.a[0] = w[2]; t.a[1] = w[3]; t.a[2] = w[4]; t.a[3] = w[5];
+            t.d[0] = w[6]; t.d[1] = w[7]; t.d[2] = w[8]; t.d[3] = w[9];
+            t.ports = w[10]; t.proto = w[11] & 0xff; t.flags = (w[11] >> 8) & 0xff;
+        }
+    }
+    return k;
 }
 
 }  // namespace emurx

@@ -131,7 +131,136 @@ __global__ __launch_bounds__(kScanThreads) void k_route_scan(uint32_t* __restric
     }
 }
 
+// ---- partitioned path -------------------------------------------------------------------
+// k_route_lk: k_route<true> for the 80-byte lookup records of k_rx kind 2 (every record that
+// reached a callback goes to the owner of its CTunnelKey; k_rx took the per-tile counts)
+__global__ __launch_bounds__(kBlock) void k_route_lk(const emurx_lookup_rec* __restrict__ lk, uint32_t n,
+                                                     uint32_t n_parts, const uint32_t* __restrict__ tile_cnt,
+                                                     const uint32_t* __restrict__ grp_off,
+                                                     emurx_lookup_rec* __restrict__ send, uint32_t cap) {
+    __shared__ uint32_t s_wcnt[kWaves][16];
+    __shared__ uint32_t s_toff[EMURX_MAX_PARTS];
+    const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / kWave, tile = blockIdx.x;
+    const uint32_t i = tile * kBlock + tid;
+    if (lane < 16) s_wcnt[wv][lane] = 0;
+    const uint4* p = reinterpret_cast<const uint4*>(lk + (i < n ? i : 0));
+    uint4 a = make_uint4(0, 0, 0, 0), b = make_uint4(0, 0, 0, EMURX_ST_HOLE);
+    if (i < n) {
+        a = p[0];
+        b = p[1];
+    }
+    // {src index, src rank, vlan0, vlan1} {vport | l3 << 16, l4 | l7 << 16, .., status | flags << 8}
+    const bool ok = i < n && (b.w & 0xffu) == EMURX_ST_OK;
+    const uint32_t d = ok ? emurx_owner(emurx_tk_hash(b.x & 0xffffu, a.z, a.w), n_parts) : 0xffu;
+    if (wv == 0) {  // this tile's offset: group offset + the group's earlier tiles
+        const uint32_t g0 = tile & ~(kGroup - 1);
+        uint4 x = make_uint4(0, 0, 0, 0), y = x;
+        if (g0 + lane < tile) {
+            const uint4* q = reinterpret_cast<const uint4*>(tile_cnt + (g0 + lane) * 16);
+            x = q[0];
+            y = q[1];
+        }
+        const uint32_t c[EMURX_MAX_PARTS] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+#pragma unroll
+        for (uint32_t k = 0; k < EMURX_MAX_PARTS; ++k) {
+            if (k >= n_parts) break;
+            const uint32_t sum = wave_reduce(c[k], [](uint32_t u, uint32_t v) { return u + v; });
+            if (lane == 0) s_toff[k] = grp_off[(tile / kGroup) * 16 + k] + sum;
+        }
+    }
+    uint32_t rank = 0;
+    uint64_t left = __ballot(d != 0xffu);
+    while (left) {
+        const uint32_t lead = (uint32_t)__ffsll((long long)left) - 1;
+        const uint32_t dd = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)lead);
+        const uint64_t m = __ballot(d == dd);
+        if (d == dd) rank = mbcnt(m);
+        if (lane == lead) s_wcnt[wv][dd] = (uint32_t)__popcll(m);
+        left &= ~m;
+    }
+    __syncthreads();
+    if (d == 0xffu) return;
+    uint32_t pos = s_toff[d] + rank;
+    for (uint32_t w = 0; w < wv; ++w) pos += s_wcnt[w][d];
+    if (pos >= cap) return;  // overflow: send_count[d] > cap tells the caller
+    const uint4 k0 = p[2], k1 = p[3], k2 = p[4];
+    uint4* o = reinterpret_cast<uint4*>(send + (size_t)d * cap + pos);  // 80 B, 16-B aligned
+    o[0] = a;
+    o[1] = b;
+    o[2] = k0;
+    o[3] = k1;
+    o[4] = k2;
+}
+
+// k_lookup: the owner's half — GetNs + the callback's client rule + the flow decision for
+// every received lookup record, against this partition's tables (classify()'s resolve).
+// Output slot j = the input slot: n_parts regions of cap emurx_route_rec, valid up to
+// recv_count[source].
+__global__ __launch_bounds__(kBlock) void k_lookup(const emurx_lookup_rec* __restrict__ recv,
+                                                   const uint32_t* __restrict__ recv_count, uint32_t n_parts,
+                                                   uint32_t cap, emurx_dev_tables T,
+                                                   emurx_route_rec* __restrict__ out, uint32_t* __restrict__ flow) {
+    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t src = (uint32_t)(j / cap), idx = (uint32_t)(j % cap);
+    if (src >= n_parts || idx >= recv_count[src]) return;
+    const uint4* p = reinterpret_cast<const uint4*>(recv + j);
+    const uint4 a = p[0], b = p[1], k0 = p[2], k1 = p[3], k2 = p[4];
+    Rec r;
+    r.ns = EMURX_ID_NONE;
+    r.cl = EMURX_ID_NONE;
+    r.vlan0 = a.z;
+    r.vlan1 = a.w;
+    r.vport = b.x & 0xffffu;
+    r.l3 = b.x >> 16;
+    r.l4 = b.y & 0xffffu;
+    r.l7 = b.y >> 16;
+    r.l7len = b.z & 0xffffu;
+    r.nh = (b.z >> 16) & 0xffu;
+    r.proto = b.z >> 24;
+    r.status = b.w & 0xffu;
+    r.flags = (b.w >> 8) & 0xffu;
+    r.dlen = 0;
+    r.flow = EMURX_FLOW_NONE;
+    const uint32_t w[12] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w, k2.x, k2.y, k2.z, k2.w};
+    Tuple t;
+    const LKey k = unpack_key(r, w, t);
+    resolve(T, r, k, [&](uint32_t cid) { return flow_probe(T, t, cid); });
+    uint2* o = reinterpret_cast<uint2*>(out + j);  // 40 B, 8-B aligned
+    o[0] = make_uint2(r.ns, r.cl);
+    o[1] = make_uint2(r.vlan0, r.vlan1);
+    o[2] = make_uint2(b.x, b.y);
+    o[3] = make_uint2(b.z, r.status | (r.flags << 8));
+    o[4] = make_uint2(a.x, a.y);
+    if (flow) flow[j] = r.flow;
+}
+
 }  // namespace emurx
+
+int emurx_launch_route_lk(const emurx_lookup_rec* lk, uint32_t n, uint32_t n_parts, uint32_t cap,
+                          emurx_lookup_rec* send, uint32_t* send_count, uint32_t* tile_cnt, uint32_t* grp,
+                          uint32_t* grp_off, hipStream_t st) {
+    using namespace emurx;
+    const uint32_t ntiles = (n + kBlock - 1) / kBlock, ngroups = (ntiles + kGroup - 1) / kGroup;
+    if (n == 0) return hipMemsetAsync(send_count, 0, n_parts * sizeof(uint32_t), st) == hipSuccess ? 0 : -1;
+    if (ngroups > kScanThreads) return -1;
+    hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(kScanThreads), 0, st, grp, ngroups, n_parts, grp_off, send_count);
+    hipLaunchKernelGGL(k_route_lk, dim3(ntiles), dim3(kBlock), 0, st, lk, n, n_parts, (const uint32_t*)tile_cnt,
+                       (const uint32_t*)grp_off, send, cap);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int emurx_launch_lookup(const emurx_lookup_rec* recv, const uint32_t* recv_count, uint32_t n_parts, uint32_t cap,
+                        const emurx_dev_tables& T, emurx_route_rec* out, uint32_t* flow, hipStream_t st) {
+    using namespace emurx;
+    const uint64_t slots = (uint64_t)n_parts * cap;
+    if (slots) {
+        const uint64_t g = (slots + kBlock - 1) / kBlock;
+        if (g > 0x7fffffffu) return -1;
+        hipLaunchKernelGGL(k_lookup, dim3((uint32_t)g), dim3(kBlock), 0, st, recv, recv_count, n_parts, cap, T, out,
+                           flow);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 int emurx_launch_route(const emurx_rec* rec, uint32_t n, uint32_t n_parts, uint32_t my_rank, uint32_t cap,
                        emurx_route_rec* send, uint32_t* send_count, uint32_t* tile_cnt, uint32_t* grp,

@@ -28,6 +28,10 @@
 #endif
 
 #define EMURX_EMPTY 0xFFFFFFFFu
+// a deleted slot: value EMURX_TOMB, every key word 0xFFFFFFFF (no probe key ever equals it:
+// vport words are < 0x10000, Namespace and client ids < EMURX_ID_NONE); a probe walks past
+// it and only a bucket with an EMPTY slot ends a chain
+#define EMURX_TOMB 0xFFFFFFFEu
 #define EMURX_BUCKET_WORDS 16u  // 64 B
 
 // 32-bit mix of up to five key words (murmur3 finaliser over a multiplicative combine).
@@ -53,11 +57,11 @@ EMURX_HD uint32_t emurx_hash(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uin
 //  ip6  [8]: ns_id, ip[0..3], ip[4..7], ip[8..11], ip[12..15], mac[0..3], mac[4..5] | client_plugins << 16,
 //            client_id
 //  (the client's MAC and plugin mask in the IP slots answer IsUnicastToMe / PluginCtx.Get)
-//  ns_info   [4]: plugin_mask, first_client, 0, 0
-//  client    [8]: mac_lo, mac_hi, plugin_mask, ra (bit0 has_ra, bits 8..15 prefix_len),
-//                 ra_prefix[0..3], ra_prefix[4..7], 0, 0
+//  ns_info   [4]: plugin_mask, first_client, 0, 0            (dense, indexed by ns id)
+//  ci   [8]: client_id, plugin_mask, ra (bit0 has_ra, bits 8..15 prefix_len), ra_prefix[0..3],
+//            ra_prefix[4..7], has_transport_ctx, 0, 0      (hashed by client id, 2 per bucket)
 // Home buckets: ns = tk & ns_mask; client tables = hash(tk, address) & mask, where
-// tk = emurx_tk_hash(CTunnelKey words) of the client's Namespace.
+// tk = emurx_tk_hash(CTunnelKey words) of the client's Namespace; ci = emurx_ci_hash(id).
 EMURX_HD uint32_t emurx_tk_hash(uint32_t w0, uint32_t w1, uint32_t w2) {
     return emurx_hash(w0, w1, w2, 0x6E73u, 0);
 }
@@ -69,6 +73,9 @@ EMURX_HD uint32_t emurx_ip4_hash(uint32_t tk, uint32_t ip) {
 }
 EMURX_HD uint32_t emurx_ip6_hash(uint32_t tk, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
     return emurx_hash(tk, a ^ 0x697036u, b, c, d);
+}
+EMURX_HD uint32_t emurx_ci_hash(uint32_t cid) {
+    return emurx_hash(cid, 0x63696eu, 0, 0, 0);
 }
 
 // Transport tables (TransportCtx.ftv4 / ftv6 / serverCb, src/emu/plugins/transport/
@@ -94,9 +101,9 @@ struct emurx_dev_tables {
     const uint32_t* mac_tab;  // [mac_mask + 1] buckets of 4 slots
     const uint32_t* ip4_tab;  // [ip4_mask + 1] buckets of 2 slots
     const uint32_t* ip6_tab;  // [ip6_mask + 1] buckets of 2 slots
-    const uint32_t* client;   // 8 words per client id
+    const uint32_t* ci_tab;   // [ci_mask + 1] buckets of 2 client-info slots
     uint32_t ns_mask, mac_mask, ip4_mask, ip6_mask;  // bucket count - 1
-    uint32_t max_ns, max_clients;
+    uint32_t ci_mask, max_ns;
     uint32_t cb_mask;         // registered callbacks (Parser.Register)
     uint32_t ft_on;           // any client has a TransportCtx: resolve transport flows
     const uint32_t* ft4_tab;  // [ft4_mask + 1] buckets of 2 slots

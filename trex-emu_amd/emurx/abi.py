@@ -71,6 +71,11 @@ REC_DTYPE = np.dtype([
 assert REC_DTYPE.itemsize == 32
 ROUTE_REC_DTYPE = np.dtype([("rec", REC_DTYPE), ("src_index", "<u4"), ("src_rank", "<u4")])
 assert ROUTE_REC_DTYPE.itemsize == 40
+# emurx_lookup_rec: the parsed record (ns_id = source frame index, client_id = source rank) +
+# the callback rule's lookup key words (owner-partitioned classification)
+LOOKUP_REC_DTYPE = np.dtype([("rec", REC_DTYPE), ("key", "<u4", 12)])
+assert LOOKUP_REC_DTYPE.itemsize == 80
+ST_HOLE = 0xFF     # EMURX_ST_HOLE: status of the record of an empty descriptor slot
 MAX_PARTS = 8
 DESC_DTYPE = np.dtype([("off", "<u4"), ("len", "<u2"), ("vport", "u1"), ("pad", "u1")])
 assert DESC_DTYPE.itemsize == 8
@@ -167,7 +172,17 @@ SIGNATURES = [
     ("emurx_last_stage", C.c_uint32, [_P]),
     ("emurx_ns_owner", C.c_uint32, [_U8P, C.c_uint32]),
     ("emurx_route_dev", C.c_int, [_P, _P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P]),
-    ("emurx_set_route_parts", C.c_int, [_P, C.c_uint32]),
+    ("emurx_classify_route_dev", C.c_int, [_P, _P, _P, C.c_uint32, C.POINTER(DevOut), C.c_uint32, C.c_uint32,
+                                           C.c_uint32, _P, _P, _P]),
+    ("emurx_parse_route_dev", C.c_int, [_P, _P, _P, C.c_uint32, C.POINTER(DevOut), C.c_uint32, C.c_uint32,
+                                        C.c_uint32, _P, _P, _P]),
+    ("emurx_lookup_dev", C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint32, _P, _P, _P]),
+    ("emurx_set_partition", C.c_int, [_P, C.c_uint32, C.c_uint32]),
+    ("emurx_table_gen", C.c_uint64, [_P]),
+    ("emurx_recs_stale", C.c_int, [_P, _P, C.c_uint32, C.c_uint64, _P]),
+    ("emurx_image_lookup", C.c_int, [_P, C.c_uint32, _P, C.POINTER(C.c_uint32)]),
+    ("emurx_image_check", C.c_int, [_P, C.POINTER(C.c_uint64)]),
+    ("emurx_table_stats", C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("emurx_ingest_buffer", C.c_int, [_P, C.c_uint32, C.c_size_t, C.POINTER(C.c_void_p)]),
     ("emurx_ingest_submit", C.c_int, [_P, C.c_uint32, _P, C.c_uint32]),
     ("emurx_ingest_wait", C.c_int, [_P, C.c_uint32, C.POINTER(IngestResult)]),

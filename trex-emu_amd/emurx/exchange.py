@@ -35,15 +35,19 @@ def grow(cap: int, counts) -> int:
     return max(cap, m + m // 16 + 1024)
 
 
-def exchange(send, send_count, cap: int, group=None):
-    """Equal-split all-to-all of `send` ([world * cap * 40] uint8 tensor) and `send_count`
+LOOKUP_BYTES = abi.LOOKUP_REC_DTYPE.itemsize
+
+
+def exchange(send, send_count, cap: int, group=None, rec_bytes: int = REC_BYTES):
+    """Equal-split all-to-all of `send` ([world * cap * rec_bytes] uint8 tensor: emurx_route_rec
+    regions, or emurx_lookup_rec regions with rec_bytes = LOOKUP_BYTES) and `send_count`
     ([world] int32 tensor).  Returns (recv, recv_count) on the device of the inputs."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    assert send.numel() == world * cap * REC_BYTES and send_count.numel() == world
+    assert send.numel() == world * cap * rec_bytes and send_count.numel() == world
     if dist.get_backend(group) == "gloo" and send.is_cuda:
-        r, c = exchange(send.cpu(), send_count.cpu(), cap, group)
+        r, c = exchange(send.cpu(), send_count.cpu(), cap, group, rec_bytes)
         return r.to(send.device), c.to(send.device)
     recv = torch.empty_like(send)
     recv_count = torch.empty_like(send_count)

@@ -32,6 +32,8 @@ def _p(a):
 
 
 class RxPath:
+    """device < 0: a host-only handle (table mirror, generations, image queries; no GPU)."""
+
     def __init__(self, device: int = 0, max_ns: int = 4096, max_clients: int = 65536,
                  max_frames: int = 1 << 20, max_bytes: int = 1 << 20):
         self.lib = abi.load()
@@ -242,16 +244,71 @@ class RxPath:
                                                    _addr(msg_off), _addr(info), _stream(stream)), "tx_zmq_dev")
 
     # ---- Namespace-partitioned exchange ---------------------------------------------------
-    def set_route_parts(self, n_parts: int):
-        """Fuse route_dev's counting pass into the following classify launches
-        (include/emu_rx.h emurx_set_route_parts); 0 turns it off."""
-        return abi.check(self.lib.emurx_set_route_parts(self.h, n_parts), "set_route_parts")
+    def classify_route_dev(self, frames, desc, n: int, rec, qlist, qcap: int, tile_cnt, hist, n_parts: int,
+                           my_rank: int, cap: int, send, send_count, stream=None, flow=None):
+        """classify_dev + route_dev in one call, the route's counting pass inside k_rx
+        (include/emu_rx.h emurx_classify_route_dev)."""
+        out = abi.DevOut(_addr(rec), _addr(qlist), qcap, _addr(tile_cnt), _addr(hist), _addr(flow))
+        return abi.check(self.lib.emurx_classify_route_dev(self.h, _addr(frames), _addr(desc), n, C.byref(out),
+                                                           n_parts, my_rank, cap, _addr(send), _addr(send_count),
+                                                           _stream(stream)), "classify_route_dev")
 
     def route_dev(self, rec, n: int, n_parts: int, my_rank: int, cap: int, send, send_count, stream=None):
         """Pack the batch's records with a Namespace into their owners' send regions
         (send[d*cap:][:send_count[d]], frame order; include/emu_rx.h emurx_route_dev)."""
         return abi.check(self.lib.emurx_route_dev(self.h, _addr(rec), n, n_parts, my_rank, cap, _addr(send),
                                                   _addr(send_count), _stream(stream)), "route_dev")
+
+    # ---- owner-partitioned classification ----------------------------------------------------
+    def set_partition(self, n_parts: int, part: int):
+        """Device tables hold only the Namespaces this partition owns (emurx_set_partition)."""
+        return abi.check(self.lib.emurx_set_partition(self.h, n_parts, part), "set_partition")
+
+    def parse_route_dev(self, frames, desc, n: int, rec, qlist, qcap: int, tile_cnt, hist, n_parts: int,
+                        my_rank: int, cap: int, send, send_count, stream=None):
+        """Parse + lookup keys, packed into the owners' regions as LOOKUP_REC_DTYPE (80 B)."""
+        out = abi.DevOut(_addr(rec), _addr(qlist), qcap, _addr(tile_cnt), _addr(hist), None)
+        return abi.check(self.lib.emurx_parse_route_dev(self.h, _addr(frames), _addr(desc), n, C.byref(out),
+                                                        n_parts, my_rank, cap, _addr(send), _addr(send_count),
+                                                        _stream(stream)), "parse_route_dev")
+
+    def lookup_dev(self, recv, recv_count, n_parts: int, cap: int, out, flow=None, stream=None):
+        """The owner's lookups over received LOOKUP_REC_DTYPE regions -> ROUTE_REC_DTYPE slots."""
+        return abi.check(self.lib.emurx_lookup_dev(self.h, _addr(recv), _addr(recv_count), n_parts, cap,
+                                                   _addr(out), _addr(flow), _stream(stream)), "lookup_dev")
+
+    # ---- table generations / image diagnostics -------------------------------------------------
+    def table_gen(self) -> int:
+        return int(self.lib.emurx_table_gen(self.h))
+
+    def recs_stale(self, rec: np.ndarray, gen: int) -> np.ndarray:
+        """emurx_recs_stale: 1 where a record may differ from the live tables' answer."""
+        r = np.ascontiguousarray(rec, dtype=abi.REC_DTYPE)
+        out = np.zeros(max(len(r), 1), np.uint8)
+        abi.check(self.lib.emurx_recs_stale(self.h, _p(r) if len(r) else None, len(r), gen, _p(out)),
+                  "recs_stale")
+        return out[: len(r)]
+
+    def image_lookup(self, table: int, key) -> int | None:
+        k = np.ascontiguousarray(key, dtype=np.uint32)
+        v = C.c_uint32()
+        rc = self.lib.emurx_image_lookup(self.h, table, _p(k), C.byref(v))
+        if rc == abi.EMURX_ENOENT:
+            return None
+        abi.check(rc, "image_lookup")
+        return v.value
+
+    def image_check(self) -> int:
+        """32-bit words where the device tables differ from the host image (0 = in sync)."""
+        v = C.c_uint64()
+        abi.check(self.lib.emurx_image_check(self.h, C.byref(v)), "image_check")
+        return v.value
+
+    def table_stats(self) -> dict:
+        """Blocks shipped as deltas, whole tables uploaded, bytes of the device tables."""
+        a, b, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        abi.check(self.lib.emurx_table_stats(self.h, C.byref(a), C.byref(b), C.byref(c)), "table_stats")
+        return dict(delta_blocks=a.value, whole_tables=b.value, table_bytes=c.value)
 
 
 def ns_owner(key: bytes, n_parts: int) -> int:
