@@ -273,7 +273,7 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
     from emurx.rx import RxPath
     w = workload(cfg, n, rank)
     max_ns = max(4096, len(w["ns"]))
-    max_cl = max(65536, len(w["clients"]["cid"]) + 8192)  # spare ids for --table-updates
+    max_cl = max(65536, len(w["clients"]["cid"]) + (8192 if a.table_updates else 0))  # spare ids
     rx = RxPath(local, max_ns=max_ns, max_clients=max_cl, max_frames=n)
     rx.register_all()
     if mode == "partitioned":
@@ -557,13 +557,13 @@ def grow_cap(xch, world, dist, torch, dev):
 def xcheck(xch, rec, n, world, rank, dist, torch, dev, mode):
     """Exchange sanity (counts only; the packing is parity-tested in tests/): every routed
     record arrives once, within capacity (replicated: records with a Namespace; partitioned:
-    every record that reached a callback)."""
+    every frame's lookup record)."""
     import numpy as np
     from emurx import abi
     cnt = xch["recv_count"].cpu().numpy().astype(np.int64)
     assert (cnt <= xch["cap"]).all(), f"exchange overflow {cnt} > {xch['cap']}"
     r = rec.cpu().numpy().view(abi.REC_DTYPE)
-    sent = (r["ns_id"] != abi.ID_NONE).sum() if mode == "replicated" else (r["status"] == 0).sum()
+    sent = (r["ns_id"] != abi.ID_NONE).sum() if mode == "replicated" else len(r)
     routed = torch.tensor([int(sent), int(cnt.sum())], dtype=torch.int64)
     if world > 1:
         routed = routed.to(dev) if dist.get_backend() == "nccl" else routed

@@ -554,12 +554,11 @@ int emurx_classify_route_dev(emurx_t* h, const uint8_t* d_frames, const emurx_de
 /* ---- owner-partitioned classification ---------------------------------
    With partitioned tables (emurx_set_partition) the lookups run on the GPU that owns the
    frame's Namespace.  The receiving GPU parses its shard and derives each frame's lookup key
-   (emurx_parse_route_dev); every frame that reached a callback travels, as an 80-byte
-   emurx_lookup_rec, to the owner of its CTunnelKey (an equal-split all-to-all, as for
-   emurx_route_rec); the owner resolves Namespace, Client and flow against its partition
-   (emurx_lookup_dev).  The owner's output for a frame equals emurx_classify_dev's record for
-   it on replicated tables, bit for bit (frames whose Namespace is unknown come back with
-   ns_id EMURX_ID_NONE and lookup EMURX_LK_NO_NS instead of staying on the receiving GPU). */
+   (emurx_parse_route_dev); every frame travels, as an 80-byte emurx_lookup_rec, to the owner
+   of its CTunnelKey (an equal-split all-to-all, as for emurx_route_rec); the owner resolves
+   Namespace, Client and flow against its partition for the frames that reached a callback
+   (emurx_lookup_dev) and keeps the records of the others as parsed.  The owner's output for a
+   frame equals emurx_classify_dev's record for it on replicated tables, bit for bit. */
 typedef struct emurx_lookup_rec {
     emurx_rec rec;     /* the parsed record, with ns_id = source frame index and
                           client_id = source rank (the lookups fill them at the owner)    */
@@ -568,9 +567,11 @@ typedef struct emurx_lookup_rec {
                           c5tuplekey + TCP flags of the flow decision (emurx_parse.h)     */
 } emurx_lookup_rec;    /* 80 bytes */
 /* Parse the batch (records without lookups into out->rec when non-NULL, queues, histogram as
-   emurx_parse_dev) and pack the lookup record of every frame that reached a callback into
-   the region of its Namespace's owner: d_send[d * cap ..  + d_send_count[d]), frame order.
-   Reads no table.  Counts > cap: overflow as in emurx_route_dev. */
+   emurx_parse_dev) and pack the lookup record of every frame (holes excepted) into the region
+   of its Namespace's owner: d_send[d * cap ..  + d_send_count[d]), frame order.  Three
+   launches: the owner counts from each frame's L2 header (8 bytes), their group scan, and
+   k_rx writing each lookup record at its final place.  Reads no table.  Counts > cap:
+   overflow as in emurx_route_dev. */
 int emurx_parse_route_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_desc, uint32_t n,
                           const emurx_dev_out* out, uint32_t n_parts, uint32_t my_rank, uint32_t cap,
                           emurx_lookup_rec* d_send, uint32_t* d_send_count, void* stream);

@@ -9,7 +9,7 @@ classification, all bit-exact against the oracle.
 * Partitioned: G handles, each holding one Namespace partition; every shard is parsed and
   its lookup records packed per owner (emurx_parse_route_dev), the all-to-all is played on
   the device, and each owner resolves its records (emurx_lookup_dev).  The owners' output
-  equals the oracle's records of every frame that reached a callback, grouped by owner, and
+  equals the oracle's records of every frame, grouped by owner, and
   the records with a Namespace equal the replicated path's routed records byte for byte;
   the transport flow decisions equal the oracle's.
 """
@@ -142,10 +142,10 @@ def test_mutation_while_batch_in_flight(rxmod):
 
 
 def _owners_by_key(rec, parts):
-    """Owner of every record that reached a callback (its CTunnelKey), 0xFF elsewhere."""
+    """Owner of every record (the CTunnelKey its parse left)."""
     from emurx.rx import ns_owner
     out = np.full(len(rec), 0xFF, np.uint32)
-    ok = np.nonzero(rec["status"] == 0)[0]
+    ok = np.arange(len(rec))
     k = np.stack([rec["vport"][ok].astype(np.uint64), rec["vlan0"][ok].astype(np.uint64),
                   rec["vlan1"][ok].astype(np.uint64)], 1)
     if len(ok):
@@ -155,64 +155,52 @@ def _owners_by_key(rec, parts):
     return out
 
 
-@pytest.mark.parametrize("parts", [2, 4])
-def test_partitioned_lookups_equal_replicated(rxmod, parts):
+def partitioned_vs_oracle(rxmod, shards, load, parts, flows=None):
+    """Shards through the partitioned path (one handle per partition) and through the
+    replicated classify + route, against the oracle.  load(target) fills a table target;
+    flows(targets, orecs) may add transport state to every target."""
     import pyoracle
     import torch
     import route_ref
     from emurx import exchange as X
-    n = 40000
-    shards = [synth.config_c(n, rank=s, syn=0.3) for s in range(parts)]
-    w0 = shards[0]
+    from gpu_util import to_dev
+    n = max(len(w["desc"]) for w in shards)
     o = pyoracle.Oracle()
-    synth.load_tables(w0, o)
+    load(o)
     full = rxmod(0, max_ns=4096, max_clients=65536, max_frames=n)
     full.register_all()
-    synth.load_tables(w0, full)
+    load(full)
     owners = []
     for p in range(parts):
         h = rxmod(0, max_ns=4096, max_clients=65536, max_frames=n)
         h.register_all()
         h.set_partition(parts, p)
-        synth.load_tables(w0, h)
+        load(h)
         owners.append(h)
-    # transport state on every handle and the oracle: flows of shard 0's frames, listeners
-    orecs = [o.rx_batch(w["buf"], w["desc"])[0] for w in shards]
-    tup = frame_tuples(shards[0]["buf"], shards[0]["desc"], orecs[0])
-    rng = np.random.default_rng(0xAB)
-    idx = [i for i, t in enumerate(tup) if t is not None]
-    for i in rng.choice(idx, len(idx) // 3, replace=False):
-        cid = int(orecs[0][i]["client_id"])
-        rcs = {t.flow_add(cid, tup[i], int(i)) for t in [o, full] + owners}
-        assert len(rcs) == 1
-    for i in rng.choice(idx, len(idx) // 5, replace=False):
-        cid, t = int(orecs[0][i]["client_id"]), tup[i]
-        dport = (t[10] << 8 | t[11]) if len(t) == 13 else (t[34] << 8 | t[35])
-        proto = 6 if orecs[0][i]["proto"] == abi.CB_TCP else 17
-        rcs = {x.server_add(cid, dport, proto) for x in [o, full] + owners}
-        assert len(rcs) == 1
+    if flows:
+        flows([o, full] + owners, [o.rx_batch(w["buf"], w["desc"])[0] for w in shards])
     orecs = [o.rx_batch(w["buf"], w["desc"])[0] for w in shards]
     ts_full = full.table_stats()["table_bytes"]
     assert max(h.table_stats()["table_bytes"] for h in owners) < 1.25 * ts_full / parts + (1 << 16)
 
     cap = X.capacity(n, parts)
     send, cnt, rep_send, rep_cnt = [], [], [], []
-    from gpu_util import to_dev
     for s, w in enumerate(shards):
+        m = len(w["desc"])
         buf, desc = to_dev(w["buf"]), to_dev(w["desc"])
-        qcap = abi.queue_cap(n)
-        mk = lambda: (torch.zeros(n * 32, dtype=torch.uint8, device="cuda"),  # noqa: E731
+        qcap = abi.queue_cap(m)
+        mk = lambda: (torch.zeros(m * 32, dtype=torch.uint8, device="cuda"),  # noqa: E731
                       torch.empty(abi.NUM_QUEUES * qcap, dtype=torch.int32, device="cuda"),
-                      torch.empty(abi.ntiles(n) * 16, dtype=torch.int32, device="cuda"),
+                      torch.empty(abi.ntiles(m) * 16, dtype=torch.int32, device="cuda"),
                       torch.zeros(abi.HIST_SHARDS * 2 * abi.HIST_BINS, dtype=torch.int64, device="cuda"))
         rec, ql, tc, hi = mk()
         sd = torch.full((parts * cap * X.LOOKUP_BYTES,), 0xEE, dtype=torch.uint8, device="cuda")
         sc = torch.full((parts,), -1, dtype=torch.int32, device="cuda")
-        owners[s].parse_route_dev(buf, desc, n, rec, ql, qcap, tc, hi, parts, s, cap, sd, sc)
+        owners[s % parts].parse_route_dev(buf, desc, m, rec, ql, qcap, tc, hi, parts, s, cap, sd, sc)
         rrec, rql, rtc, rhi = mk()
         rsd = torch.full((parts * cap * X.REC_BYTES,), 0xEE, dtype=torch.uint8, device="cuda")
         rsc = torch.full((parts,), -1, dtype=torch.int32, device="cuda")
-        full.classify_route_dev(buf, desc, n, rrec, rql, qcap, rtc, rhi, parts, s, cap, rsd, rsc)
+        full.classify_route_dev(buf, desc, m, rrec, rql, qcap, rtc, rhi, parts, s, cap, rsd, rsc)
         torch.cuda.synchronize()
         # the source's parse-only records equal the oracle's parse (no lookups)
         pr = rec.cpu().numpy().view(abi.REC_DTYPE)
@@ -251,6 +239,49 @@ def test_partitioned_lookups_equal_replicated(rxmod, parts):
             assert hasns.tobytes() == route_ref.route(orecs[s], parts, s)[p].tobytes()
             wf = o.flows(shards[s]["buf"], shards[s]["desc"][sel], orecs[s][sel])
             assert np.array_equal(fl[s, : len(sel)], wf), (s, p)
-    # the flow decisions were exercised
+    return o, orecs
+
+
+@pytest.mark.parametrize("parts", [2, 4])
+def test_partitioned_lookups_equal_replicated(rxmod, parts):
+    """Config C shards with bare SYNs, flows and listeners: records and flow decisions."""
+    n = 40000
+    shards = [synth.config_c(n, rank=s, syn=0.3) for s in range(parts)]
+
+    def flows(targets, orecs):
+        tup = frame_tuples(shards[0]["buf"], shards[0]["desc"], orecs[0])
+        rng = np.random.default_rng(0xAB)
+        idx = [i for i, t in enumerate(tup) if t is not None]
+        for i in rng.choice(idx, len(idx) // 3, replace=False):
+            cid = int(orecs[0][i]["client_id"])
+            assert len({t.flow_add(cid, tup[i], int(i)) for t in targets}) == 1
+        for i in rng.choice(idx, len(idx) // 5, replace=False):
+            cid, t = int(orecs[0][i]["client_id"]), tup[i]
+            dport = (t[10] << 8 | t[11]) if len(t) == 13 else (t[34] << 8 | t[35])
+            proto = 6 if orecs[0][i]["proto"] == abi.CB_TCP else 17
+            assert len({x.server_add(cid, dport, proto) for x in targets}) == 1
+    o, orecs = partitioned_vs_oracle(rxmod, shards, lambda t: synth.load_tables(shards[0], t), parts, flows)
     allf = o.flows(shards[0]["buf"], shards[0]["desc"], orecs[0])
     assert (allf <= abi.FLOW_ID_MAX).sum() > 1000 and (allf == abi.FLOW_NEW).sum() > 100
+
+
+def test_partitioned_edge_and_fuzz_frames(rxmod):
+    """Every return path of the parser (edge frames, the golden corpus, fuzzed frames: short
+    frames, tag errors, PPPoE after a tag, three tags ...) through the partitioned path: the
+    owner-count pass routes each frame by the CTunnelKey its full parse leaves."""
+    import edge_frames as E
+    from gpu_util import frames_tables, load_frame_tables
+    from test_gpu_parity import corpus_frames, mutate
+    base = corpus_frames() + [c[1] for c in E.cases()]
+    rng = np.random.default_rng(0x9A27)
+    shards = []
+    for s in range(3):
+        fr = mutate(base, rng, 12000) + base[s::3]
+        buf, desc = F.pack_frames(fr, list(rng.integers(0, 4, len(fr))))
+        shards.append(dict(buf=buf, desc=desc))
+    ns, cl = frames_tables(base, vport=1)
+    for v in (0, 2, 3):  # Namespaces on every vport the shards use
+        n2, _ = frames_tables(base, vport=v)
+        for k in n2:
+            ns.setdefault(k, len(ns))
+    partitioned_vs_oracle(rxmod, shards, lambda t: load_frame_tables([t], ns, cl), 3)

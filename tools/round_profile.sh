@@ -27,6 +27,7 @@ args() {  # bench arguments per config
     B) echo "--steps 200 --warmup 20" ;;
     C) echo "--config C --steps 100 --warmup 10" ;;
     D) echo "--config D --steps 50 --warmup 5" ;;
+    DR) echo "--config D --tables replicated --no-exchange-run --steps 50 --warmup 5" ;;
     E) echo "--config E --steps 50 --warmup 5" ;;
   esac
 }
@@ -39,7 +40,9 @@ for ph in $phases; do
         step bench_$c 600 python bench.py $(args $c) $extra ;;
       prof)
         step prof_$c 300 rocprofv3 --kernel-trace --stats -d $out/prof_$c -o run --output-format csv \
-          -- python bench.py $(args $c) --no-cpu-baseline ;;
+          -- python bench.py $(args $c) --no-cpu-baseline
+        f=$(ls $out/prof_$c/*/run_kernel_stats.csv $out/prof_$c/run_kernel_stats.csv 2>/dev/null | head -n 1)
+        [ -n "$f" ] && cut -d, -f1-4 "$f" | head -n 12 ;;
       pmc)
         for k in FETCH_SIZE WRITE_SIZE; do
           step pmc_${c}_$k 180 rocprofv3 --pmc $k -T --kernel-include-regex k_rx -d $out/pmc_${c}/pmc_$k -o run \

@@ -108,11 +108,11 @@ struct IngestSlot {
     }
 };
 
-// one staging slot of the table-delta ring: pinned entries -> device entries -> k_apply
+// one staging slot of the table-delta ring: pinned entries, read by k_apply over the bus
+// (no copy launch: a delta is a few KiB)
 struct DeltaSlot {
     PinBuf<emurx_delta> h;
-    DevBuf<emurx_delta> d;
-    hipEvent_t ev = nullptr;  // recorded after the k_apply that read d
+    hipEvent_t ev = nullptr;  // recorded after the k_apply that read h
     bool used = false;
 };
 constexpr int kDeltaRing = 4;
@@ -151,7 +151,6 @@ struct emurx_ctx {
     // Namespace-partition packing scratch (emurx_route_dev / emurx_classify_route_dev /
     // emurx_parse_route_dev; one route at a time per handle, stream-ordered)
     DevBuf<uint32_t> d_route_cnt, d_route_grp, d_route_goff;  // grp: zero between batches
-    DevBuf<emurx_lookup_rec> d_lk;  // emurx_parse_route_dev: lookup records in frame order
 
     // k_rx staging slab per launch (emurx_launch_batch): the narrow 6 KiB slab runs 6
     // workgroups per CU instead of 5, but a wave whose frames span 6-7 KiB then takes the
@@ -222,7 +221,7 @@ uint64_t& waited_gen(emurx_t* h, hipStream_t s) {
 // Ship the edited table blocks on `st`: after every stream that read the tables since the
 // last shipment (an event recorded on it now, waited on by st), before every later reader
 // (ship_ev, waited on by each reader stream once).  Edited blocks travel as emurx_delta
-// entries through a ring of pinned + device staging buffers (one H2D copy + one k_apply).
+// entries in a ring of pinned buffers that one k_apply launch reads directly.
 // Whole images (first upload, a rebuilt or grown table, or a quarter of a table edited)
 // are copied synchronously; growing a device table waits for the device first, since
 // batches in flight may still read the old buffer.
@@ -270,7 +269,7 @@ int ship_tables(emurx_t* h, hipStream_t st) {
     if (nd) {
         DeltaSlot& s = h->ring[h->ring_i++ % kDeltaRing];
         if (s.used && hipEventSynchronize(s.ev) != hipSuccess) return EMURX_EDEVICE;
-        if (s.h.alloc(nd) || s.d.alloc(nd)) return EMURX_ENOMEM;
+        if (s.h.alloc(nd)) return EMURX_ENOMEM;
         size_t j = 0;
         for (int k = 0; k <= kNumTabs; ++k) {
             if (img[k]->all) continue;
@@ -281,8 +280,7 @@ int ship_tables(emurx_t* h, hipStream_t st) {
                 memcpy(e.w, &img[k]->img[(size_t)b * EMURX_BUCKET_WORDS], sizeof(e.w));
             }
         }
-        if (hipMemcpyAsync(s.d.p, s.h.p, nd * sizeof(emurx_delta), hipMemcpyHostToDevice, st) != hipSuccess ||
-            emurx_launch_apply(s.d.p, (uint32_t)nd, st) || hipEventRecord(s.ev, st) != hipSuccess)
+        if (emurx_launch_apply(s.h.p, (uint32_t)nd, st) || hipEventRecord(s.ev, st) != hipSuccess)
             return EMURX_EDEVICE;
         s.used = true;
         h->shipped_blocks += nd;
@@ -381,9 +379,10 @@ int route_scratch(emurx_t* h, uint32_t n) {
 }
 
 // one k_rx launch; kind: 0 parse only, 1 classify, 2 parse + lookup keys (partitioned source);
-// rt: the route count pass fused in (emurx_classify_route_dev / emurx_parse_route_dev)
+// rt: kind 1 the route count pass fused in (emurx_classify_route_dev), kind 2 the packing
+// of the lookup records (emurx_parse_route_dev)
 int run_dev(emurx_t* h, const uint8_t* frames, const emurx_desc* desc, uint32_t n, const emurx_dev_out* out,
-            hipStream_t st, int kind, const emurx_route_counts* rt, emurx_lookup_rec* keys) {
+            hipStream_t st, int kind, const emurx_route_args* rt) {
     int rc;
     if (kind == 1 && (rc = prepare_read(h, st))) return rc;
     emurx_dev_tables T = h->tables();
@@ -395,8 +394,7 @@ int run_dev(emurx_t* h, const uint8_t* frames, const emurx_desc* desc, uint32_t 
         h->ev_count = std::min(h->ev_count + 1, h->slots);
     }
     const bool narrow = choose_stage(h);
-    int r = emurx_launch_batch(frames, desc, n, T, kind, *out, st, ev, narrow, h->d_stage_fb.p, h->stage_gen, rt,
-                               keys);
+    int r = emurx_launch_batch(frames, desc, n, T, kind, *out, st, ev, narrow, h->d_stage_fb.p, h->stage_gen, rt);
     if (!r) r = stage_copy_back(h, st);
     return r ? EMURX_EDEVICE : EMURX_OK;
 }
@@ -624,13 +622,12 @@ void emurx_close(emurx_t* h) {
     if (h->ship_ev) (void)hipEventDestroy(h->ship_ev);
     for (auto& s : h->ring) {
         s.h.release();
-        s.d.release();
         if (s.ev) (void)hipEventDestroy(s.ev);
     }
     for (auto e : h->reader_ev) (void)hipEventDestroy(e);
     for (auto& t : h->d_tab) t.release();
     h->d_nsinfo.release();
-    h->d_route_cnt.release(); h->d_route_grp.release(); h->d_route_goff.release(); h->d_lk.release();
+    h->d_route_cnt.release(); h->d_route_grp.release(); h->d_route_goff.release();
     h->d_txz.release();
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
@@ -866,13 +863,13 @@ int emurx_classify_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_
                        const emurx_dev_out* out, void* stream) {
     int rc = check_batch_args(h, d_frames, d_desc, n, out);
     if (rc) return rc;
-    return run_dev(h, d_frames, d_desc, n, out, stream ? (hipStream_t)stream : h->stream, 1, nullptr, nullptr);
+    return run_dev(h, d_frames, d_desc, n, out, stream ? (hipStream_t)stream : h->stream, 1, nullptr);
 }
 int emurx_parse_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_desc, uint32_t n,
                     const emurx_dev_out* out, void* stream) {
     int rc = check_batch_args(h, d_frames, d_desc, n, out);
     if (rc) return rc;
-    return run_dev(h, d_frames, d_desc, n, out, stream ? (hipStream_t)stream : h->stream, 0, nullptr, nullptr);
+    return run_dev(h, d_frames, d_desc, n, out, stream ? (hipStream_t)stream : h->stream, 0, nullptr);
 }
 
 int emurx_classify_route_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_desc, uint32_t n,
@@ -885,8 +882,8 @@ int emurx_classify_route_dev(emurx_t* h, const uint8_t* d_frames, const emurx_de
         return EMURX_EINVAL;
     if ((rc = route_scratch(h, n))) return rc;
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
-    const emurx_route_counts rt{n_parts, h->d_route_cnt.p, h->d_route_grp.p, my_rank};
-    if (n && (rc = run_dev(h, d_frames, d_desc, n, out, st, 1, &rt, nullptr))) return rc;
+    const emurx_route_args rt{n_parts, my_rank, cap, h->d_route_cnt.p, h->d_route_grp.p, nullptr, nullptr};
+    if (n && (rc = run_dev(h, d_frames, d_desc, n, out, st, 1, &rt))) return rc;
     return emurx_launch_route(out->rec, n, n_parts, my_rank, cap, d_send, d_send_count, h->d_route_cnt.p,
                               h->d_route_grp.p, h->d_route_goff.p, st, true)
                ? EMURX_EDEVICE
@@ -902,14 +899,13 @@ int emurx_parse_route_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc*
         (n && (!d_send || cap == 0)) || ((uintptr_t)d_send & 15))
         return EMURX_EINVAL;
     if ((rc = route_scratch(h, n))) return rc;
-    if (h->d_lk.alloc(std::max<size_t>(n, 1))) return EMURX_ENOMEM;
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
-    const emurx_route_counts rt{n_parts, h->d_route_cnt.p, h->d_route_grp.p, my_rank};
-    if (n && (rc = run_dev(h, d_frames, d_desc, n, out, st, 2, &rt, h->d_lk.p))) return rc;
-    return emurx_launch_route_lk(h->d_lk.p, n, n_parts, cap, d_send, d_send_count, h->d_route_cnt.p,
-                                 h->d_route_grp.p, h->d_route_goff.p, st)
-               ? EMURX_EDEVICE
-               : EMURX_OK;
+    // owner counts from the L2 headers + group scan, then k_rx packs at those offsets
+    if (emurx_launch_owner_count(d_frames, d_desc, n, n_parts, d_send_count, h->d_route_cnt.p, h->d_route_grp.p,
+                                 h->d_route_goff.p, st))
+        return EMURX_EDEVICE;
+    const emurx_route_args rt{n_parts, my_rank, cap, h->d_route_cnt.p, h->d_route_grp.p, h->d_route_goff.p, d_send};
+    return n ? run_dev(h, d_frames, d_desc, n, out, st, 2, &rt) : EMURX_OK;
 }
 
 int emurx_lookup_dev(emurx_t* h, const emurx_lookup_rec* d_recv, const uint32_t* d_recv_count, uint32_t n_parts,

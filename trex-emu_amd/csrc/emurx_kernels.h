@@ -11,18 +11,22 @@
 // 64 * 4 words): the sampled tiles' stage feedback, tagged with gen.  Returns 0 or -1.
 // rt (optional, classify only): the route count pass fused into k_rx: per-(tile, owner) counts
 // into cnt[ntiles * 16] and per-group sums added into grp (as emurx_launch_route's first pass).
-// kind: 0 parse only, 1 parse + classify, 2 parse + lookup keys into lk[n] (emurx_lookup_rec:
-// ns_id = frame index, client_id = rt->rank; key words only for frames that reached a callback).
-struct emurx_route_counts {
-    uint32_t parts;
+// kind: 0 parse only, 1 parse + classify, 2 parse + lookup keys.
+// rt (optional): kind 1: the route count pass fused in (per-(tile, owner) counts into cnt,
+// per-group sums added into grp, as emurx_launch_route's first pass); kind 2 (required): the
+// owner counts cnt / group offsets goff of k_owner_count + k_route_scan, and every frame's
+// emurx_lookup_rec (ns_id = frame index, client_id = rank) packed into send[owner * cap + ..).
+struct emurx_route_args {
+    uint32_t parts, rank, cap;
     uint32_t* cnt;
     uint32_t* grp;
-    uint32_t rank;
+    const uint32_t* goff;
+    emurx_lookup_rec* send;
 };
 int emurx_launch_batch(const uint8_t* frames, const emurx_desc* desc, uint32_t n,
                        const emurx_dev_tables& T, int kind, const emurx_dev_out& out,
                        hipStream_t st, const hipEvent_t* ev, bool narrow, uint32_t* fb, uint32_t gen,
-                       const emurx_route_counts* rt = nullptr, emurx_lookup_rec* lk = nullptr);
+                       const emurx_route_args* rt = nullptr);
 
 // One edited 64-byte table block (emurx_api.cpp ship_tables): k_apply copies w to dst.
 struct emurx_delta {
@@ -38,11 +42,12 @@ int emurx_launch_apply(const emurx_delta* d, uint32_t n, hipStream_t st);
 int emurx_launch_route(const emurx_rec* rec, uint32_t n, uint32_t n_parts, uint32_t my_rank, uint32_t cap,
                        emurx_route_rec* send, uint32_t* send_count, uint32_t* tile_cnt, uint32_t* grp,
                        uint32_t* grp_off, hipStream_t st, bool counted = false);
-// The same packing for lookup records (emurx_parse_route_dev): the counts were taken by k_rx
-// kind 2; scan + pack of every record that reached a callback into its owner's region (80 B).
-int emurx_launch_route_lk(const emurx_lookup_rec* lk, uint32_t n, uint32_t n_parts, uint32_t cap,
-                          emurx_lookup_rec* send, uint32_t* send_count, uint32_t* tile_cnt, uint32_t* grp,
-                          uint32_t* grp_off, hipStream_t st);
+// The owner counts of the partitioned source (emurx_parse_route_dev): k_owner_count (the
+// CTunnelKey of every frame from its L2 header alone, counted per (tile, owner) and per group)
+// + k_route_scan -> tile_cnt, grp_off, send_count; k_rx kind 2 then packs.  Two launches.
+int emurx_launch_owner_count(const uint8_t* frames, const emurx_desc* desc, uint32_t n, uint32_t n_parts,
+                             uint32_t* send_count, uint32_t* tile_cnt, uint32_t* grp, uint32_t* grp_off,
+                             hipStream_t st);
 // The owner side (emurx_lookup_dev): one lane per received slot, n_parts regions of cap.
 int emurx_launch_lookup(const emurx_lookup_rec* recv, const uint32_t* recv_count, uint32_t n_parts, uint32_t cap,
                         const emurx_dev_tables& T, emurx_route_rec* out, uint32_t* flow, hipStream_t st);

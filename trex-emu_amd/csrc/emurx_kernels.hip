@@ -30,7 +30,8 @@ __device__ __forceinline__ void glds16(const uint4* src, uint4* dst_wave_base) {
 __device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0)
 
 // kKind: 0 parse only, 1 parse + classify, 2 parse + lookup keys (the partitioned source:
-// an emurx_lookup_rec per frame into lk, no table reads)
+// every frame's emurx_lookup_rec packed straight into its Namespace owner's send region, at
+// the offsets the owner-count pass (k_owner_count + k_route_scan) fixed; no table reads)
 template <int kKind, uint32_t kStage>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage == kStageNarrow ? 6 : 5))) void k_rx(const uint8_t* __restrict__ frames,
                                                const emurx_desc* __restrict__ desc, uint32_t n,
@@ -39,9 +40,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
                                                uint32_t* __restrict__ tile_cnt,
                                                unsigned long long* __restrict__ hist,
                                                uint32_t* __restrict__ flow, uint32_t* __restrict__ fb,
-                                               uint32_t gen, uint32_t rt_parts, uint32_t* __restrict__ rt_cnt,
-                                               uint32_t* __restrict__ rt_grp, uint32_t rt_rank,
-                                               emurx_lookup_rec* __restrict__ lk) {
+                                               uint32_t gen, emurx_route_args rt) {
     constexpr bool kClassify = kKind == 1;
     constexpr uint32_t kWinVec = kStage / 16 / kWave;  // window path: 16-byte vectors per lane
     __shared__ __attribute__((aligned(16))) uint32_t slab[kWaves * kStage / 4];
@@ -56,6 +55,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
     s_hist[wv][lane] = 0;  // each wave owns its copy: no cross-wave ordering needed
     if (lane < 16) s_wcnt[wv][lane] = 0;
     if (lane < EMURX_MAX_PARTS) s_rcnt[wv][lane] = 0;
+    __shared__ uint32_t s_toff[EMURX_MAX_PARTS];  // kKind 2: this tile's offset in each region
+    if (kKind == 2 && wv == 0) tile_offsets(rt.cnt, rt.goff, rt.parts, tile, lane, s_toff, [](uint32_t v) { return wave_sum_u32(v); });
 
     const uint2 dd = i < n ? *reinterpret_cast<const uint2*>(desc + i) : make_uint2(0, EMURX_DESC_HOLE << 24);
     const bool valid = (dd.y >> 24) != EMURX_DESC_HOLE;  // an empty slot is no frame at all
@@ -130,19 +131,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
         __builtin_nontemporal_store(v4u{h0.x, h0.y, h0.z, h0.w}, reinterpret_cast<v4u*>(o));
         __builtin_nontemporal_store(v4u{h1.x, h1.y, h1.z, h1.w}, reinterpret_cast<v4u*>(o + 1));
     }
-    if (kKind == 2 && i < n) {  // the lookup record: ns_id = frame index, client_id = source rank
-        const bool ok = valid && r.status == EMURX_ST_OK;
-        v4u* o = reinterpret_cast<v4u*>(lk + i);
-        o[0] = valid ? v4u{i, rt_rank, r.vlan0, r.vlan1} : v4u{i, rt_rank, 0, 0};
-        o[1] = valid ? v4u{r.vport | (r.l3 << 16), r.l4 | (r.l7 << 16), r.l7len | (r.nh << 16) | (r.proto << 24),
-                           r.status | (r.flags << 8)}
-                     : v4u{0, 0, (uint32_t)EMURX_CB_NONE << 24, EMURX_ST_HOLE};
-        if (ok) {
-            o[2] = v4u{kwd[0], kwd[1], kwd[2], kwd[3]};
-            o[3] = v4u{kwd[4], kwd[5], kwd[6], kwd[7]};
-            o[4] = v4u{kwd[8], kwd[9], kwd[10], kwd[11]};
-        }
-    }
     if (flow && i < n) flow[i] = valid ? r.flow : EMURX_FLOW_NONE;
     // outcome histogram into the wave's LDS copy: a wave whose frames all share one
     // (status, proto) bin adds its count (ballot) and byte sum (DPP reduction) once, instead
@@ -177,25 +165,42 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
     // the route count pass fused in (emurx_set_route_parts): the owner GPU of every record
     // with a Namespace, counted per (tile, owner) and per group of 64 tiles as k_route<false>
     // counts them (emurx_route.hip)
-    if (rt_cnt) {
-        // classify: records whose Namespace was found; lookup keys: every frame that reached
-        // a callback (its Namespace is resolved by the owner)
-        const bool routed = valid && (kKind == 2 ? r.status == EMURX_ST_OK : r.ns != EMURX_ID_NONE);
-        const uint32_t d = routed ? emurx_owner(emurx_tk_hash(r.vport, r.vlan0, r.vlan1), rt_parts) : 0xffu;
-        uint64_t rl = __ballot(d != 0xffu);
+    // Namespace owners (rt.parts > 0): kind 1 counts the records whose Namespace was found
+    // (the first pass of emurx_route_dev, fused); kind 2 packs every frame's lookup record
+    // into its owner's region, ranked by ballots like the queues
+    uint32_t rrank = 0, rd = 0xffu;
+    if ((kKind == 1 && rt.cnt) || kKind == 2) {
+        const bool routed = valid && (kKind == 2 || r.ns != EMURX_ID_NONE);
+        rd = routed ? emurx_owner(emurx_tk_hash(r.vport, r.vlan0, r.vlan1), rt.parts) : 0xffu;
+        uint64_t rl = __ballot(rd != 0xffu);
         while (rl) {
             const uint32_t lead = (uint32_t)__ffsll((long long)rl) - 1;
-            const uint32_t dd = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)lead);
-            const uint64_t m = __ballot(d == dd);
+            const uint32_t dd = (uint32_t)__builtin_amdgcn_readlane((int)rd, (int)lead);
+            const uint64_t m = __ballot(rd == dd);
+            if (rd == dd) rrank = mbcnt(m);
             if (lane == lead) s_rcnt[wv][dd] = (uint32_t)__popcll(m);
             rl &= ~m;
         }
     }
     __syncthreads();
-    if (rt_cnt && tid < 16) {
-        const uint32_t c = tid < rt_parts ? s_rcnt[0][tid] + s_rcnt[1][tid] + s_rcnt[2][tid] + s_rcnt[3][tid] : 0u;
-        rt_cnt[(size_t)tile * 16 + tid] = c;
-        if (c) atomicAdd(&rt_grp[(tile / 64) * 16 + tid], c);
+    if (kKind == 1 && rt.cnt && tid < 16) {
+        const uint32_t c = tid < rt.parts ? s_rcnt[0][tid] + s_rcnt[1][tid] + s_rcnt[2][tid] + s_rcnt[3][tid] : 0u;
+        rt.cnt[(size_t)tile * 16 + tid] = c;
+        if (c) atomicAdd(&rt.grp[(tile / 64) * 16 + tid], c);
+    }
+    if (kKind == 2 && rd != 0xffu) {  // the lookup record: ns_id = frame index, client_id = source rank
+        uint32_t pos = s_toff[rd] + rrank;
+        for (uint32_t w = 0; w < wv; ++w) pos += s_rcnt[w][rd];
+        if (pos < rt.cap) {  // overflow: send_count[d] > cap tells the caller
+            const bool ok = r.status == EMURX_ST_OK;
+            v4u* o = reinterpret_cast<v4u*>(rt.send + (size_t)rd * rt.cap + pos);
+            o[0] = v4u{i, rt.rank, r.vlan0, r.vlan1};
+            o[1] = v4u{r.vport | (r.l3 << 16), r.l4 | (r.l7 << 16), r.l7len | (r.nh << 16) | (r.proto << 24),
+                       r.status | (r.flags << 8)};
+            o[2] = ok ? v4u{kwd[0], kwd[1], kwd[2], kwd[3]} : v4u{0, 0, 0, 0};
+            o[3] = ok ? v4u{kwd[4], kwd[5], kwd[6], kwd[7]} : v4u{0, 0, 0, 0};
+            o[4] = ok ? v4u{kwd[8], kwd[9], kwd[10], kwd[11]} : v4u{0, 0, 0, 0};
+        }
     }
 
     // this tile's segment of every queue: frames in (wave, lane) order == frame order
@@ -249,7 +254,7 @@ int emurx_launch_apply(const emurx_delta* d, uint32_t n, hipStream_t st) {
 int emurx_launch_batch(const uint8_t* frames, const emurx_desc* desc, uint32_t n,
                        const emurx_dev_tables& T, int kind, const emurx_dev_out& out,
                        hipStream_t st, const hipEvent_t* ev, bool narrow, uint32_t* fb, uint32_t gen,
-                       const emurx_route_counts* rt, emurx_lookup_rec* lk) {
+                       const emurx_route_args* rt) {
     using namespace emurx;
     if (ev) (void)hipEventRecord(ev[0], st);
     if (n) {
@@ -258,9 +263,9 @@ int emurx_launch_batch(const uint8_t* frames, const emurx_desc* desc, uint32_t n
         auto k = kind == 1 ? (narrow ? k_rx<1, kStageNarrow> : k_rx<1, kStageWide>)
                : kind == 2 ? (narrow ? k_rx<2, kStageNarrow> : k_rx<2, kStageWide>)
                            : (narrow ? k_rx<0, kStageNarrow> : k_rx<0, kStageWide>);
+        const emurx_route_args none{};
         hipLaunchKernelGGL(k, g, b, 0, st, frames, desc, n, T, out.rec, out.qlist, out.qcap, out.tile_cnt, hist,
-                           out.flow, fb, gen, rt ? rt->parts : 0u, rt ? rt->cnt : nullptr, rt ? rt->grp : nullptr,
-                           rt ? rt->rank : 0u, lk);
+                           out.flow, fb, gen, rt ? *rt : none);
     }
     if (ev) (void)hipEventRecord(ev[1], st);
     return hipGetLastError() == hipSuccess ? 0 : -1;

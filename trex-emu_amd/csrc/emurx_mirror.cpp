@@ -103,7 +103,9 @@ void Mirror::set_partition(uint32_t n, uint32_t p) {
     uint64_t f4 = 0;
     for (auto& kv : ft_map) f4 += kv.first.size() == 4 + 13;
     const uint64_t need[kNumTabs] = {live[0], live[1], live[2], live[3], live[4], f4, ft_map.size() - f4, live[7]};
-    const uint64_t want[kNumTabs] = {ens, ecl, ecl, 2 * ecl, ecl, 8, 8, 16};
+    // IPv6: one address per client to start (a client may hold two, Ipv6 and Dhcpv6: the
+    // table grows when they come)
+    const uint64_t want[kNumTabs] = {ens, ecl, ecl, ecl, ecl, 8, 8, 16};
     const uint32_t per[kNumTabs] = {4, 4, 2, 2, 2, 2, 1, 4};
     for (int k = 0; k < kNumTabs; ++k) {
         const uint64_t e = std::max(want[k], (need[k] + n_parts - 1) / n_parts);

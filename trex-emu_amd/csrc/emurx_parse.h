@@ -64,6 +64,41 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     return wave_reduce(v, [](uint32_t x, uint32_t y) { return max(x, y); });
 }
+// Namespace-owner packing (emurx_route.hip, k_rx kind 2): the offset of `tile` in each owner's
+// region = its group's offset (grp_off, k_route_scan) + the counts of the group's earlier
+// tiles (tile_cnt[t][owner], 64 tiles per group).  Called by one whole wave; lane 0 writes
+// s_toff[0 .. parts).
+template <class R>
+__device__ __forceinline__ void tile_offsets(const uint32_t* tile_cnt, const uint32_t* grp_off, uint32_t parts,
+                                             uint32_t tile, uint32_t lane, uint32_t* s_toff, R reduce_sum) {
+    const uint32_t g0 = tile & ~63u;
+    uint4 x = make_uint4(0, 0, 0, 0), y = x;
+    if (g0 + lane < tile) {
+        const uint4* q = reinterpret_cast<const uint4*>(tile_cnt + (size_t)(g0 + lane) * 16);
+        x = q[0];
+        y = q[1];
+    }
+    const uint32_t c[EMURX_MAX_PARTS] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+#pragma unroll
+    for (uint32_t k = 0; k < EMURX_MAX_PARTS; ++k) {
+        if (k >= parts) break;
+        const uint32_t sum = reduce_sum(c[k]);
+        if (lane == 0) s_toff[k] = grp_off[(tile / 64) * 16 + k] + sum;
+    }
+}
+
+// The CTunnelKey VLAN words ParsePacket leaves for a frame (parser.go:801-818), from its
+// length and bytes 12..19 alone: tag 0 when bytes 12..13 are 0x8100 / 0x88a8 and the frame
+// holds it, tag 1 likewise after it unless PPPoE follows tag 0.  parse_flat and parse_packet
+// set r.vlan0 / r.vlan1 to exactly these (the owner-count pass routes by them).
+__device__ __forceinline__ void l2_vlans(uint32_t len, uint32_t w12, uint32_t w16, uint32_t& v0, uint32_t& v1) {
+    const uint32_t e0 = w12 >> 16, e1 = w16 >> 16;  // big-endian words of bytes 12..15, 16..19
+    const bool g0 = len >= 18 && (e0 == 0x8100 || e0 == 0x88A8);
+    const bool g1 = g0 && len >= 22 && (e1 == 0x8100 || e1 == 0x88A8);
+    v0 = g0 ? (w12 & 0xffff0fffu) : 0u;
+    v1 = g1 ? (w16 & 0xffff0fffu) : 0u;
+}
+
 // lanes below this one in mask m
 __device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));

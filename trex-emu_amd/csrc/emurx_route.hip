@@ -44,22 +44,8 @@ __global__ __launch_bounds__(kBlock) void k_route(const emurx_rec* __restrict__ 
     }
     // {ns, client, vlan0, vlan1} {vport | l3 << 16, ...}
     const uint32_t d = a.x != EMURX_ID_NONE ? emurx_owner(emurx_tk_hash(b.x & 0xffffu, a.z, a.w), n_parts) : 0xffu;
-    if (kPack && wv == 0) {  // this tile's offset: group offset + the group's earlier tiles
-        const uint32_t g0 = tile & ~(kGroup - 1);
-        uint4 x = make_uint4(0, 0, 0, 0), y = x;
-        if (g0 + lane < tile) {
-            const uint4* p = reinterpret_cast<const uint4*>(tile_cnt + (g0 + lane) * 16);
-            x = p[0];
-            y = p[1];
-        }
-        const uint32_t c[EMURX_MAX_PARTS] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
-#pragma unroll
-        for (uint32_t k = 0; k < EMURX_MAX_PARTS; ++k) {
-            if (k >= n_parts) break;
-            const uint32_t sum = wave_reduce(c[k], [](uint32_t u, uint32_t v) { return u + v; });
-            if (lane == 0) s_toff[k] = grp_off[(tile / kGroup) * 16 + k] + sum;
-        }
-    }
+    if (kPack && wv == 0)  // this tile's offset: group offset + the group's earlier tiles
+        tile_offsets(tile_cnt, grp_off, n_parts, tile, lane, s_toff, [](uint32_t v) { return wave_sum_u32(v); });
     uint32_t rank = 0;
     uint64_t left = __ballot(d != 0xffu);
     while (left) {
@@ -132,64 +118,48 @@ __global__ __launch_bounds__(kScanThreads) void k_route_scan(uint32_t* __restric
 }
 
 // ---- partitioned path -------------------------------------------------------------------
-// k_route_lk: k_route<true> for the 80-byte lookup records of k_rx kind 2 (every record that
-// reached a callback goes to the owner of its CTunnelKey; k_rx took the per-tile counts)
-__global__ __launch_bounds__(kBlock) void k_route_lk(const emurx_lookup_rec* __restrict__ lk, uint32_t n,
-                                                     uint32_t n_parts, const uint32_t* __restrict__ tile_cnt,
-                                                     const uint32_t* __restrict__ grp_off,
-                                                     emurx_lookup_rec* __restrict__ send, uint32_t cap) {
+// k_owner_count: the owner of every frame from its L2 header (l2_vlans: bytes 12..19 + the
+// length), counted per (tile, owner) and per group of 64 tiles, as k_route<false> counts
+// records; k_rx kind 2 then packs at the offsets k_route_scan derives.  8 bytes of frame +
+// the descriptor per frame.
+__global__ __launch_bounds__(kBlock) void k_owner_count(const uint8_t* __restrict__ frames,
+                                                        const emurx_desc* __restrict__ desc, uint32_t n,
+                                                        uint32_t n_parts, uint32_t* __restrict__ tile_cnt,
+                                                        uint32_t* __restrict__ grp) {
     __shared__ uint32_t s_wcnt[kWaves][16];
-    __shared__ uint32_t s_toff[EMURX_MAX_PARTS];
     const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / kWave, tile = blockIdx.x;
     const uint32_t i = tile * kBlock + tid;
     if (lane < 16) s_wcnt[wv][lane] = 0;
-    const uint4* p = reinterpret_cast<const uint4*>(lk + (i < n ? i : 0));
-    uint4 a = make_uint4(0, 0, 0, 0), b = make_uint4(0, 0, 0, EMURX_ST_HOLE);
-    if (i < n) {
-        a = p[0];
-        b = p[1];
+    const uint2 dd = i < n ? *reinterpret_cast<const uint2*>(desc + i) : make_uint2(0, EMURX_DESC_HOLE << 24);
+    const bool valid = (dd.y >> 24) != EMURX_DESC_HOLE;
+    uint32_t d = 0xffu;
+    if (valid) {
+        const uint32_t len = dd.y & 0xffff, vport = (dd.y >> 16) & 0xff;
+        // bytes 12..19 from three aligned dwords (the buffer is readable past every frame)
+        const uintptr_t a = (uintptr_t)(frames + dd.x + 12);
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+        const uint32_t sh = (uint32_t)(a & 3);
+        const uint32_t w0 = gld4(w), w1 = gld4(w + 1), w2 = gld4(w + 2);
+        const uint32_t b12 = __builtin_bswap32(__builtin_amdgcn_alignbyte(w1, w0, sh));
+        const uint32_t b16 = __builtin_bswap32(__builtin_amdgcn_alignbyte(w2, w1, sh));
+        uint32_t v0, v1;
+        l2_vlans(len, b12, b16, v0, v1);
+        d = emurx_owner(emurx_tk_hash(vport, v0, v1), n_parts);
     }
-    // {src index, src rank, vlan0, vlan1} {vport | l3 << 16, l4 | l7 << 16, .., status | flags << 8}
-    const bool ok = i < n && (b.w & 0xffu) == EMURX_ST_OK;
-    const uint32_t d = ok ? emurx_owner(emurx_tk_hash(b.x & 0xffffu, a.z, a.w), n_parts) : 0xffu;
-    if (wv == 0) {  // this tile's offset: group offset + the group's earlier tiles
-        const uint32_t g0 = tile & ~(kGroup - 1);
-        uint4 x = make_uint4(0, 0, 0, 0), y = x;
-        if (g0 + lane < tile) {
-            const uint4* q = reinterpret_cast<const uint4*>(tile_cnt + (g0 + lane) * 16);
-            x = q[0];
-            y = q[1];
-        }
-        const uint32_t c[EMURX_MAX_PARTS] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
-#pragma unroll
-        for (uint32_t k = 0; k < EMURX_MAX_PARTS; ++k) {
-            if (k >= n_parts) break;
-            const uint32_t sum = wave_reduce(c[k], [](uint32_t u, uint32_t v) { return u + v; });
-            if (lane == 0) s_toff[k] = grp_off[(tile / kGroup) * 16 + k] + sum;
-        }
-    }
-    uint32_t rank = 0;
     uint64_t left = __ballot(d != 0xffu);
     while (left) {
         const uint32_t lead = (uint32_t)__ffsll((long long)left) - 1;
-        const uint32_t dd = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)lead);
-        const uint64_t m = __ballot(d == dd);
-        if (d == dd) rank = mbcnt(m);
-        if (lane == lead) s_wcnt[wv][dd] = (uint32_t)__popcll(m);
+        const uint32_t q = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)lead);
+        const uint64_t m = __ballot(d == q);
+        if (lane == lead) s_wcnt[wv][q] = (uint32_t)__popcll(m);
         left &= ~m;
     }
     __syncthreads();
-    if (d == 0xffu) return;
-    uint32_t pos = s_toff[d] + rank;
-    for (uint32_t w = 0; w < wv; ++w) pos += s_wcnt[w][d];
-    if (pos >= cap) return;  // overflow: send_count[d] > cap tells the caller
-    const uint4 k0 = p[2], k1 = p[3], k2 = p[4];
-    uint4* o = reinterpret_cast<uint4*>(send + (size_t)d * cap + pos);  // 80 B, 16-B aligned
-    o[0] = a;
-    o[1] = b;
-    o[2] = k0;
-    o[3] = k1;
-    o[4] = k2;
+    if (tid < 16) {
+        const uint32_t c = s_wcnt[0][tid] + s_wcnt[1][tid] + s_wcnt[2][tid] + s_wcnt[3][tid];
+        tile_cnt[tile * 16 + tid] = c;
+        if (c) atomicAdd(&grp[(tile / kGroup) * 16 + tid], c);
+    }
 }
 
 // k_lookup: the owner's half — GetNs + the callback's client rule + the flow decision for
@@ -224,7 +194,8 @@ __global__ __launch_bounds__(kBlock) void k_lookup(const emurx_lookup_rec* __res
     const uint32_t w[12] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w, k2.x, k2.y, k2.z, k2.w};
     Tuple t;
     const LKey k = unpack_key(r, w, t);
-    resolve(T, r, k, [&](uint32_t cid) { return flow_probe(T, t, cid); });
+    // frames that reached no callback travel too (their owner keeps their record): no lookup
+    if (r.status == EMURX_ST_OK) resolve(T, r, k, [&](uint32_t cid) { return flow_probe(T, t, cid); });
     uint2* o = reinterpret_cast<uint2*>(out + j);  // 40 B, 8-B aligned
     o[0] = make_uint2(r.ns, r.cl);
     o[1] = make_uint2(r.vlan0, r.vlan1);
@@ -236,16 +207,15 @@ __global__ __launch_bounds__(kBlock) void k_lookup(const emurx_lookup_rec* __res
 
 }  // namespace emurx
 
-int emurx_launch_route_lk(const emurx_lookup_rec* lk, uint32_t n, uint32_t n_parts, uint32_t cap,
-                          emurx_lookup_rec* send, uint32_t* send_count, uint32_t* tile_cnt, uint32_t* grp,
-                          uint32_t* grp_off, hipStream_t st) {
+int emurx_launch_owner_count(const uint8_t* frames, const emurx_desc* desc, uint32_t n, uint32_t n_parts,
+                             uint32_t* send_count, uint32_t* tile_cnt, uint32_t* grp, uint32_t* grp_off,
+                             hipStream_t st) {
     using namespace emurx;
     const uint32_t ntiles = (n + kBlock - 1) / kBlock, ngroups = (ntiles + kGroup - 1) / kGroup;
     if (n == 0) return hipMemsetAsync(send_count, 0, n_parts * sizeof(uint32_t), st) == hipSuccess ? 0 : -1;
     if (ngroups > kScanThreads) return -1;
+    hipLaunchKernelGGL(k_owner_count, dim3(ntiles), dim3(kBlock), 0, st, frames, desc, n, n_parts, tile_cnt, grp);
     hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(kScanThreads), 0, st, grp, ngroups, n_parts, grp_off, send_count);
-    hipLaunchKernelGGL(k_route_lk, dim3(ntiles), dim3(kBlock), 0, st, lk, n, n_parts, (const uint32_t*)tile_cnt,
-                       (const uint32_t*)grp_off, send, cap);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
