@@ -80,6 +80,72 @@ def test_exchange_gloo_world2(oracle_built, tmp_path):
     assert total == routed
 
 
+def lookup_regions(rec, world, rank):
+    """Host stand-in for emurx_parse_route_dev's send regions: every frame's lookup record
+    (the parsed record with ns_id = frame index, client_id = rank; key words = a function of
+    the frame) in the region of the owner of its CTunnelKey, frame order."""
+    from test_gpu_tables import _owners_by_key
+    own = _owners_by_key(rec, world)
+    out = []
+    for d in range(world):
+        idx = np.nonzero(own == d)[0]
+        lk = np.zeros(len(idx), abi.LOOKUP_REC_DTYPE)
+        lk["rec"] = rec[idx]
+        lk["rec"]["ns_id"], lk["rec"]["client_id"] = idx, rank
+        lk["key"] = (idx[:, None] * 12 + np.arange(12)[None, :]).astype(np.uint32)
+        out.append(lk)
+    return out
+
+
+def _worker_partitioned(rank, world, port, out_dir):
+    """The partitioned protocol over gloo: 80-byte lookup records to the Namespace owners,
+    and this rank's device-table bytes (host-only handle, emurx_set_partition) ~ 1/world."""
+    sys.path[:0] = [str(ROOT / "tests"), str(ROOT / "trex-emu_amd"), str(ROOT / "oracle")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    from emurx import exchange as X
+    from emurx.rx import RxPath
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        recs = [shard_records(r) for r in range(world)]
+        cap = X.capacity(N_FRAMES, world)
+        regions = lookup_regions(recs[rank], world, rank)
+        send = np.zeros((world, cap), abi.LOOKUP_REC_DTYPE)
+        for d, rr in enumerate(regions):
+            send[d, : len(rr)] = rr
+        cnt = np.array([len(rr) for rr in regions], np.int32)
+        recv, recv_count = X.exchange(torch.from_numpy(send.view(np.uint8).reshape(-1).copy()),
+                                      torch.from_numpy(cnt), cap, rec_bytes=X.LOOKUP_BYTES)
+        r = recv.numpy().view(abi.LOOKUP_REC_DTYPE).reshape(world, cap)
+        c = recv_count.numpy()
+        got = np.concatenate([r[s, : c[s]] for s in range(world)])
+        want = np.concatenate([lookup_regions(recs[s], world, s)[rank] for s in range(world)])
+        ok = got.tobytes() == want.tobytes() and len(got) > 0
+        w = synth.config_c(N_FRAMES)
+        full = RxPath(-1, max_ns=4096, max_clients=65536, max_frames=64)
+        part = RxPath(-1, max_ns=4096, max_clients=65536, max_frames=64)
+        part.set_partition(world, rank)
+        for t in (full, part):
+            synth.load_tables(w, t)
+        fb, pb = full.table_stats()["table_bytes"], part.table_stats()["table_bytes"]
+        Path(out_dir, f"p{rank}").write_text(f"{int(ok)} {len(got)} {fb} {pb}")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_partitioned_exchange_gloo_world2(oracle_built, tmp_path):
+    import torch.multiprocessing as mp
+    world = 2
+    mp.spawn(_worker_partitioned, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    res = [Path(tmp_path, f"p{r}").read_text().split() for r in range(world)]
+    assert all(r[0] == "1" for r in res), res
+    assert sum(int(r[1]) for r in res) == world * N_FRAMES  # every frame reached one owner
+    for r in res:  # per-rank device tables: half the replicated bytes (+ the dense ns info)
+        assert int(r[3]) <= int(r[2]) / world + 4096 * 16, r
+
+
 def test_owner_partition_balance(lib):
     """emurx_ns_owner spreads config D's 32K Namespaces evenly over 8 partitions."""
     from emurx.rx import ns_owner

@@ -112,7 +112,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
         WinSrc s{reinterpret_cast<const uint8_t*>(slab), slab, wv * kStage + lane * 16, head,
                  min(kWinVec * 16 - head, len), frames + off};
         if (valid) parse_packet(s, len, vport, T.cb_mask, r);
-        coop_checksum(r, frames + off, s_csum[wv]);  // the wave's long L4 spans, converged
+        // the wave's long L4 spans, converged
+        if constexpr (EMURX_COOP == 0) coop_checksum(r, frames + off, s_csum[wv]);
+        else coop_checksum_rows<EMURX_COOP>(r, frames + off, s_csum[wv]);
         if (valid && kClassify && !(EMURX_ABL & 2)) classify(s, len, T, r);
         if (kKind == 2 && valid && r.status == EMURX_ST_OK) pack_key(s, len, r, make_key(s, len, r), kwd);
     }

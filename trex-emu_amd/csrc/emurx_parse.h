@@ -26,6 +26,9 @@ constexpr uint32_t kStageWide = 7168, kStageNarrow = 6144;
 #ifndef EMURX_ABL
 #define EMURX_ABL 0  // experiment-only stage ablation (tools/ablate.sh); 0 in every real build
 #endif
+#ifndef EMURX_COOP
+#define EMURX_COOP 0  // long-span checksum: 0 the packed vector list, 2 / 4 row groups of 16 lanes
+#endif
 
 // loads through the global address space (global_load_*): pointers rebuilt from integers or
 // kept in a struct would otherwise compile to flat loads, which also count on lgkmcnt and
@@ -703,6 +706,83 @@ __device__ __forceinline__ void coop_checksum(Rec& r, const uint8_t* f, uint32_t
             const uint32_t g = (uint32_t)__shfl((int)geo, (int)own[k]);
             const uint32_t part = span_sum(x[k], g & 0xffff, (int)((g >> 16) & 0xff), (int)(g >> 24), kin[k]);
             if (b + k * kWave + lane < V) atomicAdd(&wsum[own[k]], part);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (mine) {
+        settle_deferred(r, csum_ok(wsum[lane], (uint32_t)a, r.dpcs));
+        r.dlen = 0;
+    }
+}
+
+// The same sums with the wave split into four 16-lane rows (A/B alternative, EMURX_COOP > 0):
+// the wave's deferred spans are dealt to the rows in lane order, balanced by their round
+// counts, and each row walks its spans one after the other, 16 lanes x kU consecutive vectors
+// of one span per round (coalesced 256-byte row loads, no per-vector span search); a round's
+// row total is folded by four DPP row shifts and added once into the span's LDS word.
+template <uint32_t kU>
+__device__ __forceinline__ uint32_t dpp_row_sum(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);  // row_shr:8
+    return v;  // lane 15 of each row: the row's total
+}
+template <uint32_t kU>
+__device__ __forceinline__ void coop_checksum_rows(Rec& r, const uint8_t* f, uint32_t* wsum) {
+    constexpr uint32_t kRound = 16 * kU;  // vectors of one span per row round
+    const uint32_t lane = lane_id(), l16 = lane & 15, row = lane >> 4;
+    const bool mine = r.dlen != 0;
+    const uint64_t mm = __ballot(mine);
+    if (!mm) return;
+    const uintptr_t a = (uintptr_t)(f + r.dstart), e = a + r.dlen;
+    const uint32_t nv = mine ? (uint32_t)((((e + 15) & ~(uintptr_t)15) - (a & ~(uintptr_t)15)) >> 4) : 0u;
+    const uint32_t rounds = (nv + kRound - 1) / kRound;
+    uint32_t incl = rounds;
+#pragma unroll
+    for (uint32_t o = 1; o < kWave; o <<= 1) {
+        const uint32_t up = (uint32_t)__shfl_up((int)incl, o);
+        if (lane >= o) incl += up;
+    }
+    const uint32_t R = (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
+    // row of this lane's span: its rounds' midpoint in the wave's total, in quarters
+    const uint32_t g = mine ? min(3u, (uint32_t)(((uint64_t)(2 * incl - rounds) * 4) / (2 * (uint64_t)R))) : 4u;
+    uint64_t rm = 0;  // the spans of this lane's row (lanes in order)
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint64_t b = __ballot(g == k);
+        if (row == k) rm = b;
+    }
+    const uintptr_t a16 = a & ~(uintptr_t)15;
+    const uint32_t blo = (uint32_t)a16, bhi = (uint32_t)(a16 >> 32);
+    const uint32_t geo = nv | ((uint32_t)(a & 15) << 16) | ((16u - ((0u - (uint32_t)e) & 15)) << 24);
+    wsum[lane] = 0;
+    uint32_t j = rm ? (uint32_t)__ffsll((long long)rm) - 1 : 64u, c = 0;  // the row's current span, round
+    for (;;) {  // wave-uniform: until every row has walked its spans
+        if (!__ballot(j < 64)) break;
+        const uint32_t src_lane = j < 64 ? j : 0u;
+        const uint32_t gj = (uint32_t)__shfl((int)geo, (int)src_lane);
+        const uint32_t lo = (uint32_t)__shfl((int)blo, (int)src_lane), hi = (uint32_t)__shfl((int)bhi, (int)src_lane);
+        const uint8_t* src = reinterpret_cast<const uint8_t*>(((uintptr_t)hi << 32) | lo);
+        const uint32_t nvj = j < 64 ? (gj & 0xffff) : 0u;
+        uint4 x[kU];
+#pragma unroll
+        for (uint32_t k = 0; k < kU; ++k) {
+            const uint32_t v = c * kRound + k * 16 + l16;
+            x[k] = v < nvj ? gld16(src + 16 * v) : make_uint4(0, 0, 0, 0);
+        }
+        uint32_t part = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kU; ++k)
+            part += span_sum(x[k], nvj, (int)((gj >> 16) & 0xff), (int)(gj >> 24), c * kRound + k * 16 + l16);
+        const uint32_t tot = dpp_row_sum<kU>(part);
+        if (l16 == 15 && j < 64 && tot) atomicAdd(&wsum[j], tot);
+        if (j < 64 && ++c * kRound >= nvj) {  // the span is done: the row's next one
+            c = 0;
+            const uint64_t rest = j < 63 ? rm & (~0ull << (j + 1)) : 0ull;
+            j = rest ? (uint32_t)__ffsll((long long)rest) - 1 : 64u;
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
