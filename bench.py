@@ -320,7 +320,8 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             rx.classify_route_dev(buf, desc, n, rec, qlist, qcap, tile_cnt, hist, world, rank, xch["cap"],
                                   xch["send"], xch["send_count"], stream=stream)
         else:
-            rx.parse_route_dev(buf, desc, n, rec, qlist, qcap, tile_cnt, hist, world, rank, xch["cap"],
+            # no source records: every frame's lookup record carries its parse to the owner
+            rx.parse_route_dev(buf, desc, n, None, qlist, qcap, tile_cnt, hist, world, rank, xch["cap"],
                                xch["send"], xch["send_count"], stream=stream)
         if world > 1:
             xch["recv"], xch["recv_count"] = X.exchange(xch["send"], xch["send_count"], xch["cap"], rec_bytes=rb)
@@ -381,9 +382,9 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
     ms_per_step = el / steps * 1e3
 
     # roofline of the dominant kernel (k_rx): algorithmic bytes / its mean HIP-event duration.
-    # Per frame: the frame, its 8-B descriptor, the 32-B record, the 4-B queue entry (+ the
-    # 80-B lookup record in the partitioned mode's k_rx)
-    per_frame = 8 + 32 + 4 + (80 if mode == "partitioned" else 0)
+    # Per frame: the frame, its 8-B descriptor, the 4-B queue entry and the 32-B record (the
+    # 80-B lookup record instead in the partitioned mode's k_rx)
+    per_frame = 8 + 4 + (80 if mode == "partitioned" else 32)
     alg_bytes = w["nbytes"] + per_frame * n
     parse_s = float(np.mean(pk)) * 1e-3 if len(pk) else float("nan")
     achieved = alg_bytes / parse_s / 1e9
@@ -398,7 +399,7 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
     # the Namespace + Client bucket reads of every frame that reaches a callback (two 64-B
     # buckets, issued together): outside the algorithmic bytes, served by L2 / MALL / HBM
     r = rec.cpu().numpy().view(abi.REC_DTYPE)
-    probed = int((r["status"] == 0).sum())
+    probed = int((r["status"] == 0).sum()) if mode != "partitioned" else 0
     ts = rx.table_stats()
     par = {"none": f"frame shards x{world}, replicated tables, no collective",
            "replicated": f"frame shards x{world}, replicated tables, classified records to the Namespace "
@@ -562,8 +563,7 @@ def xcheck(xch, rec, n, world, rank, dist, torch, dev, mode):
     from emurx import abi
     cnt = xch["recv_count"].cpu().numpy().astype(np.int64)
     assert (cnt <= xch["cap"]).all(), f"exchange overflow {cnt} > {xch['cap']}"
-    r = rec.cpu().numpy().view(abi.REC_DTYPE)
-    sent = (r["ns_id"] != abi.ID_NONE).sum() if mode == "replicated" else len(r)
+    sent = (rec.cpu().numpy().view(abi.REC_DTYPE)["ns_id"] != abi.ID_NONE).sum() if mode == "replicated" else n
     routed = torch.tensor([int(sent), int(cnt.sum())], dtype=torch.int64)
     if world > 1:
         routed = routed.to(dev) if dist.get_backend() == "nccl" else routed

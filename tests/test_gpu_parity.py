@@ -696,6 +696,9 @@ def test_transport_flows(rxmod):
     buf, desc = w["buf"], w["desc"]
     orec, _, _, _ = o.rx_batch(buf, desc)
     tup = frame_tuples(buf, desc, orec)
+    # no TransportCtx anywhere yet: every tcp/udp frame reaching a client is NO_CTX
+    rec0, _, _, _, flow0 = run_dev(rx, buf, desc, flows=True)
+    assert np.array_equal(flow0, o.flows(buf, desc, orec)) and (flow0 == abi.FLOW_NO_CTX).sum() > 10000
     idx = np.array([i for i, t in enumerate(tup) if t is not None])
     assert len(idx) > 15000
     for i in rng.choice(idx, len(idx) * 2 // 5, replace=False):

@@ -1221,10 +1221,11 @@ __device__ __forceinline__ void resolve(const emurx_dev_tables& T, Rec& r, const
         const uint2 c = resolve_mac(T, cbk, ce, ns, mlo, mhi);
         client_result(r, c.x, c.y, plug, true);
         // transport: the client's TransportCtx decides (plugin_transport.go:109-114, :73-80)
-        if (T.ft_on && (cb == EMURX_CB_TCP || cb == EMURX_CB_UDP) &&
+        if ((cb == EMURX_CB_TCP || cb == EMURX_CB_UDP) &&
             ((r.flags & EMURX_FLAG_LK_MASK) >> EMURX_FLAG_LK_SHIFT) == EMURX_LK_CLIENT) {
-            // GetTransportCtx() == nil -> the handler returns -1 (PluginTransClient :73-80)
-            r.flow = client_info(T, c.x).ctx & 1u ? flow(c.x) : EMURX_FLOW_NO_CTX;
+            // GetTransportCtx() == nil -> the handler returns -1 (PluginTransClient :73-80);
+            // with no TransportCtx on these tables (ft_on 0) no client info is read
+            r.flow = T.ft_on && (client_info(T, c.x).ctx & 1u) ? flow(c.x) : EMURX_FLOW_NO_CTX;
         }
         return;
     }
