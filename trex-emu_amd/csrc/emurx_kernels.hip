@@ -103,21 +103,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
     if (staged) {  // wave-uniform branch
         if (valid) {
             LdsSrc s{reinterpret_cast<const uint8_t*>(slab), slab, wv * kStage + (off - start)};
-            // A/B (EMURX_PREFETCH): touch the Namespace and MAC buckets of the frame's L2
-            // header before the parse, so the lookups after it find the lines in cache (the
-            // MAC[dst] rule of transport / dhcpv6 / ppp frames; other rules just warm a line)
-            uint32_t pf0 = 0, pf1 = 0;
-            if (kClassify && EMURX_PREFETCH) {
-                uint32_t v0, v1;
-                l2_vlans(len, be32(s, 12), be32(s, 16), v0, v1);
-                const uint32_t tk = emurx_tk_hash(vport, v0, v1);
-                pf0 = gld4(T.ns_tab + (size_t)(tk & T.ns_mask) * EMURX_BUCKET_WORDS);
-                pf1 = gld4(T.mac_tab + (size_t)(emurx_mac_hash(tk, le32(s, 0), s.u8(4) | (s.u8(5) << 8)) & T.mac_mask) *
-                           EMURX_BUCKET_WORDS);
-            }
             parse_flat(s, len, vport, T.cb_mask, r);
             if (kClassify && !(EMURX_ABL & 2)) classify(s, len, T, r);
-            if (kClassify && EMURX_PREFETCH) asm volatile("" ::"v"(pf0), "v"(pf1));  // keeps the loads
             if (kKind == 2 && r.status == EMURX_ST_OK) pack_key(s, len, r, make_key(s, len, r), kwd);
         }
     } else {

@@ -26,11 +26,10 @@ constexpr uint32_t kStageWide = 7168, kStageNarrow = 6144;
 #ifndef EMURX_ABL
 #define EMURX_ABL 0  // experiment-only stage ablation (tools/ablate.sh); 0 in every real build
 #endif
-#ifndef EMURX_PREFETCH
-#define EMURX_PREFETCH 0  // A/B: touch the lookup buckets before the parse (emurx_kernels.hip)
-#endif
 #ifndef EMURX_COOP
-#define EMURX_COOP 0  // long-span checksum: 0 the packed vector list, 2 / 4 row groups of 16 lanes
+// long-span checksum: 0 the packed vector list (coop_checksum), 2 / 4 / 8 vectors per lane per
+// round of the 16-lane row groups (coop_checksum_rows; 4 measured best)
+#define EMURX_COOP 4
 #endif
 
 // loads through the global address space (global_load_*): pointers rebuilt from integers or
