@@ -28,6 +28,7 @@ args() {  # bench arguments per config
     C) echo "--config C --steps 100 --warmup 10" ;;
     D) echo "--config D --steps 50 --warmup 5" ;;
     DR) echo "--config D --tables replicated --no-exchange-run --steps 50 --warmup 5" ;;
+    DN) echo "--config D --tables none --no-exchange-run --steps 50 --warmup 5" ;;
     E) echo "--config E --steps 50 --warmup 5" ;;
   esac
 }

@@ -97,12 +97,61 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
+    // The frame this lane parses: its own, or with the shape sort (EMURX_SORT, kinds 0 / 1, all
+    // four waves of the tile staged) a frame of the tile from the lane's position in a stable
+    // counting sort by shape class (IPv4 / IPv6 / other x UDP / TCP / other), so that a wave's
+    // lanes take the same parse and lookup branches.  Records, flows and histogram go out from
+    // the parsing lane; queue and owner ranks are taken back in frame order through LDS.
+    uint32_t pf = tid, poff = off, plen = len, pvport = vport, pbase = wv * kStage + (off - start);
+    bool pvalid = valid, sorted = false;
+    uint8_t* s_aux = reinterpret_cast<uint8_t*>(&s_csum[0][0]);  // free when every wave is staged
+    if constexpr (EMURX_SORT && kKind != 2) {
+        if (__syncthreads_and(staged)) {  // tile-uniform; every slab is visible to every wave after it
+            uint32_t* s_cls = reinterpret_cast<uint32_t*>(s_aux + 768);  // [wave][class] counts
+            uint32_t* s_st = reinterpret_cast<uint32_t*>(s_aux + 896);   // wave starts
+            const uint32_t cls =
+                valid ? frame_class(LdsSrc{reinterpret_cast<const uint8_t*>(slab), slab, pbase}, len) : 7u;
+            uint64_t mine = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k) {
+                const uint64_t b = __ballot(cls == k);
+                if (cls == k) mine = b;
+                if (lane == k) s_cls[wv * 8 + k] = (uint32_t)__popcll(b);
+            }
+            if (lane == 0) s_st[wv] = start;
+            __syncthreads();
+            uint32_t base = 0, maxc = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k) {
+                const uint32_t t = s_cls[k] + s_cls[8 + k] + s_cls[16 + k] + s_cls[24 + k];
+                maxc = max(maxc, t);
+                base += k < cls ? t : 0u;
+            }
+            for (uint32_t w = 0; w < wv; ++w) base += s_cls[w * 8 + cls];
+            sorted = maxc < kBlock;  // one shape everywhere: nothing to gain
+            if (sorted) s_aux[base + mbcnt(mine)] = (uint8_t)tid;
+            __syncthreads();
+            if (sorted) {
+                pf = s_aux[tid];
+                const uint32_t fi = tile * EMURX_QUEUE_TILE + pf;
+                const uint2 pd = fi < n ? *reinterpret_cast<const uint2*>(desc + fi) : make_uint2(0, EMURX_DESC_HOLE << 24);
+                pvalid = (pd.y >> 24) != EMURX_DESC_HOLE;
+                poff = pd.x;
+                plen = pd.y & 0xffff;
+                pvport = (pd.y >> 16) & 0xff;
+                pbase = (pf / kWave) * kStage + (poff - s_st[pf / kWave]);
+            }
+        }
+    }
+    const uint32_t pi = tile * EMURX_QUEUE_TILE + pf;  // the parsed frame's index in the batch
+
     Rec r;
     r.dlen = 0;
     uint32_t kwd[12];  // kKind 2: the lookup key words of the frame
     if (staged) {  // wave-uniform branch
-        if (valid) {
-            LdsSrc s{reinterpret_cast<const uint8_t*>(slab), slab, wv * kStage + (off - start)};
+        if (pvalid) {
+            LdsSrc s{reinterpret_cast<const uint8_t*>(slab), slab, pbase};
+            const uint32_t len = plen, vport = pvport;
             parse_flat(s, len, vport, T.cb_mask, r);
             if (kClassify && !(EMURX_ABL & 2)) classify(s, len, T, r);
             if (kKind == 2 && r.status == EMURX_ST_OK) pack_key(s, len, r, make_key(s, len, r), kwd);
@@ -119,39 +168,53 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
         if (kKind == 2 && valid && r.status == EMURX_ST_OK) pack_key(s, len, r, make_key(s, len, r), kwd);
     }
     typedef unsigned v4u __attribute__((ext_vector_type(4)));
-    if (rec && i < n && !(EMURX_ABL & 16)) {
+    if (rec && pi < n && !(EMURX_ABL & 16)) {
         // an empty descriptor slot gets a record too (no Namespace, status EMURX_ST_HOLE), so
         // every consumer of rec[0, n) sees defined bytes
-        const uint4 h0 = valid ? make_uint4(r.ns, r.cl, r.vlan0, r.vlan1)
-                               : make_uint4(EMURX_ID_NONE, EMURX_ID_NONE, 0, 0);
-        const uint4 h1 = valid ? make_uint4(r.vport | (r.l3 << 16), r.l4 | (r.l7 << 16),
-                                            r.l7len | (r.nh << 16) | (r.proto << 24), r.status | (r.flags << 8))
-                               : make_uint4(0, 0, (uint32_t)EMURX_CB_NONE << 24, EMURX_ST_HOLE);
-        uint4* o = reinterpret_cast<uint4*>(rec + i);
+        const uint4 h0 = pvalid ? make_uint4(r.ns, r.cl, r.vlan0, r.vlan1)
+                                : make_uint4(EMURX_ID_NONE, EMURX_ID_NONE, 0, 0);
+        const uint4 h1 = pvalid ? make_uint4(r.vport | (r.l3 << 16), r.l4 | (r.l7 << 16),
+                                             r.l7len | (r.nh << 16) | (r.proto << 24), r.status | (r.flags << 8))
+                                : make_uint4(0, 0, (uint32_t)EMURX_CB_NONE << 24, EMURX_ST_HOLE);
+        uint4* o = reinterpret_cast<uint4*>(rec + pi);
         // streaming stores: the records are read once, by the host copy or the route kernel
         // (measured +2.6% on config B, neutral on C)
         __builtin_nontemporal_store(v4u{h0.x, h0.y, h0.z, h0.w}, reinterpret_cast<v4u*>(o));
         __builtin_nontemporal_store(v4u{h1.x, h1.y, h1.z, h1.w}, reinterpret_cast<v4u*>(o + 1));
     }
-    if (flow && i < n) flow[i] = valid ? r.flow : EMURX_FLOW_NONE;
+    if (flow && pi < n) flow[pi] = pvalid ? r.flow : EMURX_FLOW_NONE;
     // outcome histogram into the wave's LDS copy: a wave whose frames all share one
     // (status, proto) bin adds its count (ballot) and byte sum (DPP reduction) once, instead
     // of 64 LDS atomics serialised on one address; mixed waves add per frame
     if (!(EMURX_ABL & 4)) {
-        const uint32_t bin = valid ? EMURX_HIST_BIN(r.status, r.proto) : 0xffu;
-        const uint64_t vm = __ballot(valid);
+        const uint32_t bin = pvalid ? EMURX_HIST_BIN(r.status, r.proto) : 0xffu;
+        const uint64_t vm = __ballot(pvalid);
         if (vm) {
             const uint32_t lead = (uint32_t)__ffsll((long long)vm) - 1;
             const uint32_t bb = (uint32_t)__builtin_amdgcn_readlane((int)bin, (int)lead);
             if (__ballot(bin == bb) == vm) {
-                const uint32_t bytes = wave_sum_u32(valid ? len : 0u);  // <= 64 x 65535
+                const uint32_t bytes = wave_sum_u32(pvalid ? plen : 0u);  // <= 64 x 65535
                 if (lane == lead) s_hist[wv][bb] += ((uint32_t)__popcll(vm) << 23) | bytes;
-            } else if (valid) {
-                atomicAdd(&s_hist[wv][bin], (1u << 23) | len);
+            } else if (pvalid) {
+                atomicAdd(&s_hist[wv][bin], (1u << 23) | plen);
             }
         }
     }
-    const uint32_t q = valid ? (r.status == EMURX_ST_OK ? r.proto : EMURX_Q_DROP) : 0xffu;
+    uint32_t q = pvalid ? (r.status == EMURX_ST_OK ? r.proto : EMURX_Q_DROP) : 0xffu;
+    // the Namespace owner of the record (classify + route: the records whose Namespace was
+    // found; lookup keys: every frame)
+    uint32_t rd = 0xffu;
+    if ((kKind == 1 && rt.cnt) || kKind == 2) {
+        const bool routed = pvalid && (kKind == 2 || r.ns != EMURX_ID_NONE);
+        rd = routed ? emurx_owner(emurx_tk_hash(r.vport, r.vlan0, r.vlan1), rt.parts) : 0xffu;
+    }
+    if (sorted) {  // tile-uniform: queue and owner back to frame order
+        s_aux[256 + pf] = (uint8_t)q;
+        s_aux[512 + pf] = (uint8_t)rd;
+        __syncthreads();
+        q = s_aux[256 + tid];
+        rd = s_aux[512 + tid];
+    }
 
     // rank inside (wave, queue): one ballot per distinct queue present in the wave
     uint32_t rank = 0;
@@ -170,10 +233,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
     // Namespace owners (rt.parts > 0): kind 1 counts the records whose Namespace was found
     // (the first pass of emurx_route_dev, fused); kind 2 packs every frame's lookup record
     // into its owner's region, ranked by ballots like the queues
-    uint32_t rrank = 0, rd = 0xffu;
+    uint32_t rrank = 0;
     if ((kKind == 1 && rt.cnt) || kKind == 2) {
-        const bool routed = valid && (kKind == 2 || r.ns != EMURX_ID_NONE);
-        rd = routed ? emurx_owner(emurx_tk_hash(r.vport, r.vlan0, r.vlan1), rt.parts) : 0xffu;
         uint64_t rl = __ballot(rd != 0xffu);
         while (rl) {
             const uint32_t lead = (uint32_t)__ffsll((long long)rl) - 1;

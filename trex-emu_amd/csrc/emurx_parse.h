@@ -26,6 +26,9 @@ constexpr uint32_t kStageWide = 7168, kStageNarrow = 6144;
 #ifndef EMURX_ABL
 #define EMURX_ABL 0  // experiment-only stage ablation (tools/ablate.sh); 0 in every real build
 #endif
+#ifndef EMURX_SORT
+#define EMURX_SORT 0  // A/B: shape-class sort of a staged tile's frames over its lanes (emurx_kernels.hip)
+#endif
 #ifndef EMURX_COOP
 // long-span checksum: 0 the packed vector list (coop_checksum), 2 / 4 / 8 vectors per lane per
 // round of the 16-lane row groups (coop_checksum_rows; 4 measured best)
@@ -102,6 +105,20 @@ __device__ __forceinline__ void l2_vlans(uint32_t len, uint32_t w12, uint32_t w1
     const bool g1 = g0 && len >= 22 && (e1 == 0x8100 || e1 == 0x88A8);
     v0 = g0 ? (w12 & 0xffff0fffu) : 0u;
     v1 = g1 ? (w16 & 0xffff0fffu) : 0u;
+}
+
+// shape class of a frame for the tile sort (emurx_kernels.hip, EMURX_SORT): the EtherType
+// after up to two tags, then the L4 protocol (IPv4 header / IPv6 next header): 0..2 IPv4
+// UDP / TCP / other, 3..5 IPv6 UDP / TCP / other, 6 anything else.  Only a grouping hint:
+// every frame is still parsed by the full ParsePacket restatement.
+template <class S>
+__device__ __forceinline__ uint32_t frame_class(const S& s, uint32_t len) {
+    uint32_t et = (s.u8(12) << 8) | s.u8(13), o = 14;
+    if ((et == 0x8100 || et == 0x88A8) && len >= 18) { et = (s.u8(16) << 8) | s.u8(17); o = 18; }
+    if ((et == 0x8100 || et == 0x88A8) && len >= 22) { et = (s.u8(20) << 8) | s.u8(21); o = 22; }
+    const bool v4 = et == 0x0800, v6 = et == 0x86DD;
+    const uint32_t p = v4 ? s.u8(o + 9) : v6 ? s.u8(o + 6) : 0u;
+    return v4 || v6 ? (v4 ? 0u : 3u) + (p == 17 ? 0u : p == 6 ? 1u : 2u) : 6u;
 }
 
 // lanes below this one in mask m
