@@ -59,6 +59,9 @@ def parse_args():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--time-stride", type=int, default=4,
                     help="record HIP events around every N-th launch of the timed region")
+    ap.add_argument("--time-run", type=int, default=8,
+                    help="steps that are one k_rx launch (no exchange): HIP events around runs of "
+                         "this many consecutive launches, duration = elapsed / run")
     ap.add_argument("--no-check", action="store_true",
                     help="skip the output sanity check (stage-ablation builds, tools/ablate.sh)")
     ap.add_argument("--tx-path", action="store_true",
@@ -306,8 +309,22 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
                 xch["out"] = torch.empty(world * xch["cap"] * X.REC_BYTES, dtype=torch.uint8, device=dev)
         alloc_regions()
 
+    # event pairs around runs of r consecutive k_rx launches (steps without an exchange)
+    runs = dict(on=False, k=0, ev=[], open=None, r=max(1, min(a.time_run, steps)))
+
     def step():
         if xch is None:
+            if runs["on"]:
+                if runs["k"] % runs["r"] == 0:
+                    runs["open"] = torch.cuda.Event(enable_timing=True)
+                    runs["open"].record(stream)
+                classify()
+                runs["k"] += 1
+                if runs["k"] % runs["r"] == 0:
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e1.record(stream)
+                    runs["ev"].append((runs["open"], e1))
+                return
             classify()
             return
         ev = None
@@ -353,7 +370,10 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         if xch is not None:
             xcheck(xch, rec, n, world, rank, dist, torch, dev, mode)
 
-    rx.set_timing(steps + 8, a.time_stride)
+    if xch is None:
+        runs["on"] = True  # the step is one k_rx launch: time runs of them, no per-launch events
+    else:
+        rx.set_timing(steps + 8, a.time_stride)
     if xch is not None:
         xch["timing"] = True
         xch["ev"] = []
@@ -368,8 +388,12 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    pk = rx.kernel_times()
-    rx.set_timing(0)
+    if xch is None:
+        pk = [e0.elapsed_time(e1) / runs["r"] for e0, e1 in runs["ev"]]
+        runs["on"] = False
+    else:
+        pk = rx.kernel_times()
+        rx.set_timing(0)
     if xch is not None and exchange_overflow(xch, world, dist, torch, dev):
         raise RuntimeError("exchange region overflow in the timed region")
 
@@ -443,9 +467,11 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             "alg_bytes_per_frame": round(alg_bytes / n, 2),
             "table_probe_bytes_per_launch": probed * 128 if mode != "partitioned" else 0,
             "kernel_ms_mean": round(parse_s * 1e3, 5),
-            "kernel_launches_timed": int(len(pk)),
-            "kernel_time_source": f"HIP events on the launch stream around every {a.time_stride}-th "
-                                  "launch of the timed region",
+            "kernel_launches_timed": int(len(pk)) * (runs["r"] if xch is None else 1),
+            "kernel_time_source": (f"HIP events on the launch stream around runs of {runs['r']} consecutive "
+                                   "k_rx launches (the whole step), elapsed / run" if xch is None else
+                                   f"HIP events on the launch stream around every {a.time_stride}-th "
+                                   "k_rx launch of the timed region"),
         },
         "host_submit_ms_per_step": round(t_submit / steps * 1e3, 5),
     }
