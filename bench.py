@@ -59,9 +59,11 @@ def parse_args():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--time-stride", type=int, default=4,
                     help="record HIP events around every N-th launch of the timed region")
-    ap.add_argument("--time-run", type=int, default=8,
-                    help="steps that are one k_rx launch (no exchange): HIP events around runs of "
-                         "this many consecutive launches, duration = elapsed / run")
+    ap.add_argument("--kernel-timing", default="region", choices=["region", "launch", "off"],
+                    help="steps that are one k_rx launch (no exchange): region = one HIP event pair "
+                         "around the whole timed region, duration = elapsed / launches; launch = "
+                         "events around every --time-stride-th launch (each pair adds ~1.5 us to "
+                         "the step it brackets); off = wall clock only")
     ap.add_argument("--no-check", action="store_true",
                     help="skip the output sanity check (stage-ablation builds, tools/ablate.sh)")
     ap.add_argument("--tx-path", action="store_true",
@@ -309,27 +311,13 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
                 xch["out"] = torch.empty(world * xch["cap"] * X.REC_BYTES, dtype=torch.uint8, device=dev)
         alloc_regions()
 
-    # event pairs around runs of r consecutive k_rx launches (steps without an exchange)
-    runs = dict(on=False, k=0, ev=[], open=None, r=max(1, min(a.time_run, steps)))
-
     def step():
         if xch is None:
-            if runs["on"]:
-                if runs["k"] % runs["r"] == 0:
-                    runs["open"] = torch.cuda.Event(enable_timing=True)
-                    runs["open"].record(stream)
-                classify()
-                runs["k"] += 1
-                if runs["k"] % runs["r"] == 0:
-                    e1 = torch.cuda.Event(enable_timing=True)
-                    e1.record(stream)
-                    runs["ev"].append((runs["open"], e1))
-                return
             classify()
             return
         ev = None
-        if xch["timing"] and xch["k"] % a.time_stride == 0:
-            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        if xch["timing"] and xch["k"] % a.time_stride == 0 and xch["pool"]:
+            ev = xch["pool"].pop()  # created before the timed region: creating one costs ~50 us
             ev[0].record(stream)
         xch["k"] += 1
         if mode == "replicated":
@@ -370,27 +358,34 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         if xch is not None:
             xcheck(xch, rec, n, world, rank, dist, torch, dev, mode)
 
-    if xch is None:
-        runs["on"] = True  # the step is one k_rx launch: time runs of them, no per-launch events
-    else:
+    region = xch is None and a.kernel_timing == "region"
+    if xch is not None or a.kernel_timing == "launch":
         rx.set_timing(steps + 8, a.time_stride)
     if xch is not None:
         xch["timing"] = True
         xch["ev"] = []
+        xch["pool"] = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                       for _ in range(steps // a.time_stride + 1)]
+    reg_ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    for e in reg_ev:  # instantiate the events outside the timed region
+        e.record(stream)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    if region:
+        reg_ev[0].record(stream)
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
+    if region:
+        reg_ev[1].record(stream)
     t_submit = time.perf_counter() - t0
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    if xch is None:
-        pk = [e0.elapsed_time(e1) / runs["r"] for e0, e1 in runs["ev"]]
-        runs["on"] = False
+    if region:
+        pk = [reg_ev[0].elapsed_time(reg_ev[1]) / steps]
     else:
         pk = rx.kernel_times()
         rx.set_timing(0)
@@ -467,9 +462,10 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             "alg_bytes_per_frame": round(alg_bytes / n, 2),
             "table_probe_bytes_per_launch": probed * 128 if mode != "partitioned" else 0,
             "kernel_ms_mean": round(parse_s * 1e3, 5),
-            "kernel_launches_timed": int(len(pk)) * (runs["r"] if xch is None else 1),
-            "kernel_time_source": (f"HIP events on the launch stream around runs of {runs['r']} consecutive "
-                                   "k_rx launches (the whole step), elapsed / run" if xch is None else
+            "kernel_launches_timed": steps if region else int(len(pk)),
+            "kernel_time_source": ("one HIP event pair on the launch stream around the whole timed region "
+                                   "(every step is one k_rx launch): elapsed / launches, dispatch gaps "
+                                   "between launches included" if region else
                                    f"HIP events on the launch stream around every {a.time_stride}-th "
                                    "k_rx launch of the timed region"),
         },
