@@ -1,0 +1,117 @@
+"""Timeline of one k_rx launch from the stamp build variant (experiment-only).
+
+    tools/build_variant.sh stamp "-DEMURX_STAMP=1"
+    EMURX_LIB=trex-emu_amd/lib/libemurx_stamp.so python tools/stamps.py [B C E ...]
+
+Every wave stores {entry, descriptors read, staging landed, parse + classify done, exit}
+shader-clock stamps plus HW_ID / XCC_ID (emurx_kernels.hip, EMURX_STAMP). Printed per config:
+the phase durations per wave, how many waves each CU held on average over the launch, and the
+launch span per XCD.
+"""
+import ctypes
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "trex-emu_amd"))
+sys.path.insert(0, str(ROOT))
+
+
+def run(cfg, n):
+    import torch
+    import bench
+    from emurx import abi
+    from emurx.rx import RxPath
+    from emurx import synth
+    w = bench.workload(cfg, n, 0)
+    rx = RxPath(0, max_ns=max(4096, len(w["ns"])), max_clients=max(65536, len(w["clients"]["cid"])), max_frames=n)
+    rx.register_all()
+    synth.load_tables(w, rx)
+    dev = torch.device("cuda", 0)
+    buf = torch.from_numpy(w["buf"]).to(dev)
+    desc = torch.from_numpy(w["desc"].view(np.uint8).copy()).to(dev)
+    rec = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    qcap = abi.queue_cap(n)
+    qlist = torch.empty(abi.NUM_QUEUES * qcap, dtype=torch.int32, device=dev)
+    nt = abi.ntiles(n)
+    tile_cnt = torch.empty(nt * 16, dtype=torch.int32, device=dev)
+    hist = torch.zeros(abi.HIST_SHARDS * 2 * abi.HIST_BINS, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    rx.sync(stream.cuda_stream)
+    classify = rx.classify_call(buf, desc, n, rec, qlist, qcap, tile_cnt, hist, stream=stream)
+    lib = abi.load()
+    lib.emurx_debug_set_stamps.argtypes = [ctypes.c_void_p]
+    st = torch.zeros(nt * 4 * 8, dtype=torch.int64, device=dev)
+    for _ in range(30):
+        classify()
+    torch.cuda.synchronize()
+    out = []
+    for rep in range(3):
+        st.zero_()
+        assert lib.emurx_debug_set_stamps(ctypes.c_void_p(st.data_ptr())) == 0
+        for _ in range(5):
+            classify()
+        torch.cuda.synchronize()
+        assert lib.emurx_debug_set_stamps(ctypes.c_void_p(0)) == 0
+        out.append(st.cpu().numpy().reshape(-1, 8).astype(np.uint64))
+    return out
+
+
+def report(cfg, s):
+    t = s[:, :5].astype(np.int64)
+    ok = t[:, 0] > 0
+    t, hw, xcc = t[ok], s[ok, 5], s[ok, 6]
+    cu = (xcc.astype(np.int64) << 16) | ((hw >> 8) & 0xff).astype(np.int64)
+    d = np.diff(t, axis=1)
+    life = t[:, 4] - t[:, 0]
+    print(f"== config {cfg}: {len(t)} waves, {len(np.unique(cu))} CUs, {len(np.unique(xcc))} XCDs")
+    for k, name in enumerate(["descriptors", "staging", "parse+classify", "records/queues/hist"]):
+        print(f"  {name:22s} cycles/wave mean {d[:, k].mean():8.0f}  p50 {np.median(d[:, k]):8.0f}  p90 {np.percentile(d[:, k], 90):8.0f}")
+    print(f"  {'lifetime':22s} cycles/wave mean {life.mean():8.0f}  p50 {np.median(life):8.0f}  p90 {np.percentile(life, 90):8.0f}")
+    spans, occ, nw, first, last = [], [], [], [], []
+    for c in np.unique(cu):
+        m = cu == c
+        a, b = t[m, 0].min(), t[m, 4].max()
+        spans.append(b - a)
+        occ.append(life[m].sum() / max(b - a, 1))
+        nw.append(m.sum())
+    for x in np.unique(xcc):
+        m = xcc == x
+        first.append(t[m, 0].min())
+        last.append(t[m, 4].max())
+    spans, occ = np.array(spans), np.array(occ)
+    print(f"  per CU: waves {np.mean(nw):.1f} (min {np.min(nw)} max {np.max(nw)}), span cycles mean {spans.mean():.0f} "
+          f"min {spans.min()} max {spans.max()}, mean resident waves {occ.mean():.1f} (min {occ.min():.1f})")
+    xs = np.array(last) - np.array(first)
+    print(f"  per XCD span cycles: {' '.join(str(int(v)) for v in xs)}")
+    # resident-wave profile over the launch, CU-averaged, in 10 slices of each CU's span
+    prof = np.zeros(10)
+    for c in np.unique(cu):
+        m = cu == c
+        a, b = t[m, 0].min(), t[m, 4].max()
+        edges = np.linspace(a, b, 11)
+        for j in range(10):
+            lo, hi = edges[j], edges[j + 1]
+            ov = np.clip(np.minimum(t[m, 4], hi) - np.maximum(t[m, 0], lo), 0, None)
+            prof[j] += ov.sum() / (hi - lo)
+    prof /= len(np.unique(cu))
+    print("  resident waves per CU over the span (10 slices): " + " ".join(f"{v:.1f}" for v in prof))
+
+
+def main():
+    cfgs = sys.argv[1:] or ["B"]
+    sizes = {"B": 1 << 20, "C": 1 << 20, "E": 1 << 20, "D": 1 << 21}
+    for c in cfgs:
+        outs = run(c, sizes[c])
+        for k, s in enumerate(outs):
+            report(c + f" (launch {k})", s)
+            if k == 0:
+                np.save(ROOT / "gpurun_out" / f"stamps_{c}.npy", s)
+
+
+if __name__ == "__main__":
+    os.makedirs(ROOT / "gpurun_out", exist_ok=True)
+    main()

@@ -29,6 +29,20 @@ __device__ __forceinline__ void glds16(const uint4* src, uint4* dst_wave_base) {
 }
 __device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0)
 
+// Timeline stamps (experiment-only build variant, -DEMURX_STAMP=1; tools/stamps.py): per wave
+// {shader clock at entry, after the descriptors, after the staging, after parse + classify,
+// at exit, HW_ID, XCC_ID, tile} as 8 u64, written by lane 0 with vector stores.
+#ifndef EMURX_STAMP
+#define EMURX_STAMP 0
+#endif
+#if EMURX_STAMP
+__device__ unsigned long long* g_stamp;
+#define STAMP(k) \
+    do { if constexpr (EMURX_STAMP) st_[k] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define STAMP(k) do {} while (0)
+#endif
+
 // kKind: 0 parse only, 1 parse + classify, 2 parse + lookup keys (the partitioned source:
 // every frame's emurx_lookup_rec packed straight into its Namespace owner's send region, at
 // the offsets the owner-count pass (k_owner_count + k_route_scan) fixed; no table reads)
@@ -45,14 +59,26 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
     constexpr uint32_t kWinVec = kStage / 16 / kWave;  // window path: 16-byte vectors per lane
     __shared__ __attribute__((aligned(16))) uint32_t slab[kWaves * kStage / 4];
     __shared__ uint32_t s_wcnt[kWaves][16];
-    __shared__ uint32_t s_hist[kWaves][EMURX_HIST_BINS];  // {pkts << 23 | bytes}: <= 64 x 65535 B
     __shared__ uint32_t s_csum[kWaves][kWave];                      // window path: span sums
+    // outcome histogram per wave, {pkts << 23 | bytes}: <= 64 x 65535 B.  It shares the rows
+    // of s_csum (a wave's span sums are done before its histogram is zeroed): 1 KiB less keeps
+    // the narrow slab at 6 workgroups per CU (LDS 26 KiB)
+    static_assert(EMURX_HIST_BINS == kWave, "one histogram bin per lane");
+#if EMURX_SORT
+    __shared__ uint32_t s_hist_own[kWaves][EMURX_HIST_BINS];  // the sort's s_aux lives in s_csum
+    uint32_t (*s_hist)[EMURX_HIST_BINS] = s_hist_own;
+#else
+    uint32_t (*s_hist)[EMURX_HIST_BINS] = s_csum;
+#endif
     __shared__ uint32_t s_rcnt[kWaves][EMURX_MAX_PARTS];            // Namespace owners (rt_cnt)
 
     const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / kWave;
     const uint32_t tile = blockIdx.x;
+#if EMURX_STAMP
+    unsigned long long st_[5];
+#endif
+    STAMP(0);
     const uint32_t i = tile * EMURX_QUEUE_TILE + tid;
-    s_hist[wv][lane] = 0;  // each wave owns its copy: no cross-wave ordering needed
     if (lane < 16) s_wcnt[wv][lane] = 0;
     if (lane < EMURX_MAX_PARTS) s_rcnt[wv][lane] = 0;
     __shared__ uint32_t s_toff[EMURX_MAX_PARTS];  // kKind 2: this tile's offset in each region
@@ -65,6 +91,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
     // the wave's byte range [lo, hi) -> copied HBM -> LDS by LDS-DMA when it fits the slab
     const uint32_t lo = wave_min_u32(valid ? off : 0xffffffffu);
     const uint32_t hi = wave_max_u32(valid ? off + len : 0u);
+    STAMP(1);
     const uint32_t start = lo & ~15u;
     const uint32_t nvec = hi > lo ? (hi - start + 15) >> 4 : 0;
     const bool staged = nvec > 0 && nvec <= kStage / 16;
@@ -96,6 +123,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    STAMP(2);
 
     // The frame this lane parses: its own, or with the shape sort (EMURX_SORT, kinds 0 / 1, all
     // four waves of the tile staged) a frame of the tile from the lane's position in a stable
@@ -186,9 +214,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
     // outcome histogram into the wave's LDS copy: a wave whose frames all share one
     // (status, proto) bin adds its count (ballot) and byte sum (DPP reduction) once, instead
     // of 64 LDS atomics serialised on one address; mixed waves add per frame
+    s_hist[wv][lane] = 0;  // each wave owns its copy: no cross-wave ordering needed
     if (!(EMURX_ABL & 4)) {
         const uint32_t bin = pvalid ? EMURX_HIST_BIN(r.status, r.proto) : 0xffu;
         const uint64_t vm = __ballot(pvalid);
+        STAMP(3);
         if (vm) {
             const uint32_t lead = (uint32_t)__ffsll((long long)vm) - 1;
             const uint32_t bb = (uint32_t)__builtin_amdgcn_readlane((int)bin, (int)lead);
@@ -292,6 +322,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
             atomicAdd(&hs[2 * b + 1], (unsigned long long)by);
         }
     }
+#if EMURX_STAMP
+    STAMP(4);
+    if (g_stamp && lane == 0) {
+        unsigned long long* o = g_stamp + ((size_t)tile * kWaves + wv) * 8;
+        for (int k = 0; k < 5; ++k) o[k] = st_[k];
+        o[5] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+        o[6] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+        o[7] = tile;
+    }
+#endif
 }
 
 
@@ -333,3 +373,10 @@ int emurx_launch_batch(const uint8_t* frames, const emurx_desc* desc, uint32_t n
     if (ev) (void)hipEventRecord(ev[1], st);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+#if EMURX_STAMP
+// the stamp buffer of the timeline variant (tools/stamps.py): 8 u64 per wave of the launch
+extern "C" int emurx_debug_set_stamps(void* dev_buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(emurx::g_stamp), &dev_buf, sizeof(dev_buf)) == hipSuccess ? 0 : -1;
+}
+#endif
