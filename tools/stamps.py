@@ -3,10 +3,11 @@
     tools/build_variant.sh stamp "-DEMURX_STAMP=1"
     EMURX_LIB=trex-emu_amd/lib/libemurx_stamp.so python tools/stamps.py [B C E ...]
 
-Every wave stores {entry, descriptors read, staging landed, parse + classify done, exit}
-shader-clock stamps plus HW_ID / XCC_ID (emurx_kernels.hip, EMURX_STAMP). Printed per config:
+Every wave stores shader-clock stamps {entry, descriptors read, staging landed, parsed, lookup
+key made, tables resolved, histogram, exit} plus HW_ID / XCC_ID (emurx_kernels.hip,
+EMURX_STAMP); a phase a wave skipped (no lane took it) is folded into the next one. Printed per config:
 the phase durations per wave, how many waves each CU held on average over the launch, and the
-launch span per XCD.
+resident-wave profile over the launch (the shader clock is per XCD: spans are taken per CU).
 """
 import ctypes
 import os
@@ -44,7 +45,7 @@ def run(cfg, n):
     classify = rx.classify_call(buf, desc, n, rec, qlist, qcap, tile_cnt, hist, stream=stream)
     lib = abi.load()
     lib.emurx_debug_set_stamps.argtypes = [ctypes.c_void_p]
-    st = torch.zeros(nt * 4 * 8, dtype=torch.int64, device=dev)
+    st = torch.zeros(nt * 4 * 16, dtype=torch.int64, device=dev)
     for _ in range(30):
         classify()
     torch.cuda.synchronize()
@@ -56,46 +57,44 @@ def run(cfg, n):
             classify()
         torch.cuda.synchronize()
         assert lib.emurx_debug_set_stamps(ctypes.c_void_p(0)) == 0
-        out.append(st.cpu().numpy().reshape(-1, 8).astype(np.uint64))
+        out.append(st.cpu().numpy().reshape(-1, 16).astype(np.uint64))
     return out
 
 
 def report(cfg, s):
-    t = s[:, :5].astype(np.int64)
+    t = s[:, :8].astype(np.int64)
     ok = t[:, 0] > 0
-    t, hw, xcc = t[ok], s[ok, 5], s[ok, 6]
+    t, hw, xcc = t[ok], s[ok, 8], s[ok, 9]
+    for k in range(1, 8):  # a skipped stamp takes the previous one (the phase cost nothing)
+        t[:, k] = np.where(t[:, k] == 0, t[:, k - 1], t[:, k])
+    END = 7
     cu = (xcc.astype(np.int64) << 16) | ((hw >> 8) & 0xff).astype(np.int64)
     d = np.diff(t, axis=1)
-    life = t[:, 4] - t[:, 0]
+    life = t[:, END] - t[:, 0]
     print(f"== config {cfg}: {len(t)} waves, {len(np.unique(cu))} CUs, {len(np.unique(xcc))} XCDs")
-    for k, name in enumerate(["descriptors", "staging", "parse+classify", "records/queues/hist"]):
+    for k, name in enumerate(["descriptors", "staging", "parse (+coop csum)", "lookup key", "table lookups",
+                              "records", "queues/hist"]):
         print(f"  {name:22s} cycles/wave mean {d[:, k].mean():8.0f}  p50 {np.median(d[:, k]):8.0f}  p90 {np.percentile(d[:, k], 90):8.0f}")
     print(f"  {'lifetime':22s} cycles/wave mean {life.mean():8.0f}  p50 {np.median(life):8.0f}  p90 {np.percentile(life, 90):8.0f}")
-    spans, occ, nw, first, last = [], [], [], [], []
+    spans, occ, nw = [], [], []
     for c in np.unique(cu):
         m = cu == c
-        a, b = t[m, 0].min(), t[m, 4].max()
+        a, b = t[m, 0].min(), t[m, END].max()
         spans.append(b - a)
         occ.append(life[m].sum() / max(b - a, 1))
         nw.append(m.sum())
-    for x in np.unique(xcc):
-        m = xcc == x
-        first.append(t[m, 0].min())
-        last.append(t[m, 4].max())
     spans, occ = np.array(spans), np.array(occ)
     print(f"  per CU: waves {np.mean(nw):.1f} (min {np.min(nw)} max {np.max(nw)}), span cycles mean {spans.mean():.0f} "
           f"min {spans.min()} max {spans.max()}, mean resident waves {occ.mean():.1f} (min {occ.min():.1f})")
-    xs = np.array(last) - np.array(first)
-    print(f"  per XCD span cycles: {' '.join(str(int(v)) for v in xs)}")
     # resident-wave profile over the launch, CU-averaged, in 10 slices of each CU's span
     prof = np.zeros(10)
     for c in np.unique(cu):
         m = cu == c
-        a, b = t[m, 0].min(), t[m, 4].max()
+        a, b = t[m, 0].min(), t[m, END].max()
         edges = np.linspace(a, b, 11)
         for j in range(10):
             lo, hi = edges[j], edges[j + 1]
-            ov = np.clip(np.minimum(t[m, 4], hi) - np.maximum(t[m, 0], lo), 0, None)
+            ov = np.clip(np.minimum(t[m, END], hi) - np.maximum(t[m, 0], lo), 0, None)
             prof[j] += ov.sum() / (hi - lo)
     prof /= len(np.unique(cu))
     print("  resident waves per CU over the span (10 slices): " + " ".join(f"{v:.1f}" for v in prof))
@@ -106,10 +105,7 @@ def main():
     sizes = {"B": 1 << 20, "C": 1 << 20, "E": 1 << 20, "D": 1 << 21}
     for c in cfgs:
         outs = run(c, sizes[c])
-        for k, s in enumerate(outs):
-            report(c + f" (launch {k})", s)
-            if k == 0:
-                np.save(ROOT / "gpurun_out" / f"stamps_{c}.npy", s)
+        report(c, outs[-1])
 
 
 if __name__ == "__main__":

@@ -30,8 +30,9 @@ __device__ __forceinline__ void glds16(const uint4* src, uint4* dst_wave_base) {
 __device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0)
 
 // Timeline stamps (experiment-only build variant, -DEMURX_STAMP=1; tools/stamps.py): per wave
-// {shader clock at entry, after the descriptors, after the staging, after parse + classify,
-// at exit, HW_ID, XCC_ID, tile} as 8 u64, written by lane 0 with vector stores.
+// the shader clock at entry, after the descriptors, after the staging, after the parse, after
+// the lookup key, after the table lookups, at the histogram and at exit, then HW_ID, XCC_ID
+// and the tile: 16 u64 per wave, written by lane 0 with vector stores.
 #ifndef EMURX_STAMP
 #define EMURX_STAMP 0
 #endif
@@ -75,7 +76,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
     const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / kWave;
     const uint32_t tile = blockIdx.x;
 #if EMURX_STAMP
-    unsigned long long st_[5];
+    unsigned long long st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
     STAMP(0);
     const uint32_t i = tile * EMURX_QUEUE_TILE + tid;
@@ -181,7 +182,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
             LdsSrc s{reinterpret_cast<const uint8_t*>(slab), slab, pbase};
             const uint32_t len = plen, vport = pvport;
             parse_flat(s, len, vport, T.cb_mask, r);
+#if EMURX_STAMP
+            STAMP(3);
+            const bool go = kClassify && r.status == EMURX_ST_OK;
+            LKey k{};
+            if (go) k = make_key(s, len, r);
+            STAMP(4);
+            if (go) resolve(T, r, k, [&](uint32_t cid) { return flow_probe(T, get_tuple(s, len, r), cid); });
+            STAMP(5);
+#else
             if (kClassify && !(EMURX_ABL & 2)) classify(s, len, T, r);
+#endif
             if (kKind == 2 && r.status == EMURX_ST_OK) pack_key(s, len, r, make_key(s, len, r), kwd);
         }
     } else {
@@ -192,7 +203,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
         // the wave's long L4 spans, converged
         if constexpr (EMURX_COOP == 0) coop_checksum(r, frames + off, s_csum[wv]);
         else coop_checksum_rows<EMURX_COOP>(r, frames + off, s_csum[wv]);
+#if EMURX_STAMP
+        STAMP(3);
+        const bool go = valid && kClassify && r.status == EMURX_ST_OK;
+        LKey k{};
+        if (go) k = make_key(s, len, r);
+        STAMP(4);
+        if (go) resolve(T, r, k, [&](uint32_t cid) { return flow_probe(T, get_tuple(s, len, r), cid); });
+        STAMP(5);
+#else
         if (valid && kClassify && !(EMURX_ABL & 2)) classify(s, len, T, r);
+#endif
         if (kKind == 2 && valid && r.status == EMURX_ST_OK) pack_key(s, len, r, make_key(s, len, r), kwd);
     }
     typedef unsigned v4u __attribute__((ext_vector_type(4)));
@@ -218,7 +239,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
     if (!(EMURX_ABL & 4)) {
         const uint32_t bin = pvalid ? EMURX_HIST_BIN(r.status, r.proto) : 0xffu;
         const uint64_t vm = __ballot(pvalid);
-        STAMP(3);
+        STAMP(6);
         if (vm) {
             const uint32_t lead = (uint32_t)__ffsll((long long)vm) - 1;
             const uint32_t bb = (uint32_t)__builtin_amdgcn_readlane((int)bin, (int)lead);
@@ -323,13 +344,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
         }
     }
 #if EMURX_STAMP
-    STAMP(4);
+    STAMP(7);
     if (g_stamp && lane == 0) {
-        unsigned long long* o = g_stamp + ((size_t)tile * kWaves + wv) * 8;
-        for (int k = 0; k < 5; ++k) o[k] = st_[k];
-        o[5] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
-        o[6] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
-        o[7] = tile;
+        unsigned long long* o = g_stamp + ((size_t)tile * kWaves + wv) * 16;
+        for (int k = 0; k < 8; ++k) o[k] = st_[k];
+        o[8] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+        o[9] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+        o[10] = tile;
     }
 #endif
 }
@@ -375,7 +396,7 @@ int emurx_launch_batch(const uint8_t* frames, const emurx_desc* desc, uint32_t n
 }
 
 #if EMURX_STAMP
-// the stamp buffer of the timeline variant (tools/stamps.py): 8 u64 per wave of the launch
+// the stamp buffer of the timeline variant (tools/stamps.py): 16 u64 per wave of the launch
 extern "C" int emurx_debug_set_stamps(void* dev_buf) {
     return hipMemcpyToSymbol(HIP_SYMBOL(emurx::g_stamp), &dev_buf, sizeof(dev_buf)) == hipSuccess ? 0 : -1;
 }

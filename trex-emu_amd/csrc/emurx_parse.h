@@ -411,6 +411,8 @@ __device__ __forceinline__ void parse_packet(const S& s, uint32_t len, uint32_t 
     uint32_t offset = 14;
     uint32_t nextHdr = be16(s, 12);
     int vlanIndex = 0;
+    uint32_t l4 = 0, l4len = 0, nh = 0, pcs = 0;  // the L4 tail's inputs
+    bool v6 = false;
     for (;;) {
         if (nextHdr == 0x8100 || nextHdr == 0x88A8) {
             if (len < offset + 4) { fail(r, EMURX_ST_DOT1Q_TOO_SHORT); return; }
@@ -436,12 +438,11 @@ __device__ __forceinline__ void parse_packet(const S& s, uint32_t len, uint32_t 
             uint32_t totlen = be16(s, offset + 2);
             if (len < ((offset + totlen) & 0xffff)) { fail(r, EMURX_ST_IPV4_TOO_SHORT); return; }
             if (!csum(s, offset, hdr, 0)) { fail(r, EMURX_ST_IPV4_CS); return; }
-            uint32_t l4len = (totlen - hdr) & 0xffff;
-            r.l4 = offset + hdr;
-            uint32_t proto = s.u8(offset + 9);
-            uint32_t pcs = pseudo(s, offset + 12, 8) + proto + l4len;  // src, dst, 0|proto, len
-            parse_l4(s, len, r, proto, pcs, l4len, false, cb_mask);
-            return;
+            l4len = (totlen - hdr) & 0xffff;
+            l4 = offset + hdr;
+            nh = s.u8(offset + 9);
+            pcs = pseudo(s, offset + 12, 8) + nh + l4len;  // src, dst, 0|proto, len
+            break;
         }
         if (nextHdr == 0x86DD) {  // IPv6
             r.l3 = offset;
@@ -450,8 +451,10 @@ __device__ __forceinline__ void parse_packet(const S& s, uint32_t len, uint32_t 
             uint32_t plen = be16(s, offset + 4);
             if (len < ((offset + 40 + plen) & 0xffff)) { fail(r, EMURX_ST_IPV6_TOO_SHORT); return; }
             if (s.u8(offset + 7) == 0) { fail(r, EMURX_ST_IPV6_HOPLIMIT); return; }
-            uint32_t l4 = offset + 40, l4len = plen, osize = 0;
-            uint32_t nh = s.u8(offset + 6);
+            uint32_t osize = 0;
+            l4 = offset + 40;
+            l4len = plen;
+            nh = s.u8(offset + 6);
             for (;;) {
                 bool ext = nh == 0 || nh == 60 || nh == 43 || nh == 51 || nh == 50 || nh == 135 ||
                            nh == 139 || nh == 140;
@@ -471,10 +474,9 @@ __device__ __forceinline__ void parse_packet(const S& s, uint32_t len, uint32_t 
             if (nh == 44) { fail(r, EMURX_ST_IPV6_FRAGMENT); return; }
             if (nh == 194) { fail(r, EMURX_ST_IPV6_JUMBO); return; }
             if (nh == 59) { fail(r, EMURX_ST_IPV6_EMPTY); return; }
-            r.l4 = l4;
-            uint32_t pcs = pseudo(s, offset + 8, 32) + ((plen - osize) & 0xffff) + nh;
-            parse_l4(s, len, r, nh, pcs, l4len, true, cb_mask);
-            return;
+            v6 = true;
+            pcs = pseudo(s, offset + 8, 32) + ((plen - osize) & 0xffff) + nh;  // src, dst, len, 0|nh
+            break;
         }
         if (nextHdr == 0x888E) {  // EAPOL
             if (len < offset + 4) { fail(r, EMURX_ST_EAPOL_TOO_SHORT); return; }
@@ -492,6 +494,9 @@ __device__ __forceinline__ void parse_packet(const S& s, uint32_t len, uint32_t 
         fail(r, EMURX_ST_L3_UNSUPPORTED);
         return;
     }
+    // IPv4 / IPv6: one parsePacketL4 for the wave
+    r.l4 = l4;
+    parse_l4(s, len, r, nh, pcs, l4len, v6, cb_mask);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -591,6 +596,8 @@ __device__ __forceinline__ void parse_flat(const LdsSrc& s, uint32_t len, uint32
     const uint32_t offset = 14 + (g0 ? 4u : 0u) + (g1 ? 4u : 0u);
     const uint32_t et = g1 ? e2 : g0 ? e1 : e0;
 
+    uint32_t l4 = 0, l4len = 0, nh = 0, pcs = 0;  // the L4 tail's inputs
+    bool v6 = false;
     if (et == 0x0800) {  // IPv4
         r.l3 = offset;
         const uint32_t b0 = s.u8(offset), frag = be16(s, offset + 6), totlen = be16(s, offset + 2);
@@ -604,14 +611,11 @@ __device__ __forceinline__ void parse_flat(const LdsSrc& s, uint32_t len, uint32
         const bool hok = csum(s, offset, st == EMURX_ST_OK ? hdr : 0u, 0);
         first(st, !hok, EMURX_ST_IPV4_CS);
         if (st != EMURX_ST_OK) { fail(r, st); return; }
-        const uint32_t l4len = (totlen - hdr) & 0xffff;
-        r.l4 = offset + hdr;
-        const uint32_t proto = s.u8(offset + 9);
-        const uint32_t pcs = pseudo(s, offset + 12, 8) + proto + l4len;  // src, dst, 0|proto, len
-        parse_l4_flat(s, len, r, proto, pcs, l4len, false, cb_mask);
-        return;
-    }
-    if (et == 0x86DD) {  // IPv6
+        l4len = (totlen - hdr) & 0xffff;
+        l4 = offset + hdr;
+        nh = s.u8(offset + 9);
+        pcs = pseudo(s, offset + 12, 8) + nh + l4len;  // src, dst, 0|proto, len
+    } else if (et == 0x86DD) {  // IPv6
         r.l3 = offset;
         const uint32_t plen = be16(s, offset + 4);
         first(st, len < offset + 40, EMURX_ST_IPV6_TOO_SHORT);
@@ -619,8 +623,10 @@ __device__ __forceinline__ void parse_flat(const LdsSrc& s, uint32_t len, uint32
         first(st, len < ((offset + 40 + plen) & 0xffff), EMURX_ST_IPV6_TOO_SHORT);
         first(st, s.u8(offset + 7) == 0, EMURX_ST_IPV6_HOPLIMIT);
         if (st != EMURX_ST_OK) { fail(r, st); return; }
-        uint32_t l4 = offset + 40, l4len = plen, osize = 0;
-        uint32_t nh = s.u8(offset + 6);
+        uint32_t osize = 0;
+        l4 = offset + 40;
+        l4len = plen;
+        nh = s.u8(offset + 6);
         for (;;) {  // extension headers (parser.go:886-931): rare, kept as Go's loop
             const bool ext = nh == 0 || nh == 60 || nh == 43 || nh == 51 || nh == 50 || nh == 135 ||
                              nh == 139 || nh == 140;
@@ -641,19 +647,23 @@ __device__ __forceinline__ void parse_flat(const LdsSrc& s, uint32_t len, uint32
         first(st, nh == 194, EMURX_ST_IPV6_JUMBO);
         first(st, nh == 59, EMURX_ST_IPV6_EMPTY);
         if (st != EMURX_ST_OK) { fail(r, st); return; }
-        r.l4 = l4;
-        const uint32_t pcs = pseudo(s, offset + 8, 32) + ((plen - osize) & 0xffff) + nh;
-        parse_l4_flat(s, len, r, nh, pcs, l4len, true, cb_mask);
+        v6 = true;
+        pcs = pseudo(s, offset + 8, 32) + ((plen - osize) & 0xffff) + nh;  // src, dst, len, 0|nh
+    } else {
+        // EAPOL, ARP (ARPHeaderSize 28), PPPoE, anything else
+        const bool eap = et == 0x888E, arp = et == 0x0806;
+        first(st, eap && len < offset + 4, EMURX_ST_EAPOL_TOO_SHORT);
+        first(st, arp && len < offset + 28, EMURX_ST_ARP_TOO_SHORT);
+        first(st, !eap && !arp && !is_ppp(et), EMURX_ST_L3_UNSUPPORTED);
+        if (st != EMURX_ST_OK) { fail(r, st); return; }
+        if (eap || arp) r.l3 = offset;
+        invoke(r, eap ? EMURX_CB_EAPOL : arp ? EMURX_CB_ARP : EMURX_CB_PPP, cb_mask);
         return;
     }
-    // EAPOL, ARP (ARPHeaderSize 28), PPPoE, anything else
-    const bool eap = et == 0x888E, arp = et == 0x0806;
-    first(st, eap && len < offset + 4, EMURX_ST_EAPOL_TOO_SHORT);
-    first(st, arp && len < offset + 28, EMURX_ST_ARP_TOO_SHORT);
-    first(st, !eap && !arp && !is_ppp(et), EMURX_ST_L3_UNSUPPORTED);
-    if (st != EMURX_ST_OK) { fail(r, st); return; }
-    if (eap || arp) r.l3 = offset;
-    invoke(r, eap ? EMURX_CB_EAPOL : arp ? EMURX_CB_ARP : EMURX_CB_PPP, cb_mask);
+    // IPv4 and IPv6 share parsePacketL4 (and its checksum span): one pass for a wave that
+    // holds both
+    r.l4 = l4;
+    parse_l4_flat(s, len, r, nh, pcs, l4len, v6, cb_mask);
 }
 
 // ---------------------------------------------------------------------------------------
