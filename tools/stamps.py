@@ -4,7 +4,7 @@
     EMURX_LIB=trex-emu_amd/lib/libemurx_stamp.so python tools/stamps.py [B C E ...]
 
 Every wave stores shader-clock stamps {entry, descriptors read, staging landed, parsed, lookup
-key made, tables resolved, histogram, exit} plus HW_ID / XCC_ID (emurx_kernels.hip,
+key made, tables resolved, histogram, tile barrier entered / left, exit} plus HW_ID / XCC_ID (emurx_kernels.hip,
 EMURX_STAMP); a phase a wave skipped (no lane took it) is folded into the next one. Printed per config:
 the phase durations per wave, how many waves each CU held on average over the launch, and the
 resident-wave profile over the launch (the shader clock is per XCD: spans are taken per CU).
@@ -62,18 +62,18 @@ def run(cfg, n):
 
 
 def report(cfg, s):
-    t = s[:, :8].astype(np.int64)
+    t = s[:, :10].astype(np.int64)
     ok = t[:, 0] > 0
-    t, hw, xcc = t[ok], s[ok, 8], s[ok, 9]
-    for k in range(1, 8):  # a skipped stamp takes the previous one (the phase cost nothing)
+    t, hw, xcc = t[ok], s[ok, 10], s[ok, 11]
+    for k in range(1, 10):  # a skipped stamp takes the previous one (the phase cost nothing)
         t[:, k] = np.where(t[:, k] == 0, t[:, k - 1], t[:, k])
-    END = 7
+    END = 9
     cu = (xcc.astype(np.int64) << 16) | ((hw >> 8) & 0xff).astype(np.int64)
     d = np.diff(t, axis=1)
     life = t[:, END] - t[:, 0]
     print(f"== config {cfg}: {len(t)} waves, {len(np.unique(cu))} CUs, {len(np.unique(xcc))} XCDs")
     for k, name in enumerate(["descriptors", "staging", "parse (+coop csum)", "lookup key", "table lookups",
-                              "records", "queues/hist"]):
+                              "records", "ranks/hist", "tile barrier", "queues/counts out"]):
         print(f"  {name:22s} cycles/wave mean {d[:, k].mean():8.0f}  p50 {np.median(d[:, k]):8.0f}  p90 {np.percentile(d[:, k], 90):8.0f}")
     print(f"  {'lifetime':22s} cycles/wave mean {life.mean():8.0f}  p50 {np.median(life):8.0f}  p90 {np.percentile(life, 90):8.0f}")
     spans, occ, nw = [], [], []

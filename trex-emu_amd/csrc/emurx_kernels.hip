@@ -31,8 +31,9 @@ __device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70);
 
 // Timeline stamps (experiment-only build variant, -DEMURX_STAMP=1; tools/stamps.py): per wave
 // the shader clock at entry, after the descriptors, after the staging, after the parse, after
-// the lookup key, after the table lookups, at the histogram and at exit, then HW_ID, XCC_ID
-// and the tile: 16 u64 per wave, written by lane 0 with vector stores.
+// the lookup key, after the table lookups, at the histogram, before and after the tile
+// barrier and at exit, then HW_ID, XCC_ID and the tile: 16 u64 per wave, written by lane 0
+// with vector stores.
 #ifndef EMURX_STAMP
 #define EMURX_STAMP 0
 #endif
@@ -76,7 +77,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
     const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / kWave;
     const uint32_t tile = blockIdx.x;
 #if EMURX_STAMP
-    unsigned long long st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long st_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
     STAMP(0);
     const uint32_t i = tile * EMURX_QUEUE_TILE + tid;
@@ -296,7 +297,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
             rl &= ~m;
         }
     }
+    STAMP(7);
     __syncthreads();
+    STAMP(8);
     if (kKind == 1 && rt.cnt && tid < 16) {
         const uint32_t c = tid < rt.parts ? s_rcnt[0][tid] + s_rcnt[1][tid] + s_rcnt[2][tid] + s_rcnt[3][tid] : 0u;
         rt.cnt[(size_t)tile * 16 + tid] = c;
@@ -344,13 +347,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
         }
     }
 #if EMURX_STAMP
-    STAMP(7);
+    STAMP(9);
     if (g_stamp && lane == 0) {
         unsigned long long* o = g_stamp + ((size_t)tile * kWaves + wv) * 16;
-        for (int k = 0; k < 8; ++k) o[k] = st_[k];
-        o[8] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
-        o[9] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
-        o[10] = tile;
+        for (int k = 0; k < 10; ++k) o[k] = st_[k];
+        o[10] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+        o[11] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+        o[12] = tile;
     }
 #endif
 }

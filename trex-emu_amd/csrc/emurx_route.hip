@@ -165,14 +165,17 @@ __global__ __launch_bounds__(kBlock) void k_owner_count(const uint8_t* __restric
 // k_lookup: the owner's half — GetNs + the callback's client rule + the flow decision for
 // every received lookup record, against this partition's tables (classify()'s resolve).
 // Output slot j = the input slot: n_parts regions of cap emurx_route_rec, valid up to
-// recv_count[source].
-__global__ __launch_bounds__(kBlock) void k_lookup(const emurx_lookup_rec* __restrict__ recv,
+// recv_count[source].  Grid: (records of a region / kBlock, source region): no division.
+#ifndef EMURX_LOOKUP_WPE
+#define EMURX_LOOKUP_WPE 6
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EMURX_LOOKUP_WPE))) void k_lookup(const emurx_lookup_rec* __restrict__ recv,
                                                    const uint32_t* __restrict__ recv_count, uint32_t n_parts,
                                                    uint32_t cap, emurx_dev_tables T,
                                                    emurx_route_rec* __restrict__ out, uint32_t* __restrict__ flow) {
-    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t src = (uint32_t)(j / cap), idx = (uint32_t)(j % cap);
-    if (src >= n_parts || idx >= recv_count[src]) return;
+    const uint32_t src = blockIdx.y, idx = blockIdx.x * kBlock + threadIdx.x;
+    if (idx >= recv_count[src] || idx >= cap) return;
+    const uint64_t j = (uint64_t)src * cap + idx;
     const uint4* p = reinterpret_cast<const uint4*>(recv + j);
     const uint4 a = p[0], b = p[1], k0 = p[2], k1 = p[3], k2 = p[4];
     Rec r;
@@ -222,12 +225,10 @@ int emurx_launch_owner_count(const uint8_t* frames, const emurx_desc* desc, uint
 int emurx_launch_lookup(const emurx_lookup_rec* recv, const uint32_t* recv_count, uint32_t n_parts, uint32_t cap,
                         const emurx_dev_tables& T, emurx_route_rec* out, uint32_t* flow, hipStream_t st) {
     using namespace emurx;
-    const uint64_t slots = (uint64_t)n_parts * cap;
-    if (slots) {
-        const uint64_t g = (slots + kBlock - 1) / kBlock;
-        if (g > 0x7fffffffu) return -1;
-        hipLaunchKernelGGL(k_lookup, dim3((uint32_t)g), dim3(kBlock), 0, st, recv, recv_count, n_parts, cap, T, out,
-                           flow);
+    if (n_parts && cap) {
+        if (n_parts > 65535) return -1;
+        hipLaunchKernelGGL(k_lookup, dim3((cap + kBlock - 1) / kBlock, n_parts), dim3(kBlock), 0, st, recv, recv_count,
+                           n_parts, cap, T, out, flow);
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
