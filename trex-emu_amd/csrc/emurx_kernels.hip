@@ -37,6 +37,9 @@ __device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70);
 #ifndef EMURX_STAMP
 #define EMURX_STAMP 0
 #endif
+#ifndef EMURX_CSTAGE
+#define EMURX_CSTAGE 0  // client buckets staged in the slab by quad-cooperative LDS-DMA
+#endif
 #if EMURX_STAMP
 __device__ unsigned long long* g_stamp;
 #define STAMP(k) \
@@ -178,7 +181,54 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
     Rec r;
     r.dlen = 0;
     uint32_t kwd[12];  // kKind 2: the lookup key words of the frame
-    if (staged) {  // wave-uniform branch
+    if (staged && kClassify && EMURX_CSTAGE && !T.ft_on && !(EMURX_ABL & 2)) {  // wave-uniform branch
+        // The client buckets of the wave staged in its slab.  Once the lookup keys are made the
+        // frame bytes are not read again (no TransportCtx: no flow tuple), so the slab takes
+        // the 64 client buckets, 4 KiB: each LDS-DMA instruction loads 16 whole buckets, a
+        // quad of lanes per bucket (16 lines per instruction instead of 64), bucket i landing
+        // at slab byte 64 i.  The Namespace buckets load into registers alongside.
+        LdsSrc s{reinterpret_cast<const uint8_t*>(slab), slab, pbase};
+        const uint32_t len = plen;
+        bool go = false;
+        LKey k{};
+        Probe pr{};
+        if (pvalid) {
+            parse_flat(s, len, pvport, T.cb_mask, r);
+            go = r.status == EMURX_ST_OK;
+            if (go) {
+                k = make_key(s, len, r);
+                pr = probe_issue(T, r, k);
+            }
+        }
+        STAMP(3);
+        STAMP(4);
+        const uintptr_t ca = go && pr.ctab ? (uintptr_t)(pr.ctab + (size_t)pr.cbk * EMURX_BUCKET_WORDS) : 0;
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): every read of the frame bytes has returned
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+            const uint32_t src = 16 * q + (lane >> 2);
+            const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)ca, (int)src);
+            const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)ca >> 32), (int)src);
+            const uintptr_t a = ((uintptr_t)hi << 32) | lo;
+            if (a) glds16(reinterpret_cast<const uint4*>(a) + (lane & 3), wslab + 64 * q);
+        }
+        wait_vm0();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (go) {
+            Bucket ce{};
+            if (pr.ctab) {
+                const uint4* b = wslab + 4 * lane;
+                ce = Bucket{{b[0], b[1], b[2], b[3]}};
+            }
+            resolve_done(T, r, k, pr, ce, [](uint32_t) { return EMURX_FLOW_NO_CTX; });  // ft_on == 0: never called
+        }
+        STAMP(5);
+    } else if (staged) {  // wave-uniform branch
         if (pvalid) {
             LdsSrc s{reinterpret_cast<const uint8_t*>(slab), slab, pbase};
             const uint32_t len = plen, vport = pvport;

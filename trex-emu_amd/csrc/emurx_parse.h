@@ -1160,37 +1160,50 @@ __device__ __forceinline__ LKey make_key(const S& s, uint32_t len, const Rec& r)
     return k;
 }
 
-// GetNs + the callback's client rule against the tables.  `flow(cid)` gives the transport
+// The two bucket reads of a frame's lookups, issued together: its Namespace bucket (loaded
+// here) and the first bucket of its client table (ctab == nullptr: the rule reads none).
+struct Probe {
+    uint32_t nb, cbk, mlo, mhi;  // mlo / mhi: the MAC probed for kMac / kEui
+    const uint32_t* ctab;
+    Bucket ne;
+};
+__device__ __forceinline__ Probe probe_issue(const emurx_dev_tables& T, const Rec& r, const LKey& k) {
+    Probe p;
+    const uint32_t key = k.key;
+    p.mlo = k.kw[0];
+    p.mhi = k.kw[1];
+    if (key == kEui) {
+        p.mlo = ((k.kw[2] & 0xff) ^ 2) | (((k.kw[2] >> 8) & 0xff) << 8) | (((k.kw[2] >> 16) & 0xff) << 16) |
+                (((k.kw[3] >> 8) & 0xff) << 24);
+        p.mhi = ((k.kw[3] >> 16) & 0xff) | ((k.kw[3] >> 24) << 8);
+    }
+    const uint32_t tk = emurx_tk_hash(r.vport, r.vlan0, r.vlan1);  // CTunnelKey words
+    p.nb = tk & T.ns_mask;
+    p.ne = ld_bucket(T.ns_tab, p.nb);
+    p.cbk = 0;
+    p.ctab = nullptr;
+    if (key == kMac || key == kEui) {
+        p.cbk = emurx_mac_hash(tk, p.mlo, p.mhi) & T.mac_mask;
+        p.ctab = T.mac_tab;
+    } else if (key == kIp4) {
+        p.cbk = emurx_ip4_hash(tk, k.kw[0]) & T.ip4_mask;
+        p.ctab = T.ip4_tab;
+    } else if (key == kIp6) {
+        p.cbk = emurx_ip6_hash(tk, k.kw[0], k.kw[1], k.kw[2], k.kw[3]) & T.ip6_mask;
+        p.ctab = T.ip6_tab;
+    }
+    return p;
+}
+
+// GetNs + the callback's client rule, given the two buckets.  `flow(cid)` gives the transport
 // flow decision of a tcp/udp frame whose client was found with the transport plugin.
 template <class Flow>
-__device__ __forceinline__ void resolve(const emurx_dev_tables& T, Rec& r, const LKey& k, Flow flow) {
+__device__ __forceinline__ void resolve_done(const emurx_dev_tables& T, Rec& r, const LKey& k, const Probe& p,
+                                             const Bucket& ce, Flow flow) {
     const uint32_t cb = r.proto, plug = kCbPlugin[cb];
-    const uint32_t key = k.key;
-    uint32_t mlo = k.kw[0], mhi = k.kw[1];  // the MAC probed for kMac / kEui
-    if (key == kEui) {
-        mlo = ((k.kw[2] & 0xff) ^ 2) | (((k.kw[2] >> 8) & 0xff) << 8) | (((k.kw[2] >> 16) & 0xff) << 16) |
-              (((k.kw[3] >> 8) & 0xff) << 24);
-        mhi = ((k.kw[3] >> 16) & 0xff) | ((k.kw[3] >> 24) << 8);
-    }
-    // ---- issue the Namespace and client bucket reads together ----
-    const uint32_t tk = emurx_tk_hash(r.vport, r.vlan0, r.vlan1);  // CTunnelKey words
-    const uint32_t nb = tk & T.ns_mask;
-    const Bucket ne = ld_bucket(T.ns_tab, nb);
-    uint32_t cbk = 0;
-    Bucket ce{};
-    if (key == kMac || key == kEui) {
-        cbk = emurx_mac_hash(tk, mlo, mhi) & T.mac_mask;
-        ce = ld_bucket(T.mac_tab, cbk);
-    } else if (key == kIp4) {
-        cbk = emurx_ip4_hash(tk, k.kw[0]) & T.ip4_mask;
-        ce = ld_bucket(T.ip4_tab, cbk);
-    } else if (key == kIp6) {
-        cbk = emurx_ip6_hash(tk, k.kw[0], k.kw[1], k.kw[2], k.kw[3]) & T.ip6_mask;
-        ce = ld_bucket(T.ip6_tab, cbk);
-    }
-
+    const uint32_t key = k.key, cbk = p.cbk, mlo = p.mlo, mhi = p.mhi;
     // ---- GetNs + ns.PluginCtx.Get(plugin) ----
-    const uint2 nsr = resolve_ns(T, nb, ne, r.vport, r.vlan0, r.vlan1);
+    const uint2 nsr = resolve_ns(T, p.nb, p.ne, r.vport, r.vlan0, r.vlan1);
     const uint32_t ns = nsr.x;
     if (ns == EMURX_ID_NONE) { set_lk(r, EMURX_LK_NO_NS); return; }
     r.ns = ns;
@@ -1256,6 +1269,15 @@ __device__ __forceinline__ void resolve(const emurx_dev_tables& T, Rec& r, const
         return;
     }
     }
+}
+
+// GetNs + the callback's client rule against the tables (both bucket reads in flight together)
+template <class Flow>
+__device__ __forceinline__ void resolve(const emurx_dev_tables& T, Rec& r, const LKey& k, Flow flow) {
+    const Probe p = probe_issue(T, r, k);
+    Bucket ce{};
+    if (p.ctab) ce = ld_bucket(p.ctab, p.cbk);
+    resolve_done(T, r, k, p, ce, flow);
 }
 
 // parse state -> Namespace / Client ids, lookup outcome, flow decision (replicated tables:
