@@ -171,6 +171,18 @@ __device__ __forceinline__ uint32_t dword_sum(const A& w, uint32_t a, uint32_t n
     for (; k < k1; ++k) acc = sad16(w[k], acc);
     return sad16(w[k1] & tm, acc);
 }
+// the same over a fixed length N (a multiple of 4) from byte a: N/4 + 1 dwords, straight-line
+// (the last one masked to nothing when a is dword-aligned; reading it is harmless in LDS)
+template <uint32_t N>
+__device__ __forceinline__ uint32_t dword_sum_fixed(const uint32_t* w, uint32_t a) {
+    static_assert(N % 4 == 0 && N >= 4, "whole dwords");
+    const uint32_t k0 = a >> 2, sh = 8 * (a & 3);
+    const uint32_t hm = 0xffffffffu << sh;
+    uint32_t acc = sad16(w[k0] & hm, 0);
+#pragma unroll
+    for (uint32_t j = 1; j < N / 4; ++j) acc = sad16(w[k0 + j], acc);
+    return sad16(w[k0 + N / 4] & ~hm, acc);
+}
 // bytes [lo, hi) of a 16-byte vector (indices may fall outside 0..16)
 __device__ __forceinline__ uint32_t keep(int lo, int hi, int d) {
     const int a = lo - 4 * d, b = hi - 4 * d;
@@ -215,6 +227,8 @@ struct LdsSrc {
     uint32_t base;        // LDS byte index of frame byte 0 (== global address mod 16)
     __device__ __forceinline__ uint32_t u8(uint32_t i) const { return b8[base + i]; }
     __device__ __forceinline__ uint32_t sum(uint32_t s, uint32_t n) const { return dword_sum(b32, base + s, n); }
+    template <uint32_t N>
+    __device__ __forceinline__ uint32_t sum_fixed(uint32_t s) const { return dword_sum_fixed<N>(b32, base + s); }
     __device__ __forceinline__ uint32_t at(uint32_t s) const { return base + s; }
 };
 // window layout: vector k of lane l at wave slab byte k * 1024 + l * 16 (LDS-DMA order)
@@ -608,13 +622,15 @@ __device__ __forceinline__ void parse_flat(const LdsSrc& s, uint32_t len, uint32
         first(st, hdr < 20, EMURX_ST_IPV4_HDR_TOO_SHORT);
         first(st, len < offset + hdr, EMURX_ST_IPV4_HDR_TOO_SHORT);
         first(st, len < ((offset + totlen) & 0xffff), EMURX_ST_IPV4_TOO_SHORT);
-        const bool hok = csum(s, offset, st == EMURX_ST_OK ? hdr : 0u, 0);
+        // the header sum: straight-line for the usual 20 bytes (a failed frame's value is unused)
+        const uint32_t th = hdr == 20 ? s.sum_fixed<20>(offset) : s.sum(offset, st == EMURX_ST_OK ? hdr : 0u);
+        const bool hok = (EMURX_ABL & 1) || csum_ok(th, s.at(offset), 0);
         first(st, !hok, EMURX_ST_IPV4_CS);
         if (st != EMURX_ST_OK) { fail(r, st); return; }
         l4len = (totlen - hdr) & 0xffff;
         l4 = offset + hdr;
         nh = s.u8(offset + 9);
-        pcs = pseudo(s, offset + 12, 8) + nh + l4len;  // src, dst, 0|proto, len
+        pcs = be_domain(s.sum_fixed<8>(offset + 12), s.at(offset + 12)) + nh + l4len;  // src, dst, 0|proto, len
     } else if (et == 0x86DD) {  // IPv6
         r.l3 = offset;
         const uint32_t plen = be16(s, offset + 4);
@@ -648,7 +664,7 @@ __device__ __forceinline__ void parse_flat(const LdsSrc& s, uint32_t len, uint32
         first(st, nh == 59, EMURX_ST_IPV6_EMPTY);
         if (st != EMURX_ST_OK) { fail(r, st); return; }
         v6 = true;
-        pcs = pseudo(s, offset + 8, 32) + ((plen - osize) & 0xffff) + nh;  // src, dst, len, 0|nh
+        pcs = be_domain(s.sum_fixed<32>(offset + 8), s.at(offset + 8)) + ((plen - osize) & 0xffff) + nh;  // src, dst, len, 0|nh
     } else {
         // EAPOL, ARP (ARPHeaderSize 28), PPPoE, anything else
         const bool eap = et == 0x888E, arp = et == 0x0806;
