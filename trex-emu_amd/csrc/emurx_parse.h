@@ -173,8 +173,8 @@ __device__ __forceinline__ uint32_t dword_sum(const A& w, uint32_t a, uint32_t n
 }
 // the same over a fixed length N (a multiple of 4) from byte a: N/4 + 1 dwords, straight-line
 // (the last one masked to nothing when a is dword-aligned; reading it is harmless in LDS)
-template <uint32_t N>
-__device__ __forceinline__ uint32_t dword_sum_fixed(const uint32_t* w, uint32_t a) {
+template <uint32_t N, class A>
+__device__ __forceinline__ uint32_t dword_sum_fixed(const A& w, uint32_t a) {
     static_assert(N % 4 == 0 && N >= 4, "whole dwords");
     const uint32_t k0 = a >> 2, sh = 8 * (a & 3);
     const uint32_t hm = 0xffffffffu << sh;
@@ -257,6 +257,11 @@ struct WinSrc {
         const uint32_t g = max(s, wlim);
         if (e > g) acc += glb_sum(f + g, e - g);
         return acc;
+    }
+    // fixed length N inside the window: straight-line (dword N/4 + 1 still lies in it)
+    template <uint32_t N>
+    __device__ __forceinline__ uint32_t sum_fixed(uint32_t s) const {
+        return s + N <= wlim ? dword_sum_fixed<N>(WinDw{b32 + (wbase >> 2)}, head + s) : sum(s, N);
     }
     __device__ __forceinline__ uint32_t at(uint32_t s) const { return (uint32_t)(uintptr_t)(f + s); }
 };
@@ -451,11 +456,12 @@ __device__ __forceinline__ void parse_packet(const S& s, uint32_t len, uint32_t 
             if (len < offset + hdr) { fail(r, EMURX_ST_IPV4_HDR_TOO_SHORT); return; }
             uint32_t totlen = be16(s, offset + 2);
             if (len < ((offset + totlen) & 0xffff)) { fail(r, EMURX_ST_IPV4_TOO_SHORT); return; }
-            if (!csum(s, offset, hdr, 0)) { fail(r, EMURX_ST_IPV4_CS); return; }
+            const uint32_t th = hdr == 20 ? s.template sum_fixed<20>(offset) : s.sum(offset, hdr);
+            if (!(EMURX_ABL & 1) && !csum_ok(th, s.at(offset), 0)) { fail(r, EMURX_ST_IPV4_CS); return; }
             l4len = (totlen - hdr) & 0xffff;
             l4 = offset + hdr;
             nh = s.u8(offset + 9);
-            pcs = pseudo(s, offset + 12, 8) + nh + l4len;  // src, dst, 0|proto, len
+            pcs = be_domain(s.template sum_fixed<8>(offset + 12), s.at(offset + 12)) + nh + l4len;  // src, dst, 0|proto, len
             break;
         }
         if (nextHdr == 0x86DD) {  // IPv6
@@ -489,7 +495,7 @@ __device__ __forceinline__ void parse_packet(const S& s, uint32_t len, uint32_t 
             if (nh == 194) { fail(r, EMURX_ST_IPV6_JUMBO); return; }
             if (nh == 59) { fail(r, EMURX_ST_IPV6_EMPTY); return; }
             v6 = true;
-            pcs = pseudo(s, offset + 8, 32) + ((plen - osize) & 0xffff) + nh;  // src, dst, len, 0|nh
+            pcs = be_domain(s.template sum_fixed<32>(offset + 8), s.at(offset + 8)) + ((plen - osize) & 0xffff) + nh;  // src, dst, len, 0|nh
             break;
         }
         if (nextHdr == 0x888E) {  // EAPOL
@@ -623,14 +629,14 @@ __device__ __forceinline__ void parse_flat(const LdsSrc& s, uint32_t len, uint32
         first(st, len < offset + hdr, EMURX_ST_IPV4_HDR_TOO_SHORT);
         first(st, len < ((offset + totlen) & 0xffff), EMURX_ST_IPV4_TOO_SHORT);
         // the header sum: straight-line for the usual 20 bytes (a failed frame's value is unused)
-        const uint32_t th = hdr == 20 ? s.sum_fixed<20>(offset) : s.sum(offset, st == EMURX_ST_OK ? hdr : 0u);
+        const uint32_t th = hdr == 20 ? s.template sum_fixed<20>(offset) : s.sum(offset, st == EMURX_ST_OK ? hdr : 0u);
         const bool hok = (EMURX_ABL & 1) || csum_ok(th, s.at(offset), 0);
         first(st, !hok, EMURX_ST_IPV4_CS);
         if (st != EMURX_ST_OK) { fail(r, st); return; }
         l4len = (totlen - hdr) & 0xffff;
         l4 = offset + hdr;
         nh = s.u8(offset + 9);
-        pcs = be_domain(s.sum_fixed<8>(offset + 12), s.at(offset + 12)) + nh + l4len;  // src, dst, 0|proto, len
+        pcs = be_domain(s.template sum_fixed<8>(offset + 12), s.at(offset + 12)) + nh + l4len;  // src, dst, 0|proto, len
     } else if (et == 0x86DD) {  // IPv6
         r.l3 = offset;
         const uint32_t plen = be16(s, offset + 4);
@@ -664,7 +670,7 @@ __device__ __forceinline__ void parse_flat(const LdsSrc& s, uint32_t len, uint32
         first(st, nh == 59, EMURX_ST_IPV6_EMPTY);
         if (st != EMURX_ST_OK) { fail(r, st); return; }
         v6 = true;
-        pcs = be_domain(s.sum_fixed<32>(offset + 8), s.at(offset + 8)) + ((plen - osize) & 0xffff) + nh;  // src, dst, len, 0|nh
+        pcs = be_domain(s.template sum_fixed<32>(offset + 8), s.at(offset + 8)) + ((plen - osize) & 0xffff) + nh;  // src, dst, len, 0|nh
     } else {
         // EAPOL, ARP (ARPHeaderSize 28), PPPoE, anything else
         const bool eap = et == 0x888E, arp = et == 0x0806;
