@@ -331,7 +331,7 @@ int emurx_table_stats(const emurx_t* h, uint64_t* delta_blocks, uint64_t* whole_
    Rebuilds and ships every table.  (1, 0) = replicated (the default). */
 int emurx_set_partition(emurx_t* h, uint32_t n_parts, uint32_t part);
 
-/* ---- mid-batch table mutations (DESIGN.md §3.7) ---------------------------------------
+/* ---- mid-batch table mutations (DESIGN.md §2.2) ---------------------------------------
    A batch is classified against the tables as they stand when it is launched (a snapshot);
    the Go loop dispatches its records in frame order, and a callback may mutate the maps
    (DHCP's UpdateClientIpv4 dhcp.go:718, a TCP accept adding a flow) before later frames of
@@ -378,7 +378,8 @@ int emurx_classify_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_
                        uint32_t n, const emurx_dev_out* out, void* stream);
 
 /* Device-resident, parse only (no table lookups): records with ns_id/client_id NONE and
-   lookup EMURX_LK_NONE.  Used by the multi-GPU path before the Namespace all-to-all. */
+   lookup EMURX_LK_NONE (ParsePacket alone).  The multi-GPU path uses emurx_parse_route_dev,
+   which parses and packs the lookup records for the Namespace owners in the same pass. */
 int emurx_parse_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_desc,
                     uint32_t n, const emurx_dev_out* out, void* stream);
 

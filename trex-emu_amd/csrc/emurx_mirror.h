@@ -15,7 +15,7 @@
 //
 // Generations: every mutation advances `gen` and stamps the Namespace it touched.  A record
 // classified against the tables as they stood at generation g is stale iff its Namespace
-// (found by its tunnel key now, or removed since) was stamped after g (DESIGN.md §3.7).
+// (found by its tunnel key now, or removed since) was stamped after g (DESIGN.md §2.2).
 //
 // No HIP here: host-only handles (cfg.device < 0) use the mirror alone.
 #pragma once
