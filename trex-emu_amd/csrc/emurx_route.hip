@@ -173,10 +173,27 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EMURX_LO
                                                    const uint32_t* __restrict__ recv_count, uint32_t n_parts,
                                                    uint32_t cap, emurx_dev_tables T,
                                                    emurx_route_rec* __restrict__ out, uint32_t* __restrict__ flow) {
-    const uint32_t src = blockIdx.y, idx = blockIdx.x * kBlock + threadIdx.x;
-    if (idx >= recv_count[src] || idx >= cap) return;
+    // the wave's 64 records are contiguous: 5 KiB copied into LDS by five fully coalesced
+    // LDS-DMA loads (a lane-strided 80-byte read would touch 40 lines per instruction)
+    __shared__ __attribute__((aligned(16))) uint4 s_rec[kWaves][kWave * 5];
+    const uint32_t lane = threadIdx.x % kWave, wv = threadIdx.x / kWave;
+    const uint32_t src = blockIdx.y, idx0 = blockIdx.x * kBlock + wv * kWave, idx = idx0 + lane;
+    const uint32_t cnt = min(recv_count[src], cap);
+    if (idx0 >= cnt) return;  // wave-uniform
     const uint64_t j = (uint64_t)src * cap + idx;
-    const uint4* p = reinterpret_cast<const uint4*>(recv + j);
+    const uint4* base = reinterpret_cast<const uint4*>(recv + (uint64_t)src * cap + idx0);
+    const uint32_t nvec = min(kWave, cnt - idx0) * 5;  // never past the region's valid records
+#pragma unroll
+    for (uint32_t k = 0; k < 5; ++k)
+        if (k * kWave + lane < nvec)
+            __builtin_amdgcn_global_load_lds(base + k * kWave + lane,
+                                             (__attribute__((address_space(3))) void*)&s_rec[wv][k * kWave], 16, 0, 0);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (idx >= cnt) return;
+    const uint4* p = &s_rec[wv][lane * 5];
     const uint4 a = p[0], b = p[1], k0 = p[2], k1 = p[3], k2 = p[4];
     Rec r;
     r.ns = EMURX_ID_NONE;
