@@ -13,7 +13,7 @@ for f in emurx_kernels emurx_route emurx_ingest emurx_tx emurx_txzmq; do
   objs="$objs $out/$f.o"
 done
 /opt/rocm/bin/hipcc $F -x hip -c csrc/emurx_api.cpp -o $out/emurx_api.o &
-${CXX:-g++} -O2 -std=c++17 -fPIC -Wall -c csrc/emurx_mirror.cpp -o $out/emurx_mirror.o &
+${CXX:-g++} -O2 -std=c++17 -fPIC -Wall $flags -c csrc/emurx_mirror.cpp -o $out/emurx_mirror.o &
 wait
 /opt/rocm/bin/hipcc $F -shared -o lib/libemurx_$name.so $objs $out/emurx_api.o $out/emurx_mirror.o
 echo lib/libemurx_$name.so
