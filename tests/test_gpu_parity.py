@@ -140,6 +140,11 @@ def test_corpus(rxmod):
     rec = check_batch(rx, o, buf, desc)
     lk = (rec["flags"] >> 4) & 7
     assert (lk == abi.LK["CLIENT"]).sum() > 1000     # the lookups are exercised
+    # every answered rx frame reaches the callback of the plugin its capture simulates
+    toc = __import__("test_oracle_corpus")
+    z = np.load(toc.GOLD, allow_pickle=False)
+    for i in np.nonzero(z["meta"] == 1)[0]:
+        assert rec["status"][i] == 0 and abi.CB_NAMES[rec["proto"][i]] == toc.capture_callback(str(z["files"][z["src"][i]]))
     # reorder the descriptors: records follow descriptor order, not buffer order
     perm = np.random.default_rng(3).permutation(len(desc))
     check_batch(rx, o, buf, desc[perm])

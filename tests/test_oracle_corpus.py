@@ -2,7 +2,10 @@
 extracted from unit-test/exp by tests/golden/make_corpus.py).
 
 Pins: every rx frame the reference's plugin simulations answered reaches a callback
-(SURVEY.md §4), and the per-callback distribution of the whole corpus.
+(SURVEY.md §4), and the callback it reaches is the one of the plugin whose simulation the
+capture records (its file name: arp*.json -> arp, dns*.json -> udp, the DNS plugin's sockets
+ride the transport plugin's UDP, ipv6nd / mld / ipv6ping -> icmpv6, dot1x -> eapol, ...); the
+per-callback distribution of the whole corpus is recomputed here (scratch counts).
 """
 import collections
 from pathlib import Path
@@ -21,6 +24,21 @@ TX_EXPECT = {"udp": 4398, "tcp": 1214, "igmp": 703, "arp": 620, "icmpv6": 377, "
              "eapol": 13, "icmp": 11}
 
 
+# capture name prefix -> the callback of the plugin under simulation (src/emu/plugins/<name>,
+# registered as in src/cmd/trex-emu.go:47-67; dns rides transport UDP sockets)
+CAPTURE_CB = [("dhcpsrv", "dhcpsrv"), ("dhcpv6", "dhcpv6"), ("dhcp", "dhcp"), ("arp", "arp"),
+              ("dns", "udp"), ("dot1x", "eapol"), ("icmpv6", "icmpv6"), ("icmp", "icmp"),
+              ("igmp", "igmp"), ("ipv6nd", "icmpv6"), ("ipv6ping", "icmpv6"), ("mdns", "mdns"),
+              ("mld", "icmpv6")]
+
+
+def capture_callback(name):
+    for pre, cb in CAPTURE_CB:
+        if name.startswith(pre):
+            return cb
+    return None
+
+
 def load_corpus():
     z = np.load(GOLD, allow_pickle=False)
     return z["data"], z["off"], z["len"], z["meta"]
@@ -33,6 +51,24 @@ def corpus_batch():
     fr = [data[o:o + l].tobytes() for o, l in zip(off, ln)]
     buf, desc = F.pack_frames(fr, vports=[1] * len(fr))
     return buf, desc, meta
+
+
+def test_rx_frames_reach_their_plugin(oracle_built):
+    """Each answered rx frame reaches the callback of the plugin its capture simulates."""
+    import pyoracle
+    z = np.load(GOLD, allow_pickle=False)
+    files, src = z["files"], z["src"]
+    buf, desc, meta = corpus_batch()
+    rec, _, _, _ = pyoracle.Oracle().rx_batch(buf, desc)
+    rx = np.nonzero(meta == 1)[0]
+    assert len(rx) == sum(RX_EXPECT.values())
+    checked = 0
+    for i in rx:
+        want = capture_callback(str(files[src[i]]))
+        assert want is not None, files[src[i]]
+        assert rec["status"][i] == 0 and abi.CB_NAMES[rec["proto"][i]] == want, (files[src[i]], i)
+        checked += 1
+    assert checked == len(rx)
 
 
 def test_corpus_distribution(oracle_built):
