@@ -1,0 +1,74 @@
+"""Classification outcomes pinned by the reference's own plugin simulations.
+
+Each capture in unit-test/exp (tests/golden/corpus_frames.npz) was recorded by a Go test that
+builds one Namespace and its clients (createSimulationEnv in the plugin's *_test.go), injects
+the rx frames and records what the plugins sent.  Rebuilding that environment from the test's
+source and classifying the capture's rx frames gives an outcome the capture itself vouches
+for: the plugin answered with frames that only a found client sends (an ARP or echo reply
+from the client's MAC, the client's next DHCP / DHCPv6 / EAPOL message), or, for arp5, sent
+no reply at all.  This pins the lookup rules -- MAC[dst], IPv4[dst] + IsUnicastToMe, IPv4 of
+the ARP target, the IPv6 map behind CLookupByIPv6LocalGlobal, the DHCP chaddr of a broadcast
+OFFER, the first client of an EAPOL PAE frame -- against the reference rather than against
+the oracle's reading of the Go code.
+"""
+import struct
+
+# the one Namespace of every environment: vport 1, tags 0x8100/1 and 0x8100/2 (CTunnelKey bytes)
+NS_KEY = struct.pack("<HHII", 1, 0, 0x81000001, 0x81000002)
+PLUG = ["arp", "icmp", "igmp", "dhcp", "dhcpsrv", "dhcpv6", "mdns", "transport", "ipv6", "dot1x", "ppp"]
+
+# createSimulationEnv of each plugin test: client 0's MAC / IPv4 / IPv6 and the one plugin the
+# test creates on the Namespace and the client
+ENVS = {
+    # src/emu/plugins/icmp/icmp_test.go:76-100 (num = 1: a = b = 0)
+    "icmp": dict(mac=bytes([0, 0, 1, 0, 0, 0]), ipv4=bytes([16, 0, 0, 0]), ipv6=None, plugin="icmp"),
+    # src/emu/plugins/arp/arp_test.go:78-106
+    "arp": dict(mac=bytes([0, 0, 1, 0, 0, 0]), ipv4=bytes([16, 0, 0, 0]), ipv6=None, plugin="arp"),
+    # src/emu/plugins/ipv6/ipv6_test.go:81-113 (static Ipv6 2001:db8::2)
+    "ipv6": dict(mac=bytes([0, 0, 1, 0, 0, 0]), ipv4=bytes([16, 0, 0, 0]),
+                 ipv6=bytes([0x20, 0x01, 0x0D, 0xB8] + [0] * 11 + [2]), plugin="ipv6"),
+    # src/emu/plugins/dhcpv4/dhcp_test.go:83-101 (no IPv4 yet)
+    "dhcp": dict(mac=bytes([0, 0, 1, 0, 0, 1]), ipv4=None, ipv6=None, plugin="dhcp"),
+    # src/emu/plugins/dhcpv6/dhcpv6_test.go:83-109
+    "dhcpv6": dict(mac=bytes([0, 0, 1, 0, 0, 1]), ipv4=None, ipv6=None, plugin="dhcpv6"),
+    # src/emu/plugins/dot1x/dot1x_test.go:82-102
+    "dot1x": dict(mac=bytes([0, 0, 1, 0, 0, 1]), ipv4=None, ipv6=None, plugin="dot1x"),
+}
+
+# (capture, environment, lookup outcome of every rx frame, client id or None, the capture's evidence)
+CASES = [
+    ("icmp1.json", "icmp", "CLIENT", 0, "6 echo requests, 6 echo replies from 00:00:01:00:00:00"),
+    ("arp4.json", "arp", "CLIENT", 0, "6 requests for 16.0.0.0, 6 ARP replies (op 2) from the client"),
+    ("arp5.json", "arp", "NO_CLIENT", None, "6 requests for 16.0.0.5, no ARP reply in the capture"),
+    ("icmpv6_1.json", "ipv6", "CLIENT", 0, "6 echo requests to 2001:db8::2, 6 echo replies from it"),
+    ("icmpv6_2.json", "ipv6", "CLIENT", 0, "6 echo requests to 2001:db8::2, 6 echo replies from it"),
+    ("dhcp1.json", "dhcp", "CLIENT", 0, "unicast OFFER / ACKs, the client's REQUESTs follow"),
+    ("dhcp4.json", "dhcp", "CLIENT", 0, "unicast OFFERs, the client's REQUESTs follow"),
+    ("dhcp5.json", "dhcp", "CLIENT", 0, "broadcast OFFERs (chaddr rule), the client's REQUESTs follow"),
+    ("dhcp6.json", "dhcp", "CLIENT", 0, "broadcast OFFERs (chaddr rule), the client's REQUESTs follow"),
+    ("dhcp7.json", "dhcp", "CLIENT", 0, "broadcast OFFERs (chaddr rule), the client's REQUESTs follow"),
+    ("dhcpv6_1.json", "dhcpv6", "CLIENT", 0, "ADVERTISE / REPLY to the client's MAC, its next messages follow"),
+    ("dhcpv6_3.json", "dhcpv6", "CLIENT", 0, "ADVERTISE / REPLY to the client's MAC, its next messages follow"),
+    ("dhcpv6_4.json", "dhcpv6", "CLIENT", 0, "ADVERTISE / REPLY to the client's MAC, its next messages follow"),
+    ("dhcpv6_5.json", "dhcpv6", "CLIENT", 0, "ADVERTISE / REPLY to the client's MAC, its next messages follow"),
+    ("dot1x_1.json", "dot1x", "CLIENT", 0, "PAE group frames (first-client rule), EAPOL answers follow"),
+    ("dot1x_4.json", "dot1x", "CLIENT", 0, "PAE group frames (first-client rule), EAPOL answers follow"),
+    ("dot1x_7.json", "dot1x", "CLIENT", 0, "PAE group frames (first-client rule), EAPOL answers follow"),
+]
+
+
+def rx_frames(z, capture):
+    """The capture's rx frames, in order (z: the corpus npz)."""
+    import numpy as np
+    files = [str(x) for x in z["files"]]
+    src, meta, off, ln, data = z["src"], z["meta"], z["off"], z["len"], z["data"]
+    idx = np.nonzero((src == files.index(capture)) & (meta == 1))[0]
+    return [data[off[i]:off[i] + ln[i]].tobytes() for i in idx]
+
+
+def load_env(target, env):
+    """One Namespace with the environment's plugin, client 0 with it (ns id 0, client id 0)."""
+    e = ENVS[env]
+    m = 1 << PLUG.index(e["plugin"])
+    assert target.ns_add(NS_KEY, 0, m) == 0
+    assert target.client_add(0, 0, e["mac"], e["ipv4"], e["ipv6"], None, m) == 0

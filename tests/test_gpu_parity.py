@@ -740,3 +740,21 @@ def test_transport_flows(rxmod):
         assert rx.client_remove(int(c["ns"][k]), c["mac"][k].tobytes()) == \
             o.client_remove(int(c["ns"][k]), c["mac"][k].tobytes())
     check()
+
+
+# ---- lookup outcomes the reference's plugin simulations vouch for (tests/sim_envs.py) --------
+def test_reference_simulations(rxmod):
+    import sim_envs as S
+    toc = __import__("test_oracle_corpus")
+    z = np.load(toc.GOLD, allow_pickle=False)
+    for capture, env, lk, cid, _ in S.CASES:
+        fr = S.rx_frames(z, capture)
+        rx, o = new_pair(rxmod, max_ns=16, max_clients=64, max_frames=1024)
+        S.load_env(rx, env)
+        S.load_env(o, env)
+        buf, desc = F.pack_frames(fr, [1] * len(fr))
+        rec = check_batch(rx, o, buf, desc)
+        assert (rec["status"] == 0).all() and (rec["ns_id"] == 0).all(), capture
+        assert (((rec["flags"] >> 4) & 7) == abi.LK[lk]).all(), capture
+        assert (rec["client_id"] == (0xFFFFFFFF if cid is None else cid)).all(), capture
+        rx.close()
