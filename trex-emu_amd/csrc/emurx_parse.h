@@ -43,6 +43,11 @@ __device__ __forceinline__ uint4 gld16(const void* p) {
     const emurx_v4u v = *(const __attribute__((address_space(1))) emurx_v4u*)p;
     return make_uint4(v.x, v.y, v.z, v.w);
 }
+typedef unsigned emurx_v3u __attribute__((ext_vector_type(3)));
+__device__ __forceinline__ uint3 gld12(const void* p) {  // 4-byte aligned
+    const emurx_v3u v = *(const __attribute__((address_space(1))) emurx_v3u*)p;
+    return make_uint3(v.x, v.y, v.z);
+}
 __device__ __forceinline__ uint32_t gld4(const void* p) { return *(const __attribute__((address_space(1))) uint32_t*)p; }
 __device__ __forceinline__ uint32_t gld1(const void* p) { return *(const __attribute__((address_space(1))) uint8_t*)p; }
 

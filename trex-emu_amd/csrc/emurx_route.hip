@@ -137,9 +137,9 @@ __global__ __launch_bounds__(kBlock) void k_owner_count(const uint8_t* __restric
         const uint32_t len = dd.y & 0xffff, vport = (dd.y >> 16) & 0xff;
         // bytes 12..19 from three aligned dwords (the buffer is readable past every frame)
         const uintptr_t a = (uintptr_t)(frames + dd.x + 12);
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
         const uint32_t sh = (uint32_t)(a & 3);
-        const uint32_t w0 = gld4(w), w1 = gld4(w + 1), w2 = gld4(w + 2);
+        const uint3 w3 = gld12(reinterpret_cast<const void*>(a & ~(uintptr_t)3));
+        const uint32_t w0 = w3.x, w1 = w3.y, w2 = w3.z;  // one 12-byte load
         const uint32_t b12 = __builtin_bswap32(__builtin_amdgcn_alignbyte(w1, w0, sh));
         const uint32_t b16 = __builtin_bswap32(__builtin_amdgcn_alignbyte(w2, w1, sh));
         uint32_t v0, v1;
