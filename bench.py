@@ -64,6 +64,9 @@ def parse_args():
                          "around the whole timed region, duration = elapsed / launches; launch = "
                          "events around every --time-stride-th launch (each pair adds ~1.5 us to "
                          "the step it brackets); off = wall clock only")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="N > 1 with an exchange: run each timed batch's all-to-all to completion "
+                         "before the next batch's parse (default: overlap them, two buffer sets)")
     ap.add_argument("--no-check", action="store_true",
                     help="skip the output sanity check (stage-ablation builds, tools/ablate.sh)")
     ap.add_argument("--tx-path", action="store_true",
@@ -304,12 +307,60 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         rb = X.LOOKUP_BYTES if mode == "partitioned" else X.REC_BYTES
         xch = dict(cap=X.capacity(n, world), ev=[], timing=False, k=0, rb=rb)
 
+        # two buffer sets when the timed steps overlap batch k's exchange with batch k+1's parse
+        nsets = 2 if world > 1 and not a.no_overlap else 1
+
         def alloc_regions():
-            xch["send"] = torch.empty(world * xch["cap"] * rb, dtype=torch.uint8, device=dev)
-            xch["send_count"] = torch.zeros(world, dtype=torch.int32, device=dev)
-            if mode == "partitioned":
-                xch["out"] = torch.empty(world * xch["cap"] * X.REC_BYTES, dtype=torch.uint8, device=dev)
+            xch["sets"] = []
+            for _ in range(nsets):
+                b = dict(send=torch.empty(world * xch["cap"] * rb, dtype=torch.uint8, device=dev),
+                         send_count=torch.zeros(world, dtype=torch.int32, device=dev), pending=None)
+                if mode == "partitioned":
+                    b["out"] = torch.empty(world * xch["cap"] * X.REC_BYTES, dtype=torch.uint8, device=dev)
+                xch["sets"].append(b)
+            xch.update(send=xch["sets"][0]["send"], send_count=xch["sets"][0]["send_count"],
+                       out=xch["sets"][0].get("out"))
         alloc_regions()
+
+        def produce(b):
+            if mode == "replicated":
+                # classify + route in one call: the route's owner counts are taken inside k_rx
+                rx.classify_route_dev(buf, desc, n, rec, qlist, qcap, tile_cnt, hist, world, rank, xch["cap"],
+                                      b["send"], b["send_count"], stream=stream)
+            else:
+                # no source records: every frame's lookup record carries its parse to the owner
+                rx.parse_route_dev(buf, desc, n, None, qlist, qcap, tile_cnt, hist, world, rank, xch["cap"],
+                                   b["send"], b["send_count"], stream=stream)
+
+        def consume(b):
+            xch["recv"], xch["recv_count"] = X.exchange_finish(b["pending"])
+            b["pending"] = None
+            if mode == "partitioned":
+                rx.lookup_dev(xch["recv"], xch["recv_count"], world, xch["cap"], b["out"], stream=stream)
+
+        def step_overlapped():
+            """Batch k: parse + pack, then its all-to-all starts on the collective stream while
+            the previous batch's owner lookups (behind its own all-to-all) and the next batch's
+            parse queue up on this stream."""
+            k = xch["k"]
+            xch["k"] += 1
+            b, prev = xch["sets"][k % 2], xch["sets"][(k + 1) % 2]
+            ev = None
+            if xch["timing"] and k % a.time_stride == 0 and xch["pool"]:
+                ev = xch["pool"].pop()
+                ev[0].record(stream)
+            produce(b)
+            b["pending"] = X.exchange_start(b["send"], b["send_count"], xch["cap"], rec_bytes=rb)
+            if prev["pending"] is not None:
+                consume(prev)
+            if ev is not None:
+                ev[1].record(stream)
+                xch["ev"].append(ev)
+
+        def drain():
+            for b in xch["sets"]:
+                if b["pending"] is not None:
+                    consume(b)
 
     def step():
         if xch is None:
@@ -320,14 +371,7 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             ev = xch["pool"].pop()  # created before the timed region: creating one costs ~50 us
             ev[0].record(stream)
         xch["k"] += 1
-        if mode == "replicated":
-            # classify + route in one call: the route's owner counts are taken inside k_rx
-            rx.classify_route_dev(buf, desc, n, rec, qlist, qcap, tile_cnt, hist, world, rank, xch["cap"],
-                                  xch["send"], xch["send_count"], stream=stream)
-        else:
-            # no source records: every frame's lookup record carries its parse to the owner
-            rx.parse_route_dev(buf, desc, n, None, qlist, qcap, tile_cnt, hist, world, rank, xch["cap"],
-                               xch["send"], xch["send_count"], stream=stream)
+        produce(xch["sets"][0])
         if world > 1:
             xch["recv"], xch["recv_count"] = X.exchange(xch["send"], xch["send_count"], xch["cap"], rec_bytes=rb)
         else:
@@ -372,11 +416,16 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    overlapped = xch is not None and len(xch["sets"]) > 1
+    if overlapped:
+        xch["k"] = 0
     if region:
         reg_ev[0].record(stream)
     t0 = time.perf_counter()
     for _ in range(steps):
-        step()
+        step_overlapped() if overlapped else step()
+    if overlapped:
+        drain()
     if region:
         reg_ev[1].record(stream)
     t_submit = time.perf_counter() - t0
@@ -389,7 +438,8 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
     else:
         pk = rx.kernel_times()
         rx.set_timing(0)
-    if xch is not None and exchange_overflow(xch, world, dist, torch, dev):
+    if xch is not None and any(exchange_overflow(dict(xch, send_count=b["send_count"]), world, dist, torch, dev)
+                               for b in xch["sets"]):
         raise RuntimeError("exchange region overflow in the timed region")
 
     if world > 1:
@@ -482,6 +532,7 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             "records_per_region_cap": xch["cap"],
             "record_bytes": xch["rb"],
             "collective": f"all_to_all_single x2 ({a.backend})" if world > 1 else "none (1 rank)",
+            "overlapped": overlapped,  # batch k's all-to-all beside batch k+1's parse (two buffer sets)
             "includes": ("k_rx + group scan + pack" + (" + all-to-all" if world > 1 else "") +
                          (" + owner lookups (k_lookup)" if mode == "partitioned" else "")),
         }

@@ -56,6 +56,33 @@ def exchange(send, send_count, cap: int, group=None, rec_bytes: int = REC_BYTES)
     return recv, recv_count
 
 
+def exchange_start(send, send_count, cap: int, group=None, rec_bytes: int = REC_BYTES):
+    """exchange() without waiting: the all-to-alls are enqueued on the collective's stream
+    behind the work already on the caller's stream, and the caller's stream goes on (the next
+    batch's parse overlaps this batch's transfer).  exchange_finish() makes the caller's
+    stream wait for them and returns (recv, recv_count).  gloo on device tensors (CPU
+    rehearsals) completes here."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    assert send.numel() == world * cap * rec_bytes and send_count.numel() == world
+    if dist.get_backend(group) == "gloo" and send.is_cuda:
+        return (None,) + exchange(send, send_count, cap, group, rec_bytes)
+    recv = torch.empty_like(send)
+    recv_count = torch.empty_like(send_count)
+    works = (dist.all_to_all_single(recv_count, send_count, group=group, async_op=True),
+             dist.all_to_all_single(recv, send, group=group, async_op=True))
+    return works, recv, recv_count
+
+
+def exchange_finish(pending):
+    """(recv, recv_count) of an exchange_start(), the caller's stream ordered after it."""
+    works, recv, recv_count = pending
+    for w in works or ():
+        w.wait()
+    return recv, recv_count
+
+
 def received(recv: np.ndarray, recv_count: np.ndarray, cap: int) -> np.ndarray:
     """Valid records of a receive buffer (host copy), source-rank order."""
     r = np.ascontiguousarray(recv).view(np.uint8).reshape(-1)[: len(recv_count) * cap * REC_BYTES]
