@@ -110,6 +110,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
     }
     if (staged) {  // all copies in flight before the wait; clamped sources stay in bounds
         static_assert(kStage / 16 <= 8 * kWave, "staging issues at most 8 vectors per lane");
+        // each LDS-DMA instruction writes 64 vectors (1 KiB) of the slab; a slab that is not a
+        // whole number of them would let the last one run into the next wave's slab
+        static_assert(kStage % (16 * kWave) == 0, "slab = whole 1 KiB DMA rows");
         const uint4* src = reinterpret_cast<const uint4*>(frames + start);
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k)
