@@ -465,6 +465,7 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             pmc_src = str(pmc.relative_to(ROOT))
         except Exception:  # noqa: BLE001
             traffic = None
+    copy_gbs = copy_ceiling(torch, dev, stream)
     # the Namespace + Client bucket reads of every frame that reaches a callback (two 64-B
     # buckets, issued together): outside the algorithmic bytes, served by L2 / MALL / HBM
     r = rec.cpu().numpy().view(abi.REC_DTYPE)
@@ -507,6 +508,8 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
             "traffic_source": pmc_src,
+            "copy_ceiling_gbs": round(copy_gbs, 1),  # a streaming copy on this GPU, measured here
+            "frac_of_copy_ceiling": round(achieved / copy_gbs, 4) if copy_gbs > 0 else None,
             "kernel": "k_rx" + (" (parse + lookup keys)" if mode == "partitioned" else ""),
             "alg_bytes_per_launch": alg_bytes,
             "alg_bytes_per_frame": round(alg_bytes / n, 2),
@@ -607,6 +610,33 @@ def table_update_cost(a, rx, w, torch, rounds=8):
     torch.cuda.synchronize()
     out["full_rebuild_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
     return out
+
+
+def copy_ceiling(torch, dev, stream, mib=1024, reps=8):
+    """HBM ceiling as this GPU runs it: a 1 GiB streaming copy (emurx_copy_ceiling_dev: 16-byte
+    non-temporal loads and stores, 8 in flight per lane), read + write bytes over the
+    HIP-event time of `reps` copies."""
+    try:
+        from emurx import abi
+        lib = abi.load()
+        n = mib << 20
+        src = torch.empty(n, dtype=torch.uint8, device=dev)
+        dst = torch.empty_like(src)
+
+        def once():
+            abi.check(lib.emurx_copy_ceiling_dev(dst.data_ptr(), src.data_ptr(), n, stream.cuda_stream), "copy")
+        once()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            once()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        del src, dst
+        return 2 * n / (ms * 1e-3) / 1e9
+    except Exception:  # noqa: BLE001 - a reported context figure, never the metric
+        return 0.0
 
 
 def exchange_overflow(xch, world, dist, torch, dev):

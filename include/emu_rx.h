@@ -521,6 +521,11 @@ int emurx_kernel_times(emurx_t* h, float* batch_ms, uint32_t cap, uint32_t* n_ou
    observable of this implementation. */
 uint32_t emurx_last_stage(const emurx_t* h);
 
+/* HBM copy ceiling of this GPU for the roofline context (bench.py): a streaming 16-byte copy
+   of `bytes` (a multiple of 16, 16-byte aligned device pointers) on `stream`, one launch.
+   Not part of the receive path. */
+int emurx_copy_ceiling_dev(void* d_dst, const void* d_src, size_t bytes, void* stream);
+
 /* ---- Namespace-partitioned exchange (multi-GPU, one process per GPU) -------------------
    Frames shard by input offset across the GPUs of a node; each Namespace is owned by one
    partition, emurx_ns_owner(key) = a hash of its CTunnelKey (thread_ctx.go:92-97) mapped

@@ -170,6 +170,7 @@ SIGNATURES = [
     ("emurx_set_timing", C.c_int, [_P, C.c_uint32, C.c_uint32]),
     ("emurx_kernel_times", C.c_int, [_P, _P, C.c_uint32, C.POINTER(C.c_uint32)]),
     ("emurx_last_stage", C.c_uint32, [_P]),
+    ("emurx_copy_ceiling_dev", C.c_int, [_P, _P, C.c_size_t, _P]),
     ("emurx_ns_owner", C.c_uint32, [_U8P, C.c_uint32]),
     ("emurx_route_dev", C.c_int, [_P, _P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P]),
     ("emurx_classify_route_dev", C.c_int, [_P, _P, _P, C.c_uint32, C.POINTER(DevOut), C.c_uint32, C.c_uint32,
