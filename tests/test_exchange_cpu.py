@@ -61,6 +61,16 @@ def _worker(rank, world, port, out_dir):
         ok = got.tobytes() == want.tobytes() and len(got) > 0
         owners = route_ref.owners(got["rec"], world)
         ok = ok and bool((owners == rank).all())
+        # two exchanges in flight at once (the bench's overlapped steps): started A then B,
+        # finished B then A; A equals the blocking exchange, B (no records) delivers none
+        send_t = torch.from_numpy(send.view(np.uint8).reshape(-1).copy())
+        junk = torch.from_numpy(np.random.default_rng(rank).integers(0, 256, send_t.numel(), dtype=np.uint8))
+        pa = X.exchange_start(send_t, torch.from_numpy(cnt), cap)
+        pb = X.exchange_start(junk, torch.zeros(world, dtype=torch.int32), cap)
+        rb, cb = X.exchange_finish(pb)
+        ra, ca = X.exchange_finish(pa)
+        ok = ok and bool((cb == 0).all()) and torch.equal(ca, recv_count)
+        ok = ok and X.received(ra.numpy(), ca.numpy(), cap).tobytes() == got.tobytes()
         Path(out_dir, f"r{rank}").write_text(f"{int(ok)} {len(got)}")
     finally:
         dist.destroy_process_group()
