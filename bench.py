@@ -68,7 +68,7 @@ def parse_args():
                     help="N > 1 with an exchange: run each timed batch's all-to-all to completion "
                          "before the next batch's parse (default: overlap them, two buffer sets)")
     ap.add_argument("--no-check", action="store_true",
-                    help="skip the output sanity check (stage-ablation builds, tools/ablate.sh)")
+                    help="skip the output sanity check (stage-ablation builds, tools/abl_counts.sh)")
     ap.add_argument("--tx-path", action="store_true",
                     help="also time the device tx ZMQ framing (emurx_tx_zmq_dev) over the same frames")
     ap.add_argument("--launch-check", action="store_true",

@@ -24,7 +24,7 @@ constexpr int kWaves = kBlock / kWave;
 constexpr uint32_t kStageWide = 7168, kStageNarrow = 6144;
 
 #ifndef EMURX_ABL
-#define EMURX_ABL 0  // experiment-only stage ablation (tools/ablate.sh); 0 in every real build
+#define EMURX_ABL 0  // experiment-only stage ablation (tools/abl_counts.sh); 0 in every real build
 #endif
 #ifndef EMURX_SORT
 #define EMURX_SORT 0  // A/B: shape-class sort of a staged tile's frames over its lanes (emurx_kernels.hip)
