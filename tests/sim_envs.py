@@ -8,8 +8,8 @@ for: the plugin answered with frames that only a found client sends (an ARP or e
 from the client's MAC, the client's next DHCP / DHCPv6 / EAPOL message), or, for arp5, sent
 no reply at all.  This pins the lookup rules -- MAC[dst], IPv4[dst] + IsUnicastToMe, IPv4 of
 the ARP target, the IPv6 map behind CLookupByIPv6LocalGlobal, the DHCP chaddr of a broadcast
-OFFER, the first client of an EAPOL PAE frame -- against the reference rather than against
-the oracle's reading of the Go code.
+OFFER, the first client of an EAPOL PAE frame or of a broadcast to the DHCP server --
+against the reference rather than against the oracle's reading of the Go code.
 """
 import struct
 
@@ -33,6 +33,11 @@ ENVS = {
     "dhcpv6": dict(mac=bytes([0, 0, 1, 0, 0, 1]), ipv4=None, ipv6=None, plugin="dhcpv6"),
     # src/emu/plugins/dot1x/dot1x_test.go:82-102
     "dot1x": dict(mac=bytes([0, 0, 1, 0, 0, 1]), ipv4=None, ipv6=None, plugin="dot1x"),
+    # src/emu/plugins/dhcpv4srv/dhcpsrv_test.go:413-455: vport 1 without tags, client 0 runs the
+    # DHCP server (its plugins dhcpsrv + transport, the Namespace's dhcpsrv)
+    "dhcpsrv": dict(mac=bytes([0, 0, 1, 0, 0, 0]), ipv4=bytes([16, 0, 0, 0]),
+                    ipv6=bytes([0x20, 0x01, 0x0D, 0xB8] + [0] * 12), plugin="dhcpsrv",
+                    client_plugins=("dhcpsrv", "transport"), key=struct.pack("<HHII", 1, 0, 0, 0)),
 }
 
 # (capture, environment, lookup outcome of every rx frame, client id or None, the capture's evidence)
@@ -54,6 +59,11 @@ CASES = [
     ("dot1x_1.json", "dot1x", "CLIENT", 0, "PAE group frames (first-client rule), EAPOL answers follow"),
     ("dot1x_4.json", "dot1x", "CLIENT", 0, "PAE group frames (first-client rule), EAPOL answers follow"),
     ("dot1x_7.json", "dot1x", "CLIENT", 0, "PAE group frames (first-client rule), EAPOL answers follow"),
+] + [
+    # broadcast DISCOVER / REQUEST -> GetFirstClient (the server), unicast ones -> MAC[dst]; the
+    # server client answers from 00:00:01:00:00:00 in every capture but dhcpsrv7 (no answer)
+    (f"dhcpsrv{i}.json", "dhcpsrv", "CLIENT", 0, "the server client (first client) answers")
+    for i in (1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19)
 ]
 
 
@@ -70,5 +80,8 @@ def load_env(target, env):
     """One Namespace with the environment's plugin, client 0 with it (ns id 0, client id 0)."""
     e = ENVS[env]
     m = 1 << PLUG.index(e["plugin"])
-    assert target.ns_add(NS_KEY, 0, m) == 0
-    assert target.client_add(0, 0, e["mac"], e["ipv4"], e["ipv6"], None, m) == 0
+    cm = 0
+    for pl in e.get("client_plugins", (e["plugin"],)):
+        cm |= 1 << PLUG.index(pl)
+    assert target.ns_add(e.get("key", NS_KEY), 0, m) == 0
+    assert target.client_add(0, 0, e["mac"], e["ipv4"], e["ipv6"], None, cm) == 0
