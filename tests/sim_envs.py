@@ -38,7 +38,19 @@ ENVS = {
     "dhcpsrv": dict(mac=bytes([0, 0, 1, 0, 0, 0]), ipv4=bytes([16, 0, 0, 0]),
                     ipv6=bytes([0x20, 0x01, 0x0D, 0xB8] + [0] * 12), plugin="dhcpsrv",
                     client_plugins=("dhcpsrv", "transport"), key=struct.pack("<HHII", 1, 0, 0, 0)),
+    # src/emu/plugins/igmp/igmp_test.go:114-132
+    "igmp": dict(mac=bytes([0, 0, 1, 0, 0, 1]), ipv4=None, ipv6=None, plugin="igmp"),
+    # src/emu/plugins/mdns/mdns_test.go:128-150 (vport 1 without tags)
+    "mdns": dict(mac=bytes([0, 0, 1, 0, 0, 0]), ipv4=bytes([16, 0, 0, 0]), ipv6=None, plugin="mdns",
+                 key=struct.pack("<HHII", 1, 0, 0, 0)),
+    # src/emu/plugins/dns/dns_test.go:138-184: "dns:N" = clients 0..N-1 (N = the test's
+    # clientsToSim), MAC 00:00:01:00:00:j, 16.0.0.j, 2001:db8::j, plugins dns + transport; the
+    # DNS traffic rides transport UDP sockets, so the Namespace's transport plugin takes it
+    "dns": dict(mac=None, ipv4=None, ipv6=None, plugin="transport", key=struct.pack("<HHII", 1, 0, 0, 0)),
 }
+# clientsToSim of each DNS capture (dns_test.go testname / clientsToSim pairs)
+DNS_CLIENTS = {3: 1, 4: 1, 5: 2, 6: 2, 7: 2, 8: 2, 9: 2, 10: 2, 12: 2, 13: 3, 14: 4, 15: 4, 16: 4, 17: 4,
+               18: 3, 19: 3, 20: 4, 21: 4}
 
 # (capture, environment, lookup outcome of every rx frame, client id or None, the capture's evidence)
 CASES = [
@@ -64,6 +76,21 @@ CASES = [
     # server client answers from 00:00:01:00:00:00 in every capture but dhcpsrv7 (no answer)
     (f"dhcpsrv{i}.json", "dhcpsrv", "CLIENT", 0, "the server client (first client) answers")
     for i in (1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19)
+] + [
+    # Namespace-level callbacks: the Namespace found with the plugin, no client lookup; the
+    # Namespace's plugin answered (IGMP / MLD reports, mDNS responses, ND advertisements)
+    (f"igmp{i}.json", "igmp", "NS_LEVEL", None, "the Namespace's IGMP plugin reports")
+    for i in (3, 4, 6, 10, 11)
+] + [
+    (f"mdns{i}.json", "mdns", "NS_LEVEL", None, "the Namespace's mDNS plugin answers every query")
+    for i in range(3, 23)
+] + [
+    (f"{c}.json", "ipv6", "NS_LEVEL", None, "the Namespace's IPv6 plugin answers (NA, MLD reports)")
+    for c in ("ipv6nd_1", "ipv6nd_2", "ipv6nd_3", "ipv6nd_4", "ipv6nd_rpc", "mld1_1", "mld2_1", "mld2_2", "mld2_10")
+] + [
+    # client "dst": the client whose MAC the frame is sent to (MAC[dst], the transport rule)
+    (f"dns{i}.json", f"dns:{n}", "CLIENT", "dst", "the DNS plugins' queries and answers around them")
+    for i, n in sorted(DNS_CLIENTS.items())
 ]
 
 
@@ -77,11 +104,26 @@ def rx_frames(z, capture):
 
 
 def load_env(target, env):
-    """One Namespace with the environment's plugin, client 0 with it (ns id 0, client id 0)."""
-    e = ENVS[env]
+    """One Namespace with the environment's plugin and its client(s): client 0 (ns id 0,
+    client id 0), or for "dns:N" clients 0..N-1."""
+    name, _, count = env.partition(":")
+    e = ENVS[name]
     m = 1 << PLUG.index(e["plugin"])
     cm = 0
     for pl in e.get("client_plugins", (e["plugin"],)):
         cm |= 1 << PLUG.index(pl)
     assert target.ns_add(e.get("key", NS_KEY), 0, m) == 0
+    if name == "dns":
+        for j in range(int(count)):
+            assert target.client_add(0, j, bytes([0, 0, 1, 0, 0, j]), bytes([16, 0, 0, j]),
+                                     bytes([0x20, 0x01, 0x0D, 0xB8] + [0] * 11 + [j]), None, cm) == 0
+        return
     assert target.client_add(0, 0, e["mac"], e["ipv4"], e["ipv6"], None, cm) == 0
+
+
+def expected_clients(frames, cid):
+    """The client id every frame must resolve to (None: no client)."""
+    import numpy as np
+    if cid == "dst":
+        return np.array([f[5] for f in frames], np.uint32)
+    return np.full(len(frames), 0xFFFFFFFF if cid is None else cid, np.uint32)

@@ -756,5 +756,5 @@ def test_reference_simulations(rxmod):
         rec = check_batch(rx, o, buf, desc)
         assert (rec["status"] == 0).all() and (rec["ns_id"] == 0).all(), capture
         assert (((rec["flags"] >> 4) & 7) == abi.LK[lk]).all(), capture
-        assert (rec["client_id"] == (0xFFFFFFFF if cid is None else cid)).all(), capture
+        assert (rec["client_id"] == S.expected_clients(fr, cid)).all(), capture
         rx.close()

@@ -8,7 +8,6 @@ import sim_envs as S
 from emurx import abi, frames as F
 from test_oracle_corpus import GOLD
 
-NONE = 0xFFFFFFFF
 
 
 @pytest.mark.parametrize("case", S.CASES, ids=[c[0] for c in S.CASES])
@@ -25,4 +24,4 @@ def test_simulation_outcome(oracle_built, case):
     assert (rec["status"] == 0).all()
     assert (rec["ns_id"] == 0).all()
     assert (((rec["flags"] >> 4) & 7) == abi.LK[lk]).all()
-    assert (rec["client_id"] == (NONE if cid is None else cid)).all()
+    assert (rec["client_id"] == S.expected_clients(fr, cid)).all()
