@@ -8,7 +8,10 @@ A step = one batch through the hot path: emurx_classify_dev = one k_rx launch (d
 checksums + Namespace/Client lookups + 32-B records + stable per-callback queue segments +
 outcome histogram) over F frames already resident in HBM.  Default workload = config B
 (1M x 64 B untagged IPv4/UDP, 1 Namespace / 1 Client), the configuration the metric is
-quoted on.  For N > 1 (torchrun, one rank per GPU) every rank processes its own F-frame
+quoted on.  Consecutive batches alternate between two streams (--streams, default 2), each
+with its own output buffers, as the ingest path's two slots do: a batch's launch runs beside
+the previous one instead of waiting for its last workgroups.  For N > 1 (torchrun, one rank
+per GPU) every rank processes its own F-frame
 shard against replicated tables: frames are independent, so there is no data-path
 collective (weak scaling); value = frames over all ranks / max-over-ranks time.
 
@@ -18,7 +21,8 @@ Namespace was found into the owners' regions and an equal-split all-to-all (RCCL
 xGMI) delivers them, with the per-region counts in a second all-to-all.
 
 The JSON line carries `roofline` (algorithmic bytes per frame = frame_len + 8 B descriptor
-+ 32 B record + 4 B queue entry, over k_rx's mean HIP-event duration on the launch stream) and
++ 32 B record + 4 B queue entry, over k_rx's launch interval from one HIP event pair around
+the timed region; `roofline.one_stream` has the same launches back to back on one stream) and
 `cpu_baseline` (the oracle, a single-threaded C restatement of the Go path, timed on this
 host's cores over a bounded sample of the same workload; rank 0 at N=1 only).
 """
@@ -64,6 +68,10 @@ def parse_args():
                          "around the whole timed region, duration = elapsed / launches; launch = "
                          "events around every --time-stride-th launch (each pair adds ~1.5 us to "
                          "the step it brackets); off = wall clock only")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="steps without an exchange: consecutive batches go round-robin to this many "
+                         "streams, each with its own output buffers, so a batch's k_rx runs beside the "
+                         "previous one (as the ingest path's two slots do); 1 = back to back on one stream")
     ap.add_argument("--no-overlap", action="store_true",
                     help="N > 1 with an exchange: run each timed batch's all-to-all to completion "
                          "before the next batch's parse (default: overlap them, two buffer sets)")
@@ -300,6 +308,15 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
     stream = torch.cuda.current_stream(dev)
     rx.sync(stream.cuda_stream)
     classify = rx.classify_call(buf, desc, n, rec, qlist, qcap, tile_cnt, hist, stream=stream)
+    # pipelined batches (--streams S, no exchange): batch k on stream k % S with its own
+    # records / queues / tile counts (the histogram accumulates atomically: shared)
+    pipe = []
+    if mode == "none" and a.streams > 1:
+        for _ in range(a.streams - 1):
+            s2 = torch.cuda.Stream(dev)
+            o2 = (torch.empty_like(rec), torch.empty_like(qlist), torch.empty_like(tile_cnt))
+            pipe.append((s2, rx.classify_call(buf, desc, n, o2[0], o2[1], qcap, o2[2], hist, stream=s2), o2))
+    calls = [classify] + [p[1] for p in pipe]
 
     xch = None
     if mode != "none":
@@ -362,9 +379,45 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
                 if b["pending"] is not None:
                     consume(b)
 
+    kk = [0]
+
+    def pipelined_rate():
+        """N = 1 with the exchange's packing (no collective): consecutive batches alternate
+        between two streams, each with its own records, queues, regions and owner outputs, as
+        the timed steps of B / C / E do; wall clock over `steps` batches."""
+        sets = []
+        for j in range(a.streams):
+            b = dict(st=stream if j == 0 else torch.cuda.Stream(dev), send=torch.empty_like(xch["send"]),
+                     send_count=torch.zeros_like(xch["send_count"]), r=torch.empty_like(rec),
+                     q=torch.empty_like(qlist), t=torch.empty_like(tile_cnt))
+            if mode == "partitioned":
+                b["out"] = torch.empty_like(xch["out"])
+            sets.append(b)
+
+        def one(b):
+            if mode == "replicated":
+                rx.classify_route_dev(buf, desc, n, b["r"], b["q"], qcap, b["t"], hist, 1, 0, xch["cap"],
+                                      b["send"], b["send_count"], stream=b["st"])
+            else:
+                rx.parse_route_dev(buf, desc, n, None, b["q"], qcap, b["t"], hist, 1, 0, xch["cap"],
+                                   b["send"], b["send_count"], stream=b["st"])
+                rx.lookup_dev(b["send"], b["send_count"], 1, xch["cap"], b["out"], stream=b["st"])
+        for k in range(2 * len(sets)):
+            one(sets[k % len(sets)])
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for k in range(steps):
+            one(sets[k % len(sets)])
+        torch.cuda.synchronize()
+        el1 = time.perf_counter() - t1
+        return {"value": round(n * steps / el1 / 1e6, 2), "unit": "Mpkt/s", "ms_per_step": round(el1 / steps * 1e3, 4),
+                "steps": steps, "streams": len(sets),
+                "source": "wall clock; batch k on stream k mod streams with its own buffers"}
+
     def step():
         if xch is None:
-            classify()
+            calls[kk[0] % len(calls)]()
+            kk[0] += 1
             return
         ev = None
         if xch["timing"] and xch["k"] % a.time_stride == 0 and xch["pool"]:
@@ -413,6 +466,19 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
     reg_ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     for e in reg_ev:  # instantiate the events outside the timed region
         e.record(stream)
+    one = None  # pipelined steps: the same launches back to back on one stream, for comparison
+    if region and pipe:
+        torch.cuda.synchronize()
+        reg_ev[0].record(stream)
+        for _ in range(steps):
+            classify()
+        reg_ev[1].record(stream)
+        torch.cuda.synchronize()
+        one = reg_ev[0].elapsed_time(reg_ev[1]) / steps
+        kk[0] = 0
+    # pipelined steps: every other stream starts behind the region's first event and the last
+    # event waits for all of them, so the pair brackets every launch of the timed region
+    pipe_ev = [torch.cuda.Event() for _ in pipe]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -421,12 +487,17 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         xch["k"] = 0
     if region:
         reg_ev[0].record(stream)
+        for s2, _, _ in pipe:
+            s2.wait_event(reg_ev[0])
     t0 = time.perf_counter()
     for _ in range(steps):
         step_overlapped() if overlapped else step()
     if overlapped:
         drain()
     if region:
+        for e, (s2, _, _) in zip(pipe_ev, pipe):
+            e.record(s2)
+            stream.wait_event(e)
         reg_ev[1].record(stream)
     t_submit = time.perf_counter() - t0
     torch.cuda.synchronize()
@@ -442,6 +513,9 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
                                for b in xch["sets"]):
         raise RuntimeError("exchange region overflow in the timed region")
 
+    pipelined = None
+    if xch is not None and world == 1 and a.streams > 1:
+        pipelined = pipelined_rate()
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev if a.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -499,6 +573,7 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             "parallelism": par,
             "tables": mode if mode != "none" else "replicated",
             "table_bytes_per_gpu": ts["table_bytes"],
+            "streams": len(calls) if xch is None else 1,
         },
         "roofline": {
             "bound": "hbm",
@@ -518,12 +593,22 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             "kernel_launches_timed": steps if region else int(len(pk)),
             "kernel_time_source": ("one HIP event pair on the launch stream around the whole timed region "
                                    "(every step is one k_rx launch): elapsed / launches, dispatch gaps "
-                                   "between launches included" if region else
+                                   "between launches included" +
+                                   (f"; batches pipelined over {len(calls)} streams (batch k on stream k mod "
+                                    f"{len(calls)}, its own output buffers): the pair brackets every stream, so "
+                                    "this is the launch interval in steady state, each launch overlapping "
+                                    "its neighbours" if pipe else "") if region else
                                    f"HIP events on the launch stream around every {a.time_stride}-th "
                                    "k_rx launch of the timed region"),
         },
         "host_submit_ms_per_step": round(t_submit / steps * 1e3, 5),
     }
+    if one is not None:
+        out["roofline"]["one_stream"] = {
+            "kernel_ms_mean": round(one, 5), "achieved": round(alg_bytes / (one * 1e-3) / 1e9, 1),
+            "frac": round(alg_bytes / (one * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "source": f"the same {steps} launches back to back on one stream just before the timed region "
+                      "(one HIP event pair, elapsed / launches): each launch alone, as rocprofv3 times it"}
     if xch is not None:
         xm = [e0.elapsed_time(e1) for e0, e1 in xch["ev"]]
         step_ms = float(np.mean(xm)) if xm else float("nan")
@@ -539,6 +624,8 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             "includes": ("k_rx + group scan + pack" + (" + all-to-all" if world > 1 else "") +
                          (" + owner lookups (k_lookup)" if mode == "partitioned" else "")),
         }
+        if pipelined is not None:
+            out["exchange"]["pipelined"] = pipelined
     return out, rx, w
 
 

@@ -440,6 +440,46 @@ def test_classify_route_dev(rxmod, n_parts, my_rank):
             assert sreg[k, : c[k]].tobytes() == want[k].tobytes(), k
 
 
+def test_routes_on_many_streams(rxmod):
+    """Batches classified and routed on six streams at once (more streams than route scratch
+    sets, so sets change hands behind events): every batch's records and send regions equal
+    the oracle's and the host restatement's."""
+    import torch
+    import route_ref
+    from emurx import exchange as X
+    rx, o = new_pair(rxmod)
+    n_parts, my_rank = 4, 2
+    jobs = []
+    for j in range(12):
+        n = 20000 + 3 * j
+        w = synth.config_c(n, rank=40 + j)
+        if j == 0:
+            synth.load_tables(w, rx)
+            synth.load_tables(w, o)
+        cap = X.capacity(n, n_parts)
+        d = _dev_out(n)
+        jobs.append(dict(w=w, n=n, cap=cap, d=d, buf=torch.from_numpy(w["buf"]).cuda(),
+                         desc=torch.from_numpy(w["desc"].view(np.uint8).copy()).cuda(),
+                         send=torch.full((n_parts * cap * X.REC_BYTES,), 0xEE, dtype=torch.uint8, device="cuda"),
+                         cnt=torch.full((n_parts,), -1, dtype=torch.int32, device="cuda")))
+    streams = [torch.cuda.Stream() for _ in range(6)]
+    torch.cuda.synchronize()
+    for j, b in enumerate(jobs):
+        d = b["d"]
+        rx.classify_route_dev(b["buf"], b["desc"], b["n"], d["rec"], d["qlist"], d["qcap"], d["tile_cnt"], d["hist"],
+                              n_parts, my_rank, b["cap"], b["send"], b["cnt"], stream=streams[j % len(streams)])
+    torch.cuda.synchronize()
+    for j, b in enumerate(jobs):
+        orec, _, _, _ = o.rx_batch(b["w"]["buf"], b["w"]["desc"])
+        assert b["d"]["rec"].cpu().numpy()[: b["n"] * 32].view(abi.REC_DTYPE).tobytes() == orec.tobytes(), j
+        want = route_ref.route(orec, n_parts, my_rank)
+        c = b["cnt"].cpu().numpy()
+        assert list(c) == [len(x) for x in want], j
+        sreg = b["send"].cpu().numpy().view(abi.ROUTE_REC_DTYPE).reshape(n_parts, b["cap"])
+        for k in range(n_parts):
+            assert sreg[k, : c[k]].tobytes() == want[k].tobytes(), (j, k)
+
+
 def _hole_rec():
     h = np.zeros(1, abi.REC_DTYPE)
     h["ns_id"] = h["client_id"] = abi.ID_NONE

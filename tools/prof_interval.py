@@ -1,0 +1,45 @@
+"""k_rx launch duration and launch interval from a rocprofv3 kernel trace of one bench run.
+
+    python tools/prof_interval.py <run_kernel_trace.csv> <steps>
+
+bench.py's pipelined steps (--streams 2) enqueue: the warmup launches, then `steps` launches
+back to back on one stream (roofline.one_stream), then the `steps` launches of the timed
+region alternating between the streams.  For the last two groups of `steps` k_rx dispatches
+this prints the mean per-dispatch duration (what `--stats` averages) and the interval
+(last end - first start) / launches, which is what the bench's one event pair around the
+timed region measures when launches overlap.
+"""
+import csv
+import json
+import sys
+
+
+def col(row, *names):
+    for n in names:
+        if n in row:
+            return row[n]
+    raise KeyError(names)
+
+
+def main(path, steps):
+    ks = []
+    for row in csv.DictReader(open(path)):
+        name = col(row, "Kernel_Name", "Kernel-Name", "KernelName")
+        if "k_rx" not in name:
+            continue
+        ks.append((int(col(row, "Start_Timestamp", "Start-Timestamp", "BeginNs")),
+                   int(col(row, "End_Timestamp", "End-Timestamp", "EndNs"))))
+    ks.sort()
+    out = {"k_rx_dispatches": len(ks), "steps": steps}
+    for label, grp in (("timed_region", ks[-steps:]), ("one_stream", ks[-2 * steps:-steps])):
+        if len(grp) < steps:
+            continue
+        dur = sum(e - s for s, e in grp) / len(grp)
+        span = max(e for _, e in grp) - min(s for s, _ in grp)
+        out[label] = {"mean_duration_us": round(dur / 1e3, 3), "interval_us": round(span / len(grp) / 1e3, 3),
+                      "overlap": round(dur * len(grp) / span, 3)}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], int(sys.argv[2]))

@@ -43,7 +43,10 @@ for ph in $phases; do
         step prof_$c 300 rocprofv3 --kernel-trace --stats -d $out/prof_$c -o run --output-format csv \
           -- python bench.py $(args $c) --no-cpu-baseline
         f=$(ls $out/prof_$c/*/run_kernel_stats.csv $out/prof_$c/run_kernel_stats.csv 2>/dev/null | head -n 1)
-        [ -n "$f" ] && cut -d, -f1-4 "$f" | head -n 12 ;;
+        [ -n "$f" ] && cut -d, -f1-4 "$f" | head -n 12
+        t=$(ls $out/prof_$c/*/run_kernel_trace.csv $out/prof_$c/run_kernel_trace.csv 2>/dev/null | head -n 1)
+        [ -n "$t" ] && python tools/prof_interval.py "$t" $(args $c | sed 's/.*--steps \([0-9]*\).*/\1/') \
+          | tee $out/prof_${c}_interval.json ;;
       pmc)
         for k in FETCH_SIZE WRITE_SIZE; do
           step pmc_${c}_$k 180 rocprofv3 --pmc $k -T --kernel-include-regex k_rx -d $out/pmc_${c}/pmc_$k -o run \

@@ -149,8 +149,22 @@ struct emurx_ctx {
     DevBuf<uint8_t> d_txz;
 
     // Namespace-partition packing scratch (emurx_route_dev / emurx_classify_route_dev /
-    // emurx_parse_route_dev; one route at a time per handle, stream-ordered)
-    DevBuf<uint32_t> d_route_cnt, d_route_grp, d_route_goff;  // grp: zero between batches
+    // emurx_parse_route_dev): one set per stream, so routes of batches pipelined over several
+    // streams run side by side; past kRouteSets streams a set changes hands behind an event
+    struct RouteScratch {
+        hipStream_t st = nullptr;
+        bool used = false;
+        hipEvent_t done = nullptr;                      // recorded after each route on st
+        DevBuf<uint32_t> cnt, grp, goff;                // grp: zero between batches
+        void release() {
+            cnt.release(); grp.release(); goff.release();
+            if (done) (void)hipEventDestroy(done);
+            done = nullptr;
+        }
+    };
+    static constexpr size_t kRouteSets = 4;
+    RouteScratch route[kRouteSets];
+    uint32_t route_next = 0;  // the set a new stream takes over when all are in use
 
     // k_rx staging slab per launch (emurx_launch_batch): the narrow 6 KiB slab runs 6
     // workgroups per CU instead of 5, but a wave whose frames span 6-7 KiB then takes the
@@ -365,17 +379,35 @@ bool choose_stage(emurx_t* h) {
     return narrow;
 }
 
-// route scratch for batches of up to max_frames: per-tile counts, per-group sums (kept zero
-// between routes) and group offsets
-int route_scratch(emurx_t* h, uint32_t n) {
+// route scratch of stream st for batches of up to max_frames: per-tile counts, per-group sums
+// (kept zero between routes) and group offsets.  A stream keeps its set; a new stream takes a
+// free one, or the next in turn after waiting (on the device) for its last route.
+int route_scratch(emurx_t* h, uint32_t n, hipStream_t st, emurx_t::RouteScratch** out) {
     const size_t gw = 1024 * 16, tiles = std::max<size_t>(ntiles(std::max(n, h->cfg.max_frames)), 1);
     if (tiles > 1024u * 64u) return EMURX_EINVAL;  // 16M frames per batch
-    if (!h->d_route_grp.p) {
-        if (h->d_route_grp.alloc(gw) || hipMemset(h->d_route_grp.p, 0, gw * sizeof(uint32_t)) != hipSuccess)
-            return EMURX_ENOMEM;
+    emurx_t::RouteScratch* r = nullptr;
+    for (auto& x : h->route)
+        if (x.used && x.st == st) r = &x;
+    if (!r)
+        for (auto& x : h->route)
+            if (!r && !x.used) r = &x;
+    if (!r) {
+        r = &h->route[h->route_next++ % emurx_t::kRouteSets];
+        if (hipStreamWaitEvent(st, r->done, 0) != hipSuccess) return EMURX_EDEVICE;
     }
-    if (h->d_route_cnt.alloc(tiles * 16) || h->d_route_goff.alloc(gw)) return EMURX_ENOMEM;
+    if (!r->done && hipEventCreateWithFlags(&r->done, hipEventDisableTiming) != hipSuccess) return EMURX_EDEVICE;
+    r->st = st;
+    r->used = true;
+    if (!r->grp.p) {
+        if (r->grp.alloc(gw) || hipMemset(r->grp.p, 0, gw * sizeof(uint32_t)) != hipSuccess) return EMURX_ENOMEM;
+    }
+    if (r->cnt.alloc(tiles * 16) || r->goff.alloc(gw)) return EMURX_ENOMEM;
+    *out = r;
     return EMURX_OK;
+}
+// after a route's last launch on st: its scratch set may change hands behind this event
+int route_done(emurx_t::RouteScratch* r, hipStream_t st) {
+    return hipEventRecord(r->done, st) == hipSuccess ? EMURX_OK : EMURX_EDEVICE;
 }
 
 // one k_rx launch; kind: 0 parse only, 1 classify, 2 parse + lookup keys (partitioned source);
@@ -599,7 +631,8 @@ int emurx_open(const emurx_cfg* cfg, emurx_t** out) {
             return EMURX_EDEVICE;
         }
     memset(h->stage_fb.p, 0, 256 * sizeof(uint32_t));
-    if ((rc = ship_tables(h, h->stream)) || (rc = route_scratch(h, cfg->max_frames)) == EMURX_ENOMEM) {
+    emurx_t::RouteScratch* rs = nullptr;
+    if ((rc = ship_tables(h, h->stream)) || (rc = route_scratch(h, cfg->max_frames, h->stream, &rs)) == EMURX_ENOMEM) {
         emurx_close(h);
         return rc ? rc : EMURX_ENOMEM;
     }
@@ -627,7 +660,7 @@ void emurx_close(emurx_t* h) {
     for (auto e : h->reader_ev) (void)hipEventDestroy(e);
     for (auto& t : h->d_tab) t.release();
     h->d_nsinfo.release();
-    h->d_route_cnt.release(); h->d_route_grp.release(); h->d_route_goff.release();
+    for (auto& r : h->route) r.release();
     h->d_txz.release();
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
@@ -880,14 +913,15 @@ int emurx_classify_route_dev(emurx_t* h, const uint8_t* d_frames, const emurx_de
     if (!out->rec || !d_send_count || n_parts == 0 || n_parts > EMURX_MAX_PARTS || my_rank >= n_parts ||
         (n && (!d_send || cap == 0)) || ((uintptr_t)d_send & 7))
         return EMURX_EINVAL;
-    if ((rc = route_scratch(h, n))) return rc;
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
-    const emurx_route_args rt{n_parts, my_rank, cap, h->d_route_cnt.p, h->d_route_grp.p, nullptr, nullptr};
+    emurx_t::RouteScratch* rs = nullptr;
+    if ((rc = route_scratch(h, n, st, &rs))) return rc;
+    const emurx_route_args rt{n_parts, my_rank, cap, rs->cnt.p, rs->grp.p, nullptr, nullptr};
     if (n && (rc = run_dev(h, d_frames, d_desc, n, out, st, 1, &rt))) return rc;
-    return emurx_launch_route(out->rec, n, n_parts, my_rank, cap, d_send, d_send_count, h->d_route_cnt.p,
-                              h->d_route_grp.p, h->d_route_goff.p, st, true)
-               ? EMURX_EDEVICE
-               : EMURX_OK;
+    if (emurx_launch_route(out->rec, n, n_parts, my_rank, cap, d_send, d_send_count, rs->cnt.p, rs->grp.p,
+                           rs->goff.p, st, true))
+        return EMURX_EDEVICE;
+    return route_done(rs, st);
 }
 
 int emurx_parse_route_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_desc, uint32_t n,
@@ -898,14 +932,15 @@ int emurx_parse_route_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc*
     if (!d_send_count || n_parts == 0 || n_parts > EMURX_MAX_PARTS || my_rank >= n_parts ||
         (n && (!d_send || cap == 0)) || ((uintptr_t)d_send & 15))
         return EMURX_EINVAL;
-    if ((rc = route_scratch(h, n))) return rc;
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    emurx_t::RouteScratch* rs = nullptr;
+    if ((rc = route_scratch(h, n, st, &rs))) return rc;
     // owner counts from the L2 headers + group scan, then k_rx packs at those offsets
-    if (emurx_launch_owner_count(d_frames, d_desc, n, n_parts, d_send_count, h->d_route_cnt.p, h->d_route_grp.p,
-                                 h->d_route_goff.p, st))
+    if (emurx_launch_owner_count(d_frames, d_desc, n, n_parts, d_send_count, rs->cnt.p, rs->grp.p, rs->goff.p, st))
         return EMURX_EDEVICE;
-    const emurx_route_args rt{n_parts, my_rank, cap, h->d_route_cnt.p, h->d_route_grp.p, h->d_route_goff.p, d_send};
-    return n ? run_dev(h, d_frames, d_desc, n, out, st, 2, &rt) : EMURX_OK;
+    const emurx_route_args rt{n_parts, my_rank, cap, rs->cnt.p, rs->grp.p, rs->goff.p, d_send};
+    if (n && (rc = run_dev(h, d_frames, d_desc, n, out, st, 2, &rt))) return rc;
+    return route_done(rs, st);
 }
 
 int emurx_lookup_dev(emurx_t* h, const emurx_lookup_rec* d_recv, const uint32_t* d_recv_count, uint32_t n_parts,
@@ -1051,12 +1086,13 @@ int emurx_route_dev(emurx_t* h, const emurx_rec* d_rec, uint32_t n, uint32_t n_p
     if (((uintptr_t)d_rec & 15) || ((uintptr_t)d_send & 7)) return EMURX_EINVAL;
     int rc = bind(h);
     if (rc) return rc;
-    if ((rc = route_scratch(h, n))) return rc;
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
-    return emurx_launch_route(d_rec, n, n_parts, my_rank, cap, d_send, d_send_count, h->d_route_cnt.p,
-                              h->d_route_grp.p, h->d_route_goff.p, st, false)
-               ? EMURX_EDEVICE
-               : EMURX_OK;
+    emurx_t::RouteScratch* rs = nullptr;
+    if ((rc = route_scratch(h, n, st, &rs))) return rc;
+    if (emurx_launch_route(d_rec, n, n_parts, my_rank, cap, d_send, d_send_count, rs->cnt.p, rs->grp.p, rs->goff.p,
+                           st, false))
+        return EMURX_EDEVICE;
+    return route_done(rs, st);
 }
 
 }  // extern "C"

@@ -23,9 +23,16 @@ namespace emurx {
 static_assert(EMURX_QUEUE_TILE == kBlock, "one frame per lane per tile");
 
 
+// cache policy of the frame-byte staging loads (aux bits: 2 = nt); A/B knob
+#ifndef EMURX_NT
+#define EMURX_NT 0
+#endif
 // LDS-DMA (global_load_lds_dwordx4): lane l's 16 source bytes land at dst + 16 * l
 __device__ __forceinline__ void glds16(const uint4* src, uint4* dst_wave_base) {
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst_wave_base, 16, 0, 0);
+}
+__device__ __forceinline__ void glds16_stream(const uint4* src, uint4* dst_wave_base) {
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst_wave_base, 16, 0, EMURX_NT);
 }
 __device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0)
 
@@ -51,8 +58,18 @@ __device__ unsigned long long* g_stamp;
 // kKind: 0 parse only, 1 parse + classify, 2 parse + lookup keys (the partitioned source:
 // every frame's emurx_lookup_rec packed straight into its Namespace owner's send region, at
 // the offsets the owner-count pass (k_owner_count + k_route_scan) fixed; no table reads)
+// Tiles per workgroup: the narrow slab runs EMURX_TPW tiles (EMURX_TPW x 4 waves) in one
+// workgroup, each tile exactly as a one-tile workgroup would (its own waves, counts, queue
+// segment and histogram fold; one shared barrier), so the grid has EMURX_TPW times fewer
+// workgroups to dispatch at the same waves per CU (LDS: 2 x 26 KiB -> 3 workgroups per CU).
+#ifndef EMURX_TPW
+#define EMURX_TPW 1
+#endif
+template <uint32_t kStage>
+constexpr uint32_t tiles_per_wg() { return kStage == kStageNarrow ? EMURX_TPW : 1u; }
+
 template <int kKind, uint32_t kStage>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage == kStageNarrow ? 6 : 5))) void k_rx(const uint8_t* __restrict__ frames,
+__global__ __launch_bounds__(kBlock * tiles_per_wg<kStage>()) __attribute__((amdgpu_waves_per_eu(kStage == kStageNarrow ? 6 : 5))) void k_rx(const uint8_t* __restrict__ frames,
                                                const emurx_desc* __restrict__ desc, uint32_t n,
                                                emurx_dev_tables T, emurx_rec* __restrict__ rec,
                                                uint32_t* __restrict__ qlist, uint32_t qcap,
@@ -62,9 +79,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
                                                uint32_t gen, emurx_route_args rt) {
     constexpr bool kClassify = kKind == 1;
     constexpr uint32_t kWinVec = kStage / 16 / kWave;  // window path: 16-byte vectors per lane
-    __shared__ __attribute__((aligned(16))) uint32_t slab[kWaves * kStage / 4];
-    __shared__ uint32_t s_wcnt[kWaves][16];
-    __shared__ uint32_t s_csum[kWaves][kWave];                      // window path: span sums
+    constexpr uint32_t kTpw = tiles_per_wg<kStage>(), kWgWaves = kWaves * kTpw;
+    static_assert(!(EMURX_SORT && kTpw > 1), "the tile sort assumes one tile per workgroup");
+    __shared__ __attribute__((aligned(16))) uint32_t slab[kWgWaves * kStage / 4];
+    __shared__ uint32_t s_wcnt[kWgWaves][16];
+    __shared__ uint32_t s_csum[kWgWaves][kWave];                    // window path: span sums
     // outcome histogram per wave, {pkts << 23 | bytes}: <= 64 x 65535 B.  It shares the rows
     // of s_csum (a wave's span sums are done before its histogram is zeroed): 1 KiB less keeps
     // the narrow slab at 6 workgroups per CU (LDS 26 KiB)
@@ -75,10 +94,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
 #else
     uint32_t (*s_hist)[EMURX_HIST_BINS] = s_csum;
 #endif
-    __shared__ uint32_t s_rcnt[kWaves][EMURX_MAX_PARTS];            // Namespace owners (rt_cnt)
+    __shared__ uint32_t s_rcnt[kWgWaves][EMURX_MAX_PARTS];          // Namespace owners (rt_cnt)
 
-    const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / kWave;
-    const uint32_t tile = blockIdx.x;
+    // tid: the lane's place in its tile; wv: its wave in the workgroup; wt: in the tile; w0:
+    // the tile's first wave
+    const uint32_t ts = kTpw > 1 ? threadIdx.x / kBlock : 0u, tid = kTpw > 1 ? threadIdx.x % kBlock : threadIdx.x;
+    const uint32_t lane = lane_id(), wv = threadIdx.x / kWave, wt = tid / kWave, w0 = ts * kWaves;
+    const uint32_t tile = blockIdx.x * kTpw + ts;
+    const bool tile_in = kTpw == 1 || tile * EMURX_QUEUE_TILE < n;  // false: a spare tile slot past the batch
 #if EMURX_STAMP
     unsigned long long st_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -86,8 +109,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
     const uint32_t i = tile * EMURX_QUEUE_TILE + tid;
     if (lane < 16) s_wcnt[wv][lane] = 0;
     if (lane < EMURX_MAX_PARTS) s_rcnt[wv][lane] = 0;
-    __shared__ uint32_t s_toff[EMURX_MAX_PARTS];  // kKind 2: this tile's offset in each region
-    if (kKind == 2 && wv == 0) tile_offsets(rt.cnt, rt.goff, rt.parts, tile, lane, s_toff, [](uint32_t v) { return wave_sum_u32(v); });
+    __shared__ uint32_t s_toff_all[kTpw][EMURX_MAX_PARTS];  // kKind 2: the tile's offset in each region
+    uint32_t* s_toff = s_toff_all[ts];
+    if (kKind == 2 && wt == 0 && tile_in)
+        tile_offsets(rt.cnt, rt.goff, rt.parts, tile, lane, s_toff, [](uint32_t v) { return wave_sum_u32(v); });
 
     const uint2 dd = i < n ? *reinterpret_cast<const uint2*>(desc + i) : make_uint2(0, EMURX_DESC_HOLE << 24);
     const bool valid = (dd.y >> 24) != EMURX_DESC_HOLE;  // an empty slot is no frame at all
@@ -106,7 +131,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
     if (fb && (tile & 63) == 0 && lane == 0) {
         const uint32_t bytes = nvec * 16;
         const uint32_t mid = bytes > kStageNarrow && bytes <= kStageWide;
-        fb[((tile >> 6) & 63) * kWaves + wv] = (gen << 2) | ((nvec > 0) << 1) | mid;
+        fb[((tile >> 6) & 63) * kWaves + wt] = (gen << 2) | ((nvec > 0) << 1) | mid;
     }
     if (staged) {  // all copies in flight before the wait; clamped sources stay in bounds
         static_assert(kStage / 16 <= 8 * kWave, "staging issues at most 8 vectors per lane");
@@ -116,7 +141,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
         const uint4* src = reinterpret_cast<const uint4*>(frames + start);
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k)
-            if (k * kWave < nvec) glds16(src + min(lane + k * kWave, nvec - 1), wslab + k * kWave);
+            if (k * kWave < nvec) glds16_stream(src + min(lane + k * kWave, nvec - 1), wslab + k * kWave);
         wait_vm0();
     } else {  // too wide: each lane stages a 128-byte window of its own frame (headers)
         const uintptr_t fa = (uintptr_t)(frames + off);
@@ -124,7 +149,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
         const uint32_t nv = valid ? (uint32_t)(((fa & 15) + len + 15) >> 4) : 0;  // vectors of the frame
 #pragma unroll
         for (uint32_t k = 0; k < kWinVec; ++k)
-            if (k < nv) glds16(src + k, wslab + k * kWave);
+            if (k < nv) glds16_stream(src + k, wslab + k * kWave);
         wait_vm0();
     }
     // each wave reads only its own slab: a wave-level barrier orders it
@@ -141,7 +166,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
     uint32_t pf = tid, poff = off, plen = len, pvport = vport, pbase = wv * kStage + (off - start);
     bool pvalid = valid, sorted = false;
     uint8_t* s_aux = reinterpret_cast<uint8_t*>(&s_csum[0][0]);  // free when every wave is staged
-    if constexpr (EMURX_SORT && kKind != 2) {
+    if constexpr (EMURX_SORT && kKind != 2 && kTpw == 1) {
         if (__syncthreads_and(staged)) {  // tile-uniform; every slab is visible to every wave after it
             uint32_t* s_cls = reinterpret_cast<uint32_t*>(s_aux + 768);  // [wave][class] counts
             uint32_t* s_st = reinterpret_cast<uint32_t*>(s_aux + 896);   // wave starts
@@ -353,14 +378,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
     STAMP(7);
     __syncthreads();
     STAMP(8);
-    if (kKind == 1 && rt.cnt && tid < 16) {
-        const uint32_t c = tid < rt.parts ? s_rcnt[0][tid] + s_rcnt[1][tid] + s_rcnt[2][tid] + s_rcnt[3][tid] : 0u;
+    if (kKind == 1 && rt.cnt && tid < 16 && tile_in) {
+        const uint32_t c = tid < rt.parts ? s_rcnt[w0][tid] + s_rcnt[w0 + 1][tid] + s_rcnt[w0 + 2][tid] + s_rcnt[w0 + 3][tid] : 0u;
         rt.cnt[(size_t)tile * 16 + tid] = c;
         if (c) atomicAdd(&rt.grp[(tile / 64) * 16 + tid], c);
     }
     if (kKind == 2 && rd != 0xffu) {  // the lookup record: ns_id = frame index, client_id = source rank
         uint32_t pos = s_toff[rd] + rrank;
-        for (uint32_t w = 0; w < wv; ++w) pos += s_rcnt[w][rd];
+        for (uint32_t w = w0; w < wv; ++w) pos += s_rcnt[w][rd];
         if (pos < rt.cap) {  // overflow: send_count[d] > cap tells the caller
             const bool ok = r.status == EMURX_ST_OK;
             v4u* o = reinterpret_cast<v4u*>(rt.send + (size_t)rd * rt.cap + pos);
@@ -376,20 +401,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
     // this tile's segment of every queue: frames in (wave, lane) order == frame order
     if (qlist && q < EMURX_NUM_QUEUES && !(EMURX_ABL & 8)) {
         uint32_t pos = rank;
-        for (uint32_t w = 0; w < wv; ++w) pos += s_wcnt[w][q];
+        for (uint32_t w = w0; w < wv; ++w) pos += s_wcnt[w][q];
         const size_t at = (size_t)q * qcap + (size_t)tile * EMURX_QUEUE_TILE + pos;
         if ((size_t)tile * EMURX_QUEUE_TILE + pos < qcap) qlist[at] = i;
     }
-    if (tile_cnt && tid < 16)
+    if (tile_cnt && tid < 16 && tile_in)
         tile_cnt[(size_t)tile * 16 + tid] =
-            s_wcnt[0][tid] + s_wcnt[1][tid] + s_wcnt[2][tid] + s_wcnt[3][tid];
+            s_wcnt[w0][tid] + s_wcnt[w0 + 1][tid] + s_wcnt[w0 + 2][tid] + s_wcnt[w0 + 3][tid];
     // one of EMURX_HIST_SHARDS copies per workgroup: same-address memory-side atomics from
     // every workgroup would serialise; the shards are folded on the host
     if (tid >= 64 && tid < 64 + EMURX_HIST_BINS) {
         const uint32_t b = tid - 64;
         uint32_t pk = 0, by = 0;
 #pragma unroll
-        for (uint32_t w = 0; w < kWaves; ++w) {
+        for (uint32_t w = w0; w < w0 + kWaves; ++w) {
             pk += s_hist[w][b] >> 23;
             by += s_hist[w][b] & ((1u << 23) - 1);
         }
@@ -402,7 +427,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
 #if EMURX_STAMP
     STAMP(9);
     if (g_stamp && lane == 0) {
-        unsigned long long* o = g_stamp + ((size_t)tile * kWaves + wv) * 16;
+        unsigned long long* o = g_stamp + ((size_t)tile * kWaves + wt) * 16;
         for (int k = 0; k < 10; ++k) o[k] = st_[k];
         o[10] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
         o[11] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
@@ -438,7 +463,9 @@ int emurx_launch_batch(const uint8_t* frames, const emurx_desc* desc, uint32_t n
     using namespace emurx;
     if (ev) (void)hipEventRecord(ev[0], st);
     if (n) {
-        const dim3 g((n + EMURX_QUEUE_TILE - 1) / EMURX_QUEUE_TILE), b(kBlock);
+        const uint32_t tpw = narrow ? tiles_per_wg<kStageNarrow>() : tiles_per_wg<kStageWide>();
+        const uint32_t ntiles = (n + EMURX_QUEUE_TILE - 1) / EMURX_QUEUE_TILE;
+        const dim3 g((ntiles + tpw - 1) / tpw), b(kBlock * tpw);
         unsigned long long* hist = reinterpret_cast<unsigned long long*>(out.hist);
         auto k = kind == 1 ? (narrow ? k_rx<1, kStageNarrow> : k_rx<1, kStageWide>)
                : kind == 2 ? (narrow ? k_rx<2, kStageNarrow> : k_rx<2, kStageWide>)
