@@ -551,8 +551,9 @@ int emurx_route_dev(emurx_t* h, const emurx_rec* d_rec, uint32_t n, uint32_t n_p
                     uint32_t cap, emurx_route_rec* d_send, uint32_t* d_send_count, void* stream);
 /* Classify + route in one call: emurx_classify_dev of the batch (out->rec required) with the
    route's per-owner counts taken inside the k_rx launch, then the group scan and the packing
-   of emurx_route_dev into d_send / d_send_count.  Equal to the two calls in sequence.  One
-   route at a time per handle (the route scratch is the handle's). */
+   of emurx_route_dev into d_send / d_send_count.  Equal to the two calls in sequence.  The
+   route scratch is one set per stream (4 sets; a further stream takes a set over behind an
+   event), so routes of batches pipelined over several streams run side by side. */
 int emurx_classify_route_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_desc, uint32_t n,
                              const emurx_dev_out* out, uint32_t n_parts, uint32_t my_rank, uint32_t cap,
                              emurx_route_rec* d_send, uint32_t* d_send_count, void* stream);
