@@ -44,6 +44,13 @@ __device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70);
 #ifndef EMURX_STAMP
 #define EMURX_STAMP 0
 #endif
+// Table lookups of a tile regrouped by key kind (A/B knob, -DEMURX_LSORT=1): after make_key
+// the tile's lookups are counting-sorted by kind (MAC / IPv4 / IPv6 / other) through the free
+// slab, resolved in that order (a wave then runs one or two resolvers instead of every kind
+// its frames need) and the results go back to the frames' lanes before the records.
+#ifndef EMURX_LSORT
+#define EMURX_LSORT 0
+#endif
 #ifndef EMURX_CSTAGE
 #define EMURX_CSTAGE 0  // client buckets staged in the slab by quad-cooperative LDS-DMA
 #endif
@@ -69,18 +76,22 @@ template <uint32_t kStage>
 constexpr uint32_t tiles_per_wg() { return kStage == kStageNarrow ? EMURX_TPW : 1u; }
 
 template <int kKind, uint32_t kStage>
-__global__ __launch_bounds__(kBlock * tiles_per_wg<kStage>()) __attribute__((amdgpu_waves_per_eu(kStage == kStageNarrow ? 6 : 5))) void k_rx(const uint8_t* __restrict__ frames,
-                                               const emurx_desc* __restrict__ desc, uint32_t n,
-                                               emurx_dev_tables T, emurx_rec* __restrict__ rec,
-                                               uint32_t* __restrict__ qlist, uint32_t qcap,
-                                               uint32_t* __restrict__ tile_cnt,
-                                               unsigned long long* __restrict__ hist,
-                                               uint32_t* __restrict__ flow, uint32_t* __restrict__ fb,
-                                               uint32_t gen, emurx_route_args rt) {
+__device__ __forceinline__ void rx_tile(const uint8_t* __restrict__ frames,
+                                        const emurx_desc* __restrict__ desc, uint32_t n,
+                                        const emurx_dev_tables& T, emurx_rec* __restrict__ rec,
+                                        uint32_t* __restrict__ qlist, uint32_t qcap,
+                                        uint32_t* __restrict__ tile_cnt,
+                                        unsigned long long* __restrict__ hist,
+                                        uint32_t* __restrict__ flow, uint32_t* __restrict__ fb,
+                                        uint32_t gen, const emurx_route_args& rt, uint32_t tile_base) {
     constexpr bool kClassify = kKind == 1;
     constexpr uint32_t kWinVec = kStage / 16 / kWave;  // window path: 16-byte vectors per lane
     constexpr uint32_t kTpw = tiles_per_wg<kStage>(), kWgWaves = kWaves * kTpw;
     static_assert(!(EMURX_SORT && kTpw > 1), "the tile sort assumes one tile per workgroup");
+    static_assert(!(EMURX_LSORT && kTpw > 1), "the lookup sort assumes one tile per workgroup");
+    static_assert(!(EMURX_LSORT && (EMURX_SORT || EMURX_CSTAGE || EMURX_STAMP)), "one regrouping at a time");
+    static_assert(kWaves * kStage >= EMURX_QUEUE_TILE * 64, "lookup sort payload + results fit the slab");
+    __shared__ uint32_t s_lcls[kWaves][4];  // EMURX_LSORT: lookups per (wave, kind)
     __shared__ __attribute__((aligned(16))) uint32_t slab[kWgWaves * kStage / 4];
     __shared__ uint32_t s_wcnt[kWgWaves][16];
     __shared__ uint32_t s_csum[kWgWaves][kWave];                    // window path: span sums
@@ -100,7 +111,7 @@ __global__ __launch_bounds__(kBlock * tiles_per_wg<kStage>()) __attribute__((amd
     // the tile's first wave
     const uint32_t ts = kTpw > 1 ? threadIdx.x / kBlock : 0u, tid = kTpw > 1 ? threadIdx.x % kBlock : threadIdx.x;
     const uint32_t lane = lane_id(), wv = threadIdx.x / kWave, wt = tid / kWave, w0 = ts * kWaves;
-    const uint32_t tile = blockIdx.x * kTpw + ts;
+    const uint32_t tile = tile_base * kTpw + ts;
     const bool tile_in = kTpw == 1 || tile * EMURX_QUEUE_TILE < n;  // false: a spare tile slot past the batch
 #if EMURX_STAMP
     unsigned long long st_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -209,6 +220,9 @@ __global__ __launch_bounds__(kBlock * tiles_per_wg<kStage>()) __attribute__((amd
     Rec r;
     r.dlen = 0;
     uint32_t kwd[12];  // kKind 2: the lookup key words of the frame
+    LKey lk{};         // EMURX_LSORT: the frame's lookup, resolved after the parse of the tile
+    bool lgo = false;
+    const bool lsort = EMURX_LSORT && kClassify && !T.ft_on && !(EMURX_ABL & 2);  // uniform
     if (staged && kClassify && EMURX_CSTAGE && !T.ft_on && !(EMURX_ABL & 2)) {  // wave-uniform branch
         // The client buckets of the wave staged in its slab.  Once the lookup keys are made the
         // frame bytes are not read again (no TransportCtx: no flow tuple), so the slab takes
@@ -270,7 +284,12 @@ __global__ __launch_bounds__(kBlock * tiles_per_wg<kStage>()) __attribute__((amd
             if (go) resolve(T, r, k, [&](uint32_t cid) { return flow_probe(T, get_tuple(s, len, r), cid); });
             STAMP(5);
 #else
-            if (kClassify && !(EMURX_ABL & 2)) classify(s, len, T, r);
+            if (lsort) {
+                lgo = r.status == EMURX_ST_OK;
+                if (lgo) lk = make_key(s, len, r);
+            } else if (kClassify && !(EMURX_ABL & 2)) {
+                classify(s, len, T, r);
+            }
 #endif
             if (kKind == 2 && r.status == EMURX_ST_OK) pack_key(s, len, r, make_key(s, len, r), kwd);
         }
@@ -291,9 +310,72 @@ __global__ __launch_bounds__(kBlock * tiles_per_wg<kStage>()) __attribute__((amd
         if (go) resolve(T, r, k, [&](uint32_t cid) { return flow_probe(T, get_tuple(s, len, r), cid); });
         STAMP(5);
 #else
-        if (valid && kClassify && !(EMURX_ABL & 2)) classify(s, len, T, r);
+        if (lsort) {
+            lgo = valid && r.status == EMURX_ST_OK;
+            if (lgo) lk = make_key(s, len, r);
+        } else if (valid && kClassify && !(EMURX_ABL & 2)) {
+            classify(s, len, T, r);
+        }
 #endif
         if (kKind == 2 && valid && r.status == EMURX_ST_OK) pack_key(s, len, r, make_key(s, len, r), kwd);
+    }
+    if constexpr (EMURX_LSORT && kClassify) {
+        if (lsort) {  // tile-uniform: every wave of the tile takes part
+            const uint32_t key = lk.key;
+            const uint32_t cls = !lgo ? 4u : key == kMac ? 0u : key == kIp4 ? 1u : (key == kIp6 || key == kEui) ? 2u : 3u;
+            uint64_t mine = 0;
+#pragma unroll
+            for (uint32_t c = 0; c < 4; ++c) {
+                const uint64_t b = __ballot(cls == c);
+                if (cls == c) mine = b;
+                if (lane == c) s_lcls[wt][c] = (uint32_t)__popcll(b);
+            }
+            __syncthreads();  // counts visible; every wave is done with its slab
+            uint32_t tot[4], kinds = 0, ngo = 0, pos = 0;
+#pragma unroll
+            for (uint32_t c = 0; c < 4; ++c) {
+                tot[c] = s_lcls[0][c] + s_lcls[1][c] + s_lcls[2][c] + s_lcls[3][c];
+                kinds += tot[c] ? 1u : 0u;
+                pos += c < cls ? tot[c] : 0u;
+                ngo += tot[c];
+            }
+            if (kinds > 1) {  // tile-uniform
+                for (uint32_t w = 0; w < wt; ++w) pos += s_lcls[w][cls < 4 ? cls : 0];
+                pos += mbcnt(mine);
+                uint4* P = reinterpret_cast<uint4*>(slab);          // 3 x 16 B per lookup
+                uint4* R = P + 3 * EMURX_QUEUE_TILE;                 // 16 B per frame: the results
+                if (lgo) {
+                    P[3 * pos] = make_uint4(key | (r.proto << 8) | (lk.mc6 << 16), lk.kw[0], lk.kw[1], lk.kw[2]);
+                    P[3 * pos + 1] = make_uint4(lk.kw[3], lk.dlo, lk.dhi, r.vport);
+                    P[3 * pos + 2] = make_uint4(r.vlan0, r.vlan1, tid, 0);
+                }
+                __syncthreads();
+                if (tid < ngo) {
+                    const uint4 a = P[3 * tid], b = P[3 * tid + 1], c = P[3 * tid + 2];
+                    LKey q;
+                    q.key = a.x & 0xff;
+                    q.mc6 = (a.x >> 16) & 1;
+                    q.kw[0] = a.y; q.kw[1] = a.z; q.kw[2] = a.w; q.kw[3] = b.x;
+                    q.dlo = b.y; q.dhi = b.z;
+                    Rec rr;
+                    rr.proto = (a.x >> 8) & 0xff;
+                    rr.vport = b.w; rr.vlan0 = c.x; rr.vlan1 = c.y;
+                    rr.ns = EMURX_ID_NONE; rr.cl = EMURX_ID_NONE; rr.flags = 0; rr.flow = EMURX_FLOW_NONE;
+                    resolve(T, rr, q, [](uint32_t) { return EMURX_FLOW_NO_CTX; });  // ft_on == 0: never called
+                    R[c.z] = make_uint4(rr.ns, rr.cl, rr.flags & EMURX_FLAG_LK_MASK, rr.flow);
+                }
+                __syncthreads();
+                if (lgo) {
+                    const uint4 x = R[tid];
+                    r.ns = x.x;
+                    r.cl = x.y;
+                    r.flags = (r.flags & ~EMURX_FLAG_LK_MASK) | x.z;
+                    r.flow = x.w;  // EMURX_FLOW_NO_CTX for a transport frame's client (ft_on == 0)
+                }
+            } else if (lgo) {
+                resolve(T, r, lk, [](uint32_t) { return EMURX_FLOW_NO_CTX; });
+            }
+        }
     }
     typedef unsigned v4u __attribute__((ext_vector_type(4)));
     if (rec && pi < n && !(EMURX_ABL & 16)) {
@@ -436,6 +518,30 @@ __global__ __launch_bounds__(kBlock * tiles_per_wg<kStage>()) __attribute__((amd
 #endif
 }
 
+// k_rx's arguments as one struct (a single kernarg block; 91 SGPRs and 76 VGPRs against 106
+// and 79 for the same arguments passed one by one)
+struct RxArgs {
+    const uint8_t* frames;
+    const emurx_desc* desc;
+    uint32_t n;
+    emurx_dev_tables T;
+    emurx_rec* rec;
+    uint32_t* qlist;
+    uint32_t qcap;
+    uint32_t* tile_cnt;
+    unsigned long long* hist;
+    uint32_t* flow;
+    uint32_t* fb;
+    uint32_t gen;
+    emurx_route_args rt;
+};
+
+template <int kKind, uint32_t kStage>
+__global__ __launch_bounds__(kBlock * tiles_per_wg<kStage>()) __attribute__((amdgpu_waves_per_eu(kStage == kStageNarrow ? 6 : 5))) void k_rx(const RxArgs a) {
+    rx_tile<kKind, kStage>(a.frames, a.desc, a.n, a.T, a.rec, a.qlist, a.qcap, a.tile_cnt, a.hist, a.flow, a.fb, a.gen, a.rt,
+                           blockIdx.x);
+}
+
 
 // table deltas (emurx_api.cpp ship_tables): 4 lanes per 64-byte block, 16 bytes each
 __global__ __launch_bounds__(kBlock) void k_apply(const emurx_delta* __restrict__ d, uint32_t n) {
@@ -471,8 +577,9 @@ int emurx_launch_batch(const uint8_t* frames, const emurx_desc* desc, uint32_t n
                : kind == 2 ? (narrow ? k_rx<2, kStageNarrow> : k_rx<2, kStageWide>)
                            : (narrow ? k_rx<0, kStageNarrow> : k_rx<0, kStageWide>);
         const emurx_route_args none{};
-        hipLaunchKernelGGL(k, g, b, 0, st, frames, desc, n, T, out.rec, out.qlist, out.qcap, out.tile_cnt, hist,
-                           out.flow, fb, gen, rt ? *rt : none);
+        const RxArgs args{frames, desc, n, T, out.rec, out.qlist, out.qcap, out.tile_cnt, hist, out.flow, fb, gen,
+                          rt ? *rt : none};
+        hipLaunchKernelGGL(k, g, b, 0, st, args);
     }
     if (ev) (void)hipEventRecord(ev[1], st);
     return hipGetLastError() == hipSuccess ? 0 : -1;
