@@ -194,6 +194,37 @@ def test_big_frames_global_path(rxmod):
     check_batch(rx, o, buf, desc)
 
 
+def test_long_spans_across_the_window(rxmod):
+    """Window-path waves (frames too wide for the stage) whose L4 spans start inside the
+    lane's header window and end past it: TCP / UDP / ICMPv4 / ICMPv6 over IPv4 and IPv6,
+    valid and corrupted checksums, all-zero ICMPv4 spans (Go's all-zero case), spans ending
+    just past the window edge and frames at every 4-byte alignment within a 16-byte vector."""
+    from emurx import frames as Fr
+    rng = np.random.default_rng(17)
+    frames = []
+    for size in (130, 200, 600, 1500):
+        body = rng.integers(0, 256, size, dtype=np.uint8).tobytes()
+        frames.append(E.tcp4(body))
+        frames.append(E.udp4(5000, 5001, body))
+        frames.append(E.udp6(5000, 5001, body))
+        frames.append(E.icmp6(128, body=body))
+        frames.append(E.v4(1, Fr.icmp4(8, 0, 7, 9, body)))
+        frames.append(E.v4(1, bytes(8 + size)))  # all-zero ICMPv4 span: errIcmpv4Cse
+        for good in (E.tcp4(body), E.udp6(5000, 5001, body), E.icmp6(128, body=body)):
+            bad = bytearray(good)
+            bad[-1 - (size % 7)] ^= 0x40  # a payload byte past the window
+            frames.append(bytes(bad))
+            bad = bytearray(good)
+            bad[70] ^= 0x01  # a byte inside the window
+            frames.append(bytes(bad))
+    frames.append(E.udp4(1, 2, bytes(9000)))  # keeps the waves on the window path
+    rx, o = new_pair(rxmod)
+    for rot in range(4):  # frame starts at 4, 8, 12, 0 mod 16 (4-byte ZMQ gap per frame)
+        fr = frames[rot:] + frames[:rot]
+        buf, desc = F.pack_frames(fr)
+        check_batch(rx, o, buf, desc)
+
+
 def test_empty_and_single(rxmod):
     rx, o = new_pair(rxmod)
     rec, qlist, qoff, hist = run_dev(rx, np.zeros(64, np.uint8), np.zeros(0, abi.DESC_DTYPE))

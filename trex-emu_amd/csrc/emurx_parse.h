@@ -325,14 +325,27 @@ template <class S>
 __device__ __forceinline__ bool csum_l4(const S& s, Rec& r, uint32_t at, uint32_t n, uint32_t pcs, uint32_t fail_st) {
     return csum(s, at, n, pcs);
 }
+// EMURX_WSKIP: the span's bytes inside the window are summed from LDS here and folded into
+// the deferred pseudo sum (the byte-pair sum is linear mod 0xffff, and be_domain with the
+// span's own start parity orients both parts alike), so the cooperative pass reads only the
+// bytes past the window; dfail carries that parity in bit 16.
+#ifndef EMURX_WSKIP
+#define EMURX_WSKIP 0
+#endif
 template <>
 __device__ __forceinline__ bool csum_l4<WinSrc>(const WinSrc& s, Rec& r, uint32_t at, uint32_t n, uint32_t pcs,
                                                 uint32_t fail_st) {
     if (at + n <= s.wlim || n == 0) return csum(s, at, n, pcs);
-    r.dstart = at;
-    r.dlen = n;
-    r.dpcs = pcs;
-    r.dfail = fail_st;
+    uint32_t st = at, pw = pcs;
+    if (EMURX_WSKIP && at < s.wlim) {
+        const uint32_t tw = dword_sum(WinDw{s.b32 + (s.wbase >> 2)}, s.head + at, s.wlim - at);
+        pw = pcs + be_domain(tw, s.at(at));  // tw == 0 leaves pcs as it was (Go's all-zero case)
+        st = s.wlim;
+    }
+    r.dstart = st;
+    r.dlen = at + n - st;
+    r.dpcs = pw;
+    r.dfail = fail_st | ((s.at(at) & 1u) << 16);
     return true;
 }
 
@@ -704,7 +717,7 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 }
 __device__ __forceinline__ void settle_deferred(Rec& r, bool ok) {
     if (ok) return;
-    const uint32_t st = r.dfail;
+    const uint32_t st = r.dfail & 0xffffu;
     if (st == EMURX_ST_ICMPV4_CS || st == EMURX_ST_UDP_CS) r.l7 = 0;  // Go sets L7 after the check
     fail(r, st);
 }
@@ -768,7 +781,7 @@ __device__ __forceinline__ void coop_checksum(Rec& r, const uint8_t* f, uint32_t
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (mine) {
-        settle_deferred(r, csum_ok(wsum[lane], (uint32_t)a, r.dpcs));
+        settle_deferred(r, csum_ok(wsum[lane], r.dfail >> 16, r.dpcs));  // parity of the span's start
         r.dlen = 0;
     }
 }
@@ -845,7 +858,7 @@ __device__ __forceinline__ void coop_checksum_rows(Rec& r, const uint8_t* f, uin
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (mine) {
-        settle_deferred(r, csum_ok(wsum[lane], (uint32_t)a, r.dpcs));
+        settle_deferred(r, csum_ok(wsum[lane], r.dfail >> 16, r.dpcs));  // parity of the span's start
         r.dlen = 0;
     }
 }
