@@ -625,7 +625,11 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
                          (" + owner lookups (k_lookup)" if mode == "partitioned" else "")),
         }
         if pipelined is not None:
+            # N = 1: the line's value is the pipelined rate, as for the one-launch steps of
+            # B / C / E; the back-to-back steps above stay beside it
             out["exchange"]["pipelined"] = pipelined
+            out["exchange"]["one_stream_steps"] = {"value": out["value"], "ms_per_step": out["ms_per_step"]}
+            out["value"], out["ms_per_step"] = pipelined["value"], pipelined["ms_per_step"]
     return out, rx, w
 
 
@@ -701,7 +705,7 @@ def table_update_cost(a, rx, w, torch, rounds=8):
 
 def copy_ceiling(torch, dev, stream, mib=1024, reps=8):
     """HBM ceiling as this GPU runs it: a 1 GiB streaming copy (emurx_copy_ceiling_dev: 16-byte
-    non-temporal loads and stores, 8 in flight per lane), read + write bytes over the
+    non-temporal loads and stores, 4 in flight per lane over 16,384 workgroups), read + write bytes over the
     HIP-event time of `reps` copies."""
     try:
         from emurx import abi

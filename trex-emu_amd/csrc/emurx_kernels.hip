@@ -586,20 +586,24 @@ int emurx_launch_batch(const uint8_t* frames, const emurx_desc* desc, uint32_t n
 }
 
 namespace emurx {
-// streaming copy for the measured HBM ceiling (emurx_copy_ceiling_dev): 8 independent 16-byte
-// loads per lane in flight, non-temporal both ways, grid-stride over 2,048 workgroups
+// streaming copy for the measured HBM ceiling (emurx_copy_ceiling_dev): 4 independent 16-byte
+// loads per lane in flight, non-temporal both ways, grid-stride over 16,384 workgroups (the
+// fastest of the variants tools/copy_probe.hip times: 6.13 TB/s read + write on a 1 GiB copy,
+// against 5.74 for 8 in flight over 2,048 workgroups)
+constexpr int kCopyInFlight = 4;
+constexpr int kCopyGrid = 16384;
 __global__ __launch_bounds__(kBlock) void k_copy(uint4* __restrict__ dst, const uint4* __restrict__ src, size_t nv) {
     typedef unsigned v4 __attribute__((ext_vector_type(4)));
-    const size_t stride = (size_t)gridDim.x * kBlock * 8;
-    for (size_t base = (size_t)blockIdx.x * kBlock * 8 + threadIdx.x; base < nv; base += stride) {
-        v4 x[8];
+    const size_t stride = (size_t)gridDim.x * kBlock * kCopyInFlight;
+    for (size_t base = (size_t)blockIdx.x * kBlock * kCopyInFlight + threadIdx.x; base < nv; base += stride) {
+        v4 x[kCopyInFlight];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        for (int k = 0; k < kCopyInFlight; ++k) {
             const size_t i = base + (size_t)k * kBlock;
             x[k] = i < nv ? __builtin_nontemporal_load(reinterpret_cast<const v4*>(src) + i) : v4{0, 0, 0, 0};
         }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        for (int k = 0; k < kCopyInFlight; ++k) {
             const size_t i = base + (size_t)k * kBlock;
             if (i < nv) __builtin_nontemporal_store(x[k], reinterpret_cast<v4*>(dst) + i);
         }
@@ -617,7 +621,7 @@ extern "C" int emurx_debug_set_stamps(void* dev_buf) {
 extern "C" int emurx_copy_ceiling_dev(void* d_dst, const void* d_src, size_t bytes, void* stream) {
     if (!d_dst || !d_src || (bytes & 15) || ((uintptr_t)d_dst & 15) || ((uintptr_t)d_src & 15)) return EMURX_EINVAL;
     if (bytes)
-        hipLaunchKernelGGL(emurx::k_copy, dim3(2048), dim3(emurx::kBlock), 0, (hipStream_t)stream,
+        hipLaunchKernelGGL(emurx::k_copy, dim3(emurx::kCopyGrid), dim3(emurx::kBlock), 0, (hipStream_t)stream,
                            reinterpret_cast<uint4*>(d_dst), reinterpret_cast<const uint4*>(d_src), bytes / 16);
     return hipGetLastError() == hipSuccess ? EMURX_OK : EMURX_EDEVICE;
 }
