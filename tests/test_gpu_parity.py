@@ -511,6 +511,50 @@ def test_routes_on_many_streams(rxmod):
             assert sreg[k, : c[k]].tobytes() == want[k].tobytes(), (j, k)
 
 
+def test_max_batch(rxmod):
+    """The largest batch one call takes: 16,777,216 descriptors (65,536 tiles: config D's whole
+    batch on one GPU, and the route scan's limit of 1,024 groups of 64 tiles), 1M config-C
+    frames each referenced 16 times.  Records, queues and counters against the oracle over the
+    same descriptors; then classify + route to 8 owners against the host restatement."""
+    import torch
+    import route_ref
+    from emurx import exchange as X
+    n1, rep = 1 << 20, 16
+    w = synth.config_c(n1, rank=3)
+    desc = np.tile(w["desc"], rep)
+    n = len(desc)
+    rx, o = new_pair(rxmod, max_frames=n)
+    synth.load_tables(w, rx)
+    synth.load_tables(w, o)
+    rec = check_batch(rx, o, w["buf"], desc)
+    n_parts, my_rank = 8, 5
+    own = np.tile(route_ref.owners(rec[:n1], n_parts), rep)
+    want = np.bincount(own[own != 0xFF], minlength=n_parts)
+    tb, td = torch.from_numpy(w["buf"]).cuda(), torch.from_numpy(desc.view(np.uint8).copy()).cuda()
+    d = _dev_out(n)
+    cap = X.capacity(n, n_parts)
+    for attempt in range(2):  # the fair share + 6 % overflows here: true counts, then grow and redo
+        send = torch.empty(n_parts * cap * X.REC_BYTES, dtype=torch.uint8, device="cuda")
+        cnt = torch.full((n_parts,), -1, dtype=torch.int32, device="cuda")
+        rx.classify_route_dev(tb, td, n, d["rec"], d["qlist"], d["qcap"], d["tile_cnt"], d["hist"], n_parts, my_rank,
+                              cap, send, cnt)
+        torch.cuda.synchronize()
+        c = cnt.cpu().numpy()
+        assert list(c) == list(want)
+        if (c <= cap).all():
+            break
+        cap = X.grow(cap, c)
+    assert (c <= cap).all()
+    sreg = send.cpu().numpy().view(abi.ROUTE_REC_DTYPE).reshape(n_parts, cap)
+    for k in range(n_parts):
+        idx = np.nonzero(own == k)[0]
+        assert c[k] == len(idx), k
+        got = sreg[k, : c[k]]
+        assert np.array_equal(got["src_index"], idx.astype(got["src_index"].dtype)), k
+        assert got["rec"].tobytes() == rec[idx].tobytes(), k
+        assert (got["src_rank"] == my_rank).all()
+
+
 def _hole_rec():
     h = np.zeros(1, abi.REC_DTYPE)
     h["ns_id"] = h["client_id"] = abi.ID_NONE
