@@ -445,8 +445,8 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         xch["cap"] = grow_cap(xch, world, dist, torch, dev)
         alloc_regions()
         hist.zero_()
-    # sanity of the outcome on this rank (counts only; parity lives in tests/)
-    if not a.no_check:
+    def sanity():
+        """The outcome on this rank (counts only; parity lives in tests/), after some steps."""
         from emurx.rx import hist_fold, pack_queues
         h = hist_fold(hist.cpu().numpy().view(np.uint64))
         assert int(h[0::2].sum()) % n == 0, "histogram does not cover the batches"
@@ -454,6 +454,8 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         assert int(qoff[-1]) == n, "queues do not cover the batch"
         if xch is not None:
             xcheck(xch, rec, n, world, rank, dist, torch, dev, mode)
+    if not a.no_check and warmup > 0:
+        sanity()
 
     region = xch is None and a.kernel_timing == "region"
     if xch is not None or a.kernel_timing == "launch":
@@ -504,6 +506,8 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    if not a.no_check and warmup == 0 and steps > 0:  # no warmup: check the timed steps' outputs
+        sanity()
     if region:
         pk = [reg_ev[0].elapsed_time(reg_ev[1]) / steps]
     else:
