@@ -305,6 +305,11 @@ __device__ __forceinline__ uint32_t le32(const LdsSrc& s, uint32_t i) {
 }
 __device__ __forceinline__ uint32_t be32(const LdsSrc& s, uint32_t i) { return __builtin_bswap32(le32(s, i)); }
 #endif
+// the big-endian 16-bit value of the two low bytes of a little-endian word
+__device__ __forceinline__ uint32_t bs16(uint32_t w) { return ((w & 0xffu) << 8) | ((w >> 8) & 0xffu); }
+#ifndef EMURX_LDF
+#define EMURX_LDF 0  // A/B knob: parse_flat's header fields from shared dwords (le32) too
+#endif
 
 // ---------------------------------------------------------------------------------------
 // parse state == ParserPacketState + CTunnelData + outcome
@@ -602,7 +607,12 @@ __device__ __forceinline__ void parse_l4_flat(const LdsSrc& s, uint32_t len, Rec
     // before it for UDP, L7 only on success for ICMP and UDP)
     r.l7len = tcp_hdr ? ((l4len - tcplen) & 0xffff) : (p17 && len >= L4_8) ? ((l4len - 8) & 0xffff) : 0u;
     r.l7 = tcp_hdr ? ((L4 + tcplen) & 0xffff) : ((p1 || p17) && st == EMURX_ST_OK) ? L4_8 : 0u;
+#if EMURX_LDF
+    const uint32_t p0 = le32(s, L4);  // sport, dport as on the wire
+    const uint32_t src = bs16(p0), dst = bs16(p0 >> 16), t6 = p0 & 0xffu;
+#else
     const uint32_t src = be16(s, L4), dst = be16(s, L4 + 2), t6 = s.u8(L4);
+#endif
     uint32_t cb = p1 ? EMURX_CB_ICMP : p2 ? EMURX_CB_IGMP : p6 ? EMURX_CB_TCP : p58 ? EMURX_CB_ICMPV6 : EMURX_CB_UDP;
     if (p17) {
         cb = dst == 5353 ? EMURX_CB_MDNS
@@ -628,7 +638,12 @@ __device__ __forceinline__ void parse_flat(const LdsSrc& s, uint32_t len, uint32
     auto is_ppp = [](uint32_t x) { return x == 0x8863 || x == 0x8864; };
     uint32_t st = EMURX_ST_OK;
     first(st, len < 14, EMURX_ST_PACKET_TOO_SHORT);
+#if EMURX_LDF
+    const uint32_t w12 = le32(s, 12), w16 = le32(s, 16);  // also the VLAN words below
+    const uint32_t e0 = bs16(w12), e1 = bs16(w16), e2 = bs16(le32(s, 20));
+#else
     const uint32_t e0 = be16(s, 12), e1 = be16(s, 16), e2 = be16(s, 20);
+#endif
     const bool t0 = st == EMURX_ST_OK && is_tag(e0);
     first(st, t0 && len < 18, EMURX_ST_DOT1Q_TOO_SHORT);
     const bool g0 = t0 && st == EMURX_ST_OK;  // tag 0 parsed
@@ -651,7 +666,12 @@ __device__ __forceinline__ void parse_flat(const LdsSrc& s, uint32_t len, uint32
     bool v6 = false;
     if (et == 0x0800) {  // IPv4
         r.l3 = offset;
+#if EMURX_LDF
+        const uint32_t h0 = le32(s, offset), h4 = le32(s, offset + 4);
+        const uint32_t b0 = h0 & 0xffu, frag = bs16(h4 >> 16), totlen = bs16(h0 >> 16);
+#else
         const uint32_t b0 = s.u8(offset), frag = be16(s, offset + 6), totlen = be16(s, offset + 2);
+#endif
         const uint32_t hdr = (b0 & 0xf) << 2;
         first(st, len < offset + 20, EMURX_ST_IPV4_TOO_SHORT);
         first(st, (b0 >> 4) != 4, EMURX_ST_IPV4_HDR_TOO_SHORT);
