@@ -2,28 +2,36 @@
 """Benchmark: Mpkt/s of device-resident rx parse+classify (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config B|C|D|E] [--frames F]
-                    [--exchange] [--backend nccl|gloo]
+                    [--exchange] [--backend nccl|gloo] [--batches R] [--streams S]
 
 A step = one batch through the hot path: emurx_classify_dev = one k_rx launch (decode +
 checksums + Namespace/Client lookups + 32-B records + stable per-callback queue segments +
 outcome histogram) over F frames already resident in HBM.  Default workload = config B
 (1M x 64 B untagged IPv4/UDP, 1 Namespace / 1 Client), the configuration the metric is
-quoted on.  Consecutive batches alternate between two streams (--streams, default 2), each
-with its own output buffers, as the ingest path's two slots do: a batch's launch runs beside
-the previous one instead of waiting for its last workgroups.  For N > 1 (torchrun, one rank
-per GPU) every rank processes its own F-frame
-shard against replicated tables: frames are independent, so there is no data-path
-collective (weak scaling); value = frames over all ranks / max-over-ranks time.
+quoted on.  The steps rotate through R distinct device-resident batches (--batches, default
+8: seeded permutations of the workload's frames at distinct addresses, each slot with its own
+outputs), so every byte's reuse distance is above the 256 MiB Infinity Cache and the input
+comes from HBM, as fresh ZMQ batches do (veth_zmq.go:277-320).  Consecutive batches alternate
+between two streams (--streams, default 2; slot j on stream j mod S, so the streams never share
+an input), as the ingest path's two slots do: a batch's launch runs beside the previous one
+instead of waiting for its last workgroups.  Warmup runs --warmup steps and then keeps going
+until --warmup-seconds of wall time have passed (settled clocks for short runs).  For N > 1
+(torchrun, one rank per GPU) every rank processes its own F-frame shard against replicated
+tables: frames are independent, so there is no data-path collective (weak scaling); value =
+frames over all ranks / max-over-ranks time; the Namespace-owner exchange (config D) is timed
+beside it with the same steps and warmup (`namespace_exchange`).
 
 --exchange (default for config D: 2M frames per GPU, 32K Namespaces / 1M Clients) adds the
-Namespace-partitioned exchange to every step: emurx_route_dev packs the records whose
-Namespace was found into the owners' regions and an equal-split all-to-all (RCCL over
-xGMI) delivers them, with the per-region counts in a second all-to-all.
+Namespace-partitioned exchange to every step: emurx_parse_route_dev packs every frame's
+lookup record into its Namespace owner's region, an all-to-all (RCCL over xGMI) delivers the
+regions, with the per-region counts in a second all-to-all, and the owner resolves them.
 
 The JSON line carries `roofline` (algorithmic bytes per frame = frame_len + 8 B descriptor
-+ 32 B record + 4 B queue entry, over k_rx's launch interval from one HIP event pair around
-the timed region; `roofline.one_stream` has the same launches back to back on one stream) and
-`cpu_baseline` (the oracle, a single-threaded C restatement of the Go path, timed on this
++ 32 B record + 4 B queue entry, over k_rx's duration with each launch alone: the same --steps
+launches back to back on one stream over the rotating slots, one HIP event pair around them;
+`roofline.pipelined` is the timed region's launch interval on the S streams, and
+`roofline.cache_resident_replay` the round-2 replay of one batch per stream, labelled as such)
+and `cpu_baseline` (the oracle, a single-threaded C restatement of the Go path, timed on this
 host's cores over a bounded sample of the same workload; rank 0 at N=1 only).
 """
 import argparse
@@ -72,6 +80,13 @@ def parse_args():
                     help="steps without an exchange: consecutive batches go round-robin to this many "
                          "streams, each with its own output buffers, so a batch's k_rx runs beside the "
                          "previous one (as the ingest path's two slots do); 1 = back to back on one stream")
+    ap.add_argument("--batches", type=int, default=8,
+                    help="distinct device-resident batches the steps rotate through (batch k uses batch slot "
+                         "k mod this, each slot its own frames, descriptors and outputs; the default 8 keeps "
+                         "every byte's reuse distance above the 256 MiB Infinity Cache: the frames come from "
+                         "HBM, as fresh batches do in production); 1 = the round-2 replay of one batch")
+    ap.add_argument("--warmup-seconds", type=float, default=0.3,
+                    help="keep launching warmup steps until this much wall time has passed (clocks settle)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="N > 1 with an exchange: run each timed batch's all-to-all to completion "
                          "before the next batch's parse (default: overlap them, two buffer sets)")
@@ -237,8 +252,8 @@ def main():
         # shards with the partitioned lookups in every step; the headline value stays config B's
         try:
             rx.close()
-            xo, rx, _ = measure(a, "D", 1 << 21, "partitioned", max(10, a.steps // 4), max(2, a.warmup // 4),
-                                rank, world, local, dist, torch)
+            # the headline's steps and warmup: a first-class measurement, not a side sample
+            xo, rx, _ = measure(a, "D", 1 << 21, "partitioned", a.steps, a.warmup, rank, world, local, dist, torch)
             out["namespace_exchange"] = {k: xo[k] for k in ("value", "unit", "ms_per_step", "steps", "config",
                                                               "exchange")}
             out["namespace_exchange"]["k_rx_ms_mean"] = xo["roofline"]["kernel_ms_mean"]
@@ -278,12 +293,38 @@ def launch_check(a, rank, world, dist, torch):
     return 0
 
 
+def permuted_batch(torch, buf_dev, desc_np, seed, dev):
+    """Another device-resident batch of the same workload: the frames (each with its 4-byte ZMQ
+    header) in a seeded permutation, laid out contiguously at new addresses, and its
+    descriptors.  Same tables, same mix of shapes, distinct bytes at every address; gathered on
+    the device (one index per byte)."""
+    import numpy as np
+    n = len(desc_np)
+    perm = np.random.default_rng(seed).permutation(n)
+    d = desc_np[perm].copy()
+    seg = d["len"].astype(np.int64) + 4
+    start = np.zeros(n, np.int64)
+    if n > 1:
+        start[1:] = np.cumsum(seg[:-1])
+    total = int(seg.sum())
+    shift = torch.from_numpy(desc_np["off"][perm].astype(np.int64) - 4 - start).to(dev)
+    idx = torch.arange(total, device=dev, dtype=torch.int64)
+    idx += torch.repeat_interleave(shift, torch.from_numpy(seg).to(dev), output_size=total)
+    out = torch.zeros(total + 64, dtype=torch.uint8, device=dev)
+    out[:total] = buf_dev[idx]
+    del idx, shift
+    d["off"] = (start + 4).astype(d["off"].dtype)
+    return out, torch.from_numpy(d.view(np.uint8).copy()).to(dev)
+
+
 def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
     """Run `steps` timed batches of workload `cfg` (n frames per rank) -> (JSON dict, rx, w).
     mode: "none" (classify, no collective), "replicated" (every GPU holds every table:
     classify + route the found records to their Namespace owners + all-to-all), or
     "partitioned" (each GPU holds its Namespace partition: parse + lookup keys, all-to-all of
-    the lookup records to the owners, lookups at the owner)."""
+    the lookup records to the owners, lookups at the owner).  Step k reads batch slot k mod
+    --batches (distinct frames and descriptors each, permuted_batch), so the input comes from
+    HBM and not from the Infinity Cache a replayed batch would stay in."""
     import numpy as np
     from emurx import abi
     from emurx.rx import RxPath
@@ -298,25 +339,34 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
     synth.load_tables(w, rx)
 
     dev = torch.device("cuda", local)
+    S = max(1, a.streams) if mode == "none" else 1
+    R = max(1, a.batches, S)
+    R -= R % S  # every stream reads its own batch slots (slot j on stream j mod S)
     buf = torch.from_numpy(w["buf"]).to(dev)
     desc = torch.from_numpy(w["desc"].view(np.uint8).copy()).to(dev)
-    rec = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    inputs = [(buf, desc)] + [permuted_batch(torch, buf, w["desc"], (int(w["seed"]) << 8) + j + 1000 * rank, dev)
+                              for j in range(1, R)]
     qcap = abi.queue_cap(n)
-    qlist = torch.empty(abi.NUM_QUEUES * qcap, dtype=torch.int32, device=dev)
-    tile_cnt = torch.empty(abi.ntiles(n) * 16, dtype=torch.int32, device=dev)
+
+    def outputs():
+        return (torch.empty(n * 32, dtype=torch.uint8, device=dev),
+                torch.empty(abi.NUM_QUEUES * qcap, dtype=torch.int32, device=dev),
+                torch.empty(abi.ntiles(n) * 16, dtype=torch.int32, device=dev))
+    rec, qlist, tile_cnt = outputs()
     hist = torch.zeros(abi.HIST_SHARDS * 2 * abi.HIST_BINS, dtype=torch.int64, device=dev)  # accumulates
     stream = torch.cuda.current_stream(dev)
+    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
     rx.sync(stream.cuda_stream)
-    classify = rx.classify_call(buf, desc, n, rec, qlist, qcap, tile_cnt, hist, stream=stream)
-    # pipelined batches (--streams S, no exchange): batch k on stream k % S with its own
-    # records / queues / tile counts (the histogram accumulates atomically: shared)
-    pipe = []
-    if mode == "none" and a.streams > 1:
-        for _ in range(a.streams - 1):
-            s2 = torch.cuda.Stream(dev)
-            o2 = (torch.empty_like(rec), torch.empty_like(qlist), torch.empty_like(tile_cnt))
-            pipe.append((s2, rx.classify_call(buf, desc, n, o2[0], o2[1], qcap, o2[2], hist, stream=s2), o2))
-    calls = [classify] + [p[1] for p in pipe]
+    calls = one_calls = None
+    if mode == "none":
+        # batch slot j: its own frames, descriptors, records, queues and tile counts (the
+        # histogram accumulates atomically: shared); launched on stream j mod S in the timed
+        # steps, and all on one stream for the one-launch-at-a-time figure
+        outs = [(rec, qlist, tile_cnt)] + [outputs() for _ in range(R - 1)]
+        calls = [rx.classify_call(inputs[j][0], inputs[j][1], n, *outs[j][:2], qcap, outs[j][2], hist,
+                                  stream=streams[j % S]) for j in range(R)]
+        one_calls = [rx.classify_call(inputs[j][0], inputs[j][1], n, *outs[j][:2], qcap, outs[j][2], hist,
+                                      stream=stream) for j in range(R)]
 
     xch = None
     if mode != "none":
@@ -339,14 +389,15 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
                        out=xch["sets"][0].get("out"))
         alloc_regions()
 
-        def produce(b):
+        def produce(b, k):
+            fb, fd = inputs[k % R]
             if mode == "replicated":
                 # classify + route in one call: the route's owner counts are taken inside k_rx
-                rx.classify_route_dev(buf, desc, n, rec, qlist, qcap, tile_cnt, hist, world, rank, xch["cap"],
+                rx.classify_route_dev(fb, fd, n, rec, qlist, qcap, tile_cnt, hist, world, rank, xch["cap"],
                                       b["send"], b["send_count"], stream=stream)
             else:
                 # no source records: every frame's lookup record carries its parse to the owner
-                rx.parse_route_dev(buf, desc, n, None, qlist, qcap, tile_cnt, hist, world, rank, xch["cap"],
+                rx.parse_route_dev(fb, fd, n, None, qlist, qcap, tile_cnt, hist, world, rank, xch["cap"],
                                    b["send"], b["send_count"], stream=stream)
 
         def consume(b):
@@ -366,7 +417,7 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             if xch["timing"] and k % a.time_stride == 0 and xch["pool"]:
                 ev = xch["pool"].pop()
                 ev[0].record(stream)
-            produce(b)
+            produce(b, k)
             b["pending"] = X.exchange_start(b["send"], b["send_count"], xch["cap"], rec_bytes=rb)
             if prev["pending"] is not None:
                 consume(prev)
@@ -386,7 +437,7 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         between two streams, each with its own records, queues, regions and owner outputs, as
         the timed steps of B / C / E do; wall clock over `steps` batches."""
         sets = []
-        for j in range(a.streams):
+        for j in range(max(2, a.streams)):
             b = dict(st=stream if j == 0 else torch.cuda.Stream(dev), send=torch.empty_like(xch["send"]),
                      send_count=torch.zeros_like(xch["send_count"]), r=torch.empty_like(rec),
                      q=torch.empty_like(qlist), t=torch.empty_like(tile_cnt))
@@ -394,37 +445,39 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
                 b["out"] = torch.empty_like(xch["out"])
             sets.append(b)
 
-        def one(b):
+        def one(b, k):
+            fb, fd = inputs[k % R]
             if mode == "replicated":
-                rx.classify_route_dev(buf, desc, n, b["r"], b["q"], qcap, b["t"], hist, 1, 0, xch["cap"],
+                rx.classify_route_dev(fb, fd, n, b["r"], b["q"], qcap, b["t"], hist, 1, 0, xch["cap"],
                                       b["send"], b["send_count"], stream=b["st"])
             else:
-                rx.parse_route_dev(buf, desc, n, None, b["q"], qcap, b["t"], hist, 1, 0, xch["cap"],
+                rx.parse_route_dev(fb, fd, n, None, b["q"], qcap, b["t"], hist, 1, 0, xch["cap"],
                                    b["send"], b["send_count"], stream=b["st"])
                 rx.lookup_dev(b["send"], b["send_count"], 1, xch["cap"], b["out"], stream=b["st"])
         for k in range(2 * len(sets)):
-            one(sets[k % len(sets)])
+            one(sets[k % len(sets)], k)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         for k in range(steps):
-            one(sets[k % len(sets)])
+            one(sets[k % len(sets)], k)
         torch.cuda.synchronize()
         el1 = time.perf_counter() - t1
         return {"value": round(n * steps / el1 / 1e6, 2), "unit": "Mpkt/s", "ms_per_step": round(el1 / steps * 1e3, 4),
-                "steps": steps, "streams": len(sets),
+                "steps": steps, "streams": len(sets), "batches": R,
                 "source": "wall clock; batch k on stream k mod streams with its own buffers"}
 
     def step():
         if xch is None:
-            calls[kk[0] % len(calls)]()
+            calls[kk[0] % R]()
             kk[0] += 1
             return
         ev = None
         if xch["timing"] and xch["k"] % a.time_stride == 0 and xch["pool"]:
             ev = xch["pool"].pop()  # created before the timed region: creating one costs ~50 us
             ev[0].record(stream)
+        k = xch["k"]
         xch["k"] += 1
-        produce(xch["sets"][0])
+        produce(xch["sets"][0], k)
         if world > 1:
             xch["recv"], xch["recv_count"] = X.exchange(xch["send"], xch["send_count"], xch["cap"], rec_bytes=rb)
         else:
@@ -434,6 +487,22 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         if ev is not None:
             ev[1].record(stream)
             xch["ev"].append(ev)
+
+    def warm_for_time():
+        """Warmup floor in wall time (--warmup-seconds): a short --warmup would otherwise time
+        the first launches at unsettled clocks.  Every rank runs the same number of rounds."""
+        t_w = time.perf_counter()
+        more = warmup > 0
+        while more:
+            for _ in range(max(R, 16)):
+                step()
+            torch.cuda.synchronize()
+            go = torch.tensor([int(time.perf_counter() - t_w < a.warmup_seconds)], dtype=torch.int64)
+            if world > 1:
+                go = go.to(dev) if dist.get_backend() == "nccl" else go
+                dist.all_reduce(go, op=dist.ReduceOp.MAX)
+            more = bool(go.cpu().item())
+        return time.perf_counter() - t_w
 
     for attempt in range(4):
         for _ in range(warmup):
@@ -445,6 +514,8 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         xch["cap"] = grow_cap(xch, world, dist, torch, dev)
         alloc_regions()
         hist.zero_()
+    warm_s = warm_for_time()
+
     def sanity():
         """The outcome on this rank (counts only; parity lives in tests/), after some steps."""
         from emurx.rx import hist_fold, pack_queues
@@ -468,19 +539,38 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
     reg_ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     for e in reg_ev:  # instantiate the events outside the timed region
         e.record(stream)
-    one = None  # pipelined steps: the same launches back to back on one stream, for comparison
-    if region and pipe:
+    pipe_ev = [torch.cuda.Event() for _ in streams[1:]]
+
+    def region_open():
+        reg_ev[0].record(stream)
+        for s2 in streams[1:]:  # every other stream starts behind the region's first event
+            s2.wait_event(reg_ev[0])
+
+    def region_close():
+        for e, s2 in zip(pipe_ev, streams[1:]):  # and the last event waits for all of them
+            e.record(s2)
+            stream.wait_event(e)
+        reg_ev[1].record(stream)
+
+    one = replay = None
+    if region:
+        # each launch alone: the same rotation of batch slots, back to back on one stream
         torch.cuda.synchronize()
         reg_ev[0].record(stream)
-        for _ in range(steps):
-            classify()
+        for k in range(steps):
+            one_calls[k % R]()
         reg_ev[1].record(stream)
         torch.cuda.synchronize()
         one = reg_ev[0].elapsed_time(reg_ev[1]) / steps
+        if R > S:
+            # the round-2 replay: each stream re-reads one batch, which stays in the Infinity Cache
+            region_open()
+            for k in range(steps):
+                calls[k % S]()
+            region_close()
+            torch.cuda.synchronize()
+            replay = reg_ev[0].elapsed_time(reg_ev[1]) / steps
         kk[0] = 0
-    # pipelined steps: every other stream starts behind the region's first event and the last
-    # event waits for all of them, so the pair brackets every launch of the timed region
-    pipe_ev = [torch.cuda.Event() for _ in pipe]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -488,19 +578,14 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
     if overlapped:
         xch["k"] = 0
     if region:
-        reg_ev[0].record(stream)
-        for s2, _, _ in pipe:
-            s2.wait_event(reg_ev[0])
+        region_open()
     t0 = time.perf_counter()
     for _ in range(steps):
         step_overlapped() if overlapped else step()
     if overlapped:
         drain()
     if region:
-        for e, (s2, _, _) in zip(pipe_ev, pipe):
-            e.record(s2)
-            stream.wait_event(e)
-        reg_ev[1].record(stream)
+        region_close()
     t_submit = time.perf_counter() - t0
     torch.cuda.synchronize()
     if world > 1:
@@ -508,8 +593,10 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
     el = time.perf_counter() - t0
     if not a.no_check and warmup == 0 and steps > 0:  # no warmup: check the timed steps' outputs
         sanity()
+    interval = None
     if region:
-        pk = [reg_ev[0].elapsed_time(reg_ev[1]) / steps]
+        interval = reg_ev[0].elapsed_time(reg_ev[1]) / steps
+        pk = [one]
     else:
         pk = rx.kernel_times()
         rx.set_timing(0)
@@ -528,9 +615,10 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
     value = total_frames / el / 1e6
     ms_per_step = el / steps * 1e3
 
-    # roofline of the dominant kernel (k_rx): algorithmic bytes / its mean HIP-event duration.
-    # Per frame: the frame, its 8-B descriptor, the 4-B queue entry and the 32-B record (the
-    # 80-B lookup record instead in the partitioned mode's k_rx)
+    # roofline of the dominant kernel (k_rx): algorithmic bytes / its mean launch duration.
+    # Per frame: the frame, its 8-B descriptor and the 32-B record (104 B for a
+    # 64-B frame), plus the 4-B queue entry k_rx also writes (the 80-B lookup record instead of
+    # the record in the partitioned mode's k_rx)
     per_frame = 8 + 4 + (80 if mode == "partitioned" else 32)
     alg_bytes = w["nbytes"] + per_frame * n
     parse_s = float(np.mean(pk)) * 1e-3 if len(pk) else float("nan")
@@ -554,6 +642,7 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
                          f"owners (all-to-all, {a.backend})",
            "partitioned": f"frame shards x{world}, Namespace-partitioned tables, lookup records to the "
                           f"Namespace owners (all-to-all, {a.backend}), lookups at the owner"}[mode]
+    in_bytes = w["nbytes"] + 4 * n + 64 + 8 * n  # a batch slot's frames (ZMQ layout) + descriptors
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -566,7 +655,8 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (seeded, valid wire-format frames)",
+        "data": f"synthetic (seeded, valid wire-format frames); {R} distinct device-resident batches per GPU "
+                f"(seeded permutations of the workload's frames at distinct addresses), step k reads batch k mod {R}",
         "config": {
             "workload": {"B": "B: 1M x 64B untagged IPv4/UDP, 1 ns / 1 client",
                          "D": "D: 2M mixed dot1q/QinQ IPv4/IPv6 per GPU (16M over 8), 32K ns / 1M clients",
@@ -577,7 +667,10 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             "parallelism": par,
             "tables": mode if mode != "none" else "replicated",
             "table_bytes_per_gpu": ts["table_bytes"],
-            "streams": len(calls) if xch is None else 1,
+            "streams": S,
+            "batches": R,
+            "input_bytes_per_batch": in_bytes,
+            "input_reuse_distance_bytes": R * in_bytes,  # > 256 MiB: not served by the Infinity Cache
         },
         "roofline": {
             "bound": "hbm",
@@ -592,27 +685,33 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             "kernel": "k_rx" + (" (parse + lookup keys)" if mode == "partitioned" else ""),
             "alg_bytes_per_launch": alg_bytes,
             "alg_bytes_per_frame": round(alg_bytes / n, 2),
+            "alg_bytes_note": "frame + 8-B descriptor + 32-B record (SURVEY.md §8d) + the 4-B queue entry k_rx also "
+                              "writes" + ("; the 80-B lookup record instead of the record" if mode == "partitioned" else ""),
             "table_probe_bytes_per_launch": probed * 128 if mode != "partitioned" else 0,
             "kernel_ms_mean": round(parse_s * 1e3, 5),
             "kernel_launches_timed": steps if region else int(len(pk)),
-            "kernel_time_source": ("one HIP event pair on the launch stream around the whole timed region "
-                                   "(every step is one k_rx launch): elapsed / launches, dispatch gaps "
-                                   "between launches included" +
-                                   (f"; batches pipelined over {len(calls)} streams (batch k on stream k mod "
-                                    f"{len(calls)}, its own output buffers): the pair brackets every stream, so "
-                                    "this is the launch interval in steady state, each launch overlapping "
-                                    "its neighbours" if pipe else "") if region else
+            "kernel_time_source": ("one HIP event pair on the launch stream around the same --steps launches back "
+                                   f"to back on one stream, rotating over the {R} batch slots, just before the timed "
+                                   "region: elapsed / launches = each launch alone (what rocprofv3's kernel "
+                                   "trace times, plus the ~1 us dispatch gap between launches)" if region else
                                    f"HIP events on the launch stream around every {a.time_stride}-th "
                                    "k_rx launch of the timed region"),
         },
+        "warmup_seconds": round(warm_s, 3),
         "host_submit_ms_per_step": round(t_submit / steps * 1e3, 5),
     }
-    if one is not None:
-        out["roofline"]["one_stream"] = {
-            "kernel_ms_mean": round(one, 5), "achieved": round(alg_bytes / (one * 1e-3) / 1e9, 1),
-            "frac": round(alg_bytes / (one * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "source": f"the same {steps} launches back to back on one stream just before the timed region "
-                      "(one HIP event pair, elapsed / launches): each launch alone, as rocprofv3 times it"}
+    if interval is not None:
+        out["roofline"]["pipelined"] = {
+            "interval_ms": round(interval, 5), "achieved": round(alg_bytes / (interval * 1e-3) / 1e9, 1),
+            "frac": round(alg_bytes / (interval * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "streams": S,
+            "source": f"the timed region: one HIP event pair bracketing all {S} streams, elapsed / launches = the "
+                      "launch interval in steady state (each launch overlaps its neighbours)"}
+    if replay is not None:
+        out["roofline"]["cache_resident_replay"] = {
+            "interval_ms": round(replay, 5), "value": round(n / (replay * 1e-3) / 1e6, 2),
+            "frac": round(alg_bytes / (replay * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "source": f"the round-2 measurement: {S} streams each replaying one batch slot (its input stays in the "
+                      "256 MiB Infinity Cache); same event pair, not the metric"}
     if xch is not None:
         xm = [e0.elapsed_time(e1) for e0, e1 in xch["ev"]]
         step_ms = float(np.mean(xm)) if xm else float("nan")

@@ -21,16 +21,19 @@ run() {  # name seconds cmd...
 for what in "${@:-all}"; do
   case $what in
   tests|all)
-    run pytest_gpu 1200 python -m pytest tests -m gpu -x -q -p no:cacheprovider; stop_on_fault $? ;;&
+    run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread; stop_on_fault $? ;;&
   smoke|all)
     run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"; stop_on_fault $? ;;&
   bench|all)
-    run bench_B 600 python bench.py --steps 200 --warmup 20; stop_on_fault $?
+    run bench_B 600 python -u bench.py --steps 200 --warmup 20; stop_on_fault $?
+    run bench_B_driver 600 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline; stop_on_fault $?
     run bench_C 600 python bench.py --config C --steps 100 --warmup 10 --no-cpu-baseline; stop_on_fault $?
     run bench_E 600 python bench.py --config E --steps 50 --warmup 5 --no-cpu-baseline; stop_on_fault $? ;;&
   prof|all)
     run prof_B 600 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof_B -o run --output-format csv \
-        -- python bench.py --steps 50 --warmup 5 --no-cpu-baseline; stop_on_fault $? ;;&
+        -- python bench.py --steps 50 --warmup 5 --no-cpu-baseline; stop_on_fault $?
+    t=$(ls gpurun_out/prof_B/*/run_kernel_trace.csv gpurun_out/prof_B/run_kernel_trace.csv 2>/dev/null | head -n 1)
+    [ -n "$t" ] && python tools/prof_interval.py "$t" 50 | tee gpurun_out/prof_B_interval.json ;;&
   exchange)
     run bench_D1 900 python bench.py --config D --steps 50 --warmup 5 --no-cpu-baseline; stop_on_fault $?
     run bench_D2_gloo 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \

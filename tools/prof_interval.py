@@ -2,12 +2,15 @@
 
     python tools/prof_interval.py <run_kernel_trace.csv> <steps>
 
-bench.py's pipelined steps (--streams 2) enqueue: the warmup launches, then `steps` launches
-back to back on one stream (roofline.one_stream), then the `steps` launches of the timed
-region alternating between the streams.  For the last two groups of `steps` k_rx dispatches
-this prints the mean per-dispatch duration (what `--stats` averages) and the interval
-(last end - first start) / launches, which is what the bench's one event pair around the
-timed region measures when launches overlap.
+bench.py's pipelined steps (--streams 2, --batches 8) enqueue: the warmup launches, then
+`steps` launches back to back on one stream over the rotating batch slots (each launch alone:
+roofline.kernel_ms_mean / frac), then `steps` launches replaying one batch per stream
+(roofline.cache_resident_replay), then the `steps` launches of the timed region alternating
+between the streams over the rotating slots (roofline.pipelined).  For those three groups of
+`steps` k_rx dispatches this prints the mean per-dispatch duration (what `--stats` averages)
+and the interval (last end - first start) / launches, which is what the bench's one event pair
+around a group measures.  With --batches <= --streams there is no replay group: pass
+`--no-replay` as the third argument.
 """
 import csv
 import json
@@ -21,7 +24,7 @@ def col(row, *names):
     raise KeyError(names)
 
 
-def main(path, steps):
+def main(path, steps, replay=True):
     ks = []
     for row in csv.DictReader(open(path)):
         name = col(row, "Kernel_Name", "Kernel-Name", "KernelName")
@@ -31,7 +34,12 @@ def main(path, steps):
                    int(col(row, "End_Timestamp", "End-Timestamp", "EndNs"))))
     ks.sort()
     out = {"k_rx_dispatches": len(ks), "steps": steps}
-    for label, grp in (("timed_region", ks[-steps:]), ("one_stream", ks[-2 * steps:-steps])):
+    groups = [("timed_region", ks[-steps:])]
+    if replay:
+        groups += [("cache_resident_replay", ks[-2 * steps:-steps]), ("one_stream", ks[-3 * steps:-2 * steps])]
+    else:
+        groups += [("one_stream", ks[-2 * steps:-steps])]
+    for label, grp in groups:
         if len(grp) < steps:
             continue
         dur = sum(e - s for s, e in grp) / len(grp)
@@ -42,4 +50,4 @@ def main(path, steps):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]))
+    main(sys.argv[1], int(sys.argv[2]), replay=not (len(sys.argv) > 3 and sys.argv[3] == "--no-replay"))

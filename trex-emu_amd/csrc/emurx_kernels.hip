@@ -23,36 +23,19 @@ namespace emurx {
 static_assert(EMURX_QUEUE_TILE == kBlock, "one frame per lane per tile");
 
 
-// cache policy of the frame-byte staging loads (aux bits: 2 = nt); A/B knob
-#ifndef EMURX_NT
-#define EMURX_NT 0
-#endif
 // LDS-DMA (global_load_lds_dwordx4): lane l's 16 source bytes land at dst + 16 * l
 __device__ __forceinline__ void glds16(const uint4* src, uint4* dst_wave_base) {
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst_wave_base, 16, 0, 0);
 }
-__device__ __forceinline__ void glds16_stream(const uint4* src, uint4* dst_wave_base) {
-    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst_wave_base, 16, 0, EMURX_NT);
-}
 __device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0)
 
-// Timeline stamps (experiment-only build variant, -DEMURX_STAMP=1; tools/stamps.py): per wave
-// the shader clock at entry, after the descriptors, after the staging, after the parse, after
-// the lookup key, after the table lookups, at the histogram, before and after the tile
-// barrier and at exit, then HW_ID, XCC_ID and the tile: 16 u64 per wave, written by lane 0
-// with vector stores.
+// Timeline stamps (measurement-only build, -DEMURX_STAMP=1; tools/stamps.py): per wave the
+// shader clock at entry, after the descriptors, after the staging, after the parse, after the
+// lookup key, after the table lookups, at the histogram, before and after the tile barrier and
+// at exit, then HW_ID, XCC_ID and the tile: 16 u64 per wave, written by lane 0 with vector
+// stores.
 #ifndef EMURX_STAMP
 #define EMURX_STAMP 0
-#endif
-// Table lookups of a tile regrouped by key kind (A/B knob, -DEMURX_LSORT=1): after make_key
-// the tile's lookups are counting-sorted by kind (MAC / IPv4 / IPv6 / other) through the free
-// slab, resolved in that order (a wave then runs one or two resolvers instead of every kind
-// its frames need) and the results go back to the frames' lanes before the records.
-#ifndef EMURX_LSORT
-#define EMURX_LSORT 0
-#endif
-#ifndef EMURX_CSTAGE
-#define EMURX_CSTAGE 0  // client buckets staged in the slab by quad-cooperative LDS-DMA
 #endif
 #if EMURX_STAMP
 __device__ unsigned long long* g_stamp;
@@ -65,16 +48,6 @@ __device__ unsigned long long* g_stamp;
 // kKind: 0 parse only, 1 parse + classify, 2 parse + lookup keys (the partitioned source:
 // every frame's emurx_lookup_rec packed straight into its Namespace owner's send region, at
 // the offsets the owner-count pass (k_owner_count + k_route_scan) fixed; no table reads)
-// Tiles per workgroup: the narrow slab runs EMURX_TPW tiles (EMURX_TPW x 4 waves) in one
-// workgroup, each tile exactly as a one-tile workgroup would (its own waves, counts, queue
-// segment and histogram fold; one shared barrier), so the grid has EMURX_TPW times fewer
-// workgroups to dispatch at the same waves per CU (LDS: 2 x 26 KiB -> 3 workgroups per CU).
-#ifndef EMURX_TPW
-#define EMURX_TPW 1
-#endif
-template <uint32_t kStage>
-constexpr uint32_t tiles_per_wg() { return kStage == kStageNarrow ? EMURX_TPW : 1u; }
-
 template <int kKind, uint32_t kStage>
 __device__ __forceinline__ void rx_tile(const uint8_t* __restrict__ frames,
                                         const emurx_desc* __restrict__ desc, uint32_t n,
@@ -83,36 +56,21 @@ __device__ __forceinline__ void rx_tile(const uint8_t* __restrict__ frames,
                                         uint32_t* __restrict__ tile_cnt,
                                         unsigned long long* __restrict__ hist,
                                         uint32_t* __restrict__ flow, uint32_t* __restrict__ fb,
-                                        uint32_t gen, const emurx_route_args& rt, uint32_t tile_base) {
+                                        uint32_t gen, const emurx_route_args& rt, uint32_t tile) {
     constexpr bool kClassify = kKind == 1;
     constexpr uint32_t kWinVec = kStage / 16 / kWave;  // window path: 16-byte vectors per lane
-    constexpr uint32_t kTpw = tiles_per_wg<kStage>(), kWgWaves = kWaves * kTpw;
-    static_assert(!(EMURX_SORT && kTpw > 1), "the tile sort assumes one tile per workgroup");
-    static_assert(!(EMURX_LSORT && kTpw > 1), "the lookup sort assumes one tile per workgroup");
-    static_assert(!(EMURX_LSORT && (EMURX_SORT || EMURX_CSTAGE || EMURX_STAMP)), "one regrouping at a time");
-    static_assert(kWaves * kStage >= EMURX_QUEUE_TILE * 64, "lookup sort payload + results fit the slab");
-    __shared__ uint32_t s_lcls[kWaves][4];  // EMURX_LSORT: lookups per (wave, kind)
-    __shared__ __attribute__((aligned(16))) uint32_t slab[kWgWaves * kStage / 4];
-    __shared__ uint32_t s_wcnt[kWgWaves][16];
-    __shared__ uint32_t s_csum[kWgWaves][kWave];                    // window path: span sums
+    __shared__ __attribute__((aligned(16))) uint32_t slab[kWaves * kStage / 4];
+    __shared__ uint32_t s_wcnt[kWaves][16];
+    __shared__ uint32_t s_csum[kWaves][kWave];                    // window path: span sums
     // outcome histogram per wave, {pkts << 23 | bytes}: <= 64 x 65535 B.  It shares the rows
     // of s_csum (a wave's span sums are done before its histogram is zeroed): 1 KiB less keeps
     // the narrow slab at 6 workgroups per CU (LDS 26 KiB)
     static_assert(EMURX_HIST_BINS == kWave, "one histogram bin per lane");
-#if EMURX_SORT
-    __shared__ uint32_t s_hist_own[kWaves][EMURX_HIST_BINS];  // the sort's s_aux lives in s_csum
-    uint32_t (*s_hist)[EMURX_HIST_BINS] = s_hist_own;
-#else
     uint32_t (*s_hist)[EMURX_HIST_BINS] = s_csum;
-#endif
-    __shared__ uint32_t s_rcnt[kWgWaves][EMURX_MAX_PARTS];          // Namespace owners (rt_cnt)
+    __shared__ uint32_t s_rcnt[kWaves][EMURX_MAX_PARTS];          // Namespace owners (rt_cnt)
+    __shared__ uint32_t s_toff[EMURX_MAX_PARTS];                   // kKind 2: the tile's offset in each region
 
-    // tid: the lane's place in its tile; wv: its wave in the workgroup; wt: in the tile; w0:
-    // the tile's first wave
-    const uint32_t ts = kTpw > 1 ? threadIdx.x / kBlock : 0u, tid = kTpw > 1 ? threadIdx.x % kBlock : threadIdx.x;
-    const uint32_t lane = lane_id(), wv = threadIdx.x / kWave, wt = tid / kWave, w0 = ts * kWaves;
-    const uint32_t tile = tile_base * kTpw + ts;
-    const bool tile_in = kTpw == 1 || tile * EMURX_QUEUE_TILE < n;  // false: a spare tile slot past the batch
+    const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / kWave;
 #if EMURX_STAMP
     unsigned long long st_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -120,9 +78,7 @@ __device__ __forceinline__ void rx_tile(const uint8_t* __restrict__ frames,
     const uint32_t i = tile * EMURX_QUEUE_TILE + tid;
     if (lane < 16) s_wcnt[wv][lane] = 0;
     if (lane < EMURX_MAX_PARTS) s_rcnt[wv][lane] = 0;
-    __shared__ uint32_t s_toff_all[kTpw][EMURX_MAX_PARTS];  // kKind 2: the tile's offset in each region
-    uint32_t* s_toff = s_toff_all[ts];
-    if (kKind == 2 && wt == 0 && tile_in)
+    if (kKind == 2 && wv == 0)
         tile_offsets(rt.cnt, rt.goff, rt.parts, tile, lane, s_toff, [](uint32_t v) { return wave_sum_u32(v); });
 
     const uint2 dd = i < n ? *reinterpret_cast<const uint2*>(desc + i) : make_uint2(0, EMURX_DESC_HOLE << 24);
@@ -142,7 +98,7 @@ __device__ __forceinline__ void rx_tile(const uint8_t* __restrict__ frames,
     if (fb && (tile & 63) == 0 && lane == 0) {
         const uint32_t bytes = nvec * 16;
         const uint32_t mid = bytes > kStageNarrow && bytes <= kStageWide;
-        fb[((tile >> 6) & 63) * kWaves + wt] = (gen << 2) | ((nvec > 0) << 1) | mid;
+        fb[((tile >> 6) & 63) * kWaves + wv] = (gen << 2) | ((nvec > 0) << 1) | mid;
     }
     if (staged) {  // all copies in flight before the wait; clamped sources stay in bounds
         static_assert(kStage / 16 <= 8 * kWave, "staging issues at most 8 vectors per lane");
@@ -152,15 +108,15 @@ __device__ __forceinline__ void rx_tile(const uint8_t* __restrict__ frames,
         const uint4* src = reinterpret_cast<const uint4*>(frames + start);
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k)
-            if (k * kWave < nvec) glds16_stream(src + min(lane + k * kWave, nvec - 1), wslab + k * kWave);
+            if (k * kWave < nvec) glds16(src + min(lane + k * kWave, nvec - 1), wslab + k * kWave);
         wait_vm0();
-    } else {  // too wide: each lane stages a 128-byte window of its own frame (headers)
+    } else {  // too wide: each lane stages a window of its own frame (headers)
         const uintptr_t fa = (uintptr_t)(frames + off);
         const uint4* src = reinterpret_cast<const uint4*>(fa & ~(uintptr_t)15);
         const uint32_t nv = valid ? (uint32_t)(((fa & 15) + len + 15) >> 4) : 0;  // vectors of the frame
 #pragma unroll
         for (uint32_t k = 0; k < kWinVec; ++k)
-            if (k < nv) glds16_stream(src + k, wslab + k * kWave);
+            if (k < nv) glds16(src + k, wslab + k * kWave);
         wait_vm0();
     }
     // each wave reads only its own slab: a wave-level barrier orders it
@@ -169,111 +125,12 @@ __device__ __forceinline__ void rx_tile(const uint8_t* __restrict__ frames,
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     STAMP(2);
 
-    // The frame this lane parses: its own, or with the shape sort (EMURX_SORT, kinds 0 / 1, all
-    // four waves of the tile staged) a frame of the tile from the lane's position in a stable
-    // counting sort by shape class (IPv4 / IPv6 / other x UDP / TCP / other), so that a wave's
-    // lanes take the same parse and lookup branches.  Records, flows and histogram go out from
-    // the parsing lane; queue and owner ranks are taken back in frame order through LDS.
-    uint32_t pf = tid, poff = off, plen = len, pvport = vport, pbase = wv * kStage + (off - start);
-    bool pvalid = valid, sorted = false;
-    uint8_t* s_aux = reinterpret_cast<uint8_t*>(&s_csum[0][0]);  // free when every wave is staged
-    if constexpr (EMURX_SORT && kKind != 2 && kTpw == 1) {
-        if (__syncthreads_and(staged)) {  // tile-uniform; every slab is visible to every wave after it
-            uint32_t* s_cls = reinterpret_cast<uint32_t*>(s_aux + 768);  // [wave][class] counts
-            uint32_t* s_st = reinterpret_cast<uint32_t*>(s_aux + 896);   // wave starts
-            const uint32_t cls =
-                valid ? frame_class(LdsSrc{reinterpret_cast<const uint8_t*>(slab), slab, pbase}, len) : 7u;
-            uint64_t mine = 0;
-#pragma unroll
-            for (uint32_t k = 0; k < 8; ++k) {
-                const uint64_t b = __ballot(cls == k);
-                if (cls == k) mine = b;
-                if (lane == k) s_cls[wv * 8 + k] = (uint32_t)__popcll(b);
-            }
-            if (lane == 0) s_st[wv] = start;
-            __syncthreads();
-            uint32_t base = 0, maxc = 0;
-#pragma unroll
-            for (uint32_t k = 0; k < 8; ++k) {
-                const uint32_t t = s_cls[k] + s_cls[8 + k] + s_cls[16 + k] + s_cls[24 + k];
-                maxc = max(maxc, t);
-                base += k < cls ? t : 0u;
-            }
-            for (uint32_t w = 0; w < wv; ++w) base += s_cls[w * 8 + cls];
-            sorted = maxc < kBlock;  // one shape everywhere: nothing to gain
-            if (sorted) s_aux[base + mbcnt(mine)] = (uint8_t)tid;
-            __syncthreads();
-            if (sorted) {
-                pf = s_aux[tid];
-                const uint32_t fi = tile * EMURX_QUEUE_TILE + pf;
-                const uint2 pd = fi < n ? *reinterpret_cast<const uint2*>(desc + fi) : make_uint2(0, EMURX_DESC_HOLE << 24);
-                pvalid = (pd.y >> 24) != EMURX_DESC_HOLE;
-                poff = pd.x;
-                plen = pd.y & 0xffff;
-                pvport = (pd.y >> 16) & 0xff;
-                pbase = (pf / kWave) * kStage + (poff - s_st[pf / kWave]);
-            }
-        }
-    }
-    const uint32_t pi = tile * EMURX_QUEUE_TILE + pf;  // the parsed frame's index in the batch
-
     Rec r;
     r.dlen = 0;
     uint32_t kwd[12];  // kKind 2: the lookup key words of the frame
-    LKey lk{};         // EMURX_LSORT: the frame's lookup, resolved after the parse of the tile
-    bool lgo = false;
-    const bool lsort = EMURX_LSORT && kClassify && !T.ft_on && !(EMURX_ABL & 2);  // uniform
-    if (staged && kClassify && EMURX_CSTAGE && !T.ft_on && !(EMURX_ABL & 2)) {  // wave-uniform branch
-        // The client buckets of the wave staged in its slab.  Once the lookup keys are made the
-        // frame bytes are not read again (no TransportCtx: no flow tuple), so the slab takes
-        // the 64 client buckets, 4 KiB: each LDS-DMA instruction loads 16 whole buckets, a
-        // quad of lanes per bucket (16 lines per instruction instead of 64), bucket i landing
-        // at slab byte 64 i.  The Namespace buckets load into registers alongside.
-        LdsSrc s{reinterpret_cast<const uint8_t*>(slab), slab, pbase};
-        const uint32_t len = plen;
-        bool go = false;
-        LKey k{};
-        Probe pr{};
-        if (pvalid) {
-            parse_flat(s, len, pvport, T.cb_mask, r);
-            go = r.status == EMURX_ST_OK;
-            if (go) {
-                k = make_key(s, len, r);
-                pr = probe_issue(T, r, k);
-            }
-        }
-        STAMP(3);
-        STAMP(4);
-        const uintptr_t ca = go && pr.ctab ? (uintptr_t)(pr.ctab + (size_t)pr.cbk * EMURX_BUCKET_WORDS) : 0;
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): every read of the frame bytes has returned
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-        for (uint32_t q = 0; q < 4; ++q) {
-            const uint32_t src = 16 * q + (lane >> 2);
-            const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)ca, (int)src);
-            const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)ca >> 32), (int)src);
-            const uintptr_t a = ((uintptr_t)hi << 32) | lo;
-            if (a) glds16(reinterpret_cast<const uint4*>(a) + (lane & 3), wslab + 64 * q);
-        }
-        wait_vm0();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (go) {
-            Bucket ce{};
-            if (pr.ctab) {
-                const uint4* b = wslab + 4 * lane;
-                ce = Bucket{{b[0], b[1], b[2], b[3]}};
-            }
-            resolve_done(T, r, k, pr, ce, [](uint32_t) { return EMURX_FLOW_NO_CTX; });  // ft_on == 0: never called
-        }
-        STAMP(5);
-    } else if (staged) {  // wave-uniform branch
-        if (pvalid) {
-            LdsSrc s{reinterpret_cast<const uint8_t*>(slab), slab, pbase};
-            const uint32_t len = plen, vport = pvport;
+    if (staged) {  // wave-uniform branch
+        if (valid) {
+            LdsSrc s{reinterpret_cast<const uint8_t*>(slab), slab, wv * kStage + (off - start)};
             parse_flat(s, len, vport, T.cb_mask, r);
 #if EMURX_STAMP
             STAMP(3);
@@ -284,12 +141,7 @@ __device__ __forceinline__ void rx_tile(const uint8_t* __restrict__ frames,
             if (go) resolve(T, r, k, [&](uint32_t cid) { return flow_probe(T, get_tuple(s, len, r), cid); });
             STAMP(5);
 #else
-            if (lsort) {
-                lgo = r.status == EMURX_ST_OK;
-                if (lgo) lk = make_key(s, len, r);
-            } else if (kClassify && !(EMURX_ABL & 2)) {
-                classify(s, len, T, r);
-            }
+            if (kClassify) classify(s, len, T, r);
 #endif
             if (kKind == 2 && r.status == EMURX_ST_OK) pack_key(s, len, r, make_key(s, len, r), kwd);
         }
@@ -298,9 +150,7 @@ __device__ __forceinline__ void rx_tile(const uint8_t* __restrict__ frames,
         WinSrc s{reinterpret_cast<const uint8_t*>(slab), slab, wv * kStage + lane * 16, head,
                  min(kWinVec * 16 - head, len), frames + off};
         if (valid) parse_packet(s, len, vport, T.cb_mask, r);
-        // the wave's long L4 spans, converged
-        if constexpr (EMURX_COOP == 0) coop_checksum(r, frames + off, s_csum[wv]);
-        else coop_checksum_rows<EMURX_COOP>(r, frames + off, s_csum[wv]);
+        coop_checksum_rows(r, frames + off, s_csum[wv]);  // the wave's long L4 spans, converged
 #if EMURX_STAMP
         STAMP(3);
         const bool go = valid && kClassify && r.status == EMURX_ST_OK;
@@ -310,127 +160,57 @@ __device__ __forceinline__ void rx_tile(const uint8_t* __restrict__ frames,
         if (go) resolve(T, r, k, [&](uint32_t cid) { return flow_probe(T, get_tuple(s, len, r), cid); });
         STAMP(5);
 #else
-        if (lsort) {
-            lgo = valid && r.status == EMURX_ST_OK;
-            if (lgo) lk = make_key(s, len, r);
-        } else if (valid && kClassify && !(EMURX_ABL & 2)) {
-            classify(s, len, T, r);
-        }
+        if (valid && kClassify) classify(s, len, T, r);
 #endif
         if (kKind == 2 && valid && r.status == EMURX_ST_OK) pack_key(s, len, r, make_key(s, len, r), kwd);
     }
-    if constexpr (EMURX_LSORT && kClassify) {
-        if (lsort) {  // tile-uniform: every wave of the tile takes part
-            const uint32_t key = lk.key;
-            const uint32_t cls = !lgo ? 4u : key == kMac ? 0u : key == kIp4 ? 1u : (key == kIp6 || key == kEui) ? 2u : 3u;
-            uint64_t mine = 0;
-#pragma unroll
-            for (uint32_t c = 0; c < 4; ++c) {
-                const uint64_t b = __ballot(cls == c);
-                if (cls == c) mine = b;
-                if (lane == c) s_lcls[wt][c] = (uint32_t)__popcll(b);
-            }
-            __syncthreads();  // counts visible; every wave is done with its slab
-            uint32_t tot[4], kinds = 0, ngo = 0, pos = 0;
-#pragma unroll
-            for (uint32_t c = 0; c < 4; ++c) {
-                tot[c] = s_lcls[0][c] + s_lcls[1][c] + s_lcls[2][c] + s_lcls[3][c];
-                kinds += tot[c] ? 1u : 0u;
-                pos += c < cls ? tot[c] : 0u;
-                ngo += tot[c];
-            }
-            if (kinds > 1) {  // tile-uniform
-                for (uint32_t w = 0; w < wt; ++w) pos += s_lcls[w][cls < 4 ? cls : 0];
-                pos += mbcnt(mine);
-                uint4* P = reinterpret_cast<uint4*>(slab);          // 3 x 16 B per lookup
-                uint4* R = P + 3 * EMURX_QUEUE_TILE;                 // 16 B per frame: the results
-                if (lgo) {
-                    P[3 * pos] = make_uint4(key | (r.proto << 8) | (lk.mc6 << 16), lk.kw[0], lk.kw[1], lk.kw[2]);
-                    P[3 * pos + 1] = make_uint4(lk.kw[3], lk.dlo, lk.dhi, r.vport);
-                    P[3 * pos + 2] = make_uint4(r.vlan0, r.vlan1, tid, 0);
-                }
-                __syncthreads();
-                if (tid < ngo) {
-                    const uint4 a = P[3 * tid], b = P[3 * tid + 1], c = P[3 * tid + 2];
-                    LKey q;
-                    q.key = a.x & 0xff;
-                    q.mc6 = (a.x >> 16) & 1;
-                    q.kw[0] = a.y; q.kw[1] = a.z; q.kw[2] = a.w; q.kw[3] = b.x;
-                    q.dlo = b.y; q.dhi = b.z;
-                    Rec rr;
-                    rr.proto = (a.x >> 8) & 0xff;
-                    rr.vport = b.w; rr.vlan0 = c.x; rr.vlan1 = c.y;
-                    rr.ns = EMURX_ID_NONE; rr.cl = EMURX_ID_NONE; rr.flags = 0; rr.flow = EMURX_FLOW_NONE;
-                    resolve(T, rr, q, [](uint32_t) { return EMURX_FLOW_NO_CTX; });  // ft_on == 0: never called
-                    R[c.z] = make_uint4(rr.ns, rr.cl, rr.flags & EMURX_FLAG_LK_MASK, rr.flow);
-                }
-                __syncthreads();
-                if (lgo) {
-                    const uint4 x = R[tid];
-                    r.ns = x.x;
-                    r.cl = x.y;
-                    r.flags = (r.flags & ~EMURX_FLAG_LK_MASK) | x.z;
-                    r.flow = x.w;  // EMURX_FLOW_NO_CTX for a transport frame's client (ft_on == 0)
-                }
-            } else if (lgo) {
-                resolve(T, r, lk, [](uint32_t) { return EMURX_FLOW_NO_CTX; });
-            }
-        }
-    }
     typedef unsigned v4u __attribute__((ext_vector_type(4)));
-    if (rec && pi < n && !(EMURX_ABL & 16)) {
+    if (rec && i < n) {
         // an empty descriptor slot gets a record too (no Namespace, status EMURX_ST_HOLE), so
         // every consumer of rec[0, n) sees defined bytes
-        const uint4 h0 = pvalid ? make_uint4(r.ns, r.cl, r.vlan0, r.vlan1)
-                                : make_uint4(EMURX_ID_NONE, EMURX_ID_NONE, 0, 0);
-        const uint4 h1 = pvalid ? make_uint4(r.vport | (r.l3 << 16), r.l4 | (r.l7 << 16),
-                                             r.l7len | (r.nh << 16) | (r.proto << 24), r.status | (r.flags << 8))
-                                : make_uint4(0, 0, (uint32_t)EMURX_CB_NONE << 24, EMURX_ST_HOLE);
-        uint4* o = reinterpret_cast<uint4*>(rec + pi);
+        const uint4 h0 = valid ? make_uint4(r.ns, r.cl, r.vlan0, r.vlan1)
+                               : make_uint4(EMURX_ID_NONE, EMURX_ID_NONE, 0, 0);
+        const uint4 h1 = valid ? make_uint4(r.vport | (r.l3 << 16), r.l4 | (r.l7 << 16),
+                                            r.l7len | (r.nh << 16) | (r.proto << 24), r.status | (r.flags << 8))
+                               : make_uint4(0, 0, (uint32_t)EMURX_CB_NONE << 24, EMURX_ST_HOLE);
+        uint4* o = reinterpret_cast<uint4*>(rec + i);
         // streaming stores: the records are read once, by the host copy or the route kernel
         // (measured +2.6% on config B, neutral on C)
         __builtin_nontemporal_store(v4u{h0.x, h0.y, h0.z, h0.w}, reinterpret_cast<v4u*>(o));
         __builtin_nontemporal_store(v4u{h1.x, h1.y, h1.z, h1.w}, reinterpret_cast<v4u*>(o + 1));
     }
-    if (flow && pi < n) flow[pi] = pvalid ? r.flow : EMURX_FLOW_NONE;
+    if (flow && i < n) flow[i] = valid ? r.flow : EMURX_FLOW_NONE;
     // outcome histogram into the wave's LDS copy: a wave whose frames all share one
     // (status, proto) bin adds its count (ballot) and byte sum (DPP reduction) once, instead
     // of 64 LDS atomics serialised on one address; mixed waves add per frame
     s_hist[wv][lane] = 0;  // each wave owns its copy: no cross-wave ordering needed
-    if (!(EMURX_ABL & 4)) {
-        const uint32_t bin = pvalid ? EMURX_HIST_BIN(r.status, r.proto) : 0xffu;
-        const uint64_t vm = __ballot(pvalid);
+    {
+        const uint32_t bin = valid ? EMURX_HIST_BIN(r.status, r.proto) : 0xffu;
+        const uint64_t vm = __ballot(valid);
         STAMP(6);
         if (vm) {
             const uint32_t lead = (uint32_t)__ffsll((long long)vm) - 1;
             const uint32_t bb = (uint32_t)__builtin_amdgcn_readlane((int)bin, (int)lead);
             if (__ballot(bin == bb) == vm) {
-                const uint32_t bytes = wave_sum_u32(pvalid ? plen : 0u);  // <= 64 x 65535
+                const uint32_t bytes = wave_sum_u32(valid ? len : 0u);  // <= 64 x 65535
                 if (lane == lead) s_hist[wv][bb] += ((uint32_t)__popcll(vm) << 23) | bytes;
-            } else if (pvalid) {
-                atomicAdd(&s_hist[wv][bin], (1u << 23) | plen);
+            } else if (valid) {
+                atomicAdd(&s_hist[wv][bin], (1u << 23) | len);
             }
         }
     }
-    uint32_t q = pvalid ? (r.status == EMURX_ST_OK ? r.proto : EMURX_Q_DROP) : 0xffu;
+    const uint32_t q = valid ? (r.status == EMURX_ST_OK ? r.proto : EMURX_Q_DROP) : 0xffu;
     // the Namespace owner of the record (classify + route: the records whose Namespace was
     // found; lookup keys: every frame)
     uint32_t rd = 0xffu;
     if ((kKind == 1 && rt.cnt) || kKind == 2) {
-        const bool routed = pvalid && (kKind == 2 || r.ns != EMURX_ID_NONE);
+        const bool routed = valid && (kKind == 2 || r.ns != EMURX_ID_NONE);
         rd = routed ? emurx_owner(emurx_tk_hash(r.vport, r.vlan0, r.vlan1), rt.parts) : 0xffu;
-    }
-    if (sorted) {  // tile-uniform: queue and owner back to frame order
-        s_aux[256 + pf] = (uint8_t)q;
-        s_aux[512 + pf] = (uint8_t)rd;
-        __syncthreads();
-        q = s_aux[256 + tid];
-        rd = s_aux[512 + tid];
     }
 
     // rank inside (wave, queue): one ballot per distinct queue present in the wave
     uint32_t rank = 0;
-    uint64_t left = (EMURX_ABL & 8) ? 0 : __ballot(valid);
+    uint64_t left = __ballot(valid);
     while (left) {
         const uint32_t lead = (uint32_t)__ffsll((long long)left) - 1;
         const uint32_t qq = (uint32_t)__builtin_amdgcn_readlane((int)q, (int)lead);
@@ -439,12 +219,10 @@ __device__ __forceinline__ void rx_tile(const uint8_t* __restrict__ frames,
         if (lane == lead) s_wcnt[wv][qq] = (uint32_t)__popcll(m);
         left &= ~m;
     }
-    // the route count pass fused in (emurx_set_route_parts): the owner GPU of every record
-    // with a Namespace, counted per (tile, owner) and per group of 64 tiles as k_route<false>
-    // counts them (emurx_route.hip)
     // Namespace owners (rt.parts > 0): kind 1 counts the records whose Namespace was found
-    // (the first pass of emurx_route_dev, fused); kind 2 packs every frame's lookup record
-    // into its owner's region, ranked by ballots like the queues
+    // (the first pass of emurx_route_dev, fused; k_route<false> counts them the same way,
+    // emurx_route.hip); kind 2 packs every frame's lookup record into its owner's region,
+    // ranked by ballots like the queues
     uint32_t rrank = 0;
     if ((kKind == 1 && rt.cnt) || kKind == 2) {
         uint64_t rl = __ballot(rd != 0xffu);
@@ -460,14 +238,14 @@ __device__ __forceinline__ void rx_tile(const uint8_t* __restrict__ frames,
     STAMP(7);
     __syncthreads();
     STAMP(8);
-    if (kKind == 1 && rt.cnt && tid < 16 && tile_in) {
-        const uint32_t c = tid < rt.parts ? s_rcnt[w0][tid] + s_rcnt[w0 + 1][tid] + s_rcnt[w0 + 2][tid] + s_rcnt[w0 + 3][tid] : 0u;
+    if (kKind == 1 && rt.cnt && tid < 16) {
+        const uint32_t c = tid < rt.parts ? s_rcnt[0][tid] + s_rcnt[1][tid] + s_rcnt[2][tid] + s_rcnt[3][tid] : 0u;
         rt.cnt[(size_t)tile * 16 + tid] = c;
         if (c) atomicAdd(&rt.grp[(tile / 64) * 16 + tid], c);
     }
     if (kKind == 2 && rd != 0xffu) {  // the lookup record: ns_id = frame index, client_id = source rank
         uint32_t pos = s_toff[rd] + rrank;
-        for (uint32_t w = w0; w < wv; ++w) pos += s_rcnt[w][rd];
+        for (uint32_t w = 0; w < wv; ++w) pos += s_rcnt[w][rd];
         if (pos < rt.cap) {  // overflow: send_count[d] > cap tells the caller
             const bool ok = r.status == EMURX_ST_OK;
             v4u* o = reinterpret_cast<v4u*>(rt.send + (size_t)rd * rt.cap + pos);
@@ -481,22 +259,21 @@ __device__ __forceinline__ void rx_tile(const uint8_t* __restrict__ frames,
     }
 
     // this tile's segment of every queue: frames in (wave, lane) order == frame order
-    if (qlist && q < EMURX_NUM_QUEUES && !(EMURX_ABL & 8)) {
+    if (qlist && q < EMURX_NUM_QUEUES) {
         uint32_t pos = rank;
-        for (uint32_t w = w0; w < wv; ++w) pos += s_wcnt[w][q];
+        for (uint32_t w = 0; w < wv; ++w) pos += s_wcnt[w][q];
         const size_t at = (size_t)q * qcap + (size_t)tile * EMURX_QUEUE_TILE + pos;
         if ((size_t)tile * EMURX_QUEUE_TILE + pos < qcap) qlist[at] = i;
     }
-    if (tile_cnt && tid < 16 && tile_in)
-        tile_cnt[(size_t)tile * 16 + tid] =
-            s_wcnt[w0][tid] + s_wcnt[w0 + 1][tid] + s_wcnt[w0 + 2][tid] + s_wcnt[w0 + 3][tid];
+    if (tile_cnt && tid < 16)
+        tile_cnt[(size_t)tile * 16 + tid] = s_wcnt[0][tid] + s_wcnt[1][tid] + s_wcnt[2][tid] + s_wcnt[3][tid];
     // one of EMURX_HIST_SHARDS copies per workgroup: same-address memory-side atomics from
     // every workgroup would serialise; the shards are folded on the host
     if (tid >= 64 && tid < 64 + EMURX_HIST_BINS) {
         const uint32_t b = tid - 64;
         uint32_t pk = 0, by = 0;
 #pragma unroll
-        for (uint32_t w = w0; w < w0 + kWaves; ++w) {
+        for (uint32_t w = 0; w < kWaves; ++w) {
             pk += s_hist[w][b] >> 23;
             by += s_hist[w][b] & ((1u << 23) - 1);
         }
@@ -509,7 +286,7 @@ __device__ __forceinline__ void rx_tile(const uint8_t* __restrict__ frames,
 #if EMURX_STAMP
     STAMP(9);
     if (g_stamp && lane == 0) {
-        unsigned long long* o = g_stamp + ((size_t)tile * kWaves + wt) * 16;
+        unsigned long long* o = g_stamp + ((size_t)tile * kWaves + wv) * 16;
         for (int k = 0; k < 10; ++k) o[k] = st_[k];
         o[10] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
         o[11] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
@@ -537,7 +314,7 @@ struct RxArgs {
 };
 
 template <int kKind, uint32_t kStage>
-__global__ __launch_bounds__(kBlock * tiles_per_wg<kStage>()) __attribute__((amdgpu_waves_per_eu(kStage == kStageNarrow ? 6 : 5))) void k_rx(const RxArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage == kStageNarrow ? 6 : 5))) void k_rx(const RxArgs a) {
     rx_tile<kKind, kStage>(a.frames, a.desc, a.n, a.T, a.rec, a.qlist, a.qcap, a.tile_cnt, a.hist, a.flow, a.fb, a.gen, a.rt,
                            blockIdx.x);
 }
@@ -569,9 +346,8 @@ int emurx_launch_batch(const uint8_t* frames, const emurx_desc* desc, uint32_t n
     using namespace emurx;
     if (ev) (void)hipEventRecord(ev[0], st);
     if (n) {
-        const uint32_t tpw = narrow ? tiles_per_wg<kStageNarrow>() : tiles_per_wg<kStageWide>();
         const uint32_t ntiles = (n + EMURX_QUEUE_TILE - 1) / EMURX_QUEUE_TILE;
-        const dim3 g((ntiles + tpw - 1) / tpw), b(kBlock * tpw);
+        const dim3 g(ntiles), b(kBlock);
         unsigned long long* hist = reinterpret_cast<unsigned long long*>(out.hist);
         auto k = kind == 1 ? (narrow ? k_rx<1, kStageNarrow> : k_rx<1, kStageWide>)
                : kind == 2 ? (narrow ? k_rx<2, kStageNarrow> : k_rx<2, kStageWide>)

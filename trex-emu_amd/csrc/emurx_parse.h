@@ -23,18 +23,6 @@ constexpr int kWaves = kBlock / kWave;
 // gives 6 workgroups per CU instead of 5; waves wider than it take the window path)
 constexpr uint32_t kStageWide = 7168, kStageNarrow = 6144;
 
-#ifndef EMURX_ABL
-#define EMURX_ABL 0  // experiment-only stage ablation (tools/abl_counts.sh); 0 in every real build
-#endif
-#ifndef EMURX_SORT
-#define EMURX_SORT 0  // A/B: shape-class sort of a staged tile's frames over its lanes (emurx_kernels.hip)
-#endif
-#ifndef EMURX_COOP
-// long-span checksum: 0 the packed vector list (coop_checksum), 2 / 4 / 8 vectors per lane per
-// round of the 16-lane row groups (coop_checksum_rows; 4 measured best)
-#define EMURX_COOP 4
-#endif
-
 // loads through the global address space (global_load_*): pointers rebuilt from integers or
 // kept in a struct would otherwise compile to flat loads, which also count on lgkmcnt and
 // make the compiler serialise them with LDS traffic
@@ -110,20 +98,6 @@ __device__ __forceinline__ void l2_vlans(uint32_t len, uint32_t w12, uint32_t w1
     const bool g1 = g0 && len >= 22 && (e1 == 0x8100 || e1 == 0x88A8);
     v0 = g0 ? (w12 & 0xffff0fffu) : 0u;
     v1 = g1 ? (w16 & 0xffff0fffu) : 0u;
-}
-
-// shape class of a frame for the tile sort (emurx_kernels.hip, EMURX_SORT): the EtherType
-// after up to two tags, then the L4 protocol (IPv4 header / IPv6 next header): 0..2 IPv4
-// UDP / TCP / other, 3..5 IPv6 UDP / TCP / other, 6 anything else.  Only a grouping hint:
-// every frame is still parsed by the full ParsePacket restatement.
-template <class S>
-__device__ __forceinline__ uint32_t frame_class(const S& s, uint32_t len) {
-    uint32_t et = (s.u8(12) << 8) | s.u8(13), o = 14;
-    if ((et == 0x8100 || et == 0x88A8) && len >= 18) { et = (s.u8(16) << 8) | s.u8(17); o = 18; }
-    if ((et == 0x8100 || et == 0x88A8) && len >= 22) { et = (s.u8(20) << 8) | s.u8(21); o = 22; }
-    const bool v4 = et == 0x0800, v6 = et == 0x86DD;
-    const uint32_t p = v4 ? s.u8(o + 9) : v6 ? s.u8(o + 6) : 0u;
-    return v4 || v6 ? (v4 ? 0u : 3u) + (p == 17 ? 0u : p == 6 ? 1u : 2u) : 6u;
 }
 
 // lanes below this one in mask m
@@ -273,7 +247,6 @@ struct WinSrc {
 // tcpipChecksum(p[s:s+n], pcs) == 0
 template <class S>
 __device__ __forceinline__ bool csum(const S& src, uint32_t s, uint32_t n, uint32_t pcs) {
-    if (EMURX_ABL & 1) return true;
     return csum_ok(src.sum(s, n), src.at(s), pcs);
 }
 // sum of the big-endian 16-bit words of p[s:s+n] (n even), mod 0xffff: GetPhCs's address part
@@ -292,25 +265,14 @@ template <class S>  // bytes i..i+3 as a little-endian word (the table key encod
 __device__ __forceinline__ uint32_t le32(const S& s, uint32_t i) {
     return s.u8(i) | (s.u8(i + 1) << 8) | (s.u8(i + 2) << 16) | (s.u8(i + 3) << 24);
 }
-// Staged frames (EMURX_LDW, on; measured C -3 %, D -1.6 %, B -2 %): 32-bit fields from the two aligned LDS dwords that hold
-// them (v_alignbyte) instead of four byte reads; the second dword may lie past the frame,
-// harmless in LDS and masked out by the shift when the field is aligned
-#ifndef EMURX_LDW
-#define EMURX_LDW 1
-#endif
-#if EMURX_LDW
+// Staged frames: 32-bit fields from the two aligned LDS dwords that hold them (v_alignbyte)
+// instead of four byte reads (measured C -3 %, D -1.6 %, B -2 %); the second dword may lie
+// past the frame, harmless in LDS and masked out by the shift when the field is aligned
 __device__ __forceinline__ uint32_t le32(const LdsSrc& s, uint32_t i) {
     const uint32_t a = s.base + i, k = a >> 2;
     return __builtin_amdgcn_alignbyte(s.b32[k + 1], s.b32[k], a & 3);
 }
 __device__ __forceinline__ uint32_t be32(const LdsSrc& s, uint32_t i) { return __builtin_bswap32(le32(s, i)); }
-#endif
-// the big-endian 16-bit value of the two low bytes of a little-endian word
-__device__ __forceinline__ uint32_t bs16(uint32_t w) { return ((w & 0xffu) << 8) | ((w >> 8) & 0xffu); }
-#ifndef EMURX_LDF
-#define EMURX_LDF 0  // A/B knob: parse_flat's header fields from shared dwords (le32) too
-#endif
-
 // ---------------------------------------------------------------------------------------
 // parse state == ParserPacketState + CTunnelData + outcome
 // ---------------------------------------------------------------------------------------
@@ -337,33 +299,20 @@ __device__ __forceinline__ bool span_ok(uint32_t l4, uint32_t l4len) {
 }
 
 // the L4 checksum of parsePacketL4.  LdsSrc: now.  WinSrc: now when the span lies in the
-// lane's window, else deferred to coop_checksum() (the caller proceeds as if it passed; the
+// lane's window, else deferred to coop_checksum_rows() (the caller proceeds as if it passed; the
 // cooperative pass applies `fail_st` afterwards, see settle_deferred)
 template <class S>
 __device__ __forceinline__ bool csum_l4(const S& s, Rec& r, uint32_t at, uint32_t n, uint32_t pcs, uint32_t fail_st) {
     return csum(s, at, n, pcs);
 }
-// EMURX_WSKIP: the span's bytes inside the window are summed from LDS here and folded into
-// the deferred pseudo sum (the byte-pair sum is linear mod 0xffff, and be_domain with the
-// span's own start parity orients both parts alike), so the cooperative pass reads only the
-// bytes past the window; dfail carries that parity in bit 16.
-#ifndef EMURX_WSKIP
-#define EMURX_WSKIP 0
-#endif
 template <>
 __device__ __forceinline__ bool csum_l4<WinSrc>(const WinSrc& s, Rec& r, uint32_t at, uint32_t n, uint32_t pcs,
                                                 uint32_t fail_st) {
     if (at + n <= s.wlim || n == 0) return csum(s, at, n, pcs);
-    uint32_t st = at, pw = pcs;
-    if (EMURX_WSKIP && at < s.wlim) {
-        const uint32_t tw = dword_sum(WinDw{s.b32 + (s.wbase >> 2)}, s.head + at, s.wlim - at);
-        pw = pcs + be_domain(tw, s.at(at));  // tw == 0 leaves pcs as it was (Go's all-zero case)
-        st = s.wlim;
-    }
-    r.dstart = st;
-    r.dlen = at + n - st;
-    r.dpcs = pw;
-    r.dfail = fail_st | ((s.at(at) & 1u) << 16);
+    r.dstart = at;
+    r.dlen = n;
+    r.dpcs = pcs;
+    r.dfail = fail_st | ((s.at(at) & 1u) << 16);  // the span's start parity (csum_ok's a_start)
     return true;
 }
 
@@ -493,7 +442,7 @@ __device__ __forceinline__ void parse_packet(const S& s, uint32_t len, uint32_t 
             uint32_t totlen = be16(s, offset + 2);
             if (len < ((offset + totlen) & 0xffff)) { fail(r, EMURX_ST_IPV4_TOO_SHORT); return; }
             const uint32_t th = hdr == 20 ? s.template sum_fixed<20>(offset) : s.sum(offset, hdr);
-            if (!(EMURX_ABL & 1) && !csum_ok(th, s.at(offset), 0)) { fail(r, EMURX_ST_IPV4_CS); return; }
+            if (!csum_ok(th, s.at(offset), 0)) { fail(r, EMURX_ST_IPV4_CS); return; }
             l4len = (totlen - hdr) & 0xffff;
             l4 = offset + hdr;
             nh = s.u8(offset + 9);
@@ -607,12 +556,7 @@ __device__ __forceinline__ void parse_l4_flat(const LdsSrc& s, uint32_t len, Rec
     // before it for UDP, L7 only on success for ICMP and UDP)
     r.l7len = tcp_hdr ? ((l4len - tcplen) & 0xffff) : (p17 && len >= L4_8) ? ((l4len - 8) & 0xffff) : 0u;
     r.l7 = tcp_hdr ? ((L4 + tcplen) & 0xffff) : ((p1 || p17) && st == EMURX_ST_OK) ? L4_8 : 0u;
-#if EMURX_LDF
-    const uint32_t p0 = le32(s, L4);  // sport, dport as on the wire
-    const uint32_t src = bs16(p0), dst = bs16(p0 >> 16), t6 = p0 & 0xffu;
-#else
     const uint32_t src = be16(s, L4), dst = be16(s, L4 + 2), t6 = s.u8(L4);
-#endif
     uint32_t cb = p1 ? EMURX_CB_ICMP : p2 ? EMURX_CB_IGMP : p6 ? EMURX_CB_TCP : p58 ? EMURX_CB_ICMPV6 : EMURX_CB_UDP;
     if (p17) {
         cb = dst == 5353 ? EMURX_CB_MDNS
@@ -638,12 +582,7 @@ __device__ __forceinline__ void parse_flat(const LdsSrc& s, uint32_t len, uint32
     auto is_ppp = [](uint32_t x) { return x == 0x8863 || x == 0x8864; };
     uint32_t st = EMURX_ST_OK;
     first(st, len < 14, EMURX_ST_PACKET_TOO_SHORT);
-#if EMURX_LDF
-    const uint32_t w12 = le32(s, 12), w16 = le32(s, 16);  // also the VLAN words below
-    const uint32_t e0 = bs16(w12), e1 = bs16(w16), e2 = bs16(le32(s, 20));
-#else
     const uint32_t e0 = be16(s, 12), e1 = be16(s, 16), e2 = be16(s, 20);
-#endif
     const bool t0 = st == EMURX_ST_OK && is_tag(e0);
     first(st, t0 && len < 18, EMURX_ST_DOT1Q_TOO_SHORT);
     const bool g0 = t0 && st == EMURX_ST_OK;  // tag 0 parsed
@@ -666,12 +605,7 @@ __device__ __forceinline__ void parse_flat(const LdsSrc& s, uint32_t len, uint32
     bool v6 = false;
     if (et == 0x0800) {  // IPv4
         r.l3 = offset;
-#if EMURX_LDF
-        const uint32_t h0 = le32(s, offset), h4 = le32(s, offset + 4);
-        const uint32_t b0 = h0 & 0xffu, frag = bs16(h4 >> 16), totlen = bs16(h0 >> 16);
-#else
         const uint32_t b0 = s.u8(offset), frag = be16(s, offset + 6), totlen = be16(s, offset + 2);
-#endif
         const uint32_t hdr = (b0 & 0xf) << 2;
         first(st, len < offset + 20, EMURX_ST_IPV4_TOO_SHORT);
         first(st, (b0 >> 4) != 4, EMURX_ST_IPV4_HDR_TOO_SHORT);
@@ -681,7 +615,7 @@ __device__ __forceinline__ void parse_flat(const LdsSrc& s, uint32_t len, uint32
         first(st, len < ((offset + totlen) & 0xffff), EMURX_ST_IPV4_TOO_SHORT);
         // the header sum: straight-line for the usual 20 bytes (a failed frame's value is unused)
         const uint32_t th = hdr == 20 ? s.template sum_fixed<20>(offset) : s.sum(offset, st == EMURX_ST_OK ? hdr : 0u);
-        const bool hok = (EMURX_ABL & 1) || csum_ok(th, s.at(offset), 0);
+        const bool hok = csum_ok(th, s.at(offset), 0);
         first(st, !hok, EMURX_ST_IPV4_CS);
         if (st != EMURX_ST_OK) { fail(r, st); return; }
         l4len = (totlen - hdr) & 0xffff;
@@ -740,11 +674,16 @@ __device__ __forceinline__ void parse_flat(const LdsSrc& s, uint32_t len, uint32
 }
 
 // ---------------------------------------------------------------------------------------
-// Wave-cooperative L4 checksums for the WinSrc path (long spans, IMIX / jumbo frames): the
-// 64 lanes stream one frame's span at a time with coalesced 16-byte loads, eight frames in
-// flight, and reduce it on the DPP network; the owner lane settles its outcome.  Replaces
-// a per-lane serial walk of up to ~90 dependent loads.  Called with the wave converged.
+// Wave-cooperative L4 checksums for the WinSrc path (long spans, IMIX / jumbo frames).  The
+// wave's deferred spans are dealt to its four 16-lane rows in lane order, balanced by their
+// round counts, and each row walks its spans one after the other, 16 lanes x kCoopVec
+// consecutive vectors of one span per round (coalesced 1 KiB row loads, no per-vector span
+// search); a round's row total is folded by four DPP row shifts and added once into the span's
+// LDS word; the owner lane settles its outcome.  Replaces a per-lane serial walk of up to ~90
+// dependent loads.  Called with the wave converged.  4 vectors per lane per round measured
+// best (2: +22 %, 8: +56 % on config E).
 // ---------------------------------------------------------------------------------------
+constexpr uint32_t kCoopVec = 4;
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
     return wave_reduce(v, [](uint32_t x, uint32_t y) { return x + y; });
 }
@@ -754,77 +693,11 @@ __device__ __forceinline__ void settle_deferred(Rec& r, bool ok) {
     if (st == EMURX_ST_ICMPV4_CS || st == EMURX_ST_UDP_CS) r.l7 = 0;  // Go sets L7 after the check
     fail(r, st);
 }
-// lane-indexed vector k of a span of nv vectors (bytes [h, t) of the first / last): the load
-// is clamped in bounds and issued unconditionally, the contribution masked afterwards
-__device__ __forceinline__ uint4 span_load(const uint8_t* v, uint32_t nv, uint32_t k) {
-    return gld16(v + 16 * min(k, nv - 1));
-}
+// vector k of a span of nv vectors (bytes [h, t) of the first / last)
 __device__ __forceinline__ uint32_t span_sum(const uint4& x, uint32_t nv, int h, int t, uint32_t k) {
     if (k >= nv) return 0;
     return sad_vec_masked(x, k == 0 ? h : 0, k == nv - 1 ? t : 16, 0);
 }
-__device__ __forceinline__ void coop_checksum(Rec& r, const uint8_t* f, uint32_t* wsum) {
-    // The wave's deferred spans are laid end to end as one list of 16-byte vectors (an
-    // exclusive prefix over lanes); each pass covers 64 x kPV consecutive vectors of that
-    // list, all loads in flight together, every lane finding the span its vector belongs to
-    // by a binary search over the prefix.  Partial sums go to the owner's LDS word.  No slot
-    // is wasted on short spans and a wave needs ceil(total / (64 kPV)) memory round trips.
-    constexpr uint32_t kPV = 4;
-    const uint32_t lane = lane_id();
-    const bool mine = r.dlen != 0;
-    if (!__ballot(mine)) return;
-    const uintptr_t a = (uintptr_t)(f + r.dstart), e = a + r.dlen;
-    const uint32_t nv = mine ? (uint32_t)((((e + 15) & ~(uintptr_t)15) - (a & ~(uintptr_t)15)) >> 4) : 0u;
-    uint32_t incl = nv;
-#pragma unroll
-    for (uint32_t o = 1; o < kWave; o <<= 1) {
-        const uint32_t up = (uint32_t)__shfl_up((int)incl, o);
-        if (lane >= o) incl += up;
-    }
-    const uint32_t P = incl - nv;
-    const uint32_t V = (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
-    const uintptr_t a16 = a & ~(uintptr_t)15;
-    const uint32_t blo = (uint32_t)a16, bhi = (uint32_t)(a16 >> 32);
-    const uint32_t geo = nv | ((uint32_t)(a & 15) << 16) | ((16u - ((0u - (uint32_t)e) & 15)) << 24);
-    wsum[lane] = 0;  // the wave's own words; its later LDS atomics are ordered after this
-    for (uint32_t b = 0; b < V; b += kWave * kPV) {  // wave-uniform
-        uint4 x[kPV];
-        uint32_t own[kPV], kin[kPV];
-#pragma unroll
-        for (uint32_t k = 0; k < kPV; ++k) {  // converged: shuffles read every lane
-            const uint32_t v = b + k * kWave + lane;
-            uint32_t j = 0;
-#pragma unroll
-            for (uint32_t s2 = kWave / 2; s2 > 0; s2 >>= 1)
-                if ((uint32_t)__shfl((int)P, (int)(j + s2)) <= v) j += s2;
-            own[k] = j;
-            kin[k] = v - (uint32_t)__shfl((int)P, (int)j);
-            const uint32_t lo = (uint32_t)__shfl((int)blo, (int)j), hi = (uint32_t)__shfl((int)bhi, (int)j);
-            const uint8_t* src = reinterpret_cast<const uint8_t*>(((uintptr_t)hi << 32) | lo);
-            x[k] = v < V ? gld16(src + 16 * kin[k]) : make_uint4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < kPV; ++k) {
-            const uint32_t g = (uint32_t)__shfl((int)geo, (int)own[k]);
-            const uint32_t part = span_sum(x[k], g & 0xffff, (int)((g >> 16) & 0xff), (int)(g >> 24), kin[k]);
-            if (b + k * kWave + lane < V) atomicAdd(&wsum[own[k]], part);
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (mine) {
-        settle_deferred(r, csum_ok(wsum[lane], r.dfail >> 16, r.dpcs));  // parity of the span's start
-        r.dlen = 0;
-    }
-}
-
-// The same sums with the wave split into four 16-lane rows (A/B alternative, EMURX_COOP > 0):
-// the wave's deferred spans are dealt to the rows in lane order, balanced by their round
-// counts, and each row walks its spans one after the other, 16 lanes x kU consecutive vectors
-// of one span per round (coalesced 256-byte row loads, no per-vector span search); a round's
-// row total is folded by four DPP row shifts and added once into the span's LDS word.
-template <uint32_t kU>
 __device__ __forceinline__ uint32_t dpp_row_sum(uint32_t v) {
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);  // row_shr:1
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);  // row_shr:2
@@ -832,9 +705,8 @@ __device__ __forceinline__ uint32_t dpp_row_sum(uint32_t v) {
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);  // row_shr:8
     return v;  // lane 15 of each row: the row's total
 }
-template <uint32_t kU>
 __device__ __forceinline__ void coop_checksum_rows(Rec& r, const uint8_t* f, uint32_t* wsum) {
-    constexpr uint32_t kRound = 16 * kU;  // vectors of one span per row round
+    constexpr uint32_t kRound = 16 * kCoopVec;  // vectors of one span per row round
     const uint32_t lane = lane_id(), l16 = lane & 15, row = lane >> 4;
     const bool mine = r.dlen != 0;
     const uint64_t mm = __ballot(mine);
@@ -869,17 +741,17 @@ __device__ __forceinline__ void coop_checksum_rows(Rec& r, const uint8_t* f, uin
         const uint32_t lo = (uint32_t)__shfl((int)blo, (int)src_lane), hi = (uint32_t)__shfl((int)bhi, (int)src_lane);
         const uint8_t* src = reinterpret_cast<const uint8_t*>(((uintptr_t)hi << 32) | lo);
         const uint32_t nvj = j < 64 ? (gj & 0xffff) : 0u;
-        uint4 x[kU];
+        uint4 x[kCoopVec];
 #pragma unroll
-        for (uint32_t k = 0; k < kU; ++k) {
+        for (uint32_t k = 0; k < kCoopVec; ++k) {
             const uint32_t v = c * kRound + k * 16 + l16;
             x[k] = v < nvj ? gld16(src + 16 * v) : make_uint4(0, 0, 0, 0);
         }
         uint32_t part = 0;
 #pragma unroll
-        for (uint32_t k = 0; k < kU; ++k)
+        for (uint32_t k = 0; k < kCoopVec; ++k)
             part += span_sum(x[k], nvj, (int)((gj >> 16) & 0xff), (int)(gj >> 24), c * kRound + k * 16 + l16);
-        const uint32_t tot = dpp_row_sum<kU>(part);
+        const uint32_t tot = dpp_row_sum(part);
         if (l16 == 15 && j < 64 && tot) atomicAdd(&wsum[j], tot);
         if (j < 64 && ++c * kRound >= nvj) {  // the span is done: the row's next one
             c = 0;
