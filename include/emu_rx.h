@@ -372,8 +372,12 @@ int emurx_rx_stream(emurx_t* h, const uint8_t* msg, size_t len, emurx_rec* out_r
    n <= cfg.max_frames, out->qcap >= ceil(n / EMURX_QUEUE_TILE) * EMURX_QUEUE_TILE.
    d_frames must be 16-byte aligned and d_desc 8-byte aligned (EMURX_EINVAL otherwise), and
    the frame buffer must stay readable up to the next 64-byte boundary past its last byte
-   (frames are staged with 16-byte loads).  One kernel launch, no host synchronisation,
-   no handle state touched on the device: capturable in a hipGraph. */
+   (frames are staged with 16-byte loads).  One k_rx launch; when table edits are pending
+   (emurx_ns_* / emurx_client_* since the last launch) a k_apply launch and cross-stream
+   events go ahead of it, and a whole-table or growing shipment synchronises the host with
+   the stream (or the device).  Not capturable in a hipGraph: the kernel arguments carry the
+   table addresses, which a later table growth reallocates; a capturing stream gets
+   EMURX_EINVAL.  Call emurx_sync first to take the shipment out of a latency-critical call. */
 int emurx_classify_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_desc,
                        uint32_t n, const emurx_dev_out* out, void* stream);
 

@@ -7,13 +7,14 @@ as the checker.  Layouts are restated here independently of the product binding
 from __future__ import annotations
 
 import ctypes as C
+import os
 import subprocess
 from pathlib import Path
 
 import numpy as np
 
 HERE = Path(__file__).resolve().parent
-LIB = HERE / "liborc.so"
+LIB = Path(os.environ.get("ORC_LIB", HERE / "liborc.so"))  # ORC_LIB: the sanitized build (tests/test_sanitizers.py)
 
 REC_DTYPE = np.dtype([
     ("ns_id", "<u4"), ("client_id", "<u4"), ("vlan0", "<u4"), ("vlan1", "<u4"),

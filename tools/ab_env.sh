@@ -9,6 +9,6 @@ for cfg in ${@:-B C E}; do
     e=$a; [ $v = b ] && e=$b
     env $e timeout -k 10 300 python bench.py --config $cfg --steps 200 --warmup 20 --no-cpu-baseline --no-check \
       > gpurun_out/ab/${cfg}_$v.log 2>&1 || { echo "fail $cfg $v"; tail -3 gpurun_out/ab/${cfg}_$v.log; exit 1; }
-    echo "$cfg [$e] $(tail -1 gpurun_out/ab/${cfg}_$v.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["roofline"]["kernel_ms_mean"], d["roofline"]["frac"])')"
+    echo "$cfg [$e] $(tail -1 gpurun_out/ab/${cfg}_$v.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], "one", d["roofline"]["kernel_ms_mean"], d["roofline"]["frac"], "pipe", d["roofline"].get("pipelined",{}).get("interval_ms"))')"
   done
 done

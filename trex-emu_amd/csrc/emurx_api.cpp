@@ -410,12 +410,22 @@ int route_done(emurx_t::RouteScratch* r, hipStream_t st) {
     return hipEventRecord(r->done, st) == hipSuccess ? EMURX_OK : EMURX_EDEVICE;
 }
 
+// A launch path may ship table edits (k_apply, cross-stream events, a synchronisation for a
+// whole or grown table) and bakes the table addresses, which a later growth reallocates, into
+// its kernel arguments: it must not be recorded into a hipGraph
+int not_capturing(hipStream_t st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess) return EMURX_EDEVICE;
+    return cs == hipStreamCaptureStatusNone ? EMURX_OK : EMURX_EINVAL;
+}
+
 // one k_rx launch; kind: 0 parse only, 1 classify, 2 parse + lookup keys (partitioned source);
 // rt: kind 1 the route count pass fused in (emurx_classify_route_dev), kind 2 the packing
 // of the lookup records (emurx_parse_route_dev)
 int run_dev(emurx_t* h, const uint8_t* frames, const emurx_desc* desc, uint32_t n, const emurx_dev_out* out,
             hipStream_t st, int kind, const emurx_route_args* rt) {
     int rc;
+    if ((rc = not_capturing(st))) return rc;
     if (kind == 1 && (rc = prepare_read(h, st))) return rc;
     emurx_dev_tables T = h->tables();
     const hipEvent_t* ev = nullptr;
@@ -917,10 +927,17 @@ int emurx_classify_route_dev(emurx_t* h, const uint8_t* d_frames, const emurx_de
     emurx_t::RouteScratch* rs = nullptr;
     if ((rc = route_scratch(h, n, st, &rs))) return rc;
     const emurx_route_args rt{n_parts, my_rank, cap, rs->cnt.p, rs->grp.p, nullptr, nullptr};
-    if (n && (rc = run_dev(h, d_frames, d_desc, n, out, st, 1, &rt))) return rc;
+    if (n && (rc = run_dev(h, d_frames, d_desc, n, out, st, 1, &rt))) {
+        // k_rx may have added its owner counts into grp before the failure; only k_route_scan
+        // clears them, so clear them here or the next route on this set starts from garbage
+        (void)hipMemsetAsync(rs->grp.p, 0, rs->grp.n * sizeof(uint32_t), st);
+        return rc;
+    }
     if (emurx_launch_route(out->rec, n, n_parts, my_rank, cap, d_send, d_send_count, rs->cnt.p, rs->grp.p,
-                           rs->goff.p, st, true))
+                           rs->goff.p, st, true)) {
+        (void)hipMemsetAsync(rs->grp.p, 0, rs->grp.n * sizeof(uint32_t), st);
         return EMURX_EDEVICE;
+    }
     return route_done(rs, st);
 }
 
@@ -951,7 +968,7 @@ int emurx_lookup_dev(emurx_t* h, const emurx_lookup_rec* d_recv, const uint32_t*
     int rc = bind(h);
     if (rc) return rc;
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
-    if ((rc = prepare_read(h, st))) return rc;
+    if ((rc = not_capturing(st)) || (rc = prepare_read(h, st))) return rc;
     return emurx_launch_lookup(d_recv, d_recv_count, n_parts, cap, h->tables(), d_out, d_flow, st) ? EMURX_EDEVICE
                                                                                                     : EMURX_OK;
 }

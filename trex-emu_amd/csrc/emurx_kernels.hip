@@ -45,71 +45,58 @@ __device__ unsigned long long* g_stamp;
 #define STAMP(k) do {} while (0)
 #endif
 
-// kKind: 0 parse only, 1 parse + classify, 2 parse + lookup keys (the partitioned source:
-// every frame's emurx_lookup_rec packed straight into its Namespace owner's send region, at
-// the offsets the owner-count pass (k_owner_count + k_route_scan) fixed; no table reads)
-template <int kKind, uint32_t kStage>
-__device__ __forceinline__ void rx_tile(const uint8_t* __restrict__ frames,
-                                        const emurx_desc* __restrict__ desc, uint32_t n,
-                                        const emurx_dev_tables& T, emurx_rec* __restrict__ rec,
-                                        uint32_t* __restrict__ qlist, uint32_t qcap,
-                                        uint32_t* __restrict__ tile_cnt,
-                                        unsigned long long* __restrict__ hist,
-                                        uint32_t* __restrict__ flow, uint32_t* __restrict__ fb,
-                                        uint32_t gen, const emurx_route_args& rt, uint32_t tile) {
-    constexpr bool kClassify = kKind == 1;
+// k_rx's arguments as one struct (a single kernarg block; 91 SGPRs and 76 VGPRs against 106
+// and 79 for the same arguments passed one by one)
+struct RxArgs {
+    const uint8_t* frames;
+    const emurx_desc* desc;
+    uint32_t n;
+    emurx_dev_tables T;
+    emurx_rec* rec;
+    uint32_t* qlist;
+    uint32_t qcap;
+    uint32_t* tile_cnt;
+    unsigned long long* hist;
+    uint32_t* flow;
+    uint32_t* fb;
+    uint32_t gen;
+    emurx_route_args rt;
+};
+
+// a lane's descriptor of tile t (an empty slot past the batch)
+__device__ __forceinline__ uint2 load_desc(const emurx_desc* __restrict__ desc, uint32_t n, uint32_t i) {
+    return i < n ? *reinterpret_cast<const uint2*>(desc + i) : make_uint2(0, EMURX_DESC_HOLE << 24);
+}
+
+// The wave's staging of its 64 frames into its slab (wslab: the wave's kStage bytes):
+// the byte range [lo, hi) of the wave's frames copied HBM -> LDS by LDS-DMA
+// (global_load_lds_dwordx4, no VGPR round trip) when it fits the slab, else a window of each
+// lane's own frame (headers; the window path).  Issues the loads and returns; the caller waits
+// (vmcnt) before reading the slab.
+struct Stage {
+    uint32_t start, nvec;
+    bool staged;
+};
+template <uint32_t kStage>
+__device__ __forceinline__ Stage stage_issue(const uint8_t* __restrict__ frames, uint2 dd, uint32_t lane, uint4* wslab) {
     constexpr uint32_t kWinVec = kStage / 16 / kWave;  // window path: 16-byte vectors per lane
-    __shared__ __attribute__((aligned(16))) uint32_t slab[kWaves * kStage / 4];
-    __shared__ uint32_t s_wcnt[kWaves][16];
-    __shared__ uint32_t s_csum[kWaves][kWave];                    // window path: span sums
-    // outcome histogram per wave, {pkts << 23 | bytes}: <= 64 x 65535 B.  It shares the rows
-    // of s_csum (a wave's span sums are done before its histogram is zeroed): 1 KiB less keeps
-    // the narrow slab at 6 workgroups per CU (LDS 26 KiB)
-    static_assert(EMURX_HIST_BINS == kWave, "one histogram bin per lane");
-    uint32_t (*s_hist)[EMURX_HIST_BINS] = s_csum;
-    __shared__ uint32_t s_rcnt[kWaves][EMURX_MAX_PARTS];          // Namespace owners (rt_cnt)
-    __shared__ uint32_t s_toff[EMURX_MAX_PARTS];                   // kKind 2: the tile's offset in each region
-
-    const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / kWave;
-#if EMURX_STAMP
-    unsigned long long st_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-#endif
-    STAMP(0);
-    const uint32_t i = tile * EMURX_QUEUE_TILE + tid;
-    if (lane < 16) s_wcnt[wv][lane] = 0;
-    if (lane < EMURX_MAX_PARTS) s_rcnt[wv][lane] = 0;
-    if (kKind == 2 && wv == 0)
-        tile_offsets(rt.cnt, rt.goff, rt.parts, tile, lane, s_toff, [](uint32_t v) { return wave_sum_u32(v); });
-
-    const uint2 dd = i < n ? *reinterpret_cast<const uint2*>(desc + i) : make_uint2(0, EMURX_DESC_HOLE << 24);
     const bool valid = (dd.y >> 24) != EMURX_DESC_HOLE;  // an empty slot is no frame at all
-    const uint32_t off = dd.x, len = dd.y & 0xffff, vport = (dd.y >> 16) & 0xff;
-
-    // the wave's byte range [lo, hi) -> copied HBM -> LDS by LDS-DMA when it fits the slab
+    const uint32_t off = dd.x, len = dd.y & 0xffff;
     const uint32_t lo = wave_min_u32(valid ? off : 0xffffffffu);
     const uint32_t hi = wave_max_u32(valid ? off + len : 0u);
-    STAMP(1);
-    const uint32_t start = lo & ~15u;
-    const uint32_t nvec = hi > lo ? (hi - start + 15) >> 4 : 0;
-    const bool staged = nvec > 0 && nvec <= kStage / 16;
-    uint4* wslab = reinterpret_cast<uint4*>(slab) + wv * (kStage / 16);
-    // stage-size feedback from every 64th tile (the launcher's choice, emurx_api.cpp): one
-    // word per wave {gen, the wave has frames, its range fits the wide slab only}
-    if (fb && (tile & 63) == 0 && lane == 0) {
-        const uint32_t bytes = nvec * 16;
-        const uint32_t mid = bytes > kStageNarrow && bytes <= kStageWide;
-        fb[((tile >> 6) & 63) * kWaves + wv] = (gen << 2) | ((nvec > 0) << 1) | mid;
-    }
-    if (staged) {  // all copies in flight before the wait; clamped sources stay in bounds
+    Stage sg;
+    sg.start = lo & ~15u;
+    sg.nvec = hi > lo ? (hi - sg.start + 15) >> 4 : 0;
+    sg.staged = sg.nvec > 0 && sg.nvec <= kStage / 16;
+    if (sg.staged) {  // all copies in flight before the wait; clamped sources stay in bounds
         static_assert(kStage / 16 <= 8 * kWave, "staging issues at most 8 vectors per lane");
         // each LDS-DMA instruction writes 64 vectors (1 KiB) of the slab; a slab that is not a
         // whole number of them would let the last one run into the next wave's slab
         static_assert(kStage % (16 * kWave) == 0, "slab = whole 1 KiB DMA rows");
-        const uint4* src = reinterpret_cast<const uint4*>(frames + start);
+        const uint4* src = reinterpret_cast<const uint4*>(frames + sg.start);
 #pragma unroll
-        for (uint32_t k = 0; k < 8; ++k)
-            if (k * kWave < nvec) glds16(src + min(lane + k * kWave, nvec - 1), wslab + k * kWave);
-        wait_vm0();
+        for (uint32_t k = 0; k < kStage / 16 / kWave; ++k)
+            if (k * kWave < sg.nvec) glds16(src + min(lane + k * kWave, sg.nvec - 1), wslab + k * kWave);
     } else {  // too wide: each lane stages a window of its own frame (headers)
         const uintptr_t fa = (uintptr_t)(frames + off);
         const uint4* src = reinterpret_cast<const uint4*>(fa & ~(uintptr_t)15);
@@ -117,20 +104,73 @@ __device__ __forceinline__ void rx_tile(const uint8_t* __restrict__ frames,
 #pragma unroll
         for (uint32_t k = 0; k < kWinVec; ++k)
             if (k < nv) glds16(src + k, wslab + k * kWave);
-        wait_vm0();
     }
-    // each wave reads only its own slab: a wave-level barrier orders it
+    return sg;
+}
+// the slab's LDS-DMA writes are visible to this wave's reads: vmcnt(0), then a wave-level
+// barrier (each wave reads only its own slab)
+__device__ __forceinline__ void stage_wait() {
+    wait_vm0();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// The workgroup's small LDS arrays of one tile
+struct TileLds {
+    uint32_t wcnt[kWaves][16];                   // queue counts per wave
+    uint32_t csum[kWaves][kWave];                // window path: span sums; then the histogram rows
+    uint32_t rcnt[kWaves][EMURX_MAX_PARTS];      // Namespace owners
+    uint32_t toff[EMURX_MAX_PARTS];              // kKind 2: the tile's offset in each region
+};
+
+// kKind: 0 parse only, 1 parse + classify, 2 parse + lookup keys (the partitioned source:
+// every frame's emurx_lookup_rec packed straight into its Namespace owner's send region, at
+// the offsets the owner-count pass (k_owner_count + k_route_scan) fixed; no table reads).
+// One tile (EMURX_QUEUE_TILE frames, one per lane) whose frames are staged in `slab` (the
+// workgroup's kWaves slabs of kStage bytes): parse, classify, record, queue segment, counts.
+template <int kKind, uint32_t kStage>
+__device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 dd, Stage sg, const uint32_t* slab,
+                                          TileLds& L) {
+    constexpr bool kClassify = kKind == 1;
+    constexpr uint32_t kWinVec = kStage / 16 / kWave;
+    const emurx_dev_tables& T = a.T;
+    const emurx_route_args& rt = a.rt;
+    const uint32_t n = a.n;
+    // outcome histogram per wave, {pkts << 23 | bytes}: <= 64 x 65535 B.  It shares the rows
+    // of csum (a wave's span sums are done before its histogram is zeroed): 1 KiB less keeps
+    // the narrow slab at 6 workgroups per CU (LDS 26 KiB)
+    static_assert(EMURX_HIST_BINS == kWave, "one histogram bin per lane");
+    uint32_t (*s_hist)[EMURX_HIST_BINS] = L.csum;
+
+    const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / kWave;
+#if EMURX_STAMP
+    unsigned long long st_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+    STAMP(0);
+    STAMP(1);
     STAMP(2);
+    const uint32_t i = tile * EMURX_QUEUE_TILE + tid;
+    if (lane < 16) L.wcnt[wv][lane] = 0;
+    if (lane < EMURX_MAX_PARTS) L.rcnt[wv][lane] = 0;
+    if (kKind == 2 && wv == 0)
+        tile_offsets(rt.cnt, rt.goff, rt.parts, tile, lane, L.toff, [](uint32_t v) { return wave_sum_u32(v); });
+    const bool valid = (dd.y >> 24) != EMURX_DESC_HOLE;
+    const uint32_t off = dd.x, len = dd.y & 0xffff, vport = (dd.y >> 16) & 0xff;
+    // stage-size feedback from every 64th tile (the launcher's choice, emurx_api.cpp): one
+    // word per wave {gen, the wave has frames, its range fits the wide slab only}
+    if (a.fb && (tile & 63) == 0 && lane == 0) {
+        const uint32_t bytes = sg.nvec * 16;
+        const uint32_t mid = bytes > kStageNarrow && bytes <= kStageWide;
+        a.fb[((tile >> 6) & 63) * kWaves + wv] = (a.gen << 2) | ((sg.nvec > 0) << 1) | mid;
+    }
 
     Rec r;
     r.dlen = 0;
     uint32_t kwd[12];  // kKind 2: the lookup key words of the frame
-    if (staged) {  // wave-uniform branch
+    if (sg.staged) {  // wave-uniform branch
         if (valid) {
-            LdsSrc s{reinterpret_cast<const uint8_t*>(slab), slab, wv * kStage + (off - start)};
+            LdsSrc s{reinterpret_cast<const uint8_t*>(slab), slab, wv * kStage + (off - sg.start)};
             parse_flat(s, len, vport, T.cb_mask, r);
 #if EMURX_STAMP
             STAMP(3);
@@ -146,11 +186,11 @@ __device__ __forceinline__ void rx_tile(const uint8_t* __restrict__ frames,
             if (kKind == 2 && r.status == EMURX_ST_OK) pack_key(s, len, r, make_key(s, len, r), kwd);
         }
     } else {
-        const uint32_t head = (uint32_t)((uintptr_t)(frames + off) & 15);
+        const uint32_t head = (uint32_t)((uintptr_t)(a.frames + off) & 15);
         WinSrc s{reinterpret_cast<const uint8_t*>(slab), slab, wv * kStage + lane * 16, head,
-                 min(kWinVec * 16 - head, len), frames + off};
+                 min(kWinVec * 16 - head, len), a.frames + off};
         if (valid) parse_packet(s, len, vport, T.cb_mask, r);
-        coop_checksum_rows(r, frames + off, s_csum[wv]);  // the wave's long L4 spans, converged
+        coop_checksum_rows(r, a.frames + off, L.csum[wv]);  // the wave's long L4 spans, converged
 #if EMURX_STAMP
         STAMP(3);
         const bool go = valid && kClassify && r.status == EMURX_ST_OK;
@@ -165,7 +205,7 @@ __device__ __forceinline__ void rx_tile(const uint8_t* __restrict__ frames,
         if (kKind == 2 && valid && r.status == EMURX_ST_OK) pack_key(s, len, r, make_key(s, len, r), kwd);
     }
     typedef unsigned v4u __attribute__((ext_vector_type(4)));
-    if (rec && i < n) {
+    if (a.rec && i < n) {
         // an empty descriptor slot gets a record too (no Namespace, status EMURX_ST_HOLE), so
         // every consumer of rec[0, n) sees defined bytes
         const uint4 h0 = valid ? make_uint4(r.ns, r.cl, r.vlan0, r.vlan1)
@@ -173,13 +213,13 @@ __device__ __forceinline__ void rx_tile(const uint8_t* __restrict__ frames,
         const uint4 h1 = valid ? make_uint4(r.vport | (r.l3 << 16), r.l4 | (r.l7 << 16),
                                             r.l7len | (r.nh << 16) | (r.proto << 24), r.status | (r.flags << 8))
                                : make_uint4(0, 0, (uint32_t)EMURX_CB_NONE << 24, EMURX_ST_HOLE);
-        uint4* o = reinterpret_cast<uint4*>(rec + i);
+        uint4* o = reinterpret_cast<uint4*>(a.rec + i);
         // streaming stores: the records are read once, by the host copy or the route kernel
         // (measured +2.6% on config B, neutral on C)
         __builtin_nontemporal_store(v4u{h0.x, h0.y, h0.z, h0.w}, reinterpret_cast<v4u*>(o));
         __builtin_nontemporal_store(v4u{h1.x, h1.y, h1.z, h1.w}, reinterpret_cast<v4u*>(o + 1));
     }
-    if (flow && i < n) flow[i] = valid ? r.flow : EMURX_FLOW_NONE;
+    if (a.flow && i < n) a.flow[i] = valid ? r.flow : EMURX_FLOW_NONE;
     // outcome histogram into the wave's LDS copy: a wave whose frames all share one
     // (status, proto) bin adds its count (ballot) and byte sum (DPP reduction) once, instead
     // of 64 LDS atomics serialised on one address; mixed waves add per frame
@@ -216,7 +256,7 @@ __device__ __forceinline__ void rx_tile(const uint8_t* __restrict__ frames,
         const uint32_t qq = (uint32_t)__builtin_amdgcn_readlane((int)q, (int)lead);
         const uint64_t m = __ballot(q == qq);
         if (q == qq) rank = mbcnt(m);
-        if (lane == lead) s_wcnt[wv][qq] = (uint32_t)__popcll(m);
+        if (lane == lead) L.wcnt[wv][qq] = (uint32_t)__popcll(m);
         left &= ~m;
     }
     // Namespace owners (rt.parts > 0): kind 1 counts the records whose Namespace was found
@@ -228,10 +268,10 @@ __device__ __forceinline__ void rx_tile(const uint8_t* __restrict__ frames,
         uint64_t rl = __ballot(rd != 0xffu);
         while (rl) {
             const uint32_t lead = (uint32_t)__ffsll((long long)rl) - 1;
-            const uint32_t dd = (uint32_t)__builtin_amdgcn_readlane((int)rd, (int)lead);
-            const uint64_t m = __ballot(rd == dd);
-            if (rd == dd) rrank = mbcnt(m);
-            if (lane == lead) s_rcnt[wv][dd] = (uint32_t)__popcll(m);
+            const uint32_t dd2 = (uint32_t)__builtin_amdgcn_readlane((int)rd, (int)lead);
+            const uint64_t m = __ballot(rd == dd2);
+            if (rd == dd2) rrank = mbcnt(m);
+            if (lane == lead) L.rcnt[wv][dd2] = (uint32_t)__popcll(m);
             rl &= ~m;
         }
     }
@@ -239,13 +279,13 @@ __device__ __forceinline__ void rx_tile(const uint8_t* __restrict__ frames,
     __syncthreads();
     STAMP(8);
     if (kKind == 1 && rt.cnt && tid < 16) {
-        const uint32_t c = tid < rt.parts ? s_rcnt[0][tid] + s_rcnt[1][tid] + s_rcnt[2][tid] + s_rcnt[3][tid] : 0u;
+        const uint32_t c = tid < rt.parts ? L.rcnt[0][tid] + L.rcnt[1][tid] + L.rcnt[2][tid] + L.rcnt[3][tid] : 0u;
         rt.cnt[(size_t)tile * 16 + tid] = c;
         if (c) atomicAdd(&rt.grp[(tile / 64) * 16 + tid], c);
     }
     if (kKind == 2 && rd != 0xffu) {  // the lookup record: ns_id = frame index, client_id = source rank
-        uint32_t pos = s_toff[rd] + rrank;
-        for (uint32_t w = 0; w < wv; ++w) pos += s_rcnt[w][rd];
+        uint32_t pos = L.toff[rd] + rrank;
+        for (uint32_t w = 0; w < wv; ++w) pos += L.rcnt[w][rd];
         if (pos < rt.cap) {  // overflow: send_count[d] > cap tells the caller
             const bool ok = r.status == EMURX_ST_OK;
             v4u* o = reinterpret_cast<v4u*>(rt.send + (size_t)rd * rt.cap + pos);
@@ -259,14 +299,14 @@ __device__ __forceinline__ void rx_tile(const uint8_t* __restrict__ frames,
     }
 
     // this tile's segment of every queue: frames in (wave, lane) order == frame order
-    if (qlist && q < EMURX_NUM_QUEUES) {
+    if (a.qlist && q < EMURX_NUM_QUEUES) {
         uint32_t pos = rank;
-        for (uint32_t w = 0; w < wv; ++w) pos += s_wcnt[w][q];
-        const size_t at = (size_t)q * qcap + (size_t)tile * EMURX_QUEUE_TILE + pos;
-        if ((size_t)tile * EMURX_QUEUE_TILE + pos < qcap) qlist[at] = i;
+        for (uint32_t w = 0; w < wv; ++w) pos += L.wcnt[w][q];
+        const size_t at = (size_t)q * a.qcap + (size_t)tile * EMURX_QUEUE_TILE + pos;
+        if ((size_t)tile * EMURX_QUEUE_TILE + pos < a.qcap) a.qlist[at] = i;
     }
-    if (tile_cnt && tid < 16)
-        tile_cnt[(size_t)tile * 16 + tid] = s_wcnt[0][tid] + s_wcnt[1][tid] + s_wcnt[2][tid] + s_wcnt[3][tid];
+    if (a.tile_cnt && tid < 16)
+        a.tile_cnt[(size_t)tile * 16 + tid] = L.wcnt[0][tid] + L.wcnt[1][tid] + L.wcnt[2][tid] + L.wcnt[3][tid];
     // one of EMURX_HIST_SHARDS copies per workgroup: same-address memory-side atomics from
     // every workgroup would serialise; the shards are folded on the host
     if (tid >= 64 && tid < 64 + EMURX_HIST_BINS) {
@@ -278,7 +318,7 @@ __device__ __forceinline__ void rx_tile(const uint8_t* __restrict__ frames,
             by += s_hist[w][b] & ((1u << 23) - 1);
         }
         if (pk) {
-            unsigned long long* hs = hist + (size_t)(tile & (EMURX_HIST_SHARDS - 1)) * 2 * EMURX_HIST_BINS;
+            unsigned long long* hs = a.hist + (size_t)(tile & (EMURX_HIST_SHARDS - 1)) * 2 * EMURX_HIST_BINS;
             atomicAdd(&hs[2 * b], (unsigned long long)pk);
             atomicAdd(&hs[2 * b + 1], (unsigned long long)by);
         }
@@ -295,30 +335,17 @@ __device__ __forceinline__ void rx_tile(const uint8_t* __restrict__ frames,
 #endif
 }
 
-// k_rx's arguments as one struct (a single kernarg block; 91 SGPRs and 76 VGPRs against 106
-// and 79 for the same arguments passed one by one)
-struct RxArgs {
-    const uint8_t* frames;
-    const emurx_desc* desc;
-    uint32_t n;
-    emurx_dev_tables T;
-    emurx_rec* rec;
-    uint32_t* qlist;
-    uint32_t qcap;
-    uint32_t* tile_cnt;
-    unsigned long long* hist;
-    uint32_t* flow;
-    uint32_t* fb;
-    uint32_t gen;
-    emurx_route_args rt;
-};
-
+// One tile per workgroup: stage, wait, process
 template <int kKind, uint32_t kStage>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage == kStageNarrow ? 6 : 5))) void k_rx(const RxArgs a) {
-    rx_tile<kKind, kStage>(a.frames, a.desc, a.n, a.T, a.rec, a.qlist, a.qcap, a.tile_cnt, a.hist, a.flow, a.fb, a.gen, a.rt,
-                           blockIdx.x);
+    __shared__ __attribute__((aligned(16))) uint32_t slab[kWaves * kStage / 4];
+    __shared__ TileLds L;
+    const uint32_t tile = blockIdx.x, wv = threadIdx.x / kWave;
+    const uint2 dd = load_desc(a.desc, a.n, tile * EMURX_QUEUE_TILE + threadIdx.x);
+    const Stage sg = stage_issue<kStage>(a.frames, dd, lane_id(), reinterpret_cast<uint4*>(slab) + wv * (kStage / 16));
+    stage_wait();
+    tile_body<kKind, kStage>(a, tile, dd, sg, slab, L);
 }
-
 
 // table deltas (emurx_api.cpp ship_tables): 4 lanes per 64-byte block, 16 bytes each
 __global__ __launch_bounds__(kBlock) void k_apply(const emurx_delta* __restrict__ d, uint32_t n) {
@@ -347,15 +374,14 @@ int emurx_launch_batch(const uint8_t* frames, const emurx_desc* desc, uint32_t n
     if (ev) (void)hipEventRecord(ev[0], st);
     if (n) {
         const uint32_t ntiles = (n + EMURX_QUEUE_TILE - 1) / EMURX_QUEUE_TILE;
-        const dim3 g(ntiles), b(kBlock);
         unsigned long long* hist = reinterpret_cast<unsigned long long*>(out.hist);
-        auto k = kind == 1 ? (narrow ? k_rx<1, kStageNarrow> : k_rx<1, kStageWide>)
-               : kind == 2 ? (narrow ? k_rx<2, kStageNarrow> : k_rx<2, kStageWide>)
-                           : (narrow ? k_rx<0, kStageNarrow> : k_rx<0, kStageWide>);
         const emurx_route_args none{};
         const RxArgs args{frames, desc, n, T, out.rec, out.qlist, out.qcap, out.tile_cnt, hist, out.flow, fb, gen,
                           rt ? *rt : none};
-        hipLaunchKernelGGL(k, g, b, 0, st, args);
+        auto k = kind == 1 ? (narrow ? k_rx<1, kStageNarrow> : k_rx<1, kStageWide>)
+               : kind == 2 ? (narrow ? k_rx<2, kStageNarrow> : k_rx<2, kStageWide>)
+                           : (narrow ? k_rx<0, kStageNarrow> : k_rx<0, kStageWide>);
+        hipLaunchKernelGGL(k, dim3(ntiles), dim3(kBlock), 0, st, args);
     }
     if (ev) (void)hipEventRecord(ev[1], st);
     return hipGetLastError() == hipSuccess ? 0 : -1;

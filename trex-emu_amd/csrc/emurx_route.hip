@@ -135,11 +135,21 @@ __global__ __launch_bounds__(kBlock) void k_owner_count(const uint8_t* __restric
     uint32_t d = 0xffu;
     if (valid) {
         const uint32_t len = dd.y & 0xffff, vport = (dd.y >> 16) & 0xff;
-        // bytes 12..19 from three aligned dwords (the buffer is readable past every frame)
+        // bytes 12..19 from the three aligned dwords around them, each loaded only when it
+        // holds a byte of the frame (an aligned dword never crosses the 64-byte boundary the
+        // buffer contract guarantees past the last byte, emu_rx.h): one 12-byte load for every
+        // frame of 21 bytes or more; l2_vlans reads a word only where len says its bytes exist
         const uintptr_t a = (uintptr_t)(frames + dd.x + 12);
-        const uint32_t sh = (uint32_t)(a & 3);
-        const uint3 w3 = gld12(reinterpret_cast<const void*>(a & ~(uintptr_t)3));
-        const uint32_t w0 = w3.x, w1 = w3.y, w2 = w3.z;  // one 12-byte load
+        const uint32_t sh = (uint32_t)(a & 3), lim = len + sh;  // dword k holds a frame byte iff 12 + 4k < lim
+        const void* wa = reinterpret_cast<const void*>(a & ~(uintptr_t)3);
+        uint32_t w0 = 0, w1 = 0, w2 = 0;
+        if (lim > 20) {
+            const uint3 w3 = gld12(wa);  // one 12-byte load
+            w0 = w3.x; w1 = w3.y; w2 = w3.z;
+        } else {
+            if (lim > 12) w0 = gld4(wa);
+            if (lim > 16) w1 = gld4(reinterpret_cast<const uint8_t*>(wa) + 4);
+        }
         const uint32_t b12 = __builtin_bswap32(__builtin_amdgcn_alignbyte(w1, w0, sh));
         const uint32_t b16 = __builtin_bswap32(__builtin_amdgcn_alignbyte(w2, w1, sh));
         uint32_t v0, v1;
