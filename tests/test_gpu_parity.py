@@ -873,3 +873,49 @@ def test_reference_simulations(rxmod):
         assert (((rec["flags"] >> 4) & 7) == abi.LK[lk]).all(), capture
         assert (rec["client_id"] == S.expected_clients(fr, cid)).all(), capture
         rx.close()
+
+
+# ---- flow decisions the reference's transport simulations vouch for (tests/transport_sims.py) ----
+def test_transport_reference_sims(rxmod):
+    """Every frame of the 17 tcp / udp captures (IPv4 and IPv6) through the GPU path as its peer's
+    rx frame: records and flow decisions bit-exact with the oracle, and the flow decision equal to
+    the outcome the capture implies -- NEW for the accepted SYN / first datagram, the server's or
+    the client's flow for the frames that a later frame of the receiver shows found it -- before
+    and after the server's flow exists; then NO_SYN / NO_SERVER with the flow / listener removed."""
+    import pyoracle
+    import transport_sims as T
+    from test_reference_transport_sims import OUT, corpus
+    z = corpus()
+    for capture in T.CAPTURES:
+        fr = T.frames(z, capture)
+        proto, ckey, skey, accept, exp = T.plan(capture, fr)
+        buf, desc = F.pack_frames(fr, [1] * len(fr))
+        rx = rxmod(0, max_ns=16, max_clients=16, max_frames=1024)
+        rx.register_all()
+        o = pyoracle.Oracle()
+        for t in (rx, o):
+            T.load(t, proto, ckey, abi.PLUG_ALL)
+
+        def both():
+            rec, _, _, _, flow = run_dev(rx, buf, desc, flows=True)
+            orec, _, _, _ = o.rx_batch(buf, desc)
+            assert rec.tobytes() == orec.tobytes(), (capture, rec_diff(rec, orec))
+            assert np.array_equal(flow, o.flows(buf, desc, orec)), capture
+            return flow
+        flow = both()
+        for i, _, k, s in exp:
+            if s == "before":
+                assert flow[i] == OUT[k], (capture, i, k, hex(int(flow[i])))
+        for t in (rx, o):
+            assert t.flow_add(T.SERVER["cid"], skey, T.SERVER_FLOW) == 0
+        flow = both()
+        for i, _, k, s in exp:
+            if s == "after":
+                assert flow[i] == OUT[k], (capture, i, k, hex(int(flow[i])))
+        for t in (rx, o):
+            assert t.server_remove(T.SERVER["cid"], T.PORT, proto) == 0 and t.flow_remove(T.SERVER["cid"], skey) == 0
+        flow = both()
+        assert flow[accept] == abi.FLOW_NO_SERVER
+        if proto == 6:
+            assert any(flow[i] == abi.FLOW_NO_SYN for i, f in enumerate(fr) if T.to_server(f) and not T.is_syn(f))
+        rx.close()
