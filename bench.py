@@ -63,6 +63,8 @@ def parse_args():
                          "(default for D: partitioned, with the replicated alternative measured too)")
     ap.add_argument("--table-updates", action="store_true",
                     help="also time batches with 1 / 64 / 4096 table mutations between them")
+    ap.add_argument("--exchange-frames", type=int, default=1 << 21,
+                    help="N > 1: frames per GPU of the config-D Namespace-exchange measurement beside the headline")
     ap.add_argument("--no-exchange-run", action="store_true",
                     help="at N > 1, skip the extra config-D Namespace-exchange measurement")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -85,6 +87,8 @@ def parse_args():
                          "k mod this, each slot its own frames, descriptors and outputs; the default 8 keeps "
                          "every byte's reuse distance above the 256 MiB Infinity Cache: the frames come from "
                          "HBM, as fresh batches do in production); 1 = the round-2 replay of one batch")
+    ap.add_argument("--no-replay", action="store_true",
+                    help="skip the cache-resident replay figure (profiling runs: every launch then reads HBM)")
     ap.add_argument("--warmup-seconds", type=float, default=0.3,
                     help="keep launching warmup steps until this much wall time has passed (clocks settle)")
     ap.add_argument("--no-overlap", action="store_true",
@@ -253,7 +257,8 @@ def main():
         try:
             rx.close()
             # the headline's steps and warmup: a first-class measurement, not a side sample
-            xo, rx, _ = measure(a, "D", 1 << 21, "partitioned", a.steps, a.warmup, rank, world, local, dist, torch)
+            xo, rx, _ = measure(a, "D", a.exchange_frames, "partitioned", a.steps, a.warmup, rank, world, local, dist,
+                                torch)
             out["namespace_exchange"] = {k: xo[k] for k in ("value", "unit", "ms_per_step", "steps", "config",
                                                               "exchange")}
             out["namespace_exchange"]["k_rx_ms_mean"] = xo["roofline"]["kernel_ms_mean"]
@@ -488,6 +493,54 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             ev[1].record(stream)
             xch["ev"].append(ev)
 
+    def phase_breakdown(reps=None):
+        """Device time per phase of the exchange step, each phase bracketed by HIP events on the
+        launch stream, over `reps` steps run one after the other (no overlap): the source side
+        (owner counts + group scan + k_rx packing the lookup records, or k_rx + scan + route
+        packing), k_rx alone (the library's events around its launch), the all-to-all (counts +
+        regions; RCCL's stream joined back into the launch stream), the owner's k_lookup; and
+        the bytes that crossed to other ranks (whole regions: the all-to-all is equal-split)."""
+        reps = reps or max(4, min(steps, 30))
+        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(reps)]
+        rx.set_timing(reps + 8, 1)
+        b = xch["sets"][0]
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        for k in range(reps):
+            e = ev[k]
+            e[0].record(stream)
+            produce(b, k)
+            e[1].record(stream)
+            if world > 1:
+                recv, rc = X.exchange(b["send"], b["send_count"], xch["cap"], rec_bytes=rb)
+            else:
+                recv, rc = b["send"], b["send_count"]
+            e[2].record(stream)
+            if mode == "partitioned":
+                rx.lookup_dev(recv, rc, world, xch["cap"], b["out"], stream=stream)
+            e[3].record(stream)
+        torch.cuda.synchronize()
+        krx = rx.kernel_times()
+        rx.set_timing(0)
+        ms = np.array([[e[j].elapsed_time(e[j + 1]) for j in range(3)] for e in ev[1:]])  # the first: warm
+        src, a2a, look = (float(np.mean(ms[:, j])) for j in range(3))
+        k_rx_ms = float(np.mean(krx[1:])) if len(krx) > 1 else float("nan")
+        sc = b["send_count"].cpu().numpy().astype(np.int64)
+        others = [d for d in range(world) if d != rank]
+        moved = len(others) * xch["cap"] * rb + 4 * len(others)
+        payload = int(sum(int(sc[d]) for d in others)) * rb
+        out = {"steps": reps - 1, "source_side_ms": round(src, 5), "k_rx_ms": round(k_rx_ms, 5),
+               ("owner_count_scan_ms" if mode == "partitioned" else "scan_pack_ms"): round(src - k_rx_ms, 5),
+               "all_to_all_ms": round(a2a, 5), "owner_lookup_ms": round(look, 5) if mode == "partitioned" else 0.0,
+               "record_bytes": rb, "bytes_to_other_ranks": moved, "payload_bytes_to_other_ranks": payload,
+               "source": "HIP events on the launch stream between the phases of non-overlapped steps; k_rx by the "
+                         "library's events around its launch"}
+        if world > 1 and a2a > 0:
+            out["xgmi_gbs"] = round(moved / (a2a * 1e-3) / 1e9, 2)
+            out["xgmi_payload_gbs"] = round(payload / (a2a * 1e-3) / 1e9, 2)
+        return out
+
     def warm_for_time():
         """Warmup floor in wall time (--warmup-seconds): a short --warmup would otherwise time
         the first launches at unsettled clocks.  Every rank runs the same number of rounds."""
@@ -562,7 +615,7 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         reg_ev[1].record(stream)
         torch.cuda.synchronize()
         one = reg_ev[0].elapsed_time(reg_ev[1]) / steps
-        if R > S:
+        if R > S and not a.no_replay:
             # the round-2 replay: each stream re-reads one batch, which stays in the Infinity Cache
             region_open()
             for k in range(steps):
@@ -604,6 +657,9 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
                                for b in xch["sets"]):
         raise RuntimeError("exchange region overflow in the timed region")
 
+    phases = None
+    if xch is not None:
+        phases = phase_breakdown()
     pipelined = None
     if xch is not None and world == 1 and a.streams > 1:
         pipelined = pipelined_rate()
@@ -617,9 +673,9 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
 
     # roofline of the dominant kernel (k_rx): algorithmic bytes / its mean launch duration.
     # Per frame: the frame, its 8-B descriptor and the 32-B record (104 B for a
-    # 64-B frame), plus the 4-B queue entry k_rx also writes (the 80-B lookup record instead of
+    # 64-B frame), plus the 4-B queue entry k_rx also writes (the 64-B lookup record instead of
     # the record in the partitioned mode's k_rx)
-    per_frame = 8 + 4 + (80 if mode == "partitioned" else 32)
+    per_frame = 8 + 4 + (64 if mode == "partitioned" else 32)
     alg_bytes = w["nbytes"] + per_frame * n
     parse_s = float(np.mean(pk)) * 1e-3 if len(pk) else float("nan")
     achieved = alg_bytes / parse_s / 1e9
@@ -686,7 +742,7 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             "alg_bytes_per_launch": alg_bytes,
             "alg_bytes_per_frame": round(alg_bytes / n, 2),
             "alg_bytes_note": "frame + 8-B descriptor + 32-B record (SURVEY.md §8d) + the 4-B queue entry k_rx also "
-                              "writes" + ("; the 80-B lookup record instead of the record" if mode == "partitioned" else ""),
+                              "writes" + ("; the 64-B lookup record instead of the record" if mode == "partitioned" else ""),
             "table_probe_bytes_per_launch": probed * 128 if mode != "partitioned" else 0,
             "kernel_ms_mean": round(parse_s * 1e3, 5),
             "kernel_launches_timed": steps if region else int(len(pk)),
@@ -726,6 +782,7 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             "overlapped": overlapped,  # batch k's all-to-all beside batch k+1's parse (two buffer sets)
             "includes": ("k_rx + group scan + pack" + (" + all-to-all" if world > 1 else "") +
                          (" + owner lookups (k_lookup)" if mode == "partitioned" else "")),
+            "phases": phases,
         }
         if pipelined is not None:
             # N = 1: the line's value is the pipelined rate, as for the one-launch steps of

@@ -565,18 +565,19 @@ int emurx_classify_route_dev(emurx_t* h, const uint8_t* d_frames, const emurx_de
 /* ---- owner-partitioned classification ---------------------------------
    With partitioned tables (emurx_set_partition) the lookups run on the GPU that owns the
    frame's Namespace.  The receiving GPU parses its shard and derives each frame's lookup key
-   (emurx_parse_route_dev); every frame travels, as an 80-byte emurx_lookup_rec, to the owner
+   (emurx_parse_route_dev); every frame travels, as a 64-byte emurx_lookup_rec, to the owner
    of its CTunnelKey (an equal-split all-to-all, as for emurx_route_rec); the owner resolves
    Namespace, Client and flow against its partition for the frames that reached a callback
    (emurx_lookup_dev) and keeps the records of the others as parsed.  The owner's output for a
    frame equals emurx_classify_dev's record for it on replicated tables, bit for bit. */
 typedef struct emurx_lookup_rec {
-    emurx_rec rec;     /* the parsed record, with ns_id = source frame index and
-                          client_id = source rank (the lookups fill them at the owner)    */
-    uint32_t key[12];  /* the callback rule's key: destination MAC, client key (MAC / IPv4 /
-                          IPv6 / EUI-64 / chaddr / first client), or for tcp/udp the
-                          c5tuplekey + TCP flags of the flow decision (emurx_parse.h)     */
-} emurx_lookup_rec;    /* 80 bytes */
+    uint32_t frame;    /* source frame index (the source rank is the region it arrives in)  */
+    uint32_t w[7];     /* the parse packed: CTunnelKey VLAN words (14-bit codes), vport, l3,
+                          next header, l4, l7, l7_len, proto, status, RTALERT; the key kind;
+                          the destination MAC, TCP flags and the ports (emurx_parse.h)      */
+    uint32_t key[8];   /* the callback rule's key: client key (MAC / IPv4 / IPv6 / EUI-64 /
+                          chaddr) or, for tcp/udp, the c5tuplekey's addresses              */
+} emurx_lookup_rec;    /* 64 bytes */
 /* Parse the batch (records without lookups into out->rec when non-NULL, queues, histogram as
    emurx_parse_dev) and pack the lookup record of every frame (holes excepted) into the region
    of its Namespace's owner: d_send[d * cap ..  + d_send_count[d]), frame order.  Three

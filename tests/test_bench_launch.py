@@ -37,3 +37,27 @@ def test_spawned_ranks_gloo(n):
 def test_failed_rank_ends_the_run():
     p = run(["--gpus", "2", "--backend", "gloo", "--launch-check"], env={"EMURX_BENCH_FAIL_RANK": "1"})
     assert p.returncode == 3, (p.returncode, p.stderr[-2000:])
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_two_rank_exchange_fields(gpu_ok):
+    """The bench's N = 2 line over gloo (both ranks on the one GPU): the config-B headline plus the
+    Namespace-partitioned exchange timed with the headline's steps and warmup, its per-phase
+    device times and the bytes that crossed to the other rank."""
+    p = run(["--gpus", "2", "--backend", "gloo", "--frames", "65536", "--exchange-frames", "65536",
+             "--steps", "6", "--warmup", "2", "--batches", "2", "--warmup-seconds", "0.05"], timeout=580)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    j = json.loads(lines[0])
+    assert j["n_gpus"] == 2 and j["value"] > 0
+    x = j["namespace_exchange"]
+    assert "error" not in x, x
+    assert x["steps"] == 6  # the headline's steps, not a side sample
+    ph = x["exchange"]["phases"]
+    for k in ("source_side_ms", "k_rx_ms", "owner_count_scan_ms", "all_to_all_ms", "owner_lookup_ms"):
+        assert ph[k] > 0, (k, ph)
+    assert ph["record_bytes"] == 64
+    assert ph["bytes_to_other_ranks"] > ph["payload_bytes_to_other_ranks"] > 0
+    assert ph["xgmi_gbs"] > 0

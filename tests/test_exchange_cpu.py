@@ -91,24 +91,24 @@ def test_exchange_gloo_world2(oracle_built, tmp_path):
 
 
 def lookup_regions(rec, world, rank):
-    """Host stand-in for emurx_parse_route_dev's send regions: every frame's lookup record
-    (the parsed record with ns_id = frame index, client_id = rank; key words = a function of
-    the frame) in the region of the owner of its CTunnelKey, frame order."""
+    """Host stand-in for emurx_parse_route_dev's send regions: every frame's 64-byte lookup record
+    (the frame index; the other words a function of frame and rank) in the region of the owner
+    of its CTunnelKey, frame order."""
     from test_gpu_tables import _owners_by_key
     own = _owners_by_key(rec, world)
     out = []
     for d in range(world):
         idx = np.nonzero(own == d)[0]
         lk = np.zeros(len(idx), abi.LOOKUP_REC_DTYPE)
-        lk["rec"] = rec[idx]
-        lk["rec"]["ns_id"], lk["rec"]["client_id"] = idx, rank
-        lk["key"] = (idx[:, None] * 12 + np.arange(12)[None, :]).astype(np.uint32)
+        lk["frame"] = idx
+        lk["vlans"], lk["w2"] = rec["vlan0"][idx] & 0xfff, rec["vport"][idx].astype(np.uint32) | (rank << 24)
+        lk["key"] = (idx[:, None] * 8 + np.arange(8)[None, :]).astype(np.uint32)
         out.append(lk)
     return out
 
 
 def _worker_partitioned(rank, world, port, out_dir):
-    """The partitioned protocol over gloo: 80-byte lookup records to the Namespace owners,
+    """The partitioned protocol over gloo: 64-byte lookup records to the Namespace owners,
     and this rank's device-table bytes (host-only handle, emurx_set_partition) ~ 1/world."""
     sys.path[:0] = [str(ROOT / "tests"), str(ROOT / "trex-emu_amd"), str(ROOT / "oracle")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))

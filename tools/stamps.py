@@ -1,7 +1,10 @@
 """Timeline of one k_rx launch from the stamp build variant (experiment-only).
 
     tools/build_variant.sh stamp "-DEMURX_STAMP=1"
-    EMURX_LIB=trex-emu_amd/lib/libemurx_stamp.so python tools/stamps.py [B C E ...]
+    EMURX_LIB=trex-emu_amd/lib/libemurx_stamp.so python tools/stamps.py [--replay] [B C E ...]
+
+By default the launches rotate over 8 distinct batches (bench.py's batch slots: the input comes
+from HBM); --replay stamps launches that re-read one batch (Infinity-Cache resident).
 
 Every wave stores shader-clock stamps {entry, descriptors read, staging landed, parsed, lookup
 key made, tables resolved, histogram, tile barrier entered / left, exit} plus HW_ID / XCC_ID (emurx_kernels.hip,
@@ -21,7 +24,7 @@ sys.path.insert(0, str(ROOT / "trex-emu_amd"))
 sys.path.insert(0, str(ROOT))
 
 
-def run(cfg, n):
+def run(cfg, n, replay=False):
     import torch
     import bench
     from emurx import abi
@@ -42,7 +45,14 @@ def run(cfg, n):
     hist = torch.zeros(abi.HIST_SHARDS * 2 * abi.HIST_BINS, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
     rx.sync(stream.cuda_stream)
-    classify = rx.classify_call(buf, desc, n, rec, qlist, qcap, tile_cnt, hist, stream=stream)
+    slots = [(buf, desc)] + ([] if replay else
+                             [bench.permuted_batch(torch, buf, w["desc"], 1000 + j, dev) for j in range(1, 8)])
+    calls = [rx.classify_call(b, d, n, rec, qlist, qcap, tile_cnt, hist, stream=stream) for b, d in slots]
+    k = [0]
+
+    def classify():
+        calls[k[0] % len(calls)]()
+        k[0] += 1
     lib = abi.load()
     lib.emurx_debug_set_stamps.argtypes = [ctypes.c_void_p]
     st = torch.zeros(nt * 4 * 16, dtype=torch.int64, device=dev)
@@ -101,10 +111,12 @@ def report(cfg, s):
 
 
 def main():
-    cfgs = sys.argv[1:] or ["B"]
+    replay = "--replay" in sys.argv
+    cfgs = [a for a in sys.argv[1:] if not a.startswith("--")] or ["B"]
     sizes = {"B": 1 << 20, "C": 1 << 20, "E": 1 << 20, "D": 1 << 21}
     for c in cfgs:
-        outs = run(c, sizes[c])
+        outs = run(c, sizes[c], replay)
+        print("input:", "one batch replayed (Infinity Cache)" if replay else "8 rotating batches (HBM)")
         report(c, outs[-1])
 
 

@@ -15,7 +15,7 @@
 // rt (optional): kind 1: the route count pass fused in (per-(tile, owner) counts into cnt,
 // per-group sums added into grp, as emurx_launch_route's first pass); kind 2 (required): the
 // owner counts cnt / group offsets goff of k_owner_count + k_route_scan, and every frame's
-// emurx_lookup_rec (ns_id = frame index, client_id = rank) packed into send[owner * cap + ..).
+// 64-byte emurx_lookup_rec (emurx_parse.h pack_lookup) packed into send[owner * cap + ..).
 struct emurx_route_args {
     uint32_t parts, rank, cap;
     uint32_t* cnt;

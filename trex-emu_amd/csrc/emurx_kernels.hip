@@ -131,7 +131,7 @@ struct TileLds {
 // workgroup's kWaves slabs of kStage bytes): parse, classify, record, queue segment, counts.
 template <int kKind, uint32_t kStage>
 __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 dd, Stage sg, const uint32_t* slab,
-                                          TileLds& L) {
+                                          TileLds& L, const unsigned long long* pre = nullptr) {
     constexpr bool kClassify = kKind == 1;
     constexpr uint32_t kWinVec = kStage / 16 / kWave;
     const emurx_dev_tables& T = a.T;
@@ -145,11 +145,9 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
 
     const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / kWave;
 #if EMURX_STAMP
-    unsigned long long st_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    // entry, descriptors, staging landed: taken by the caller
+    unsigned long long st_[10] = {pre ? pre[0] : 0, pre ? pre[1] : 0, pre ? pre[2] : 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
-    STAMP(0);
-    STAMP(1);
-    STAMP(2);
     const uint32_t i = tile * EMURX_QUEUE_TILE + tid;
     if (lane < 16) L.wcnt[wv][lane] = 0;
     if (lane < EMURX_MAX_PARTS) L.rcnt[wv][lane] = 0;
@@ -167,7 +165,11 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
 
     Rec r;
     r.dlen = 0;
-    uint32_t kwd[12];  // kKind 2: the lookup key words of the frame
+    // kKind 2: the frame's 64-byte lookup record (emurx_parse.h pack_lookup), parked in the
+    // wave's slab (64 lanes x 64 B = 4 KiB) from the end of the parse until the owner offsets are
+    // known after the tile barrier: no registers held across it
+    uint4* lrec = reinterpret_cast<uint4*>(const_cast<uint32_t*>(slab)) + wv * (kStage / 16) + lane * 4;
+    static_assert(kStage >= kWave * 64, "a wave's lookup records fit its slab");
     if (sg.staged) {  // wave-uniform branch
         if (valid) {
             LdsSrc s{reinterpret_cast<const uint8_t*>(slab), slab, wv * kStage + (off - sg.start)};
@@ -183,7 +185,7 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
 #else
             if (kClassify) classify(s, len, T, r);
 #endif
-            if (kKind == 2 && r.status == EMURX_ST_OK) pack_key(s, len, r, make_key(s, len, r), kwd);
+            if (kKind == 2) pack_lookup(s, len, r, i, r.status == EMURX_ST_OK, lrec);
         }
     } else {
         const uint32_t head = (uint32_t)((uintptr_t)(a.frames + off) & 15);
@@ -202,7 +204,7 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
 #else
         if (valid && kClassify) classify(s, len, T, r);
 #endif
-        if (kKind == 2 && valid && r.status == EMURX_ST_OK) pack_key(s, len, r, make_key(s, len, r), kwd);
+        if (kKind == 2 && valid) pack_lookup(s, len, r, i, r.status == EMURX_ST_OK, lrec);
     }
     typedef unsigned v4u __attribute__((ext_vector_type(4)));
     if (a.rec && i < n) {
@@ -283,18 +285,15 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
         rt.cnt[(size_t)tile * 16 + tid] = c;
         if (c) atomicAdd(&rt.grp[(tile / 64) * 16 + tid], c);
     }
-    if (kKind == 2 && rd != 0xffu) {  // the lookup record: ns_id = frame index, client_id = source rank
+    if (kKind == 2 && rd != 0xffu) {  // the frame's 64-byte lookup record into its owner's region
         uint32_t pos = L.toff[rd] + rrank;
         for (uint32_t w = 0; w < wv; ++w) pos += L.rcnt[w][rd];
         if (pos < rt.cap) {  // overflow: send_count[d] > cap tells the caller
-            const bool ok = r.status == EMURX_ST_OK;
-            v4u* o = reinterpret_cast<v4u*>(rt.send + (size_t)rd * rt.cap + pos);
-            o[0] = v4u{i, rt.rank, r.vlan0, r.vlan1};
-            o[1] = v4u{r.vport | (r.l3 << 16), r.l4 | (r.l7 << 16), r.l7len | (r.nh << 16) | (r.proto << 24),
-                       r.status | (r.flags << 8)};
-            o[2] = ok ? v4u{kwd[0], kwd[1], kwd[2], kwd[3]} : v4u{0, 0, 0, 0};
-            o[3] = ok ? v4u{kwd[4], kwd[5], kwd[6], kwd[7]} : v4u{0, 0, 0, 0};
-            o[4] = ok ? v4u{kwd[8], kwd[9], kwd[10], kwd[11]} : v4u{0, 0, 0, 0};
+            uint4* o = reinterpret_cast<uint4*>(rt.send + (size_t)rd * rt.cap + pos);
+            o[0] = lrec[0];
+            o[1] = lrec[1];
+            o[2] = lrec[2];
+            o[3] = lrec[3];
         }
     }
 
@@ -341,10 +340,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
     __shared__ __attribute__((aligned(16))) uint32_t slab[kWaves * kStage / 4];
     __shared__ TileLds L;
     const uint32_t tile = blockIdx.x, wv = threadIdx.x / kWave;
+#if EMURX_STAMP
+    unsigned long long pre[3];
+    pre[0] = __builtin_amdgcn_s_memtime();
+#endif
     const uint2 dd = load_desc(a.desc, a.n, tile * EMURX_QUEUE_TILE + threadIdx.x);
+#if EMURX_STAMP
+    wait_vm0();
+    pre[1] = __builtin_amdgcn_s_memtime();
+#endif
     const Stage sg = stage_issue<kStage>(a.frames, dd, lane_id(), reinterpret_cast<uint4*>(slab) + wv * (kStage / 16));
     stage_wait();
+#if EMURX_STAMP
+    pre[2] = __builtin_amdgcn_s_memtime();
+    tile_body<kKind, kStage>(a, tile, dd, sg, slab, L, pre);
+#else
     tile_body<kKind, kStage>(a, tile, dd, sg, slab, L);
+#endif
 }
 
 // table deltas (emurx_api.cpp ship_tables): 4 lanes per 64-byte block, 16 bytes each

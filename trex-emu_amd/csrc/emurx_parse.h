@@ -1234,51 +1234,103 @@ __device__ __forceinline__ void classify(const S& s, uint32_t len, const emurx_d
     resolve(T, r, k, [&](uint32_t cid) { return flow_probe(T, get_tuple(s, len, r), cid); });
 }
 
-// ---- partitioned path: the lookup record (include/emu_rx.h emurx_lookup_rec) -------------
-// words 0..7: the parsed record with ns_id = source frame index, client_id = source rank;
-// key[12]: {dlo, dhi | key << 16 | mc6 << 20 | v6 << 21, kw[4] or the flow tuple ...}
-//   tcp / udp (MAC[dst] rule): the MAC key is dlo / dhi and key[2..11] carry the c5tuplekey:
-//     IPv4 {src, dst, ports, proto | flags << 8, 0 ...}; IPv6 {src[4], dst[4], ports, nh | flags << 8}
-//   other callbacks: key[2..5] = kw[0..3]
+// ---- partitioned path: the lookup record (include/emu_rx.h emurx_lookup_rec, 64 bytes) ---
+// Everything the owner needs to finish the frame, in 16 words:
+//   w0  source frame index (the source rank is the region the record arrives in)
+//   w1  the CTunnelKey VLAN words, 14 bits each (vlan_code): TPID 0x8100 / 0x88A8 / none + VID
+//   w2  vport | l3 << 8 | next_hdr << 24          w3  l4 | l7 << 16
+//   w4  l7_len | proto << 16 (4 bits, 15 = none) | status << 20 (5 bits) | RTALERT << 25 |
+//       v6 << 26 | mc6 << 27 | key << 28 (3 bits)  (the parse's own flags bit is RTALERT alone)
+//   w5  destination MAC bytes 0..3                w6  bytes 4..5 | TCP flags << 16
+//   w7  tcp / udp: the ports as on the wire (c5tuplekey bytes 8..11 order)
+//   w8..w15  tcp / udp over IPv4: src, dst; over IPv6: src[4], dst[4] (the c5tuplekey; its
+//       protocol byte is next_hdr); other callbacks: kw[0..3] of the rule's key (MAC / IPv4 /
+//       IPv6 / EUI-64 / chaddr) in w8..w11
 __device__ __forceinline__ bool lk_transport(uint32_t cb) { return cb == EMURX_CB_TCP || cb == EMURX_CB_UDP; }
-template <class S>
-__device__ __forceinline__ void pack_key(const S& s, uint32_t len, const Rec& r, const LKey& k, uint32_t w[12]) {
-    const bool tr = lk_transport(r.proto) && k.key == kMac;
-    Tuple t{};
-    if (tr) t = get_tuple(s, len, r);
-    w[0] = k.dlo;
-    w[1] = k.dhi | (k.key << 16) | (k.mc6 << 20) | (t.v6 << 21);
-    if (!tr) {
-        w[2] = k.kw[0]; w[3] = k.kw[1]; w[4] = k.kw[2]; w[5] = k.kw[3];
-        w[6] = w[7] = w[8] = w[9] = w[10] = w[11] = 0;
-    } else if (!t.v6) {
-        w[2] = t.a[0]; w[3] = t.d[0]; w[4] = t.ports; w[5] = t.proto | (t.flags << 8);
-        w[6] = w[7] = w[8] = w[9] = w[10] = w[11] = 0;
-    } else {
-        w[2] = t.a[0]; w[3] = t.a[1]; w[4] = t.a[2]; w[5] = t.a[3];
-        w[6] = t.d[0]; w[7] = t.d[1]; w[8] = t.d[2]; w[9] = t.d[3];
-        w[10] = t.ports; w[11] = t.proto | (t.flags << 8);
-    }
+// a CTunnelKey VLAN word (TPID << 16 | VID, parser.go:810) in 14 bits: ParsePacket only takes
+// tags with TPID 0x8100 or 0x88A8, and an untagged slot is 0
+__device__ __forceinline__ uint32_t vlan_code(uint32_t v) {
+    return v == 0 ? 0u : ((((v >> 16) == 0x8100u) ? 1u : 2u) << 12) | (v & 0xfffu);
 }
-__device__ __forceinline__ LKey unpack_key(const Rec& r, const uint32_t w[12], Tuple& t) {
-    LKey k;
-    k.dlo = w[0];
-    k.dhi = w[1] & 0xffffu;
-    k.key = (w[1] >> 16) & 0xf;
-    k.mc6 = (w[1] >> 20) & 1;
-    const bool tr = lk_transport(r.proto) && k.key == kMac;
-    t = Tuple{};
+__device__ __forceinline__ uint32_t vlan_word(uint32_t c) {
+    const uint32_t t = (c >> 12) & 3u;
+    return t == 0 ? 0u : ((t == 1 ? 0x8100u : 0x88A8u) << 16) | (c & 0xfffu);
+}
+// the record of a frame; `ok`: it reached a callback (the key words are zero otherwise).
+// Written as four 16-byte stores to dst (LDS: the wave's slab, once the parse is done with it)
+template <class S>
+__device__ __forceinline__ void pack_lookup(const S& s, uint32_t len, const Rec& r, uint32_t frame, bool ok,
+                                            uint4* dst) {
+    uint32_t w[16];
+    LKey k{};
+    Tuple t{};
+    bool tr = false;
+    if (ok) {
+        k = make_key(s, len, r);
+        tr = lk_transport(r.proto) && k.key == kMac;
+        if (tr) t = get_tuple(s, len, r);
+    }
+    w[0] = frame;
+    w[1] = vlan_code(r.vlan0) | (vlan_code(r.vlan1) << 14);
+    w[2] = r.vport | (r.l3 << 8) | (r.nh << 24);
+    w[3] = r.l4 | (r.l7 << 16);
+    w[4] = r.l7len | (min(r.proto, 15u) << 16) | (r.status << 20) | ((r.flags & EMURX_FLAG_RTALERT) << 25) |
+           (t.v6 << 26) | (k.mc6 << 27) | (k.key << 28);
+    w[5] = k.dlo;
+    w[6] = k.dhi | (t.flags << 16);
+    w[7] = t.ports;
     if (!tr) {
-        k.kw[0] = w[2]; k.kw[1] = w[3]; k.kw[2] = w[4]; k.kw[3] = w[5];
+        w[8] = k.kw[0]; w[9] = k.kw[1]; w[10] = k.kw[2]; w[11] = k.kw[3];
+        w[12] = w[13] = w[14] = w[15] = 0;
+    } else if (!t.v6) {
+        w[8] = t.a[0]; w[9] = t.d[0];
+        w[10] = w[11] = w[12] = w[13] = w[14] = w[15] = 0;
+    } else {
+        w[8] = t.a[0]; w[9] = t.a[1]; w[10] = t.a[2]; w[11] = t.a[3];
+        w[12] = t.d[0]; w[13] = t.d[1]; w[14] = t.d[2]; w[15] = t.d[3];
+    }
+    dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    dst[2] = make_uint4(w[8], w[9], w[10], w[11]);
+    dst[3] = make_uint4(w[12], w[13], w[14], w[15]);
+}
+// the owner's view: the parsed record (ns / client unset), the lookup key and the flow tuple
+__device__ __forceinline__ LKey unpack_lookup(const uint32_t w[16], Rec& r, Tuple& t) {
+    r.ns = EMURX_ID_NONE;
+    r.cl = EMURX_ID_NONE;
+    r.vlan0 = vlan_word(w[1] & 0x3fffu);
+    r.vlan1 = vlan_word((w[1] >> 14) & 0x3fffu);
+    r.vport = w[2] & 0xffu;
+    r.l3 = (w[2] >> 8) & 0xffffu;
+    r.nh = w[2] >> 24;
+    r.l4 = w[3] & 0xffffu;
+    r.l7 = w[3] >> 16;
+    r.l7len = w[4] & 0xffffu;
+    const uint32_t p4 = (w[4] >> 16) & 15u;
+    r.proto = p4 == 15u ? (uint32_t)EMURX_CB_NONE : p4;
+    r.status = (w[4] >> 20) & 31u;
+    r.flags = (w[4] >> 25) & 1u;
+    r.dlen = 0;
+    r.flow = EMURX_FLOW_NONE;
+    LKey k;
+    k.dlo = w[5];
+    k.dhi = w[6] & 0xffffu;
+    k.key = (w[4] >> 28) & 7u;
+    k.mc6 = (w[4] >> 27) & 1u;
+    t = Tuple{};
+    if (!(lk_transport(r.proto) && k.key == kMac)) {
+        k.kw[0] = w[8]; k.kw[1] = w[9]; k.kw[2] = w[10]; k.kw[3] = w[11];
     } else {
         k.kw[0] = k.dlo; k.kw[1] = k.dhi; k.kw[2] = 0; k.kw[3] = 0;
-        t.v6 = (w[1] >> 21) & 1;
+        t.v6 = (w[4] >> 26) & 1u;
+        t.ports = w[7];
+        t.flags = (w[6] >> 16) & 0xffu;
+        t.proto = r.nh;  // IPv4: the header's protocol field; IPv6: ParserPacketState.NextHeader
         if (!t.v6) {
-            t.a[0] = w[2]; t.d[0] = w[3]; t.ports = w[4]; t.proto = w[5] & 0xff; t.flags = (w[5] >> 8) & 0xff;
+            t.a[0] = w[8]; t.d[0] = w[9];
         } else {
-            t.a[0] = w[2]; t.a[1] = w[3]; t.a[2] = w[4]; t.a[3] = w[5];
-            t.d[0] = w[6]; t.d[1] = w[7]; t.d[2] = w[8]; t.d[3] = w[9];
-            t.ports = w[10]; t.proto = w[11] & 0xff; t.flags = (w[11] >> 8) & 0xff;
+            t.a[0] = w[8]; t.a[1] = w[9]; t.a[2] = w[10]; t.a[3] = w[11];
+            t.d[0] = w[12]; t.d[1] = w[13]; t.d[2] = w[14]; t.d[3] = w[15];
         }
     }
     return k;

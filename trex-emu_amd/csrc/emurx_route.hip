@@ -183,18 +183,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EMURX_LO
                                                    const uint32_t* __restrict__ recv_count, uint32_t n_parts,
                                                    uint32_t cap, emurx_dev_tables T,
                                                    emurx_route_rec* __restrict__ out, uint32_t* __restrict__ flow) {
-    // the wave's 64 records are contiguous: 5 KiB copied into LDS by five fully coalesced
-    // LDS-DMA loads (a lane-strided 80-byte read would touch 40 lines per instruction)
-    __shared__ __attribute__((aligned(16))) uint4 s_rec[kWaves][kWave * 5];
+    // the wave's 64 records are contiguous: 4 KiB copied into LDS by four fully coalesced
+    // LDS-DMA loads (a lane-strided 64-byte read would touch 32 lines per instruction)
+    __shared__ __attribute__((aligned(16))) uint4 s_rec[kWaves][kWave * 4];
     const uint32_t lane = threadIdx.x % kWave, wv = threadIdx.x / kWave;
     const uint32_t src = blockIdx.y, idx0 = blockIdx.x * kBlock + wv * kWave, idx = idx0 + lane;
     const uint32_t cnt = min(recv_count[src], cap);
     if (idx0 >= cnt) return;  // wave-uniform
     const uint64_t j = (uint64_t)src * cap + idx;
     const uint4* base = reinterpret_cast<const uint4*>(recv + (uint64_t)src * cap + idx0);
-    const uint32_t nvec = min(kWave, cnt - idx0) * 5;  // never past the region's valid records
+    const uint32_t nvec = min(kWave, cnt - idx0) * 4;  // never past the region's valid records
 #pragma unroll
-    for (uint32_t k = 0; k < 5; ++k)
+    for (uint32_t k = 0; k < 4; ++k)
         if (k * kWave + lane < nvec)
             __builtin_amdgcn_global_load_lds(base + k * kWave + lane,
                                              (__attribute__((address_space(3))) void*)&s_rec[wv][k * kWave], 16, 0, 0);
@@ -203,35 +203,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EMURX_LO
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (idx >= cnt) return;
-    const uint4* p = &s_rec[wv][lane * 5];
-    const uint4 a = p[0], b = p[1], k0 = p[2], k1 = p[3], k2 = p[4];
+    const uint4* p = &s_rec[wv][lane * 4];
+    const uint4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+    const uint32_t w[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                            q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
     Rec r;
-    r.ns = EMURX_ID_NONE;
-    r.cl = EMURX_ID_NONE;
-    r.vlan0 = a.z;
-    r.vlan1 = a.w;
-    r.vport = b.x & 0xffffu;
-    r.l3 = b.x >> 16;
-    r.l4 = b.y & 0xffffu;
-    r.l7 = b.y >> 16;
-    r.l7len = b.z & 0xffffu;
-    r.nh = (b.z >> 16) & 0xffu;
-    r.proto = b.z >> 24;
-    r.status = b.w & 0xffu;
-    r.flags = (b.w >> 8) & 0xffu;
-    r.dlen = 0;
-    r.flow = EMURX_FLOW_NONE;
-    const uint32_t w[12] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w, k2.x, k2.y, k2.z, k2.w};
     Tuple t;
-    const LKey k = unpack_key(r, w, t);
+    const LKey k = unpack_lookup(w, r, t);
     // frames that reached no callback travel too (their owner keeps their record): no lookup
     if (r.status == EMURX_ST_OK) resolve(T, r, k, [&](uint32_t cid) { return flow_probe(T, t, cid); });
     uint2* o = reinterpret_cast<uint2*>(out + j);  // 40 B, 8-B aligned
     o[0] = make_uint2(r.ns, r.cl);
     o[1] = make_uint2(r.vlan0, r.vlan1);
-    o[2] = make_uint2(b.x, b.y);
-    o[3] = make_uint2(b.z, r.status | (r.flags << 8));
-    o[4] = make_uint2(a.x, a.y);
+    o[2] = make_uint2(r.vport | (r.l3 << 16), r.l4 | (r.l7 << 16));
+    o[3] = make_uint2(r.l7len | (r.nh << 16) | (r.proto << 24), r.status | (r.flags << 8));
+    o[4] = make_uint2(w[0], src);
     if (flow) flow[j] = r.flow;
 }
 

@@ -71,10 +71,12 @@ REC_DTYPE = np.dtype([
 assert REC_DTYPE.itemsize == 32
 ROUTE_REC_DTYPE = np.dtype([("rec", REC_DTYPE), ("src_index", "<u4"), ("src_rank", "<u4")])
 assert ROUTE_REC_DTYPE.itemsize == 40
-# emurx_lookup_rec: the parsed record (ns_id = source frame index, client_id = source rank) +
-# the callback rule's lookup key words (owner-partitioned classification)
-LOOKUP_REC_DTYPE = np.dtype([("rec", REC_DTYPE), ("key", "<u4", 12)])
-assert LOOKUP_REC_DTYPE.itemsize == 80
+# emurx_lookup_rec (owner-partitioned classification, 64 B): the source frame index, the packed
+# parse (VLAN codes, vport / l3 / next header, l4 / l7, l7_len / proto / status / key kind) and
+# the callback rule's key (destination MAC, ports, addresses or kw[0..3]); csrc/emurx_parse.h
+LOOKUP_REC_DTYPE = np.dtype([("frame", "<u4"), ("vlans", "<u4"), ("w2", "<u4"), ("w3", "<u4"), ("w4", "<u4"),
+                             ("dlo", "<u4"), ("dhi", "<u4"), ("ports", "<u4"), ("key", "<u4", 8)])
+assert LOOKUP_REC_DTYPE.itemsize == 64
 ST_HOLE = 0xFF     # EMURX_ST_HOLE: status of the record of an empty descriptor slot
 MAX_PARTS = 8
 DESC_DTYPE = np.dtype([("off", "<u4"), ("len", "<u2"), ("vport", "u1"), ("pad", "u1")])

@@ -266,7 +266,7 @@ class RxPath:
 
     def parse_route_dev(self, frames, desc, n: int, rec, qlist, qcap: int, tile_cnt, hist, n_parts: int,
                         my_rank: int, cap: int, send, send_count, stream=None):
-        """Parse + lookup keys, packed into the owners' regions as LOOKUP_REC_DTYPE (80 B)."""
+        """Parse + lookup keys, packed into the owners' regions as LOOKUP_REC_DTYPE (64 B)."""
         out = abi.DevOut(_addr(rec), _addr(qlist), qcap, _addr(tile_cnt), _addr(hist), None)
         return abi.check(self.lib.emurx_parse_route_dev(self.h, _addr(frames), _addr(desc), n, C.byref(out),
                                                         n_parts, my_rank, cap, _addr(send), _addr(send_count),
