@@ -170,21 +170,29 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
     // known after the tile barrier: no registers held across it
     uint4* lrec = reinterpret_cast<uint4*>(const_cast<uint32_t*>(slab)) + wv * (kStage / 16) + lane * 4;
     static_assert(kStage >= kWave * 64, "a wave's lookup records fit its slab");
+    // Lookups in two halves (no TransportCtx on these tables, T.ft_on == 0, wave-uniform): the
+    // frame's two bucket reads are issued right after its parse, the outcome histogram and the
+    // queue ranks -- which depend on the parse alone -- run while they are in flight, and the
+    // buckets are resolved after them.  With flow tables the flow tuple needs the frame bytes
+    // at resolve time, so the lookups run in one piece (classify).
+    const bool split = kClassify && !T.ft_on;
+    bool go = false;  // this lane's probes are in flight
+    LKey k{};
+    Probe pr{};
+    Bucket ce{};
     if (sg.staged) {  // wave-uniform branch
         if (valid) {
             LdsSrc s{reinterpret_cast<const uint8_t*>(slab), slab, wv * kStage + (off - sg.start)};
             parse_flat(s, len, vport, T.cb_mask, r);
-#if EMURX_STAMP
             STAMP(3);
-            const bool go = kClassify && r.status == EMURX_ST_OK;
-            LKey k{};
-            if (go) k = make_key(s, len, r);
-            STAMP(4);
-            if (go) resolve(T, r, k, [&](uint32_t cid) { return flow_probe(T, get_tuple(s, len, r), cid); });
-            STAMP(5);
-#else
-            if (kClassify) classify(s, len, T, r);
-#endif
+            if (split && r.status == EMURX_ST_OK) {
+                k = make_key(s, len, r);
+                pr = probe_issue(T, r, k);
+                if (pr.ctab) ce = ld_bucket(pr.ctab, pr.cbk);
+                go = true;
+            } else if (kClassify && !split) {
+                classify(s, len, T, r);
+            }
             if (kKind == 2) pack_lookup(s, len, r, i, r.status == EMURX_ST_OK, lrec);
         }
     } else {
@@ -193,35 +201,18 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
                  min(kWinVec * 16 - head, len), a.frames + off};
         if (valid) parse_packet(s, len, vport, T.cb_mask, r);
         coop_checksum_rows(r, a.frames + off, L.csum[wv]);  // the wave's long L4 spans, converged
-#if EMURX_STAMP
         STAMP(3);
-        const bool go = valid && kClassify && r.status == EMURX_ST_OK;
-        LKey k{};
-        if (go) k = make_key(s, len, r);
-        STAMP(4);
-        if (go) resolve(T, r, k, [&](uint32_t cid) { return flow_probe(T, get_tuple(s, len, r), cid); });
-        STAMP(5);
-#else
-        if (valid && kClassify) classify(s, len, T, r);
-#endif
+        if (valid && split && r.status == EMURX_ST_OK) {
+            k = make_key(s, len, r);
+            pr = probe_issue(T, r, k);
+            if (pr.ctab) ce = ld_bucket(pr.ctab, pr.cbk);
+            go = true;
+        } else if (valid && kClassify && !split) {
+            classify(s, len, T, r);
+        }
         if (kKind == 2 && valid) pack_lookup(s, len, r, i, r.status == EMURX_ST_OK, lrec);
     }
-    typedef unsigned v4u __attribute__((ext_vector_type(4)));
-    if (a.rec && i < n) {
-        // an empty descriptor slot gets a record too (no Namespace, status EMURX_ST_HOLE), so
-        // every consumer of rec[0, n) sees defined bytes
-        const uint4 h0 = valid ? make_uint4(r.ns, r.cl, r.vlan0, r.vlan1)
-                               : make_uint4(EMURX_ID_NONE, EMURX_ID_NONE, 0, 0);
-        const uint4 h1 = valid ? make_uint4(r.vport | (r.l3 << 16), r.l4 | (r.l7 << 16),
-                                            r.l7len | (r.nh << 16) | (r.proto << 24), r.status | (r.flags << 8))
-                               : make_uint4(0, 0, (uint32_t)EMURX_CB_NONE << 24, EMURX_ST_HOLE);
-        uint4* o = reinterpret_cast<uint4*>(a.rec + i);
-        // streaming stores: the records are read once, by the host copy or the route kernel
-        // (measured +2.6% on config B, neutral on C)
-        __builtin_nontemporal_store(v4u{h0.x, h0.y, h0.z, h0.w}, reinterpret_cast<v4u*>(o));
-        __builtin_nontemporal_store(v4u{h1.x, h1.y, h1.z, h1.w}, reinterpret_cast<v4u*>(o + 1));
-    }
-    if (a.flow && i < n) a.flow[i] = valid ? r.flow : EMURX_FLOW_NONE;
+    STAMP(4);
     // outcome histogram into the wave's LDS copy: a wave whose frames all share one
     // (status, proto) bin adds its count (ballot) and byte sum (DPP reduction) once, instead
     // of 64 LDS atomics serialised on one address; mixed waves add per frame
@@ -229,7 +220,6 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
     {
         const uint32_t bin = valid ? EMURX_HIST_BIN(r.status, r.proto) : 0xffu;
         const uint64_t vm = __ballot(valid);
-        STAMP(6);
         if (vm) {
             const uint32_t lead = (uint32_t)__ffsll((long long)vm) - 1;
             const uint32_t bb = (uint32_t)__builtin_amdgcn_readlane((int)bin, (int)lead);
@@ -242,14 +232,6 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
         }
     }
     const uint32_t q = valid ? (r.status == EMURX_ST_OK ? r.proto : EMURX_Q_DROP) : 0xffu;
-    // the Namespace owner of the record (classify + route: the records whose Namespace was
-    // found; lookup keys: every frame)
-    uint32_t rd = 0xffu;
-    if ((kKind == 1 && rt.cnt) || kKind == 2) {
-        const bool routed = valid && (kKind == 2 || r.ns != EMURX_ID_NONE);
-        rd = routed ? emurx_owner(emurx_tk_hash(r.vport, r.vlan0, r.vlan1), rt.parts) : 0xffu;
-    }
-
     // rank inside (wave, queue): one ballot per distinct queue present in the wave
     uint32_t rank = 0;
     uint64_t left = __ballot(valid);
@@ -260,6 +242,48 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
         if (q == qq) rank = mbcnt(m);
         if (lane == lead) L.wcnt[wv][qq] = (uint32_t)__popcll(m);
         left &= ~m;
+    }
+    STAMP(5);
+    // the other half of the lookups: GetNs + the callback's client rule on the two buckets
+    // (ft_on == 0: the flow callback is never called)
+    if (go) resolve_done(T, r, k, pr, ce, [](uint32_t) { return EMURX_FLOW_NO_CTX; });
+    STAMP(6);
+    typedef unsigned v4u __attribute__((ext_vector_type(4)));
+    if (a.rec) {
+        // The wave's 64 records (32 B each) go out as two contiguous 1 KiB stores: every lane
+        // parks its record in the wave's slab (free once the parse, the lookups and the lookup
+        // record are done with the frame bytes; kind 2's lookup records hold its first 4 KiB),
+        // then stores 16 B of the transposed block.  Whole lines per store instruction instead
+        // of 16 of every 32 bytes (measured against two strided stores per lane on 8 rotating
+        // batches: config B +3 %, C +0.5 %, E +1 %; non-temporal beats plain stores either way).
+        // An empty descriptor slot gets a record too (no Namespace, status EMURX_ST_HOLE), so
+        // every consumer of rec[0, n) sees defined bytes.
+        constexpr uint32_t kPark = kKind == 2 ? 256u : 0u;  // in 16-B units
+        static_assert(kPark * 16 + kWave * 32 <= kStage, "the parked records fit the slab");
+        uint4* park = reinterpret_cast<uint4*>(const_cast<uint32_t*>(slab)) + wv * (kStage / 16) + kPark;
+        park[2 * lane] = valid ? make_uint4(r.ns, r.cl, r.vlan0, r.vlan1)
+                               : make_uint4(EMURX_ID_NONE, EMURX_ID_NONE, 0, 0);
+        park[2 * lane + 1] = valid ? make_uint4(r.vport | (r.l3 << 16), r.l4 | (r.l7 << 16),
+                                                r.l7len | (r.nh << 16) | (r.proto << 24), r.status | (r.flags << 8))
+                                   : make_uint4(0, 0, (uint32_t)EMURX_CB_NONE << 24, EMURX_ST_HOLE);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t r0 = tile * EMURX_QUEUE_TILE + wv * kWave;  // the wave's first record
+        uint4* o = reinterpret_cast<uint4*>(a.rec + r0);
+        const uint4 x0 = park[lane], x1 = park[kWave + lane];
+        // streaming stores: the records are read once, by the host copy or the route kernel
+        if (r0 + lane / 2 < n) __builtin_nontemporal_store(v4u{x0.x, x0.y, x0.z, x0.w}, reinterpret_cast<v4u*>(o + lane));
+        if (r0 + kWave / 2 + lane / 2 < n)
+            __builtin_nontemporal_store(v4u{x1.x, x1.y, x1.z, x1.w}, reinterpret_cast<v4u*>(o + kWave + lane));
+    }
+    if (a.flow && i < n) a.flow[i] = valid ? r.flow : EMURX_FLOW_NONE;
+    // the Namespace owner of the record (classify + route: the records whose Namespace was
+    // found; lookup keys: every frame)
+    uint32_t rd = 0xffu;
+    if ((kKind == 1 && rt.cnt) || kKind == 2) {
+        const bool routed = valid && (kKind == 2 || r.ns != EMURX_ID_NONE);
+        rd = routed ? emurx_owner(emurx_tk_hash(r.vport, r.vlan0, r.vlan1), rt.parts) : 0xffu;
     }
     // Namespace owners (rt.parts > 0): kind 1 counts the records whose Namespace was found
     // (the first pass of emurx_route_dev, fused; k_route<false> counts them the same way,
