@@ -377,7 +377,7 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
     if mode != "none":
         from emurx import exchange as X
         rb = X.LOOKUP_BYTES if mode == "partitioned" else X.REC_BYTES
-        xch = dict(cap=X.capacity(n, world), ev=[], timing=False, k=0, rb=rb)
+        xch = dict(cap=X.capacity(n, world, slack=1.06), ev=[], timing=False, k=0, rb=rb)
 
         # two buffer sets when the timed steps overlap batch k's exchange with batch k+1's parse
         nsets = 2 if world > 1 and not a.no_overlap else 1
@@ -972,6 +972,21 @@ def host_path_rate(rx, w, per_msg=64, budget_s=3.0):
     k, el = run(False)
     out["mpkts_prefilled"] = round(k * n / el / 1e6, 2)
     out["gbs_in_prefilled"] = round(k * total / el / 1e9, 2)
+    # latency of one batch by its size in messages (one slot, nothing else in flight): submit
+    # (H2D of the staged messages + framing walk + k_rx + queue packing + D2H) until wait returns
+    lat = {}
+    for nm in (1, 16, 256, 1024, 4096, len(msgs)):
+        if nm > len(msgs):
+            continue
+        sub_msgs = msgs[:nm]
+        ts = []
+        for rep in range(7):
+            t0 = time.perf_counter()
+            rx.ingest_submit(0, sub_msgs)
+            rx.ingest_wait(0, copy=False)
+            ts.append(time.perf_counter() - t0)
+        lat[str(nm)] = {"frames": nm * per_msg, "us_median": round(float(np.median(ts[2:])) * 1e6, 1)}
+    out["batch_latency_by_msgs"] = lat
     # one ZMQ message per call (the unbatched OnRxStream shape)
     one = [stream[m["off"]:m["off"] + m["len"]].tobytes() for m in msgs[:300]]
     rx.on_rx_stream(one[0])

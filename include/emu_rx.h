@@ -437,6 +437,10 @@ int emurx_ingest_buffer(emurx_t* h, uint32_t slot, size_t bytes, uint8_t** buf);
 int emurx_ingest_submit(emurx_t* h, uint32_t slot, const emurx_msg* msgs, uint32_t nmsg);
 /* Wait for the slot's batch and point `res` at its results (library-owned pinned memory). */
 int emurx_ingest_wait(emurx_t* h, uint32_t slot, emurx_ingest_result* res);
+/* The slot's HIP stream (hipStream_t, created on first use), so that a caller can order its
+   own work with the slot's batches: make the next batch wait for a device-side producer
+   (hipStreamWaitEvent before emurx_ingest_submit), or chain a consumer after the D2H. */
+int emurx_ingest_stream(emurx_t* h, uint32_t slot, void** stream);
 
 /* ---- tx-side checksum generation -----------------------------------
    What the plugins' tx paths do to a frame before Veth.Send, for a batch of frames in

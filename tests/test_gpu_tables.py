@@ -106,8 +106,13 @@ def test_incremental_deltas(rxmod):
 def test_mutation_while_batch_in_flight(rxmod):
     """An ingest batch runs on its slot stream while the tables change and the next batch is
     classified on another stream: the in-flight batch sees the old tables, the new one the
-    new tables (the shipment waits for the in-flight reader by an event)."""
+    new tables (the shipment waits for the in-flight reader by an event).  The batch is held
+    in flight by a spin kernel queued on the slot stream ahead of it, long enough to outlast
+    the mutations (checked: the slot stream has not drained when they end)."""
+    import time
+
     import pyoracle
+    import torch
     n = 1 << 17
     w = synth.config_c(n)
     rx = rxmod(0, max_ns=4096, max_clients=65536, max_frames=n)
@@ -126,7 +131,21 @@ def test_mutation_while_batch_in_flight(rxmod):
         buf[at:at + len(m)] = np.frombuffer(m, np.uint8)
         tab[i] = (at, len(m))
         at += len(m)
+    # spin rate of torch.cuda._sleep (clock64 cycles per second), then a hold of ~2 s
+    s_cal = torch.cuda.Stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(s_cal):
+        torch.cuda._sleep(1_000_000)  # the first launch loads the module: not part of the rate
+        e0.record()
+        torch.cuda._sleep(50_000_000)
+        e1.record()
+    e1.synchronize()
+    per_s = 50_000_000 / (e0.elapsed_time(e1) / 1e3)
+    slot_st = torch.cuda.ExternalStream(rx.ingest_stream(0))
+    with torch.cuda.stream(slot_st):
+        torch.cuda._sleep(int(per_s * 2.0))
     rx.ingest_submit(0, tab)
+    t0 = time.perf_counter()
     # mutate every client's IPv4 and half the MACs' plugins while the batch is in flight
     c = w["clients"]
     for i in range(0, len(c["cid"]), 2):
@@ -134,6 +153,7 @@ def test_mutation_while_batch_in_flight(rxmod):
         ip = bytes([172, 20, cid >> 8 & 255, cid & 255])
         assert rx.client_update_ipv4(cid, ip) == o_new.client_update_ipv4(cid, ip) == 0
         assert rx.client_set_plugins(cid, 0x0FF) == o_new.client_set_plugins(cid, 0x0FF) == 0
+    assert not slot_st.query(), f"the batch finished during the mutations ({time.perf_counter() - t0:.2f} s)"
     rec_new = _check(rx, o_new, w)  # its own stream: the shipment orders after the ingest
     res = rx.ingest_wait(0)
     orec_old, _, _, _ = o_old.rx_batch(w["buf"], w["desc"])

@@ -1016,6 +1016,15 @@ int emurx_ingest_wait(emurx_t* h, uint32_t slot, emurx_ingest_result* res) {
     if (!h || !res || slot >= EMURX_INGEST_SLOTS) return EMURX_EINVAL;
     return ingest_wait(h, slot, res);
 }
+int emurx_ingest_stream(emurx_t* h, uint32_t slot, void** stream) {
+    if (!h || !stream || slot >= EMURX_INGEST_SLOTS) return EMURX_EINVAL;
+    int rc = bind(h);
+    if (rc) return rc;
+    IngestSlot& s = h->ing[slot];
+    if (!s.st && hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking) != hipSuccess) return EMURX_EDEVICE;
+    *stream = (void*)s.st;
+    return EMURX_OK;
+}
 
 void emurx_hist_fold(const uint64_t* shards, uint64_t out[2 * EMURX_HIST_BINS]) {
     for (int b = 0; b < 2 * EMURX_HIST_BINS; ++b) out[b] = 0;

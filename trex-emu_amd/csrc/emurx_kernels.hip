@@ -24,8 +24,12 @@ static_assert(EMURX_QUEUE_TILE == kBlock, "one frame per lane per tile");
 
 
 // LDS-DMA (global_load_lds_dwordx4): lane l's 16 source bytes land at dst + 16 * l
+#ifndef EMURX_GLDS_AUX
+#define EMURX_GLDS_AUX 0
+#endif
 __device__ __forceinline__ void glds16(const uint4* src, uint4* dst_wave_base) {
-    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst_wave_base, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst_wave_base, 16, 0,
+                                     EMURX_GLDS_AUX);
 }
 __device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0)
 

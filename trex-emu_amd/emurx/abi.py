@@ -189,6 +189,7 @@ SIGNATURES = [
     ("emurx_ingest_buffer", C.c_int, [_P, C.c_uint32, C.c_size_t, C.POINTER(C.c_void_p)]),
     ("emurx_ingest_submit", C.c_int, [_P, C.c_uint32, _P, C.c_uint32]),
     ("emurx_ingest_wait", C.c_int, [_P, C.c_uint32, C.POINTER(IngestResult)]),
+    ("emurx_ingest_stream", C.c_int, [_P, C.c_uint32, C.POINTER(C.c_void_p)]),
     ("emurx_tx_checksum_dev", C.c_int, [_P, _P, _P, C.c_uint32, _P, _P]),
     ("emurx_tx_zmq_dev", C.c_int, [_P, _P, _P, C.c_uint32, _P, C.c_uint64, _P, _P, _P]),
     ("emurx_flow_add", C.c_int, [_P, C.c_uint32, _U8P, C.c_uint32, C.c_uint32]),

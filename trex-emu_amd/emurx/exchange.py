@@ -19,11 +19,13 @@ from . import abi
 REC_BYTES = abi.ROUTE_REC_DTYPE.itemsize
 
 
-def capacity(n_frames: int, n_parts: int, slack: float = 1.06) -> int:
+def capacity(n_frames: int, n_parts: int, slack: float = 1.25) -> int:
     """Records per destination region: the fair share plus slack for the owner hash's
-    imbalance (config D: the fullest of 8 partitions holds 1.030x the fair share).  A
-    region that overflows anyway is reported by its count (> cap); the caller grows the
-    capacity (grow()) and routes the batch again."""
+    imbalance.  The default (1.25) covers skewed Namespace populations; bench.py passes 1.06
+    for config D's uniform synthetic keys (the fullest of 8 partitions holds 1.030x the fair
+    share).  A region that overflows anyway is reported by its count (> cap), on every rank
+    after the count exchange: the caller must check the counts of every batch, grow the
+    capacity (grow()) and route that batch again."""
     if n_parts == 1:
         return max(n_frames, 1)
     return int(n_frames / n_parts * slack) + 1024

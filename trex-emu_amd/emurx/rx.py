@@ -211,6 +211,12 @@ class RxPath:
         abi.check(self.lib.emurx_ingest_submit(self.h, slot, _p(m) if len(m) else None, len(m)),
                   "ingest_submit")
 
+    def ingest_stream(self, slot: int) -> int:
+        """The slot's hipStream_t as an integer (for torch.cuda.ExternalStream)."""
+        p = C.c_void_p()
+        abi.check(self.lib.emurx_ingest_stream(self.h, slot, C.byref(p)), "ingest_stream")
+        return int(p.value)
+
     def ingest_wait(self, slot: int, copy: bool = True) -> dict:
         """Results of the slot's batch: rec, desc, qlist, qoff, msg_frames, msg_status,
         counters (views into library memory unless copy)."""

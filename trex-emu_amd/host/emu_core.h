@@ -10,11 +10,20 @@
 //   Parser (callback fields, Init, Register, ParsePacket, stats)   parser.go:503-991
 //   CThreadCtx (AddNs/RemoveNs/GetNs, AddClient, HandleRxPacket)   thread_ctx.go:139-812
 //   VethIFZmq::OnRxStream          veth_zmq.go:277-320
+//   GetNs / CLookupByMac / CLookupByIPv4   thread_ctx.go:777-784, ns_ctx.go:262-285
+//
+// The lookups plugins make keep their Go signatures and answer from the frame being
+// dispatched when they ask for the key the GPU resolved (the frame's memo: its tunnel key,
+// Namespace, client and lookup outcome), so a plugin's GetNs + CLookupBy* per frame costs no
+// map probe; any other key, or a frame whose Namespace a callback of an earlier frame of the
+// batch has mutated (emurx_recs_stale), falls back to the host maps.  No plugin code changes.
 #pragma once
 #include <array>
 #include <cstdint>
 #include <functional>
+#include <map>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/emu_rx.h"
@@ -94,8 +103,9 @@ public:
 
     ParserCb* callback(uint32_t cb);
     uint32_t mask() const;  // callbacks set -> registered mask of the device path
-    // dispatch one device record (status OK) to its callback
-    int dispatch(const emurx_rec& r, Mbuf* m, CTunnelKey* tun);
+    // dispatch one device record (status OK) to its callback; memo: the record may answer the
+    // callback's GetNs / CLookupBy* (it is not stale)
+    int dispatch(const emurx_rec& r, Mbuf* m, CTunnelKey* tun, bool memo);
 };
 
 struct VethStats {
@@ -106,9 +116,15 @@ class VethIFZmq {
 public:
     CThreadCtx* tctx = nullptr;
     VethStats stats;
-    // veth_zmq.go:277-320 + per frame HandleRxPacket, callbacks in frame order
+    // veth_zmq.go:277-320 + per frame HandleRxPacket, callbacks in frame order.  One message
+    // per call (emurx_rx_stream): a fallback, slower than the CPU per message
     void OnRxStream(const uint8_t* stream, size_t len);
     void OnRxStream(const std::vector<uint8_t>& s) { OnRxStream(s.data(), s.size()); }
+    // The primary binding: the messages MainLoop has queued (thread_ctx.go:409-410), all in one
+    // GPU round trip (emurx_ingest_*: pinned staging, framing walk, parse + classify and queue
+    // packing on the device), then OnRxStream's per-frame dispatch in message and wire order,
+    // each callback seeing its frame's memo.  Same counters as OnRxStream once per message.
+    void OnRxBatch(const std::vector<std::vector<uint8_t>>& msgs);
 };
 
 class CThreadCtx {
@@ -128,10 +144,38 @@ public:
     int AddClient(uint32_t ns, const uint8_t mac[6], const uint8_t ipv4[4] = nullptr,
                   const uint8_t ipv6[16] = nullptr, uint32_t plugins = 0x7FF);  // -> client id
     int RemoveClient(uint32_t ns, const uint8_t mac[6]);  // ns_ctx.go RemoveClient
+    int UpdateClientIpv4(uint32_t ns, uint32_t client, const uint8_t ipv4[4]);  // ns_ctx.go:442-471
     void HandleRxPacket(Mbuf* m);  // thread_ctx.go:365-375
     emurx_t* rx() const { return h_; }
 
+    // The lookups plugins make (thread_ctx.go:777-784, ns_ctx.go:262-285): -1 for nil.  While a
+    // frame is dispatched they answer from its memo when asked for the key the GPU resolved.
+    int GetNs(const CTunnelKey& key);
+    int CLookupByMac(uint32_t ns, const uint8_t mac[6]);
+    int CLookupByIPv4(uint32_t ns, const uint8_t ip[4]);
+    struct MemoStats {
+        uint64_t hits = 0;    // answered from the frame's pre-resolved record
+        uint64_t probes = 0;  // answered from the host maps
+        uint64_t stale = 0;   // frames whose memo was off (mid-batch mutation)
+    } memo_stats;
+
 private:
+    friend class Parser;
+    friend class VethIFZmq;
+    struct Memo {
+        bool on = false;
+        CTunnelKey tun;
+        uint32_t ns = EMURX_ID_NONE, client = EMURX_ID_NONE;
+        uint8_t lookup = EMURX_LK_NONE, proto = EMURX_CB_NONE;
+        const uint8_t* frame = nullptr;
+        uint32_t len = 0;
+        uint16_t l3 = 0;
+    } memo_;
+    // the Go maps as the host keeps them (the memo's fallback; the device tables mirror them)
+    std::map<std::array<uint8_t, 12>, uint32_t> ns_map_;
+    std::map<std::pair<uint32_t, uint64_t>, uint32_t> mac_map_;
+    std::map<std::pair<uint32_t, uint32_t>, uint32_t> ip4_map_;
+    std::map<uint32_t, std::pair<uint64_t, uint32_t>> client_keys_;  // id -> (mac, ipv4)
     emurx_t* h_ = nullptr;
     uint32_t next_ns_ = 0, next_client_ = 0;
 };

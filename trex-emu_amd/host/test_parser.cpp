@@ -244,6 +244,125 @@ void TestOnRxStream() {  // veth_zmq.go:277-320 + HandleRxPacket, callbacks in f
     if (tctx.veth.stats.RxParseErr != 1 || order.size() != 3) FATALF(" truncated message ");
 }
 
+// RFC 1071 over big-endian byte pairs (layers/tcpip.go:76-94), folded and inverted
+uint16_t csum16(const uint8_t* p, size_t n, uint32_t s = 0) {
+    for (size_t i = 0; i + 1 < n; i += 2) s += (p[i] << 8) | p[i + 1];
+    if (n & 1) s += p[n - 1] << 8;
+    while (s > 0xffff) s = (s & 0xffff) + (s >> 16);
+    return (uint16_t)~s;
+}
+// Ethernet + tags 0x8100/1, 0x8100/2 + IPv4 + UDP with valid checksums (the simulation layout)
+std::vector<uint8_t> udp4(const uint8_t dst[6], const uint8_t src_ip[4], const uint8_t dst_ip[4], uint16_t sport,
+                          uint16_t dport, size_t payload) {
+    std::vector<uint8_t> f = {dst[0], dst[1], dst[2], dst[3], dst[4], dst[5], 0, 0, 1, 0, 0, 0x63,
+                              0x81, 0, 0, 1, 0x81, 0, 0, 2, 0x08, 0};
+    const uint16_t tot = (uint16_t)(20 + 8 + payload);
+    const uint8_t ip[20] = {0x45, 0, (uint8_t)(tot >> 8), (uint8_t)tot, 0, 1, 0x40, 0, 64, 17, 0, 0,
+                            src_ip[0], src_ip[1], src_ip[2], src_ip[3], dst_ip[0], dst_ip[1], dst_ip[2], dst_ip[3]};
+    f.insert(f.end(), ip, ip + 20);
+    const uint16_t hc = csum16(&f[22], 20);
+    f[22 + 10] = hc >> 8;
+    f[22 + 11] = hc & 0xff;
+    const uint16_t ul = (uint16_t)(8 + payload);
+    const uint8_t udp[8] = {(uint8_t)(sport >> 8), (uint8_t)sport, (uint8_t)(dport >> 8), (uint8_t)dport,
+                            (uint8_t)(ul >> 8), (uint8_t)ul, 0, 0};
+    f.insert(f.end(), udp, udp + 8);
+    for (size_t i = 0; i < payload; ++i) f.push_back((uint8_t)(i * 7 + sport));
+    uint32_t ps = 17 + ul;  // pseudo header: src, dst, 0 | proto, udp length
+    for (int i = 0; i < 4; i += 2) ps += ((src_ip[i] << 8) | src_ip[i + 1]) + ((dst_ip[i] << 8) | dst_ip[i + 1]);
+    uint16_t uc = csum16(&f[42], ul, ps);
+    if (uc == 0) uc = 0xffff;
+    f[42 + 6] = uc >> 8;
+    f[42 + 7] = uc & 0xff;
+    return f;
+}
+
+// The memo (emu_core.h): a transport handler's GetNs(ps.Tun) + CLookupByMac(dst MAC) per frame
+// (plugin_transport.go:83-115) is answered from the frame's pre-resolved record, with the
+// map's answer; through the batched binding (OnRxBatch, one GPU round trip for many messages);
+// and when a callback removes a later frame's client mid-batch, that frame's record is stale
+// and its lookups fall back to the maps.
+void TestMemoLookups() {
+    CThreadCtx tctx;
+    tctx.parser.Init(&tctx);
+    CTunnelKey key = tunOf(1, 0x81000001, 0x81000002);
+    const int ns = tctx.AddNs(key);
+    if (ns < 0) FATALF(" AddNs ");
+    const int kClients = 16;
+    std::vector<std::array<uint8_t, 6>> macs;
+    std::map<uint64_t, int> truth;  // MAC -> client id the maps hold
+    for (int c = 0; c < kClients; ++c) {
+        std::array<uint8_t, 6> m = {0, 0, 1, 0, 0, (uint8_t)(c + 1)};
+        const uint8_t ip[4] = {16, 0, 0, (uint8_t)(c + 1)};
+        const int id = tctx.AddClient((uint32_t)ns, m.data(), ip);
+        if (id < 0) FATALF(" AddClient ");
+        macs.push_back(m);
+        truth[m[5]] = id;
+    }
+    int victim = -1, victim_at = -1;  // the client a callback removes, and at which frame
+    int frame_no = 0, bad = 0;
+    tctx.parser.udp = [&](ParserPacketState* ps) {
+        CThreadCtx* t = ps->Tctx;
+        const int n = t->GetNs(*ps->Tun);
+        const uint8_t* dst = ps->M->GetData();
+        const int c = t->CLookupByMac((uint32_t)n, dst);
+        const auto it = truth.find(dst[5]);
+        const int want = (dst[0] == 0 && dst[1] == 0 && dst[2] == 1 && it != truth.end()) ? it->second : -1;
+        if (n != ns || c != want) bad++;
+        if (frame_no++ == victim_at && victim >= 0) {  // plugin code mutating the maps mid-batch
+            if (t->RemoveClient((uint32_t)ns, macs[victim].data()) != EMURX_OK) bad++;
+            truth.erase(macs[victim][5]);
+        }
+        return 0;
+    };
+    // 8 messages of 16 frames: every client, plus an unknown MAC per message
+    std::vector<std::vector<uint8_t>> msgs;
+    const uint8_t sip[4] = {48, 0, 0, 1};
+    int frames = 0;
+    for (int m = 0; m < 8; ++m) {
+        std::vector<std::vector<uint8_t>> fr;
+        std::vector<uint16_t> vp;
+        for (int k = 0; k < 16; ++k) {
+            const uint8_t unknown[6] = {0, 0, 1, 0, 0, 0xEE};
+            const uint8_t* dst = k == 15 ? unknown : macs[(m + k) % kClients].data();
+            const uint8_t dip[4] = {16, 0, 0, dst[5]};
+            fr.push_back(udp4(dst, sip, dip, (uint16_t)(40000 + m * 16 + k), 5000, 22 + k));
+            vp.push_back(1);
+            frames++;
+        }
+        msgs.push_back(ZmqPack(fr, vp));
+    }
+    tctx.veth.OnRxBatch(msgs);
+    const auto& s = tctx.memo_stats;
+    if (bad || frame_no != frames) FATALF(" lookups differ from the maps: %d bad, %d frames", bad, frame_no);
+    if (s.hits != 2u * frames || s.probes != 0 || s.stale != 0)
+        FATALF(" memo hits %lu probes %lu stale %lu", (unsigned long)s.hits, (unsigned long)s.probes,
+               (unsigned long)s.stale);
+    if (tctx.veth.stats.RxBatch != 8 || tctx.veth.stats.RxPkts != (uint64_t)frames) FATALF(" veth stats ");
+    if (tctx.parser.stats.get("udpPkts") != (uint64_t)frames) FATALF(" udpPkts ");
+    // the same batch again; the callback of frame 40 removes client 3: later frames of that
+    // Namespace are stale (their memo is off), the lookups go to the maps and see the removal
+    tctx.memo_stats = {};
+    frame_no = 0;
+    victim = 3;
+    victim_at = 40;
+    tctx.veth.OnRxBatch(msgs);
+    if (bad) FATALF(" lookups after the mid-batch removal differ from the maps: %d", bad);
+    if (s.stale == 0 || s.probes != 2 * s.stale || s.hits != 2u * (frames - s.stale))
+        FATALF(" stale %lu probes %lu hits %lu", (unsigned long)s.stale, (unsigned long)s.probes,
+               (unsigned long)s.hits);
+    // a key the GPU did not resolve for this frame goes to the maps
+    tctx.memo_stats = {};
+    tctx.parser.udp = [&](ParserPacketState* ps) {
+        const uint8_t o5 = ps->M->GetData()[5] == 5 ? 6 : 5;  // never the frame's own destination
+        const uint8_t other[6] = {0, 0, 1, 0, 0, o5};
+        if (ps->Tctx->CLookupByMac((uint32_t)ns, other) != truth.at(o5)) bad++;
+        return 0;
+    };
+    tctx.veth.OnRxBatch({msgs[0]});
+    if (bad || s.probes != 16 || s.hits != 0) FATALF(" other keys: bad %d probes %lu", bad, (unsigned long)s.probes);
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -258,7 +377,7 @@ int main(int argc, char** argv) {
         {"TestParserIcmp", TestParserIcmp},           {"TestParserDhcp1", TestParserDhcp1},
         {"TestParserDhcpInvalidCs", TestParserDhcpInvalidCs},
         {"TestParserIpv6Option", TestParserIpv6Option}, {"TestNsClientLookup", TestNsClientLookup},
-        {"TestOnRxStream", TestOnRxStream}};
+        {"TestOnRxStream", TestOnRxStream}, {"TestMemoLookups", TestMemoLookups}};
     int failed = 0;
     for (auto& t : tests) {
         try {
