@@ -586,15 +586,21 @@ typedef struct emurx_lookup_rec {
    emurx_parse_dev) and pack the lookup record of every frame (holes excepted) into the region
    of its Namespace's owner: d_send[d * cap ..  + d_send_count[d]), frame order.  Three
    launches: the owner counts from each frame's L2 header (8 bytes), their group scan, and
-   k_rx writing each lookup record at its final place.  Reads no table.  Counts > cap:
-   overflow as in emurx_route_dev. */
+   k_rx writing each lookup record at its final place.  Reads no table.  A region holds at
+   most cap records: d_send_count[d] is the true count, and a count > cap means records were
+   dropped from that region.  The caller must check every count of every batch (after the
+   count exchange, on every rank) and, on overflow, grow cap and route the batch again; the
+   library raises no error of its own on the device path. */
 int emurx_parse_route_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_desc, uint32_t n,
                           const emurx_dev_out* out, uint32_t n_parts, uint32_t my_rank, uint32_t cap,
                           emurx_lookup_rec* d_send, uint32_t* d_send_count, void* stream);
 /* The owner's half: d_recv holds n_parts regions of cap lookup records (the all-to-all's
    receive buffer), d_recv_count[s] of them valid in region s.  Writes d_out[s * cap + j] (the
    classified record + source index / rank, emurx_route_rec) and d_flow (optional, the
-   transport flow decision) for every valid slot.  One launch, no host synchronisation. */
+   transport flow decision) for every valid slot.  One launch, no host synchronisation.
+   d_recv_count[s] must be <= cap (the counts the sources reported; a larger count is an
+   overflow the sources must resolve first, emurx_parse_route_dev): slots past cap are not
+   read. */
 int emurx_lookup_dev(emurx_t* h, const emurx_lookup_rec* d_recv, const uint32_t* d_recv_count,
                      uint32_t n_parts, uint32_t cap, emurx_route_rec* d_out, uint32_t* d_flow, void* stream);
 

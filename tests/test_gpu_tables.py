@@ -141,6 +141,7 @@ def test_mutation_while_batch_in_flight(rxmod):
         e1.record()
     e1.synchronize()
     per_s = 50_000_000 / (e0.elapsed_time(e1) / 1e3)
+    rx.sync()  # the first shipment of whole tables waits for the device: done before the hold
     slot_st = torch.cuda.ExternalStream(rx.ingest_stream(0))
     with torch.cuda.stream(slot_st):
         torch.cuda._sleep(int(per_s * 2.0))

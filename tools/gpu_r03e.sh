@@ -1,0 +1,15 @@
+# GPU suite on the reverted (in-place) lookups, counter calibration, nt LDS-DMA A/B
+set -u
+cd "${GRAFT_REPO_ROOT:-.}"
+mkdir -p gpurun_out/r03e
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/r03e/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/r03e/pytest_gpu.log; exit 1; }
+tail -2 gpurun_out/r03e/pytest_gpu.log
+bash tools/gpu_ab_nt.sh
+# owner count with four frames per lane (default) against one (libemurx_ocold.so): partitioned D, N = 1
+for rep in 1 2; do
+  for v in default ocold; do
+    lib=$PWD/trex-emu_amd/lib/libemurx.so; [ $v != default ] && lib=$PWD/trex-emu_amd/lib/libemurx_$v.so
+    EMURX_LIB=$lib timeout -k 10 300 python bench.py --config D --steps 50 --warmup 5 --no-cpu-baseline --no-check --no-replay > gpurun_out/ab/D_${v}_$rep.log 2>&1 || exit 1
+    echo "D $v #$rep $(grep '^{' gpurun_out/ab/D_${v}_$rep.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); p=d["exchange"]["phases"]; print(d["value"], d["ms_per_step"], p["owner_count_scan_ms"], p["k_rx_ms"], p["owner_lookup_ms"])')"
+  done
+done

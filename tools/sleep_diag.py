@@ -36,3 +36,14 @@ with torch.cuda.stream(st2):
 while not st2.query():
     time.sleep(0.01)
 print(f"torch stream drained after {time.perf_counter() - t0:.3f} s", flush=True)
+# Does a not-ready query leave hipErrorNotReady (600) as the thread's last error?
+import ctypes  # noqa: E402
+
+hip = ctypes.CDLL("libamdhip64.so")
+hip.hipGetLastError.restype = ctypes.c_int
+hip.hipGetLastError()
+st3 = torch.cuda.Stream()
+with torch.cuda.stream(st3):
+    torch.cuda._sleep(int(per_s * 0.2))
+print("query while running:", st3.query(), "-> hipGetLastError() =", hip.hipGetLastError(), flush=True)
+st3.synchronize()

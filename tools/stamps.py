@@ -82,8 +82,8 @@ def report(cfg, s):
     d = np.diff(t, axis=1)
     life = t[:, END] - t[:, 0]
     print(f"== config {cfg}: {len(t)} waves, {len(np.unique(cu))} CUs, {len(np.unique(xcc))} XCDs")
-    for k, name in enumerate(["descriptors", "staging", "parse (+coop csum)", "key + probes issued",
-                              "hist + queue ranks", "lookups resolved", "records + owners", "tile barrier",
+    for k, name in enumerate(["descriptors", "staging", "parse (+coop csum)", "lookups (classify)",
+                              "hist + queue ranks", "-", "records + owners", "tile barrier",
                               "queues/counts out"]):
         print(f"  {name:22s} cycles/wave mean {d[:, k].mean():8.0f}  p50 {np.median(d[:, k]):8.0f}  p90 {np.percentile(d[:, k], 90):8.0f}")
     print(f"  {'lifetime':22s} cycles/wave mean {life.mean():8.0f}  p50 {np.median(life):8.0f}  p90 {np.percentile(life, 90):8.0f}")

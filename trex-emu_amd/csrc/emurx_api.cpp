@@ -43,7 +43,7 @@ struct DevBuf {
         if (p) (void)hipFree(p);
         p = nullptr;
         n = 0;
-        if (hipMalloc((void**)&p, std::max<size_t>(count, 1) * sizeof(T)) != hipSuccess) return -1;
+        if (!EMURX_HIP_OK(hipMalloc((void**)&p, std::max<size_t>(count, 1) * sizeof(T)))) return -1;
         n = count;
         return 0;
     }
@@ -62,7 +62,7 @@ struct PinBuf {
         if (p) (void)hipHostFree(p);
         p = nullptr;
         n = 0;
-        if (hipHostMalloc((void**)&p, std::max<size_t>(count, 1) * sizeof(T), hipHostMallocDefault) != hipSuccess)
+        if (!EMURX_HIP_OK(hipHostMalloc((void**)&p, std::max<size_t>(count, 1) * sizeof(T), hipHostMallocDefault)))
             return -1;
         n = count;
         return 0;
@@ -221,8 +221,8 @@ namespace {
 int bind(emurx_t* h) {
     if (h->host_only) return EMURX_EDEVICE;
     int cur = -1;
-    if (hipGetDevice(&cur) == hipSuccess && cur == h->cfg.device) return EMURX_OK;
-    return hipSetDevice(h->cfg.device) == hipSuccess ? EMURX_OK : EMURX_EDEVICE;
+    if (EMURX_HIP_OK(hipGetDevice(&cur)) && cur == h->cfg.device) return EMURX_OK;
+    return EMURX_HIP_OK(hipSetDevice(h->cfg.device)) ? EMURX_OK : EMURX_EDEVICE;
 }
 
 uint64_t& waited_gen(emurx_t* h, hipStream_t s) {
@@ -245,12 +245,12 @@ int ship_tables(emurx_t* h, hipStream_t st) {
     for (size_t k = 0; k < h->readers.size(); ++k) {
         const hipStream_t r = h->readers[k];
         if (r == st) continue;
-        if (k >= h->reader_ev.size()) {
+        while (h->reader_ev.size() <= k) {  // one event per reader slot (slots skipped above included)
             hipEvent_t e;
-            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return EMURX_EDEVICE;
+            if (!EMURX_HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming))) return EMURX_EDEVICE;
             h->reader_ev.push_back(e);
         }
-        if (hipEventRecord(h->reader_ev[k], r) != hipSuccess || hipStreamWaitEvent(st, h->reader_ev[k], 0) != hipSuccess)
+        if (!EMURX_HIP_OK(hipEventRecord(h->reader_ev[k], r)) || !EMURX_HIP_OK(hipStreamWaitEvent(st, h->reader_ev[k], 0)))
             return EMURX_EDEVICE;
     }
     Blocks* img[kNumTabs + 1];
@@ -269,20 +269,20 @@ int ship_tables(emurx_t* h, hipStream_t st) {
         grow = grow || (img[k]->all && img[k]->img.size() > dev[k]->n);
         if (!img[k]->all) nd += img[k]->dirty.size();
     }
-    if (grow && hipDeviceSynchronize() != hipSuccess) return EMURX_EDEVICE;
+    if (grow && !EMURX_HIP_OK(hipDeviceSynchronize())) return EMURX_EDEVICE;
     if (whole) {
-        if (hipStreamSynchronize(st) != hipSuccess) return EMURX_EDEVICE;
+        if (!EMURX_HIP_OK(hipStreamSynchronize(st))) return EMURX_EDEVICE;
         for (int k = 0; k <= kNumTabs; ++k) {
             if (!img[k]->all) continue;
             if (dev[k]->alloc(img[k]->img.size())) return EMURX_ENOMEM;
-            if (hipMemcpy(dev[k]->p, img[k]->img.data(), img[k]->img.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+            if (!EMURX_HIP_OK(hipMemcpy(dev[k]->p, img[k]->img.data(), img[k]->img.size() * 4, hipMemcpyHostToDevice)))
                 return EMURX_EDEVICE;
             h->shipped_whole++;
         }
     }
     if (nd) {
         DeltaSlot& s = h->ring[h->ring_i++ % kDeltaRing];
-        if (s.used && hipEventSynchronize(s.ev) != hipSuccess) return EMURX_EDEVICE;
+        if (s.used && !EMURX_HIP_OK(hipEventSynchronize(s.ev))) return EMURX_EDEVICE;
         if (s.h.alloc(nd)) return EMURX_ENOMEM;
         size_t j = 0;
         for (int k = 0; k <= kNumTabs; ++k) {
@@ -294,13 +294,13 @@ int ship_tables(emurx_t* h, hipStream_t st) {
                 memcpy(e.w, &img[k]->img[(size_t)b * EMURX_BUCKET_WORDS], sizeof(e.w));
             }
         }
-        if (emurx_launch_apply(s.h.p, (uint32_t)nd, st) || hipEventRecord(s.ev, st) != hipSuccess)
+        if (emurx_launch_apply(s.h.p, (uint32_t)nd, st) || !EMURX_HIP_OK(hipEventRecord(s.ev, st)))
             return EMURX_EDEVICE;
         s.used = true;
         h->shipped_blocks += nd;
     }
     m.clean_all();
-    if (hipEventRecord(h->ship_ev, st) != hipSuccess) return EMURX_EDEVICE;
+    if (!EMURX_HIP_OK(hipEventRecord(h->ship_ev, st))) return EMURX_EDEVICE;
     waited_gen(h, st) = ++h->ship_gen;
     h->readers.clear();
     return EMURX_OK;
@@ -315,13 +315,13 @@ int prepare_read(emurx_t* h, hipStream_t st) {
     } else {
         uint64_t& w = waited_gen(h, st);
         if (w < h->ship_gen) {
-            if (hipStreamWaitEvent(st, h->ship_ev, 0) != hipSuccess) return EMURX_EDEVICE;
+            if (!EMURX_HIP_OK(hipStreamWaitEvent(st, h->ship_ev, 0))) return EMURX_EDEVICE;
             w = h->ship_gen;
         }
     }
     if (std::find(h->readers.begin(), h->readers.end(), st) == h->readers.end()) {
         if (h->readers.size() >= kMaxReaders) {  // many distinct streams: drain them all once
-            if (hipDeviceSynchronize() != hipSuccess) return EMURX_EDEVICE;
+            if (!EMURX_HIP_OK(hipDeviceSynchronize())) return EMURX_EDEVICE;
             h->readers.clear();
         }
         h->readers.push_back(st);
@@ -339,7 +339,7 @@ bool choose_stage_(emurx_t* h) {
     h->stage_gen &= 0x3fffffffu;
     if (h->stage_mode) return h->stage_mode == 2;
     // decide as soon as the last copy-back has landed (an event query, no waiting)
-    if (h->stage_pending && hipEventQuery(h->stage_ev) == hipSuccess) {
+    if (h->stage_pending && hipEventQuery(h->stage_ev) == hipSuccess) {  // "not ready" is no error
         h->stage_pending = false;
         // the sampled waves of the 16 launches up to the copied one (a 1M-frame launch
         // rewrites all 256 words, a small one only the first few)
@@ -365,9 +365,8 @@ bool choose_stage_(emurx_t* h) {
 int stage_copy_back(emurx_t* h, hipStream_t st) {
     if (!h->stage_copy) return 0;
     h->stage_copy = false;
-    if (hipMemcpyAsync(h->stage_fb.p, h->d_stage_fb.p, 256 * sizeof(uint32_t), hipMemcpyDeviceToHost, st) !=
-            hipSuccess ||
-        hipEventRecord(h->stage_ev, st) != hipSuccess)
+    if (!EMURX_HIP_OK(hipMemcpyAsync(h->stage_fb.p, h->d_stage_fb.p, 256 * sizeof(uint32_t), hipMemcpyDeviceToHost, st)) ||
+        !EMURX_HIP_OK(hipEventRecord(h->stage_ev, st)))
         return -1;
     h->stage_pending = true;
     h->stage_copy_gen = h->stage_gen;
@@ -393,13 +392,13 @@ int route_scratch(emurx_t* h, uint32_t n, hipStream_t st, emurx_t::RouteScratch*
             if (!r && !x.used) r = &x;
     if (!r) {
         r = &h->route[h->route_next++ % emurx_t::kRouteSets];
-        if (hipStreamWaitEvent(st, r->done, 0) != hipSuccess) return EMURX_EDEVICE;
+        if (!EMURX_HIP_OK(hipStreamWaitEvent(st, r->done, 0))) return EMURX_EDEVICE;
     }
-    if (!r->done && hipEventCreateWithFlags(&r->done, hipEventDisableTiming) != hipSuccess) return EMURX_EDEVICE;
+    if (!r->done && !EMURX_HIP_OK(hipEventCreateWithFlags(&r->done, hipEventDisableTiming))) return EMURX_EDEVICE;
     r->st = st;
     r->used = true;
     if (!r->grp.p) {
-        if (r->grp.alloc(gw) || hipMemset(r->grp.p, 0, gw * sizeof(uint32_t)) != hipSuccess) return EMURX_ENOMEM;
+        if (r->grp.alloc(gw) || !EMURX_HIP_OK(hipMemset(r->grp.p, 0, gw * sizeof(uint32_t)))) return EMURX_ENOMEM;
     }
     if (r->cnt.alloc(tiles * 16) || r->goff.alloc(gw)) return EMURX_ENOMEM;
     *out = r;
@@ -407,7 +406,7 @@ int route_scratch(emurx_t* h, uint32_t n, hipStream_t st, emurx_t::RouteScratch*
 }
 // after a route's last launch on st: its scratch set may change hands behind this event
 int route_done(emurx_t::RouteScratch* r, hipStream_t st) {
-    return hipEventRecord(r->done, st) == hipSuccess ? EMURX_OK : EMURX_EDEVICE;
+    return EMURX_HIP_OK(hipEventRecord(r->done, st)) ? EMURX_OK : EMURX_EDEVICE;
 }
 
 // A launch path may ship table edits (k_apply, cross-stream events, a synchronisation for a
@@ -415,7 +414,7 @@ int route_done(emurx_t::RouteScratch* r, hipStream_t st) {
 // its kernel arguments: it must not be recorded into a hipGraph
 int not_capturing(hipStream_t st) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cs) != hipSuccess) return EMURX_EDEVICE;
+    if (!EMURX_HIP_OK(hipStreamIsCapturing(st, &cs))) return EMURX_EDEVICE;
     return cs == hipStreamCaptureStatusNone ? EMURX_OK : EMURX_EINVAL;
 }
 
@@ -464,8 +463,8 @@ int ingest_submit(emurx_t* h, uint32_t slot, const emurx_msg* msgs, uint32_t nms
     if (s.pending || (nmsg && (!msgs || !s.h_buf.p))) return EMURX_EINVAL;
     int rc = bind(h);
     if (rc) return rc;
-    if (!s.st && hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking) != hipSuccess) return EMURX_EDEVICE;
-    if (!s.done && hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) return EMURX_EDEVICE;
+    if (!s.st && !EMURX_HIP_OK(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking))) return EMURX_EDEVICE;
+    if (!s.done && !EMURX_HIP_OK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming))) return EMURX_EDEVICE;
     const size_t cap = s.h_buf.p ? s.h_buf.n - 64 : 0;
     if (s.h_ctl.alloc((size_t)3 * nmsg + 1)) return EMURX_ENOMEM;
     uint32_t* ctl = s.h_ctl.p;
@@ -503,9 +502,9 @@ int ingest_submit(emurx_t* h, uint32_t slot, const emurx_msg* msgs, uint32_t nms
     if ((rc = prepare_read(h, st))) return rc;  // table deltas ordered against every reader
     const auto H2D = hipMemcpyHostToDevice, D2H = hipMemcpyDeviceToHost;
     bool ok = true;
-    if (fresh_hist) ok = ok && hipMemsetAsync(s.d_hist.p, 0, hw * sizeof(uint64_t), st) == hipSuccess;
-    ok = ok && hipMemcpyAsync(s.d_ctl.p, ctl, ((size_t)3 * nmsg + 1) * 4, H2D, st) == hipSuccess;
-    if (end) ok = ok && hipMemcpyAsync(s.d_buf.p, s.h_buf.p, end, H2D, st) == hipSuccess;
+    if (fresh_hist) ok = ok && EMURX_HIP_OK(hipMemsetAsync(s.d_hist.p, 0, hw * sizeof(uint64_t), st));
+    ok = ok && EMURX_HIP_OK(hipMemcpyAsync(s.d_ctl.p, ctl, ((size_t)3 * nmsg + 1) * 4, H2D, st));
+    if (end) ok = ok && EMURX_HIP_OK(hipMemcpyAsync(s.d_buf.p, s.h_buf.p, end, H2D, st));
     if (!ok) return EMURX_EDEVICE;
     if (emurx_launch_zmq_walk(s.d_buf.p, s.d_ctl.p, nmsg, s.d_desc.p, s.d_stat.p, st)) return EMURX_EDEVICE;
     if (n) {
@@ -520,13 +519,13 @@ int ingest_submit(emurx_t* h, uint32_t slot, const emurx_msg* msgs, uint32_t nms
                                 s.d_qoff.p, s.d_hist.p, s.d_hist_out.p, st))
         return EMURX_EDEVICE;
     if (n)
-        ok = hipMemcpyAsync(s.h_rec.p, s.d_rec.p, (size_t)n * sizeof(emurx_rec), D2H, st) == hipSuccess &&
-             hipMemcpyAsync(s.h_desc.p, s.d_desc.p, (size_t)n * sizeof(emurx_desc), D2H, st) == hipSuccess &&
-             hipMemcpyAsync(s.h_qlist.p, s.d_packed.p, (size_t)n * 4, D2H, st) == hipSuccess;
-    if (nmsg) ok = ok && hipMemcpyAsync(s.h_stat.p, s.d_stat.p, (size_t)nmsg * 4, D2H, st) == hipSuccess;
-    ok = ok && hipMemcpyAsync(s.h_qoff.p, s.d_qoff.p, (EMURX_NUM_QUEUES + 1) * 4, D2H, st) == hipSuccess &&
-         hipMemcpyAsync(s.h_hist.p, s.d_hist_out.p, 2 * EMURX_HIST_BINS * 8, D2H, st) == hipSuccess &&
-         hipEventRecord(s.done, st) == hipSuccess;
+        ok = EMURX_HIP_OK(hipMemcpyAsync(s.h_rec.p, s.d_rec.p, (size_t)n * sizeof(emurx_rec), D2H, st)) &&
+             EMURX_HIP_OK(hipMemcpyAsync(s.h_desc.p, s.d_desc.p, (size_t)n * sizeof(emurx_desc), D2H, st)) &&
+             EMURX_HIP_OK(hipMemcpyAsync(s.h_qlist.p, s.d_packed.p, (size_t)n * 4, D2H, st));
+    if (nmsg) ok = ok && EMURX_HIP_OK(hipMemcpyAsync(s.h_stat.p, s.d_stat.p, (size_t)nmsg * 4, D2H, st));
+    ok = ok && EMURX_HIP_OK(hipMemcpyAsync(s.h_qoff.p, s.d_qoff.p, (EMURX_NUM_QUEUES + 1) * 4, D2H, st)) &&
+         EMURX_HIP_OK(hipMemcpyAsync(s.h_hist.p, s.d_hist_out.p, 2 * EMURX_HIST_BINS * 8, D2H, st)) &&
+         EMURX_HIP_OK(hipEventRecord(s.done, st));
     if (!ok) return EMURX_EDEVICE;
     s.pending = true;
     s.nmsg = nmsg;
@@ -540,7 +539,7 @@ int ingest_wait(emurx_t* h, uint32_t slot, emurx_ingest_result* res) {
     int rc = bind(h);
     if (rc) return rc;
     s.pending = false;
-    if (hipEventSynchronize(s.done) != hipSuccess) return EMURX_EDEVICE;
+    if (!EMURX_HIP_OK(hipEventSynchronize(s.done))) return EMURX_EDEVICE;
     memset(res, 0, sizeof(*res));
     emurx_counters& d = res->delta;
     d.rx_batch = s.nmsg;  // one OnRxStream per message, veth_zmq.go:278
@@ -626,17 +625,17 @@ int emurx_open(const emurx_cfg* cfg, emurx_t** out) {
     }
     int rc = bind(h);
     if (rc) { delete h; return rc; }
-    if (hipStreamCreate(&h->stream) != hipSuccess) { delete h; return EMURX_EDEVICE; }
+    if (!EMURX_HIP_OK(hipStreamCreate(&h->stream))) { delete h; return EMURX_EDEVICE; }
     if (const char* e = getenv("EMURX_STAGE")) h->stage_mode = !strcmp(e, "wide") ? 1 : !strcmp(e, "narrow") ? 2 : 0;
     if (h->stage_fb.alloc(256) || h->d_stage_fb.alloc(256) ||
-        hipEventCreateWithFlags(&h->stage_ev, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&h->ship_ev, hipEventDisableTiming) != hipSuccess ||
-        hipMemset(h->d_stage_fb.p, 0, 256 * sizeof(uint32_t)) != hipSuccess) {
+        !EMURX_HIP_OK(hipEventCreateWithFlags(&h->stage_ev, hipEventDisableTiming)) ||
+        !EMURX_HIP_OK(hipEventCreateWithFlags(&h->ship_ev, hipEventDisableTiming)) ||
+        !EMURX_HIP_OK(hipMemset(h->d_stage_fb.p, 0, 256 * sizeof(uint32_t)))) {
         emurx_close(h);
         return EMURX_ENOMEM;
     }
     for (auto& s : h->ring)
-        if (hipEventCreateWithFlags(&s.ev, hipEventDisableTiming) != hipSuccess) {
+        if (!EMURX_HIP_OK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming))) {
             emurx_close(h);
             return EMURX_EDEVICE;
         }
@@ -812,7 +811,7 @@ int emurx_image_check(emurx_t* h, uint64_t* mismatched) {
     int rc = bind(h);
     if (rc) return rc;
     if ((rc = prepare_read(h, h->stream))) return rc;
-    if (hipStreamSynchronize(h->stream) != hipSuccess) return EMURX_EDEVICE;
+    if (!EMURX_HIP_OK(hipStreamSynchronize(h->stream))) return EMURX_EDEVICE;
     uint64_t bad = 0;
     std::vector<uint32_t> buf;
     for (int k = 0; k <= kNumTabs; ++k) {
@@ -820,7 +819,7 @@ int emurx_image_check(emurx_t* h, uint64_t* mismatched) {
         const DevBuf<uint32_t>& d = k < kNumTabs ? h->d_tab[k] : h->d_nsinfo;
         buf.resize(b.img.size());
         if (b.img.size() > d.n) return EMURX_EDEVICE;
-        if (!buf.empty() && hipMemcpy(buf.data(), d.p, buf.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
+        if (!buf.empty() && !EMURX_HIP_OK(hipMemcpy(buf.data(), d.p, buf.size() * 4, hipMemcpyDeviceToHost)))
             return EMURX_EDEVICE;
         for (size_t i = 0; i < buf.size(); ++i) bad += buf[i] != b.img[i];
     }
@@ -1021,7 +1020,7 @@ int emurx_ingest_stream(emurx_t* h, uint32_t slot, void** stream) {
     int rc = bind(h);
     if (rc) return rc;
     IngestSlot& s = h->ing[slot];
-    if (!s.st && hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking) != hipSuccess) return EMURX_EDEVICE;
+    if (!s.st && !EMURX_HIP_OK(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking))) return EMURX_EDEVICE;
     *stream = (void*)s.st;
     return EMURX_OK;
 }
@@ -1042,7 +1041,7 @@ int emurx_set_timing(emurx_t* h, uint32_t slots, uint32_t stride) {
         if (e) (void)hipEventDestroy(e);
     h->ev.assign((size_t)slots * 2, nullptr);
     for (auto& e : h->ev)
-        if (hipEventCreate(&e) != hipSuccess) { h->slots = 0; return EMURX_EDEVICE; }
+        if (!EMURX_HIP_OK(hipEventCreate(&e))) { h->slots = 0; return EMURX_EDEVICE; }
     h->slots = slots;
     h->stride = stride ? stride : 1;
     h->ev_head = h->ev_count = h->batch_seq = 0;
@@ -1058,12 +1057,12 @@ int emurx_kernel_times(emurx_t* h, float* batch_ms, uint32_t cap, uint32_t* n_ou
     int rc = bind(h);
     if (rc) return rc;
     const uint32_t last = (h->ev_head + h->slots - 1) % h->slots;
-    if (hipEventSynchronize(h->ev[2 * last + 1]) != hipSuccess) return EMURX_EDEVICE;
+    if (!EMURX_HIP_OK(hipEventSynchronize(h->ev[2 * last + 1]))) return EMURX_EDEVICE;
     const uint32_t n = std::min(h->ev_count, cap);
     const uint32_t first = (h->ev_head + h->slots - h->ev_count) % h->slots;
     for (uint32_t k = 0; k < n; ++k) {
         const uint32_t s = (first + (h->ev_count - n) + k) % h->slots;
-        if (hipEventElapsedTime(&batch_ms[k], h->ev[2 * s], h->ev[2 * s + 1]) != hipSuccess)
+        if (!EMURX_HIP_OK(hipEventElapsedTime(&batch_ms[k], h->ev[2 * s], h->ev[2 * s + 1])))
             return EMURX_EDEVICE;
     }
     *n_out = n;

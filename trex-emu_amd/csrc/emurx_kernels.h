@@ -2,8 +2,21 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "../../include/emu_rx.h"
 #include "emurx_tables.h"
+
+// HIP status check of the host code: false on failure.  EMURX_DEBUG=1 names the failing call
+// (file:line and HIP's message) on stderr; the entry points still return EMURX_EDEVICE.
+inline bool emurx_hip_ok(hipError_t e, const char* file, int line) {
+    if (e == hipSuccess) return true;
+    static const bool dbg = getenv("EMURX_DEBUG") != nullptr;
+    if (dbg) fprintf(stderr, "emurx: HIP error at %s:%d: %s\n", file, line, hipGetErrorString(e));
+    return false;
+}
+#define EMURX_HIP_OK(x) emurx_hip_ok((x), __FILE__, __LINE__)
 
 // Enqueue one batch on `st`: a single k_rx launch, no host synchronisation (capturable in a
 // hipGraph).  ev[0..1] (optional) are recorded before and after it.  narrow: the 6 KiB

@@ -23,13 +23,12 @@ namespace emurx {
 static_assert(EMURX_QUEUE_TILE == kBlock, "one frame per lane per tile");
 
 
-// LDS-DMA (global_load_lds_dwordx4): lane l's 16 source bytes land at dst + 16 * l
-#ifndef EMURX_GLDS_AUX
-#define EMURX_GLDS_AUX 0
-#endif
+// LDS-DMA (global_load_lds_dwordx4): lane l's 16 source bytes land at dst + 16 * l.  kNt: the
+// non-temporal policy (aux bit 1, `nt`) for bytes nothing reads again from memory
+template <bool kNt>
 __device__ __forceinline__ void glds16(const uint4* src, uint4* dst_wave_base) {
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst_wave_base, 16, 0,
-                                     EMURX_GLDS_AUX);
+                                     kNt ? 2 : 0);
 }
 __device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0)
 
@@ -100,14 +99,14 @@ __device__ __forceinline__ Stage stage_issue(const uint8_t* __restrict__ frames,
         const uint4* src = reinterpret_cast<const uint4*>(frames + sg.start);
 #pragma unroll
         for (uint32_t k = 0; k < kStage / 16 / kWave; ++k)
-            if (k * kWave < sg.nvec) glds16(src + min(lane + k * kWave, sg.nvec - 1), wslab + k * kWave);
+            if (k * kWave < sg.nvec) glds16<true>(src + min(lane + k * kWave, sg.nvec - 1), wslab + k * kWave);
     } else {  // too wide: each lane stages a window of its own frame (headers)
         const uintptr_t fa = (uintptr_t)(frames + off);
         const uint4* src = reinterpret_cast<const uint4*>(fa & ~(uintptr_t)15);
         const uint32_t nv = valid ? (uint32_t)(((fa & 15) + len + 15) >> 4) : 0;  // vectors of the frame
 #pragma unroll
         for (uint32_t k = 0; k < kWinVec; ++k)
-            if (k < nv) glds16(src + k, wslab + k * kWave);
+            if (k < nv) glds16<false>(src + k, wslab + k * kWave);  // the span past it is read again
     }
     return sg;
 }
@@ -174,29 +173,12 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
     // known after the tile barrier: no registers held across it
     uint4* lrec = reinterpret_cast<uint4*>(const_cast<uint32_t*>(slab)) + wv * (kStage / 16) + lane * 4;
     static_assert(kStage >= kWave * 64, "a wave's lookup records fit its slab");
-    // Lookups in two halves (no TransportCtx on these tables, T.ft_on == 0, wave-uniform): the
-    // frame's two bucket reads are issued right after its parse, the outcome histogram and the
-    // queue ranks -- which depend on the parse alone -- run while they are in flight, and the
-    // buckets are resolved after them.  With flow tables the flow tuple needs the frame bytes
-    // at resolve time, so the lookups run in one piece (classify).
-    const bool split = kClassify && !T.ft_on;
-    bool go = false;  // this lane's probes are in flight
-    LKey k{};
-    Probe pr{};
-    Bucket ce{};
     if (sg.staged) {  // wave-uniform branch
         if (valid) {
             LdsSrc s{reinterpret_cast<const uint8_t*>(slab), slab, wv * kStage + (off - sg.start)};
             parse_flat(s, len, vport, T.cb_mask, r);
             STAMP(3);
-            if (split && r.status == EMURX_ST_OK) {
-                k = make_key(s, len, r);
-                pr = probe_issue(T, r, k);
-                if (pr.ctab) ce = ld_bucket(pr.ctab, pr.cbk);
-                go = true;
-            } else if (kClassify && !split) {
-                classify(s, len, T, r);
-            }
+            if (kClassify) classify(s, len, T, r);
             if (kKind == 2) pack_lookup(s, len, r, i, r.status == EMURX_ST_OK, lrec);
         }
     } else {
@@ -206,14 +188,7 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
         if (valid) parse_packet(s, len, vport, T.cb_mask, r);
         coop_checksum_rows(r, a.frames + off, L.csum[wv]);  // the wave's long L4 spans, converged
         STAMP(3);
-        if (valid && split && r.status == EMURX_ST_OK) {
-            k = make_key(s, len, r);
-            pr = probe_issue(T, r, k);
-            if (pr.ctab) ce = ld_bucket(pr.ctab, pr.cbk);
-            go = true;
-        } else if (valid && kClassify && !split) {
-            classify(s, len, T, r);
-        }
+        if (valid && kClassify) classify(s, len, T, r);
         if (kKind == 2 && valid) pack_lookup(s, len, r, i, r.status == EMURX_ST_OK, lrec);
     }
     STAMP(4);
@@ -248,9 +223,6 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
         left &= ~m;
     }
     STAMP(5);
-    // the other half of the lookups: GetNs + the callback's client rule on the two buckets
-    // (ft_on == 0: the flow callback is never called)
-    if (go) resolve_done(T, r, k, pr, ce, [](uint32_t) { return EMURX_FLOW_NO_CTX; });
     STAMP(6);
     typedef unsigned v4u __attribute__((ext_vector_type(4)));
     if (a.rec) {
@@ -313,15 +285,23 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
         rt.cnt[(size_t)tile * 16 + tid] = c;
         if (c) atomicAdd(&rt.grp[(tile / 64) * 16 + tid], c);
     }
-    if (kKind == 2 && rd != 0xffu) {  // the frame's 64-byte lookup record into its owner's region
-        uint32_t pos = L.toff[rd] + rrank;
-        for (uint32_t w = 0; w < wv; ++w) pos += L.rcnt[w][rd];
-        if (pos < rt.cap) {  // overflow: send_count[d] > cap tells the caller
-            uint4* o = reinterpret_cast<uint4*>(rt.send + (size_t)rd * rt.cap + pos);
-            o[0] = lrec[0];
-            o[1] = lrec[1];
-            o[2] = lrec[2];
-            o[3] = lrec[3];
+    if constexpr (kKind == 2) {  // every frame's 64-byte lookup record into its owner's region
+        uint32_t dst = 0xffffffffu;  // the record's slot in send (record units), none on overflow
+        if (rd != 0xffu) {
+            uint32_t pos = L.toff[rd] + rrank;
+            for (uint32_t w = 0; w < wv; ++w) pos += L.rcnt[w][rd];
+            if (pos < rt.cap) dst = rd * rt.cap + pos;  // overflow: send_count[d] > cap tells the caller
+        }
+        // four lanes per record, 16 records per store instruction: a record is one whole line
+        // written by one instruction, and records of one owner ranked next to each other
+        // (every one of them at N = 1) make contiguous 1 KiB stores, instead of each lane
+        // writing its own record as four 16-B pieces 64 B apart
+        const uint4* parked = reinterpret_cast<const uint4*>(slab) + wv * (kStage / 16);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t rr = k * (kWave / 4) + lane / 4, part = lane & 3;
+            const uint32_t to = (uint32_t)__shfl((int)dst, (int)rr);
+            if (to != 0xffffffffu) reinterpret_cast<uint4*>(rt.send + to)[part] = parked[rr * 4 + part];
         }
     }
 
@@ -398,9 +378,10 @@ __global__ __launch_bounds__(kBlock) void k_apply(const emurx_delta* __restrict_
 }  // namespace emurx
 
 int emurx_launch_apply(const emurx_delta* d, uint32_t n, hipStream_t st) {
+    (void)hipGetLastError();  // a status left by the caller's own failed HIP call is not this launch's
     using namespace emurx;
     if (n) hipLaunchKernelGGL(k_apply, dim3((n * 4 + kBlock - 1) / kBlock), dim3(kBlock), 0, st, d, n);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    return EMURX_HIP_OK(hipGetLastError()) ? 0 : -1;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -410,6 +391,7 @@ int emurx_launch_batch(const uint8_t* frames, const emurx_desc* desc, uint32_t n
                        const emurx_dev_tables& T, int kind, const emurx_dev_out& out,
                        hipStream_t st, const hipEvent_t* ev, bool narrow, uint32_t* fb, uint32_t gen,
                        const emurx_route_args* rt) {
+    (void)hipGetLastError();  // a status left by the caller's own failed HIP call is not this launch's
     using namespace emurx;
     if (ev) (void)hipEventRecord(ev[0], st);
     if (n) {
@@ -424,7 +406,7 @@ int emurx_launch_batch(const uint8_t* frames, const emurx_desc* desc, uint32_t n
         hipLaunchKernelGGL(k, dim3(ntiles), dim3(kBlock), 0, st, args);
     }
     if (ev) (void)hipEventRecord(ev[1], st);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    return EMURX_HIP_OK(hipGetLastError()) ? 0 : -1;
 }
 
 namespace emurx {
@@ -456,14 +438,15 @@ __global__ __launch_bounds__(kBlock) void k_copy(uint4* __restrict__ dst, const 
 #if EMURX_STAMP
 // the stamp buffer of the timeline variant (tools/stamps.py): 16 u64 per wave of the launch
 extern "C" int emurx_debug_set_stamps(void* dev_buf) {
-    return hipMemcpyToSymbol(HIP_SYMBOL(emurx::g_stamp), &dev_buf, sizeof(dev_buf)) == hipSuccess ? 0 : -1;
+    return EMURX_HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(emurx::g_stamp), &dev_buf, sizeof(dev_buf))) ? 0 : -1;
 }
 #endif
 
 extern "C" int emurx_copy_ceiling_dev(void* d_dst, const void* d_src, size_t bytes, void* stream) {
+    (void)hipGetLastError();  // a status left by the caller's own failed HIP call is not this launch's
     if (!d_dst || !d_src || (bytes & 15) || ((uintptr_t)d_dst & 15) || ((uintptr_t)d_src & 15)) return EMURX_EINVAL;
     if (bytes)
         hipLaunchKernelGGL(emurx::k_copy, dim3(emurx::kCopyGrid), dim3(emurx::kBlock), 0, (hipStream_t)stream,
                            reinterpret_cast<uint4*>(d_dst), reinterpret_cast<const uint4*>(d_src), bytes / 16);
-    return hipGetLastError() == hipSuccess ? EMURX_OK : EMURX_EDEVICE;
+    return EMURX_HIP_OK(hipGetLastError()) ? EMURX_OK : EMURX_EDEVICE;
 }

@@ -33,6 +33,7 @@ __global__ __launch_bounds__(kBlock) void k_route(const emurx_rec* __restrict__ 
                                                   emurx_route_rec* __restrict__ send, uint32_t cap) {
     __shared__ uint32_t s_wcnt[kWaves][16];
     __shared__ uint32_t s_toff[EMURX_MAX_PARTS];
+    __shared__ uint2 s_park[kPack ? kWaves : 1][kPack ? kWave * 5 : 1];  // the wave's records, 40 B each
     const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / kWave, tile = blockIdx.x;
     const uint32_t i = tile * kBlock + tid;
     if (lane < 16) s_wcnt[wv][lane] = 0;
@@ -65,16 +66,31 @@ __global__ __launch_bounds__(kBlock) void k_route(const emurx_rec* __restrict__ 
         }
         return;
     }
-    if (d == 0xffu) return;
-    uint32_t pos = s_toff[d] + rank;
-    for (uint32_t w = 0; w < wv; ++w) pos += s_wcnt[w][d];
-    if (pos >= cap) return;  // overflow: send_count[d] > cap tells the caller
-    uint32_t* o = reinterpret_cast<uint32_t*>(send + (size_t)d * cap + pos);  // 40 B, 8-B aligned
-    reinterpret_cast<uint2*>(o)[0] = make_uint2(a.x, a.y);
-    reinterpret_cast<uint2*>(o)[1] = make_uint2(a.z, a.w);
-    reinterpret_cast<uint2*>(o)[2] = make_uint2(b.x, b.y);
-    reinterpret_cast<uint2*>(o)[3] = make_uint2(b.z, b.w);
-    reinterpret_cast<uint2*>(o)[4] = make_uint2(i, my_rank);
+    uint32_t dst = 0xffffffffu;  // the record's slot in send (record units), none on overflow
+    if (d != 0xffu) {
+        uint32_t pos = s_toff[d] + rank;
+        for (uint32_t w = 0; w < wv; ++w) pos += s_wcnt[w][d];
+        if (pos < cap) dst = d * cap + pos;  // overflow: send_count[d] > cap tells the caller
+    }
+    // The wave's 40-B records go out through LDS as five 8-B pieces per record, spread over the
+    // lanes (lane l of store k writes piece (64k + l) mod 5 of record (64k + l) / 5): records of
+    // one owner ranked next to each other make contiguous 512-B stores, instead of each lane
+    // writing five 8-B pieces 40 B apart
+    uint2* park = s_park[wv];
+    park[lane * 5 + 0] = make_uint2(a.x, a.y);
+    park[lane * 5 + 1] = make_uint2(a.z, a.w);
+    park[lane * 5 + 2] = make_uint2(b.x, b.y);
+    park[lane * 5 + 3] = make_uint2(b.z, b.w);
+    park[lane * 5 + 4] = make_uint2(i, my_rank);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (uint32_t k = 0; k < 5; ++k) {
+        const uint32_t p = k * kWave + lane, rr = p / 5, part = p - rr * 5;
+        const uint32_t to = (uint32_t)__shfl((int)dst, (int)rr);
+        if (to != 0xffffffffu) reinterpret_cast<uint2*>(send + to)[part] = park[p];
+    }
 }
 
 // exclusive prefix over groups of grp[g][d], d < n_parts; one lane per group; leaves grp zero
@@ -226,32 +242,35 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EMURX_LO
 int emurx_launch_owner_count(const uint8_t* frames, const emurx_desc* desc, uint32_t n, uint32_t n_parts,
                              uint32_t* send_count, uint32_t* tile_cnt, uint32_t* grp, uint32_t* grp_off,
                              hipStream_t st) {
+    (void)hipGetLastError();  // a status left by the caller's own failed HIP call is not this launch's
     using namespace emurx;
     const uint32_t ntiles = (n + kBlock - 1) / kBlock, ngroups = (ntiles + kGroup - 1) / kGroup;
-    if (n == 0) return hipMemsetAsync(send_count, 0, n_parts * sizeof(uint32_t), st) == hipSuccess ? 0 : -1;
+    if (n == 0) return EMURX_HIP_OK(hipMemsetAsync(send_count, 0, n_parts * sizeof(uint32_t), st)) ? 0 : -1;
     if (ngroups > kScanThreads) return -1;
     hipLaunchKernelGGL(k_owner_count, dim3(ntiles), dim3(kBlock), 0, st, frames, desc, n, n_parts, tile_cnt, grp);
     hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(kScanThreads), 0, st, grp, ngroups, n_parts, grp_off, send_count);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    return EMURX_HIP_OK(hipGetLastError()) ? 0 : -1;
 }
 
 int emurx_launch_lookup(const emurx_lookup_rec* recv, const uint32_t* recv_count, uint32_t n_parts, uint32_t cap,
                         const emurx_dev_tables& T, emurx_route_rec* out, uint32_t* flow, hipStream_t st) {
+    (void)hipGetLastError();  // a status left by the caller's own failed HIP call is not this launch's
     using namespace emurx;
     if (n_parts && cap) {
         if (n_parts > 65535) return -1;
         hipLaunchKernelGGL(k_lookup, dim3((cap + kBlock - 1) / kBlock, n_parts), dim3(kBlock), 0, st, recv, recv_count,
                            n_parts, cap, T, out, flow);
     }
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    return EMURX_HIP_OK(hipGetLastError()) ? 0 : -1;
 }
 
 int emurx_launch_route(const emurx_rec* rec, uint32_t n, uint32_t n_parts, uint32_t my_rank, uint32_t cap,
                        emurx_route_rec* send, uint32_t* send_count, uint32_t* tile_cnt, uint32_t* grp,
                        uint32_t* grp_off, hipStream_t st, bool counted) {
+    (void)hipGetLastError();  // a status left by the caller's own failed HIP call is not this launch's
     using namespace emurx;
     const uint32_t ntiles = (n + kBlock - 1) / kBlock, ngroups = (ntiles + kGroup - 1) / kGroup;
-    if (n == 0) return hipMemsetAsync(send_count, 0, n_parts * sizeof(uint32_t), st) == hipSuccess ? 0 : -1;
+    if (n == 0) return EMURX_HIP_OK(hipMemsetAsync(send_count, 0, n_parts * sizeof(uint32_t), st)) ? 0 : -1;
     if (ngroups > kScanThreads) return -1;
     if (!counted)  // else k_rx counted the owners of this batch (emurx_set_route_parts)
         hipLaunchKernelGGL(k_route<false>, dim3(ntiles), dim3(kBlock), 0, st, rec, n, n_parts, my_rank, tile_cnt,
@@ -259,5 +278,5 @@ int emurx_launch_route(const emurx_rec* rec, uint32_t n, uint32_t n_parts, uint3
     hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(kScanThreads), 0, st, grp, ngroups, n_parts, grp_off, send_count);
     hipLaunchKernelGGL(k_route<true>, dim3(ntiles), dim3(kBlock), 0, st, rec, n, n_parts, my_rank, tile_cnt, grp,
                        grp_off, send, cap);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    return EMURX_HIP_OK(hipGetLastError()) ? 0 : -1;
 }

@@ -271,12 +271,13 @@ size_t emurx_txz_scratch_bytes(uint32_t n) {
 
 int emurx_launch_tx_zmq(const uint8_t* frames, const emurx_desc* desc, uint32_t n, uint8_t* out, uint64_t cap,
                         uint64_t* msg_off, uint64_t* info, void* scratch, hipStream_t st) {
+    (void)hipGetLastError();  // a status left by the caller's own failed HIP call is not this launch's
     using namespace emurx;
     unsigned long long* mo = reinterpret_cast<unsigned long long*>(msg_off);
     unsigned long long* inf = reinterpret_cast<unsigned long long*>(info);
     if (n == 0) {
         hipLaunchKernelGGL(k_txz_finish, dim3(1), dim3(64), 0, st, nullptr, nullptr, 0u, mo, inf);
-        return hipGetLastError() == hipSuccess ? 0 : -1;
+        return EMURX_HIP_OK(hipGetLastError()) ? 0 : -1;
     }
     struct Level {
         uint32_t units;
@@ -313,5 +314,5 @@ int emurx_launch_tx_zmq(const uint8_t* frames, const emurx_desc* desc, uint32_t 
                            lv[k - 1].BB);
     hipLaunchKernelGGL(k_txz_write, dim3((nt + 3) / 4), dim3(256), 0, st, frames, desc, n, nt, lv[0].E, lv[0].MB,
                        lv[0].BB, out, (unsigned long long)cap, mo);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    return EMURX_HIP_OK(hipGetLastError()) ? 0 : -1;
 }
