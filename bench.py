@@ -507,6 +507,10 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
+        # hold the launch stream (a ~20 ms spin) while the host enqueues every step, so the
+        # events time the device work back to back, not the host's enqueue of each call
+        with torch.cuda.stream(stream):
+            torch.cuda._sleep(50_000_000)
         for k in range(reps):
             e = ev[k]
             e[0].record(stream)
@@ -680,8 +684,11 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
     parse_s = float(np.mean(pk)) * 1e-3 if len(pk) else float("nan")
     achieved = alg_bytes / parse_s / 1e9
     traffic, pmc_src = None, None
-    pmc = ROOT / "profiles" / f"pmc_config{cfg}.json"
-    if pmc.exists() and mode in ("none", "replicated"):
+    # the PMC passes of the same config and table mode (tools/round_profile.sh: D = partitioned,
+    # DN = --tables none, DR = replicated)
+    tag = cfg + ({"none": "N", "replicated": "R"}.get(mode, "") if cfg == "D" else "")
+    pmc = ROOT / "profiles" / f"pmc_config{tag}.json"
+    if pmc.exists():
         try:
             traffic = json.loads(pmc.read_text()).get("k_rx_hbm_bytes_per_launch")
             pmc_src = str(pmc.relative_to(ROOT))

@@ -11,8 +11,9 @@ The batch slot (frames, their ZMQ headers, descriptors) is read once as a stream
 bytes, taken from the pass's own bench line), so FETCH_SIZE - alg_read / 2 is the excess: table-probe lines that left L2
 (config B, C, D) or, on the window path (config E), the long spans read a second time (a
 stream again).  Reported per launch (the first three dispatches dropped):
-  k_rx_hbm_bytes_per_launch     alg_read + excess x 1 + write   (excess as probe lines)
+  bytes_if_excess_probe_lines   alg_read + excess x 1 + write   (excess as probe lines)
   bytes_if_excess_streamed      alg_read + excess x 2 + write   (excess as streaming re-reads)
+  k_rx_hbm_bytes_per_launch     the first, or with --excess-streamed (config E) the second
 Both count Infinity-Cache hits as memory traffic (FETCH_SIZE cannot tell them apart).
 """
 import csv
@@ -46,6 +47,7 @@ def alg_read_bytes(d):
 
 
 d = sys.argv[1]
+streamed = "--excess-streamed" in sys.argv[2:]  # the window path's re-read spans (config E)
 f, w = per_dispatch(d, "FETCH_SIZE"), per_dispatch(d, "WRITE_SIZE")
 if not f or not w:
     print("no PMC rows found")
@@ -57,8 +59,10 @@ ar = alg_read_bytes(d)
 if ar:
     excess = max(fetch - ar / 2, 0.0)
     out.update({"alg_read_bytes": ar, "excess_fetch_bytes": round(excess),
-                "k_rx_hbm_bytes_per_launch": round(ar + excess + wr),
-                "bytes_if_excess_streamed": round(ar + 2 * excess + wr)})
+                "bytes_if_excess_probe_lines": round(ar + excess + wr),
+                "bytes_if_excess_streamed": round(ar + 2 * excess + wr),
+                "excess_read_as": "streamed (window-path re-reads)" if streamed else "probe lines"})
+    out["k_rx_hbm_bytes_per_launch"] = out["bytes_if_excess_streamed" if streamed else "bytes_if_excess_probe_lines"]
 else:  # no bench line: the round-2 rule (every fetch a streaming read)
     out["k_rx_hbm_bytes_per_launch"] = round(2 * fetch + wr)
 out["rule"] = ("calibrated (profiles/r03/pmc_calib.json): stream reads = 2 x FETCH_SIZE share, probe lines = "

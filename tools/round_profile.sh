@@ -52,7 +52,8 @@ for ph in $phases; do
           step pmc_${c}_$k 180 rocprofv3 --pmc $k -T --kernel-include-regex k_rx -d $out/pmc_${c}/pmc_$k -o run \
             --output-format csv -- python bench.py $(args $c) --steps 40 --warmup 8 --no-cpu-baseline --no-check --no-replay
         done
-        python tools/pmc_summary.py $out/pmc_${c} > $out/pmc_config$c.json 2>&1; cat $out/pmc_config$c.json ;;
+        xs=""; [ "$c" = E ] && xs="--excess-streamed"  # E's excess: long spans read again (window path)
+        python tools/pmc_summary.py $out/pmc_${c} $xs > $out/pmc_config$c.json 2>&1; cat $out/pmc_config$c.json ;;
     esac
   done
 done

@@ -218,7 +218,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EMURX_LO
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (idx >= cnt) return;
+    const bool live = idx < cnt;
     const uint4* p = &s_rec[wv][lane * 4];
     const uint4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
     const uint32_t w[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
@@ -227,14 +227,27 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EMURX_LO
     Tuple t;
     const LKey k = unpack_lookup(w, r, t);
     // frames that reached no callback travel too (their owner keeps their record): no lookup
-    if (r.status == EMURX_ST_OK) resolve(T, r, k, [&](uint32_t cid) { return flow_probe(T, t, cid); });
-    uint2* o = reinterpret_cast<uint2*>(out + j);  // 40 B, 8-B aligned
-    o[0] = make_uint2(r.ns, r.cl);
-    o[1] = make_uint2(r.vlan0, r.vlan1);
-    o[2] = make_uint2(r.vport | (r.l3 << 16), r.l4 | (r.l7 << 16));
-    o[3] = make_uint2(r.l7len | (r.nh << 16) | (r.proto << 24), r.status | (r.flags << 8));
-    o[4] = make_uint2(w[0], src);
-    if (flow) flow[j] = r.flow;
+    if (live && r.status == EMURX_ST_OK) resolve(T, r, k, [&](uint32_t cid) { return flow_probe(T, t, cid); });
+    // The wave's outputs are contiguous: its 40-B records are parked in its (now read) LDS rows
+    // and written back as five 8-B pieces per lane, 512 contiguous bytes per store instruction,
+    // instead of five 8-B stores per lane 40 B apart
+    uint2* park = reinterpret_cast<uint2*>(s_rec[wv]);
+    if (live) {
+        park[lane * 5 + 0] = make_uint2(r.ns, r.cl);
+        park[lane * 5 + 1] = make_uint2(r.vlan0, r.vlan1);
+        park[lane * 5 + 2] = make_uint2(r.vport | (r.l3 << 16), r.l4 | (r.l7 << 16));
+        park[lane * 5 + 3] = make_uint2(r.l7len | (r.nh << 16) | (r.proto << 24), r.status | (r.flags << 8));
+        park[lane * 5 + 4] = make_uint2(w[0], src);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint2* o = reinterpret_cast<uint2*>(out + (uint64_t)src * cap + idx0);  // 8-B aligned
+    const uint32_t npieces = min(kWave, cnt - idx0) * 5;
+#pragma unroll
+    for (uint32_t k5 = 0; k5 < 5; ++k5)
+        if (k5 * kWave + lane < npieces) o[k5 * kWave + lane] = park[k5 * kWave + lane];
+    if (flow && live) flow[j] = r.flow;
 }
 
 }  // namespace emurx
