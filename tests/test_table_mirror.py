@@ -251,7 +251,8 @@ def test_partitioned_image(oracle_built, parts):
             m.ip6[(int(c["ns"][i]), c["ipv6"][i].tobytes())] = int(c["cid"][i])
             m.cl[int(c["cid"][i])] = dict(ns=int(c["ns"][i]), plugins=0x7FF)
         m.check(rx, owned=lambda nsid: owner[nsid] == p)
-    assert max(sizes) <= total / parts + 4096 * 16, (sizes, total)  # + the dense ns info
+    # + the dense ns info and the transport tables' minimum sizes (a few tens of KB a partition)
+    assert max(sizes) <= total / parts + 4096 * 16 + (1 << 16), (sizes, total)
 
 
 def test_partition_growth(oracle_built):

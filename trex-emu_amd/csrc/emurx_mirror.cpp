@@ -7,6 +7,8 @@
 #include "emurx_mirror.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 
 namespace emurx_host {
 namespace {
@@ -84,8 +86,32 @@ void Mirror::clean_all() {
     for (int k = 0; k < kNumTabs; ++k) hashes(k)->clean();
 }
 
-// Every table starts at load <= 1/2 for its share of max_ns / max_clients (the whole of them
-// with one partition, 1/n of them plus slack with n) and grows on demand.
+// Slots per entry by table (ns, mac, ip4, ip6, ci, ft4, ft6, srv).  A wave's lookups take as
+// many dependent memory trips as the longest probe chain among its 64 lanes; at load 1/2,
+// 93 % of 64-lane waves hold a key outside its 4-slot home bucket (2-slot buckets: all of
+// them), at 1/8 (1/16 for 2 slots) about 2 % (4 %).  EMURX_TABLE_SPREAD="ns,mac,ip,ci"
+// overrides the first five (the ip value for both IP tables), for measurements.
+namespace {
+struct Spread {
+    uint32_t v[kNumTabs] = {8, 8, 16, 16, 16, 16, 32, 8};
+    Spread() {
+        const char* s = getenv("EMURX_TABLE_SPREAD");
+        unsigned a = 0, b = 0, c = 0, d = 0;
+        if (!s || sscanf(s, "%u,%u,%u,%u", &a, &b, &c, &d) != 4) return;
+        const unsigned w[5] = {a, b, c, c, d};
+        for (int k = 0; k < 5; ++k)
+            if (w[k] >= 2 && w[k] <= 64 && !(w[k] & (w[k] - 1))) v[k] = w[k];
+    }
+};
+const uint32_t* table_spread() {
+    static const Spread s;
+    return s.v;
+}
+constexpr uint64_t kSpreadCap = 2ull << 30;  // bytes per table
+}  // namespace
+
+// Every table starts at its target load (1 / spread) for its share of max_ns / max_clients
+// (the whole of them with one partition, 1/n of them plus slack with n) and grows on demand.
 void Mirror::set_partition(uint32_t n, uint32_t p) {
     n_parts = std::max<uint32_t>(n, 1);
     part = p;
@@ -107,9 +133,16 @@ void Mirror::set_partition(uint32_t n, uint32_t p) {
     // table grows when they come)
     const uint64_t want[kNumTabs] = {ens, ecl, ecl, ecl, ecl, 8, 8, 16};
     const uint32_t per[kNumTabs] = {4, 4, 2, 2, 2, 2, 1, 4};
+    const uint32_t* sp = table_spread();
     for (int k = 0; k < kNumTabs; ++k) {
         const uint64_t e = std::max(want[k], (need[k] + n_parts - 1) / n_parts);
-        rebuild(k, std::max<uint32_t>(pow2_at_least(2 * e) / per[k], 1));
+        // sparser tables cost bytes, not lookups; above kSpreadCap a table falls back towards
+        // the load of 1/2
+        uint32_t s = sp[k];
+        while (s > 2 && (uint64_t)pow2_at_least((uint64_t)s * e) * (EMURX_BUCKET_WORDS / per[k]) * 4 > kSpreadCap)
+            s >>= 1;
+        hashes(k)->spread = s;
+        rebuild(k, std::max<uint32_t>(pow2_at_least((uint64_t)s * e) / per[k], 1));
     }
     nsinfo.resize_blocks(nsinfo.nblocks());
     for (uint32_t i = 0; i < max_ns; ++i)

@@ -74,9 +74,12 @@ struct Blocks {
     }
 };
 
-// open addressing over 64-byte buckets (emurx_tables.h), slots of `words` words
+// open addressing over 64-byte buckets (emurx_tables.h), slots of `words` words.
+// `spread` is the table's target of slots per live entry (a power of two >= 2): a lookup's
+// wave waits for the longest probe chain among its 64 lanes, so the tables are kept sparse
+// enough that almost every key sits in its home bucket (emurx_table_spread).
 struct Hash : Blocks {
-    uint32_t words = 4, buckets = 0, live = 0, tomb = 0;
+    uint32_t words = 4, buckets = 0, live = 0, tomb = 0, spread = 2;
     uint32_t per() const { return EMURX_BUCKET_WORDS / words; }
     uint32_t nslots() const { return buckets * per(); }
     uint32_t mask() const { return buckets - 1; }
@@ -89,11 +92,15 @@ struct Hash : Blocks {
         at(s)[word] = v;
         touch(s / per());
     }
-    // k more inserts would take live + tombstones past 3/4 of the slots
-    bool full(uint32_t k = 1) const { return (uint64_t)(live + tomb + k) * 4 > (uint64_t)nslots() * 3; }
-    // bucket count for a rebuild: doubled once live would pass 1/2
+    // k more inserts would take live + tombstones past 2 / spread of the slots (3/4 at
+    // spread 2): twice the target load, then a rebuild drops the tombstones
+    bool full(uint32_t k = 1) const {
+        const uint64_t used = (uint64_t)live + tomb + k;
+        return spread <= 2 ? used * 4 > (uint64_t)nslots() * 3 : used * spread > (uint64_t)nslots() * 2;
+    }
+    // bucket count for a rebuild: doubled once live would pass the target load 1 / spread
     uint32_t next_buckets(uint32_t k = 1) const {
-        return (uint64_t)(live + k) * 2 > nslots() ? buckets * 2 : buckets;
+        return (uint64_t)(live + k) * spread > nslots() ? buckets * 2 : buckets;
     }
 };
 
