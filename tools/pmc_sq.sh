@@ -4,11 +4,13 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-out=gpurun_out/pmc_sq; rm -rf $out; mkdir -p $out
+out=gpurun_out/pmc_sq${PMC_TAG:-}; rm -rf $out; mkdir -p $out
 timeout -s KILL 60 rocprofv3 -L > $out/counters_list.txt 2>&1
 i=0
 mode=${1:-sq}; shift || true
-if [ "$mode" = mem ]; then
+if [ "$mode" = icache ]; then
+  SETS="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_IFETCH SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE GRBM_GUI_ACTIVE"
+elif [ "$mode" = mem ]; then
   SETS="TA_TA_BUSY TA_ADDR_STALLED_BY_TC_CYCLES GRBM_GUI_ACTIVE
 TA_DATA_STALLED_BY_TC_CYCLES TA_ADDR_STALLED_BY_TD_CYCLES GRBM_GUI_ACTIVE
 TCP_TCC_READ_REQ_LATENCY TCP_TCC_READ_REQ TCP_PENDING_STALL_CYCLES TCP_READ_TAGCONFLICT_STALL_CYCLES GRBM_GUI_ACTIVE
@@ -25,10 +27,10 @@ while read -r set; do
       -- python bench.py --steps 40 --warmup 8 --no-cpu-baseline --no-check "$@" > $out/p$i.log 2>&1
   rc=$?; echo "rc=$rc"; [ $rc -eq 0 ] || { tail -3 $out/p$i.log; exit $rc; }
 done <<< "$SETS"
-python - <<'PY'
-import csv, glob, collections
+OUT=$out python - <<'PY'
+import csv, glob, collections, os
 tot = collections.defaultdict(list)
-for f in glob.glob("gpurun_out/pmc_sq/p*/**/*counter_collection.csv", recursive=True):
+for f in glob.glob(os.environ["OUT"] + "/p*/**/*counter_collection.csv", recursive=True):
     per = collections.defaultdict(float)
     for r in csv.DictReader(open(f)):
         per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
