@@ -9,6 +9,10 @@
   batch start that is NOT flagged stale equals Go's classification of that frame against the
   maps as the callbacks of the earlier frames of the batch left them (DHCP's UpdateClientIpv4
   dhcp.go:718, client add / remove, plugin changes, Namespace add / remove mid-batch)."""
+import os
+import subprocess
+import sys
+
 import numpy as np
 import pytest
 
@@ -333,3 +337,40 @@ def test_mid_batch_rule(oracle_built):
             spare += op == 3
     assert differ > 20, differ           # the mutations did change later classifications
     assert stale_n < n // 2, stale_n     # and the rule flags a minority of the batch
+
+
+def _image_bytes(max_ns, max_clients):
+    return RxPath(-1, max_ns=max_ns, max_clients=max_clients, max_frames=64).table_stats()["table_bytes"]
+
+
+def _sparse_bytes(max_ns, max_clients, sp):
+    """Expected image bytes of an empty handle: slots = next power of two >= spread x entries
+    (emurx_mirror.cpp set_partition), times the slot size, plus the dense ns info."""
+    def p2(v):
+        p = 16
+        while p < v:
+            p <<= 1
+        return p
+    ns, mac, ip, ci = sp
+    return (p2(ns * max_ns) * 16 + p2(mac * max_clients) * 16 + 2 * p2(ip * max_clients) * 32
+            + p2(ci * max_clients) * 32 + p2(16 * 8) * 32 + p2(32 * 8) * 64 + p2(8 * 16) * 16 + max_ns * 16)
+
+
+def test_sparse_table_sizes(oracle_built):
+    """Tables start at their target spread (slots per entry: 8 for ns / MAC, 16 for IPv4 /
+    IPv6 / client info), so that almost every key of a 64-lane wave sits in its home bucket."""
+    assert _image_bytes(1024, 4096) == _sparse_bytes(1024, 4096, (8, 8, 16, 16))
+
+
+def test_table_spread_override():
+    """EMURX_TABLE_SPREAD="ns,mac,ip,ci" (read once per process) sets the spreads; malformed
+    values keep the defaults."""
+    code = ("import sys; sys.path.insert(0, 'trex-emu_amd'); from emurx.rx import RxPath; "
+            "print(RxPath(-1, max_ns=1024, max_clients=4096, max_frames=64).table_stats()['table_bytes'])")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for env, sp in (("2,2,2,2", (2, 2, 2, 2)), ("4,8,32,2", (4, 8, 32, 2)), ("3,8,16,16", (8, 8, 16, 16)),
+                    ("junk", (8, 8, 16, 16))):
+        out = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=120,
+                             env={**os.environ, "EMURX_TABLE_SPREAD": env})
+        assert out.returncode == 0, out.stderr
+        assert int(out.stdout.split()[-1]) == _sparse_bytes(1024, 4096, sp), env
