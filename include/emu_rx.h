@@ -220,7 +220,13 @@ typedef struct emurx_cfg {
                               generations and image queries, no device: data-path calls
                               return EMURX_EDEVICE) */
     uint32_t max_ns;       /* ns ids must be < max_ns */
-    uint32_t max_clients;  /* client ids must be < max_clients */
+    uint32_t max_clients;  /* client ids must be < max_clients.  The device tables are sized
+                              for max_ns / max_clients and kept sparse so that a lookup
+                              almost always ends in its home bucket: about 128 B of device
+                              memory per Namespace and 1.7 KB per client (MAC, IPv4, IPv6,
+                              client info), 1/n_parts of that when partitioned; env
+                              EMURX_TABLE_SPREAD="ns,mac,ip,ci" (slots per entry, powers of
+                              two >= 2; default 8,8,16,16) trades them back */
     uint32_t max_frames;   /* frames per batch (device scratch is sized for it) */
     uint32_t max_bytes;    /* bytes per host batch (emurx_rx_stream staging) */
 } emurx_cfg;
