@@ -9,6 +9,7 @@ the table mirror's random mutation sequences, partitions and mid-batch rule
 test_host_fuzz.py), and the oracle's known-answer, edge, corpus, flow, tx and fuzz tests.  Any
 sanitizer report fails the run (halt_on_error); a positive control proves the instrumentation
 is live."""
+import fcntl
 import os
 import subprocess
 import sys
@@ -26,8 +27,14 @@ SUITES = ["tests/test_table_mirror.py", "tests/test_abi.py", "tests/test_host_fu
 
 @pytest.fixture(scope="module")
 def asan_env():
-    subprocess.run(["make", "-s", "-C", str(ROOT / "trex-emu_amd"), "asan"], check=True)
-    subprocess.run(["make", "-s", "-C", str(ROOT / "oracle"), "asan"], check=True)
+    # one build at a time: with pytest-xdist both tests of this module may start in two workers,
+    # and a library being relinked by one must not be loaded by the other
+    (ROOT / "trex-emu_amd" / "build").mkdir(exist_ok=True)
+    with open(ROOT / "trex-emu_amd" / "build" / ".asan.lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.run(["make", "-s", "-C", str(ROOT / "trex-emu_amd"), "asan"], check=True)
+        subprocess.run(["make", "-s", "-C", str(ROOT / "oracle"), "asan"], check=True)
+        fcntl.flock(lk, fcntl.LOCK_UN)
     libasan = subprocess.run(["g++", "-print-file-name=libasan.so"], capture_output=True, text=True,
                              check=True).stdout.strip()
     env = dict(os.environ)
