@@ -130,7 +130,9 @@ __global__ __launch_bounds__(64) void k_txz_descend(const uint32_t* __restrict__
                                                     const uint32_t* __restrict__ Ep, const uint32_t* __restrict__ MBp,
                                                     const unsigned long long* __restrict__ BBp,
                                                     uint32_t* __restrict__ Ec, uint32_t* __restrict__ MBc,
-                                                    unsigned long long* __restrict__ BBc) {
+                                                    unsigned long long* __restrict__ BBc, uint32_t n,
+                                                    unsigned long long* __restrict__ msg_off,
+                                                    unsigned long long* __restrict__ info) {
     __shared__ uint32_t sx[64][kWave], sm[64][kWave];
     __shared__ unsigned long long sb[64];
     __shared__ uint32_t se[64], smb[64];
@@ -143,6 +145,13 @@ __global__ __launch_bounds__(64) void k_txz_descend(const uint32_t* __restrict__
     }
     sb[lane] = lane < cn ? Bc[c0 + lane] : 0ull;
     __syncthreads();
+    if (info && lane == 0) {  // the root (entry 0): message count and total size (k_txz_finish)
+        const unsigned long long nm = sm[0][0];
+        const unsigned long long total = 4ull * nm + 4ull * n + sb[0];
+        info[0] = nm;
+        info[1] = total;
+        msg_off[nm] = total;
+    }
     if (lane == 0) {
         uint32_t e = Ep ? Ep[p] : 0u, mb = MBp ? MBp[p] : 0u;
         unsigned long long bb = BBp ? BBp[p] : 0ull;
@@ -181,17 +190,48 @@ __device__ __forceinline__ void put_be32(uint8_t* out, unsigned long long at, un
         if (at + k < cap) out[at + k] = (uint8_t)(v >> (24 - 8 * k));
 }
 
+// LDS budget of the staged write path, per wave: the source blocks of the tile's frames and the
+// tile's output bytes (headers + frames), both as 16-byte rows
+constexpr uint32_t kTxSrc = 6144, kTxOut = 6144 + 32;
+static_assert(kTxSrc % (16 * kWave) == 0, "whole 1 KiB LDS-DMA rows");
+
+// OR a little-endian word v into LDS bytes [p, p + 4) (dwords at p >> 2 and the next one)
+__device__ __forceinline__ void lds_or4(uint32_t* o32, uint32_t p, uint32_t v) {
+    const uint32_t sh = 8 * (p & 3);
+    atomicOr(&o32[p >> 2], v << sh);
+    if (sh) atomicOr(&o32[(p >> 2) + 1], v >> (32 - sh));
+}
+
+// kStaged: the tiles whose source blocks and output fit the LDS budget (above), else the rest:
+// two launches, so that the long-frame tiles keep the occupancy of a kernel without the LDS
+template <bool kStaged>
 __global__ __launch_bounds__(256) void k_txz_write(const uint8_t* __restrict__ frames,
                                                    const emurx_desc* __restrict__ d, uint32_t n, uint32_t ntiles,
                                                    const uint32_t* __restrict__ E, const uint32_t* __restrict__ MB,
                                                    const unsigned long long* __restrict__ BB,
                                                    uint8_t* __restrict__ out, unsigned long long cap,
-                                                   unsigned long long* __restrict__ msg_off) {
+                                                   unsigned long long* __restrict__ msg_off,
+                                                   uint32_t* __restrict__ done) {
     __shared__ uint32_t s_q[4][2 * kWave];
     const uint32_t wv = threadIdx.x / kWave, lane = lane_id();
     const uint32_t t = blockIdx.x * 4 + wv;
     if (t >= ntiles) return;  // wave-uniform
+    if (!kStaged && done[t]) return;  // the staged launch wrote this tile
     const uint32_t base = t * kTxTile;
+    if constexpr (kStaged) {  // decided from the descriptors alone, before the chain work:
+        // the output range is at most the frame bytes + 8 per frame (its header and, at most,
+        // a message header), so this bound implies the image fits
+        const uint32_t lim0 = min(n - base, kTxTile);
+        const bool v0 = lane < lim0;
+        const emurx_desc d0 = v0 ? d[base + lane] : emurx_desc{0, 0, 0, 0};
+        const uint32_t slo = wave_min_u32(v0 ? d0.off : 0xffffffffu);
+        const uint32_t shi = wave_max_u32(v0 ? d0.off + d0.len : 0u);
+        const uint32_t nsv = shi > slo ? (shi - (slo & ~15u) + 15) >> 4 : 0u;
+        const uint32_t tot = wave_reduce((uint32_t)d0.len, [](uint32_t x, uint32_t y) { return x + y; });
+        const bool fits = nsv * 16 <= kTxSrc && tot + 8 * lim0 + 32 <= kTxOut;  // wave-uniform
+        if (lane == 0) done[t] = fits;
+        if (!fits) return;  // the long-frame launch's tile
+    }
     uint32_t len;
     const uint32_t er = tx_endrel(d, n, base, s_q[wv], len);
     const uint32_t lim = min(n - base, kTxTile);
@@ -206,6 +246,83 @@ __global__ __launch_bounds__(256) void k_txz_write(const uint8_t* __restrict__ f
     const uint32_t pre = wave_incl_scan_u32(len) - len;
     const unsigned long long fo = 4ull * (msg + 1ull) + 4ull * (base + lane) + BB[t] + pre;
     const emurx_desc dl = valid ? d[base + lane] : emurx_desc{0, 0, 0, 0};
+    const bool st = valid && ((starts >> lane) & 1);  // this frame opens a message
+    // ---- staged path: the tile's output is one contiguous range [o0, o1): built in LDS (the
+    // source blocks by coalesced LDS-DMA, headers and frame bytes OR-ed into a zeroed image at
+    // their offsets, funnel-shifted a dword at a time), then written as aligned 16-byte rows;
+    // only the partial rows at both ends go out byte by byte (they share lines with the
+    // neighbouring tiles' output)
+    {
+        const uint32_t slo = wave_min_u32(valid ? dl.off : 0xffffffffu);
+        const uint32_t shi = wave_max_u32(valid ? dl.off + len : 0u);
+        const unsigned long long o0 =
+            ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(fo >> 32)) << 32 |
+             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)fo)) - ((starts & 1) ? 4 : 0);
+        const uint32_t last = lim - 1;
+        const unsigned long long o1 =
+            ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(fo >> 32), (int)last) << 32 |
+             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)fo, (int)last)) + 4 +
+            (uint32_t)__builtin_amdgcn_readlane((int)len, (int)last);
+        const uint32_t sbase = slo & ~15u, nsv = shi > slo ? (shi - sbase + 15) >> 4 : 0u;
+        const unsigned long long obase = o0 & ~15ull;
+        const uint32_t nrow = (uint32_t)(((o1 + 15) & ~15ull) - obase) >> 4;
+        if constexpr (kStaged) {  // nsv, nrow within the budget (the test above)
+            __shared__ __attribute__((aligned(16))) uint32_t s_src[4][(kTxSrc + 16) / 4];
+            __shared__ __attribute__((aligned(16))) uint32_t s_out[4][kTxOut / 4];
+            uint32_t* src = s_src[wv];
+            uint32_t* o32 = s_out[wv];
+            // source blocks land 16 bytes into the slab: a frame's first dword read may start
+            // up to 3 bytes before it
+            const uint4* gs = reinterpret_cast<const uint4*>(frames + sbase);
+#pragma unroll
+            for (uint32_t k = 0; k < kTxSrc / 16 / kWave; ++k)
+                if (k * kWave < nsv)
+                    __builtin_amdgcn_global_load_lds(gs + min(lane + k * kWave, nsv - 1),
+                                                     (__attribute__((address_space(3))) void*)(src + 4 + k * kWave * 4),
+                                                     16, 0, 0);
+            for (uint32_t r = lane; r < kTxOut / 16; r += kWave) reinterpret_cast<uint4*>(o32)[r] = make_uint4(0, 0, 0, 0);
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (valid) {
+                const uint32_t p = (uint32_t)(fo - obase);  // the frame header in the image
+                if (st) lds_or4(o32, p - 4, __builtin_bswap32(((uint32_t)EMURX_ZMQ_MAGIC << 16) + er));
+                lds_or4(o32, p, __builtin_bswap32(((uint32_t)EMURX_ZMQ_PKT_MAGIC << 24) + ((uint32_t)dl.vport << 16) + dl.len));
+                // frame bytes: image dword j gets source bytes [4j - p4 + q, + 4), masked to the frame
+                const uint32_t p4 = p + 4, q = dl.off - sbase + 16, e = p4 + len;
+                if (len) {
+                    for (uint32_t j = p4 >> 2; j <= (e - 1) >> 2; ++j) {
+                        const uint32_t sb = 4 * j + q - p4;  // >= 13: the 16-byte lead
+                        const uint32_t v = __builtin_amdgcn_alignbyte(src[(sb >> 2) + 1], src[sb >> 2], sb & 3);
+                        const uint32_t m0 = 4 * j < p4 ? 0xffffffffu << (8 * (p4 & 3)) : 0xffffffffu;
+                        const uint32_t m1 = 4 * j + 4 > e ? 0xffffffffu >> (8 * (4 * j + 4 - e)) : 0xffffffffu;
+                        const uint32_t m = m0 & m1;
+                        if (m == 0xffffffffu) o32[j] = v;  // no other lane writes this dword
+                        else atomicOr(&o32[j], v & m);
+                    }
+                }
+                if (st) msg_off[msg] = fo - 4;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            typedef unsigned v4u __attribute__((ext_vector_type(4)));
+            for (uint32_t r = lane; r < nrow; r += kWave) {
+                const unsigned long long x = obase + 16ull * r;
+                const uint4 v = reinterpret_cast<const uint4*>(o32)[r];
+                if (x >= o0 && x + 16 <= o1 && x + 16 <= cap) {
+                    __builtin_nontemporal_store(v4u{v.x, v.y, v.z, v.w}, reinterpret_cast<v4u*>(out + x));
+                } else {
+                    const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (uint32_t j = 0; j < 16; ++j)
+                        if (x + j >= o0 && x + j < o1 && x + j < cap) out[x + j] = (uint8_t)(w4[j >> 2] >> (8 * (j & 3)));
+                }
+            }
+            return;
+        }
+    }
     if (valid) {
         if ((starts >> lane) & 1) {
             msg_off[msg] = fo - 4;
@@ -265,8 +382,8 @@ __global__ __launch_bounds__(256) void k_txz_write(const uint8_t* __restrict__ f
 // ---------------------------------------------------------------------------------------
 size_t emurx_txz_scratch_bytes(uint32_t n) {
     size_t bytes = 0;
-    for (uint32_t u = (n + 63) / 64; u; u = u > 1 ? (u + 63) / 64 : 0) bytes += (size_t)u * (64 * 8 + 8 + 8 + 8);
-    return bytes + 256;
+    for (uint32_t u = (n + 63) / 64; u; u = u > 1 ? (u + 63) / 64 : 0) bytes += (size_t)u * (64 * 8 + 8 + 8 + 8) + 16;
+    return bytes + (size_t)((n + 63) / 64) * 4 + 256;  // + the staged write's tile flags
 }
 
 int emurx_launch_tx_zmq(const uint8_t* frames, const emurx_desc* desc, uint32_t n, uint8_t* out, uint64_t cap,
@@ -300,19 +417,22 @@ int emurx_launch_tx_zmq(const uint8_t* frames, const emurx_desc* desc, uint32_t 
         if (u == 1) break;
     }
     const uint32_t nt = lv[0].units;
+    uint32_t* done = reinterpret_cast<uint32_t*>(p);  // [nt] tiles the staged write took
     hipLaunchKernelGGL(k_txz_leaf, dim3((nt + 3) / 4), dim3(256), 0, st, desc, n, nt, lv[0].X, lv[0].M, lv[0].B);
     for (int k = 1; k < L; ++k)
         hipLaunchKernelGGL(k_txz_compose, dim3(lv[k].units), dim3(64), 0, st, lv[k - 1].X, lv[k - 1].M, lv[k - 1].B,
                            lv[k - 1].units, lv[k].X, lv[k].M, lv[k].B);
-    hipLaunchKernelGGL(k_txz_finish, dim3(1), dim3(64), 0, st, lv[L - 1].M, lv[L - 1].B, n, mo, inf);
-    // the root (one unit) has entry 0, base 0: its own descend writes E/MB/BB of level L-1
+    // the root (one unit) has entry 0, base 0: its own descend writes E/MB/BB of level L-1, the
+    // message count and the total size (info, msg_off[n_msgs])
     hipLaunchKernelGGL(k_txz_descend, dim3(1), dim3(64), 0, st, lv[L - 1].X, lv[L - 1].M, lv[L - 1].B, 1u,
-                       nullptr, nullptr, nullptr, lv[L - 1].E, lv[L - 1].MB, lv[L - 1].BB);
+                       nullptr, nullptr, nullptr, lv[L - 1].E, lv[L - 1].MB, lv[L - 1].BB, n, mo, inf);
     for (int k = L - 1; k >= 1; --k)
         hipLaunchKernelGGL(k_txz_descend, dim3(lv[k].units), dim3(64), 0, st, lv[k - 1].X, lv[k - 1].M,
                            lv[k - 1].B, lv[k - 1].units, lv[k].E, lv[k].MB, lv[k].BB, lv[k - 1].E, lv[k - 1].MB,
-                           lv[k - 1].BB);
-    hipLaunchKernelGGL(k_txz_write, dim3((nt + 3) / 4), dim3(256), 0, st, frames, desc, n, nt, lv[0].E, lv[0].MB,
-                       lv[0].BB, out, (unsigned long long)cap, mo);
+                           lv[k - 1].BB, n, (unsigned long long*)nullptr, (unsigned long long*)nullptr);
+    hipLaunchKernelGGL(k_txz_write<true>, dim3((nt + 3) / 4), dim3(256), 0, st, frames, desc, n, nt, lv[0].E,
+                       lv[0].MB, lv[0].BB, out, (unsigned long long)cap, mo, done);
+    hipLaunchKernelGGL(k_txz_write<false>, dim3((nt + 3) / 4), dim3(256), 0, st, frames, desc, n, nt, lv[0].E,
+                       lv[0].MB, lv[0].BB, out, (unsigned long long)cap, mo, done);
     return EMURX_HIP_OK(hipGetLastError()) ? 0 : -1;
 }
