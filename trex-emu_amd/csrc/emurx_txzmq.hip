@@ -184,15 +184,10 @@ __global__ void k_txz_finish(const uint32_t* __restrict__ Mroot, const unsigned 
     msg_off[nm] = total;
 }
 
-__device__ __forceinline__ void put_be32(uint8_t* out, unsigned long long at, unsigned long long cap, uint32_t v) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-        if (at + k < cap) out[at + k] = (uint8_t)(v >> (24 - 8 * k));
-}
-
 // LDS budget of the staged write path, per wave: the source blocks of the tile's frames and the
 // tile's output bytes (headers + frames), both as 16-byte rows
 constexpr uint32_t kTxSrc = 6144, kTxOut = 6144 + 32;
+constexpr uint32_t kTxSlow = 512;  // long-frame tiles: rows assembled byte by byte, listed per wave
 static_assert(kTxSrc % (16 * kWave) == 0, "whole 1 KiB LDS-DMA rows");
 
 // OR a little-endian word v into LDS bytes [p, p + 4) (dwords at p >> 2 and the next one)
@@ -323,54 +318,120 @@ __global__ __launch_bounds__(256) void k_txz_write(const uint8_t* __restrict__ f
             return;
         }
     }
+    // ---- long-frame tiles: the tile's output rows [o0 & ~15, o1) dealt over the lanes, each
+    // row's source found from the frames' segments in LDS (a forward walk: a lane's rows
+    // ascend), so that a wave keeps one load per lane in flight instead of copying its frames
+    // one after another.  A row inside one frame's bytes is two aligned 16-byte loads
+    // funnel-shifted into one aligned 16-byte store; rows holding headers or frame ends are
+    // assembled byte by byte.
+    if constexpr (!kStaged) {
+    __shared__ uint32_t s_seg[4][6][kWave];  // segment start, data start, source, length, header, message header
+    __shared__ uint32_t s_slow[4][kTxSlow];  // pass 2's rows: row << 6 | the frame its walk starts from
+    const unsigned long long o0 =
+        ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(fo >> 32)) << 32 |
+         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)fo)) - ((starts & 1) ? 4 : 0);
+    const uint32_t last = lim - 1;
+    const uint32_t R = (uint32_t)(((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(fo >> 32), (int)last) << 32 |
+                                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)fo, (int)last)) + 4 - o0) +
+                       (uint32_t)__builtin_amdgcn_readlane((int)len, (int)last);  // output bytes of the tile
+    uint32_t(*sg)[kWave] = s_seg[wv];
     if (valid) {
-        if ((starts >> lane) & 1) {
-            msg_off[msg] = fo - 4;
-            put_be32(out, fo - 4, cap, ((uint32_t)EMURX_ZMQ_MAGIC << 16) + er);
-        }
-        put_be32(out, fo, cap, ((uint32_t)EMURX_ZMQ_PKT_MAGIC << 24) + ((uint32_t)dl.vport << 16) + dl.len);
+        const uint32_t fr = (uint32_t)(fo - o0);  // the frame header, relative to o0
+        sg[0][lane] = st ? fr - 4 : fr;
+        sg[1][lane] = fr + 4;
+        sg[2][lane] = dl.off;
+        sg[3][lane] = len;
+        sg[4][lane] = ((uint32_t)EMURX_ZMQ_PKT_MAGIC << 24) + ((uint32_t)dl.vport << 16) + dl.len;
+        sg[5][lane] = st ? ((uint32_t)EMURX_ZMQ_MAGIC << 16) + er : 0u;
+        if (st) msg_off[msg] = fo - 4;
     }
-    // the bytes, one frame at a time by the whole wave (coalesced).  Short frames: one byte
-    // per lane.  Longer ones: aligned 16-byte output stores, each funnel-shifted out of two
-    // aligned 16-byte source vectors, with the head and tail bytes (up to the 16-byte
-    // boundaries) stored singly by lanes 0-15 and 16-31.
-    for (uint32_t f = 0; f < lim; ++f) {
-        const uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)len, (int)f);
-        const uint8_t* s = frames + (uint32_t)__builtin_amdgcn_readlane((int)dl.off, (int)f);
-        const unsigned long long D =
-            ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(fo >> 32), (int)f) << 32 |
-             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)fo, (int)f)) + 4;
-        if (fl < 128) {
-            for (uint32_t k = lane; k < fl; k += kWave)
-                if (D + k < cap) out[D + k] = s[k];
-            continue;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t head = (uint32_t)(o0 & 15), nrow = (head + R + 15) >> 4;
+    const unsigned long long xb = o0 - head;  // 16-byte aligned (d_out is)
+    // byte j of row r (relative y): its segment walked forward from k, then the byte
+    auto row_byte = [&](uint32_t r, uint32_t j, uint32_t kk) {
+        const int y = (int)(16 * r + j) - (int)head;
+        const unsigned long long x = xb + 16ull * r + j;
+        if (y < 0 || (uint32_t)y >= R || x >= cap) return;
+        while (kk < last && sg[0][kk + 1] <= (uint32_t)y) ++kk;
+        uint32_t rel = (uint32_t)y - sg[0][kk], v;
+        const uint32_t mh = sg[5][kk];
+        if (mh && rel < 4) {
+            v = (mh >> (24 - 8 * rel)) & 0xff;
+        } else {
+            if (mh) rel -= 4;
+            v = rel < 4 ? (sg[4][kk] >> (24 - 8 * rel)) & 0xff : frames[sg[2][kk] + rel - 4];
         }
-        const unsigned long long Ee = D + fl, a0 = (D + 15) & ~15ull, a1 = Ee & ~15ull;  // a0 < a1
-        const unsigned long long hb = lane < 16 ? D + lane : a1 + (lane - 16);
-        if (lane < 32 && hb < (lane < 16 ? a0 : Ee) && hb < cap) out[hb] = s[hb - D];
-        const uintptr_t sa = (uintptr_t)(s + (a0 - D));
-        const uint4* sv = reinterpret_cast<const uint4*>(sa & ~(uintptr_t)15);
-        const uint32_t r = (uint32_t)(sa & 15), q = r >> 2, b = r & 3;
-        const uint32_t nch = (uint32_t)((a1 - a0) >> 4);
-        for (uint32_t c = lane; c < nch; c += kWave) {
-            const uint4 cur = sv[c];
-            const uint4 nxt = r ? sv[c + 1] : make_uint4(0, 0, 0, 0);  // r > 0: this chunk's tail
-            const uint32_t w[8] = {cur.x, cur.y, cur.z, cur.w, nxt.x, nxt.y, nxt.z, nxt.w};
-            uint32_t o[4];
+        out[x] = (uint8_t)v;
+    };
+    // pass 1: rows inside one frame's bytes; the others (headers, frame ends, the tile's edge
+    // rows, rows past the capacity) listed in LDS for pass 2
+    uint32_t* slow = s_slow[wv];
+    uint32_t nslow = 0, k = 0;
+    constexpr uint32_t kU = 4;  // rows per lane per round, their loads in flight together
+    for (uint32_t r0 = 0; r0 < nrow; r0 += kU * kWave) {  // wave-uniform trip count
+        uint4 cur[kU], nxt[kU];
+        uint32_t sh[kU], kk[kU];
+        bool fast[kU];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const uint32_t lo = q == 0 ? w[i] : q == 1 ? w[i + 1] : q == 2 ? w[i + 2] : w[i + 3];
-                const uint32_t hi = q == 0 ? w[i + 1] : q == 1 ? w[i + 2] : q == 2 ? w[i + 3] : w[i + 4];
-                o[i] = __builtin_amdgcn_alignbyte(hi, lo, b);
-            }
-            const unsigned long long x = a0 + 16ull * c;
-            if (x + 16 <= cap) {
-                *reinterpret_cast<uint4*>(out + x) = make_uint4(o[0], o[1], o[2], o[3]);
-            } else {
-                for (uint32_t j = 0; j < 16; ++j)
-                    if (x + j < cap) out[x + j] = (uint8_t)(o[j >> 2] >> (8 * (j & 3)));
+        for (uint32_t u = 0; u < kU; ++u) {
+            const uint32_t r = r0 + u * kWave + lane;
+            fast[u] = false;
+            kk[u] = k;
+            cur[u] = nxt[u] = make_uint4(0, 0, 0, 0);
+            sh[u] = 0;
+            if (r < nrow) {
+                const int y0 = (int)(16 * r) - (int)head;  // the row's first byte, relative to o0
+                const uint32_t yc = y0 < 0 ? 0u : (uint32_t)y0;
+                while (k < last && sg[0][k + 1] <= yc) ++k;
+                kk[u] = k;
+                const uint32_t ds = sg[1][k], fl = sg[3][k];
+                if (y0 >= (int)ds && (uint32_t)y0 + 16 <= ds + fl && xb + 16ull * r + 16 <= cap) {
+                    const uintptr_t sa = (uintptr_t)(frames + sg[2][k] + ((uint32_t)y0 - ds));
+                    const uint4* sv = reinterpret_cast<const uint4*>(sa & ~(uintptr_t)15);
+                    sh[u] = (uint32_t)(sa & 15);
+                    cur[u] = sv[0];
+                    if (sh[u]) nxt[u] = sv[1];
+                    fast[u] = true;
+                }
             }
         }
+#pragma unroll
+        for (uint32_t u = 0; u < kU; ++u) {
+            const uint32_t r = r0 + u * kWave + lane;
+            if (fast[u]) {
+                const uint32_t q = sh[u] >> 2, b = sh[u] & 3;
+                const uint32_t w[8] = {cur[u].x, cur[u].y, cur[u].z, cur[u].w, nxt[u].x, nxt[u].y, nxt[u].z, nxt[u].w};
+                uint32_t o[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t lo = q == 0 ? w[i] : q == 1 ? w[i + 1] : q == 2 ? w[i + 2] : w[i + 3];
+                    const uint32_t hi = q == 0 ? w[i + 1] : q == 1 ? w[i + 2] : q == 2 ? w[i + 3] : w[i + 4];
+                    o[i] = __builtin_amdgcn_alignbyte(hi, lo, b);
+                }
+                *reinterpret_cast<uint4*>(out + xb + 16ull * r) = make_uint4(o[0], o[1], o[2], o[3]);
+            }
+            const bool slw = r < nrow && !fast[u];
+            const uint64_t m = __ballot(slw);
+            const uint32_t at = nslow + mbcnt(m);
+            if (slw) {
+                if (at < kTxSlow) slow[at] = r << 6 | kk[u];
+                else for (uint32_t j = 0; j < 16; ++j) row_byte(r, j, kk[u]);  // list full: in place
+            }
+            nslow += (uint32_t)__popcll(m);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // pass 2: the listed rows a byte per lane, four rows per round (independent loads)
+    const uint32_t nb = min(nslow, kTxSlow) * 16;
+    for (uint32_t i = lane; i < nb; i += kWave) {
+        const uint32_t e = slow[i >> 4];
+        row_byte(e >> 6, i & 15, e & 63);
+    }
     }
 }
 
