@@ -1127,15 +1127,20 @@ __device__ __forceinline__ Probe probe_issue(const emurx_dev_tables& T, const Re
     p.ne = ld_bucket(T.ns_tab, p.nb);
     p.cbk = 0;
     p.ctab = nullptr;
+    // The three table bases as SGPR values selected per lane: left to itself the compiler
+    // turns "this lane's table pointer" into a vector load from the kernarg segment at a
+    // per-lane offset, one more dependent memory trip before the client bucket's address
+    uintptr_t tm = (uintptr_t)T.mac_tab, t4 = (uintptr_t)T.ip4_tab, t6 = (uintptr_t)T.ip6_tab;
+    asm volatile("" : "+s"(tm), "+s"(t4), "+s"(t6));
     if (key == kMac || key == kEui) {
         p.cbk = emurx_mac_hash(tk, p.mlo, p.mhi) & T.mac_mask;
-        p.ctab = T.mac_tab;
+        p.ctab = reinterpret_cast<const uint32_t*>(tm);
     } else if (key == kIp4) {
         p.cbk = emurx_ip4_hash(tk, k.kw[0]) & T.ip4_mask;
-        p.ctab = T.ip4_tab;
+        p.ctab = reinterpret_cast<const uint32_t*>(t4);
     } else if (key == kIp6) {
         p.cbk = emurx_ip6_hash(tk, k.kw[0], k.kw[1], k.kw[2], k.kw[3]) & T.ip6_mask;
-        p.ctab = T.ip6_tab;
+        p.ctab = reinterpret_cast<const uint32_t*>(t6);
     }
     return p;
 }
