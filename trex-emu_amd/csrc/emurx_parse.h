@@ -1022,10 +1022,21 @@ __device__ __forceinline__ uint32_t flow_probe(const emurx_dev_tables& T, const 
     return EMURX_FLOW_NO_SERVER;
 }
 
-__constant__ uint8_t kCbPlugin[EMURX_NUM_CB] = {
+// the plugin whose PluginCtx each callback checks, a nibble per callback in one immediate (a
+// __constant__ byte table indexed per lane costs a vector load behind the bucket reads)
+constexpr uint8_t kCbPluginTab[EMURX_NUM_CB] = {
     EMURX_PLUG_ARP, EMURX_PLUG_ICMP, EMURX_PLUG_IGMP, EMURX_PLUG_DHCP, EMURX_PLUG_DHCPSRV,
     EMURX_PLUG_DHCPV6, EMURX_PLUG_MDNS, EMURX_PLUG_TRANSPORT, EMURX_PLUG_TRANSPORT,
     EMURX_PLUG_IPV6, EMURX_PLUG_DOT1X, EMURX_PLUG_PPP};
+constexpr uint64_t cb_plugin_packed() {
+    uint64_t v = 0;
+    for (int i = 0; i < EMURX_NUM_CB; ++i) v |= (uint64_t)kCbPluginTab[i] << (4 * i);
+    return v;
+}
+static_assert(EMURX_NUM_CB <= 16 && EMURX_NUM_PLUG <= 16, "a nibble per callback");
+__device__ __forceinline__ uint32_t cb_plugin(uint32_t cb) {
+    return (uint32_t)(cb_plugin_packed() >> (4 * (cb & 15))) & 15u;
+}
 
 // what a callback's client rule looks up, decided from the frame alone (before the
 // Namespace is known, so both probes can be issued together)
@@ -1150,7 +1161,7 @@ __device__ __forceinline__ Probe probe_issue(const emurx_dev_tables& T, const Re
 template <class Flow>
 __device__ __forceinline__ void resolve_done(const emurx_dev_tables& T, Rec& r, const LKey& k, const Probe& p,
                                              const Bucket& ce, Flow flow) {
-    const uint32_t cb = r.proto, plug = kCbPlugin[cb];
+    const uint32_t cb = r.proto, plug = cb_plugin(cb);
     const uint32_t key = k.key, cbk = p.cbk, mlo = p.mlo, mhi = p.mhi;
     // ---- GetNs + ns.PluginCtx.Get(plugin) ----
     const uint2 nsr = resolve_ns(T, p.nb, p.ne, r.vport, r.vlan0, r.vlan1);
