@@ -95,59 +95,64 @@ __global__ __launch_bounds__(256) void k_txz_leaf(const emurx_desc* __restrict__
     if (lane == 0) B[t] = tot;
 }
 
-// 64 children -> one parent: X/M composed along the chain for every entry, B summed
-__global__ __launch_bounds__(64) void k_txz_compose(const uint32_t* __restrict__ Xc, const uint32_t* __restrict__ Mc,
-                                                    const unsigned long long* __restrict__ Bc, uint32_t nc,
-                                                    uint32_t* __restrict__ Xp, uint32_t* __restrict__ Mp,
-                                                    unsigned long long* __restrict__ Bp) {
-    __shared__ uint32_t sx[64][kWave], sm[64][kWave];
-    __shared__ unsigned long long sb[64];
-    const uint32_t p = blockIdx.x, lane = lane_id();
-    const uint32_t c0 = p * 64, cn = min(nc - c0, 64u);
+// One wave's LDS for a compose / descend step: the 64 children's X / M tables, B, and the
+// descend's outputs
+struct TxUnitLds {
+    uint32_t sx[64][kWave], sm[64][kWave];
+    unsigned long long sb[64];
+    uint32_t se[64], smb[64];
+    unsigned long long sbb[64];
+};
+__device__ __forceinline__ void tx_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ uint32_t tx_load_children(const uint32_t* __restrict__ Xc, const uint32_t* __restrict__ Mc,
+                                                     const unsigned long long* __restrict__ Bc, uint32_t nc, uint32_t p,
+                                                     TxUnitLds& S) {
+    const uint32_t lane = lane_id(), c0 = p * 64, cn = min(nc - c0, 64u);
     for (uint32_t c = 0; c < cn; ++c) {
-        sx[c][lane] = Xc[(size_t)(c0 + c) * kWave + lane];
-        sm[c][lane] = Mc[(size_t)(c0 + c) * kWave + lane];
+        S.sx[c][lane] = Xc[(size_t)(c0 + c) * kWave + lane];
+        S.sm[c][lane] = Mc[(size_t)(c0 + c) * kWave + lane];
     }
-    sb[lane] = lane < cn ? Bc[c0 + lane] : 0ull;
-    __syncthreads();
+    S.sb[lane] = lane < cn ? Bc[c0 + lane] : 0ull;
+    tx_wave_sync();
+    return cn;
+}
+// 64 children -> parent p (one wave): X/M composed along the chain for every entry, B summed
+__device__ __forceinline__ void tx_compose(const uint32_t* __restrict__ Xc, const uint32_t* __restrict__ Mc,
+                                           const unsigned long long* __restrict__ Bc, uint32_t nc, uint32_t p,
+                                           uint32_t* __restrict__ Xp, uint32_t* __restrict__ Mp,
+                                           unsigned long long* __restrict__ Bp, TxUnitLds& S) {
+    const uint32_t lane = lane_id(), cn = tx_load_children(Xc, Mc, Bc, nc, p, S);
     uint32_t e = lane, m = 0;
     for (uint32_t c = 0; c < cn; ++c) {
-        m += sm[c][e];
-        e = sx[c][e];
+        m += S.sm[c][e];
+        e = S.sx[c][e];
     }
     Xp[(size_t)p * kWave + lane] = e;
     Mp[(size_t)p * kWave + lane] = m;
     if (lane == 0) {
         unsigned long long b = 0;
-        for (uint32_t c = 0; c < cn; ++c) b += sb[c];
+        for (uint32_t c = 0; c < cn; ++c) b += S.sb[c];
         Bp[p] = b;
     }
 }
-
-// one parent -> its 64 children: actual entry, message base, byte base of each child
-__global__ __launch_bounds__(64) void k_txz_descend(const uint32_t* __restrict__ Xc, const uint32_t* __restrict__ Mc,
-                                                    const unsigned long long* __restrict__ Bc, uint32_t nc,
-                                                    const uint32_t* __restrict__ Ep, const uint32_t* __restrict__ MBp,
-                                                    const unsigned long long* __restrict__ BBp,
-                                                    uint32_t* __restrict__ Ec, uint32_t* __restrict__ MBc,
-                                                    unsigned long long* __restrict__ BBc, uint32_t n,
-                                                    unsigned long long* __restrict__ msg_off,
-                                                    unsigned long long* __restrict__ info) {
-    __shared__ uint32_t sx[64][kWave], sm[64][kWave];
-    __shared__ unsigned long long sb[64];
-    __shared__ uint32_t se[64], smb[64];
-    __shared__ unsigned long long sbb[64];
-    const uint32_t p = blockIdx.x, lane = lane_id();
-    const uint32_t c0 = p * 64, cn = min(nc - c0, 64u);
-    for (uint32_t c = 0; c < cn; ++c) {
-        sx[c][lane] = Xc[(size_t)(c0 + c) * kWave + lane];
-        sm[c][lane] = Mc[(size_t)(c0 + c) * kWave + lane];
-    }
-    sb[lane] = lane < cn ? Bc[c0 + lane] : 0ull;
-    __syncthreads();
-    if (info && lane == 0) {  // the root (entry 0): message count and total size (k_txz_finish)
-        const unsigned long long nm = sm[0][0];
-        const unsigned long long total = 4ull * nm + 4ull * n + sb[0];
+// parent p -> its 64 children (one wave): actual entry, message base, byte base of each child.
+// info != nullptr: p is the root (entry 0, bases 0), and its message count and total size go to
+// info and msg_off[n_msgs]
+__device__ __forceinline__ void tx_descend(const uint32_t* __restrict__ Xc, const uint32_t* __restrict__ Mc,
+                                           const unsigned long long* __restrict__ Bc, uint32_t nc, uint32_t p,
+                                           const uint32_t* __restrict__ Ep, const uint32_t* __restrict__ MBp,
+                                           const unsigned long long* __restrict__ BBp, uint32_t* __restrict__ Ec,
+                                           uint32_t* __restrict__ MBc, unsigned long long* __restrict__ BBc,
+                                           uint32_t n, unsigned long long* __restrict__ msg_off,
+                                           unsigned long long* __restrict__ info, TxUnitLds& S) {
+    const uint32_t lane = lane_id(), c0 = p * 64, cn = tx_load_children(Xc, Mc, Bc, nc, p, S);
+    if (info && lane == 0) {
+        const unsigned long long nm = S.sm[0][0];
+        const unsigned long long total = 4ull * nm + 4ull * n + S.sb[0];
         info[0] = nm;
         info[1] = total;
         msg_off[nm] = total;
@@ -156,19 +161,71 @@ __global__ __launch_bounds__(64) void k_txz_descend(const uint32_t* __restrict__
         uint32_t e = Ep ? Ep[p] : 0u, mb = MBp ? MBp[p] : 0u;
         unsigned long long bb = BBp ? BBp[p] : 0ull;
         for (uint32_t c = 0; c < cn; ++c) {
-            se[c] = e;
-            smb[c] = mb;
-            sbb[c] = bb;
-            mb += sm[c][e];
-            e = sx[c][e];
-            bb += sb[c];
+            S.se[c] = e;
+            S.smb[c] = mb;
+            S.sbb[c] = bb;
+            mb += S.sm[c][e];
+            e = S.sx[c][e];
+            bb += S.sb[c];
         }
     }
-    __syncthreads();
+    tx_wave_sync();
     if (lane < cn) {
-        Ec[c0 + lane] = se[lane];
-        MBc[c0 + lane] = smb[lane];
-        BBc[c0 + lane] = sbb[lane];
+        Ec[c0 + lane] = S.se[lane];
+        MBc[c0 + lane] = S.smb[lane];
+        BBc[c0 + lane] = S.sbb[lane];
+    }
+}
+
+__global__ __launch_bounds__(64) void k_txz_compose(const uint32_t* __restrict__ Xc, const uint32_t* __restrict__ Mc,
+                                                    const unsigned long long* __restrict__ Bc, uint32_t nc,
+                                                    uint32_t* __restrict__ Xp, uint32_t* __restrict__ Mp,
+                                                    unsigned long long* __restrict__ Bp) {
+    __shared__ TxUnitLds S;
+    tx_compose(Xc, Mc, Bc, nc, blockIdx.x, Xp, Mp, Bp, S);
+}
+__global__ __launch_bounds__(64) void k_txz_descend(const uint32_t* __restrict__ Xc, const uint32_t* __restrict__ Mc,
+                                                    const unsigned long long* __restrict__ Bc, uint32_t nc,
+                                                    const uint32_t* __restrict__ Ep, const uint32_t* __restrict__ MBp,
+                                                    const unsigned long long* __restrict__ BBp,
+                                                    uint32_t* __restrict__ Ec, uint32_t* __restrict__ MBc,
+                                                    unsigned long long* __restrict__ BBc) {
+    __shared__ TxUnitLds S;
+    tx_descend(Xc, Mc, Bc, nc, blockIdx.x, Ep, MBp, BBp, Ec, MBc, BBc, 0u, nullptr, nullptr, S);
+}
+
+// The top of the chain scan in one workgroup of kTxTopWaves waves (a launch per level would
+// cost more than the levels' work): the compose levels from k0 (<= kTxTopWaves parents) to the
+// root, the root itself (message count, total size), and the descends back down to level k0
+constexpr uint32_t kTxTopWaves = 4, kTxMaxLevels = 8;
+struct TxLevels {
+    uint32_t L, k0, n;
+    uint32_t units[kTxMaxLevels];
+    uint32_t *X[kTxMaxLevels], *M[kTxMaxLevels], *E[kTxMaxLevels], *MB[kTxMaxLevels];
+    unsigned long long *B[kTxMaxLevels], *BB[kTxMaxLevels];
+    unsigned long long *msg_off, *info;
+};
+__global__ __launch_bounds__(kTxTopWaves * kWave) void k_txz_top(const TxLevels t) {
+    __shared__ TxUnitLds S[kTxTopWaves];
+    const uint32_t wv = threadIdx.x / kWave;
+    for (uint32_t k = t.k0; k < t.L; ++k) {
+        if (wv < t.units[k])
+            tx_compose(t.X[k - 1], t.M[k - 1], t.B[k - 1], t.units[k - 1], wv, t.X[k], t.M[k], t.B[k], S[wv]);
+        __threadfence();
+        __syncthreads();
+    }
+    const uint32_t r = t.L - 1;  // the root: entry 0, bases 0
+    if (wv == 0)
+        tx_descend(t.X[r], t.M[r], t.B[r], 1u, 0u, nullptr, nullptr, nullptr, t.E[r], t.MB[r], t.BB[r], t.n,
+                   t.msg_off, t.info, S[0]);
+    __threadfence();
+    __syncthreads();
+    for (uint32_t k = t.L - 1; k >= t.k0 && k >= 1; --k) {
+        if (wv < t.units[k])
+            tx_descend(t.X[k - 1], t.M[k - 1], t.B[k - 1], t.units[k - 1], wv, t.E[k], t.MB[k], t.BB[k], t.E[k - 1],
+                       t.MB[k - 1], t.BB[k - 1], t.n, nullptr, nullptr, S[wv]);
+        __threadfence();
+        __syncthreads();
     }
 }
 
@@ -479,18 +536,27 @@ int emurx_launch_tx_zmq(const uint8_t* frames, const emurx_desc* desc, uint32_t 
     }
     const uint32_t nt = lv[0].units;
     uint32_t* done = reinterpret_cast<uint32_t*>(p);  // [nt] tiles the staged write took
+    TxLevels tl{};
+    tl.L = (uint32_t)L;
+    tl.n = n;
+    tl.msg_off = mo;
+    tl.info = inf;
+    tl.k0 = (uint32_t)L;  // the first level with at most kTxTopWaves units (its parents in the top kernel)
+    for (int k = L - 1; k >= 1 && lv[k].units <= kTxTopWaves; --k) tl.k0 = (uint32_t)k;
+    for (int k = 0; k < L; ++k) {
+        tl.units[k] = lv[k].units;
+        tl.X[k] = lv[k].X; tl.M[k] = lv[k].M; tl.E[k] = lv[k].E; tl.MB[k] = lv[k].MB;
+        tl.B[k] = lv[k].B; tl.BB[k] = lv[k].BB;
+    }
     hipLaunchKernelGGL(k_txz_leaf, dim3((nt + 3) / 4), dim3(256), 0, st, desc, n, nt, lv[0].X, lv[0].M, lv[0].B);
-    for (int k = 1; k < L; ++k)
+    for (uint32_t k = 1; k < tl.k0; ++k)
         hipLaunchKernelGGL(k_txz_compose, dim3(lv[k].units), dim3(64), 0, st, lv[k - 1].X, lv[k - 1].M, lv[k - 1].B,
                            lv[k - 1].units, lv[k].X, lv[k].M, lv[k].B);
-    // the root (one unit) has entry 0, base 0: its own descend writes E/MB/BB of level L-1, the
-    // message count and the total size (info, msg_off[n_msgs])
-    hipLaunchKernelGGL(k_txz_descend, dim3(1), dim3(64), 0, st, lv[L - 1].X, lv[L - 1].M, lv[L - 1].B, 1u,
-                       nullptr, nullptr, nullptr, lv[L - 1].E, lv[L - 1].MB, lv[L - 1].BB, n, mo, inf);
-    for (int k = L - 1; k >= 1; --k)
+    hipLaunchKernelGGL(k_txz_top, dim3(1), dim3(kTxTopWaves * kWave), 0, st, tl);
+    for (int k = (int)tl.k0 - 1; k >= 1; --k)
         hipLaunchKernelGGL(k_txz_descend, dim3(lv[k].units), dim3(64), 0, st, lv[k - 1].X, lv[k - 1].M,
                            lv[k - 1].B, lv[k - 1].units, lv[k].E, lv[k].MB, lv[k].BB, lv[k - 1].E, lv[k - 1].MB,
-                           lv[k - 1].BB, n, (unsigned long long*)nullptr, (unsigned long long*)nullptr);
+                           lv[k - 1].BB);
     hipLaunchKernelGGL(k_txz_write<true>, dim3((nt + 3) / 4), dim3(256), 0, st, frames, desc, n, nt, lv[0].E,
                        lv[0].MB, lv[0].BB, out, (unsigned long long)cap, mo, done);
     hipLaunchKernelGGL(k_txz_write<false>, dim3((nt + 3) / 4), dim3(256), 0, st, frames, desc, n, nt, lv[0].E,
