@@ -571,8 +571,6 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         xch["cap"] = grow_cap(xch, world, dist, torch, dev)
         alloc_regions()
         hist.zero_()
-    warm_s = warm_for_time()
-
     def sanity():
         """The outcome on this rank (counts only; parity lives in tests/), after some steps."""
         from emurx.rx import hist_fold, pack_queues
@@ -584,6 +582,9 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             xcheck(xch, rec, n, world, rank, dist, torch, dev, mode)
     if not a.no_check and warmup > 0:
         sanity()
+    # the time-based warmup last, right before the measurements: the host-side check above
+    # leaves the GPU idle long enough for its clocks to drop, which a 20-step region would time
+    warm_s = warm_for_time()
 
     region = xch is None and a.kernel_timing == "region"
     if xch is not None or a.kernel_timing == "launch":
@@ -610,24 +611,6 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         reg_ev[1].record(stream)
 
     one = replay = None
-    if region:
-        # each launch alone: the same rotation of batch slots, back to back on one stream
-        torch.cuda.synchronize()
-        reg_ev[0].record(stream)
-        for k in range(steps):
-            one_calls[k % R]()
-        reg_ev[1].record(stream)
-        torch.cuda.synchronize()
-        one = reg_ev[0].elapsed_time(reg_ev[1]) / steps
-        if R > S and not a.no_replay:
-            # the round-2 replay: each stream re-reads one batch, which stays in the Infinity Cache
-            region_open()
-            for k in range(steps):
-                calls[k % S]()
-            region_close()
-            torch.cuda.synchronize()
-            replay = reg_ev[0].elapsed_time(reg_ev[1]) / steps
-        kk[0] = 0
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -653,6 +636,22 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
     interval = None
     if region:
         interval = reg_ev[0].elapsed_time(reg_ev[1]) / steps
+        # each launch alone (after the timed region, which runs straight after the time-based
+        # warmup): the same rotation of batch slots, back to back on one stream
+        reg_ev[0].record(stream)
+        for k in range(steps):
+            one_calls[k % R]()
+        reg_ev[1].record(stream)
+        torch.cuda.synchronize()
+        one = reg_ev[0].elapsed_time(reg_ev[1]) / steps
+        if R > S and not a.no_replay:
+            # the round-2 replay: each stream re-reads one batch, which stays in the Infinity Cache
+            region_open()
+            for k in range(steps):
+                calls[k % S]()
+            region_close()
+            torch.cuda.synchronize()
+            replay = reg_ev[0].elapsed_time(reg_ev[1]) / steps
         pk = [one]
     else:
         pk = rx.kernel_times()
