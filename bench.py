@@ -753,7 +753,7 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             "kernel_ms_mean": round(parse_s * 1e3, 5),
             "kernel_launches_timed": steps if region else int(len(pk)),
             "kernel_time_source": ("one HIP event pair on the launch stream around the same --steps launches back "
-                                   f"to back on one stream, rotating over the {R} batch slots, just before the timed "
+                                   f"to back on one stream, rotating over the {R} batch slots, right after the timed "
                                    "region: elapsed / launches = each launch alone (what rocprofv3's kernel "
                                    "trace times, plus the ~1 us dispatch gap between launches)" if region else
                                    f"HIP events on the launch stream around every {a.time_stride}-th "
