@@ -638,12 +638,15 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         interval = reg_ev[0].elapsed_time(reg_ev[1]) / steps
         # each launch alone (after the timed region, which runs straight after the time-based
         # warmup): the same rotation of batch slots, back to back on one stream
+        # at least 100 launches, so that a short --steps still times the launch, not the
+        # clocks' first reaction to the work
+        n_one = max(steps, 100)
         reg_ev[0].record(stream)
-        for k in range(steps):
+        for k in range(n_one):
             one_calls[k % R]()
         reg_ev[1].record(stream)
         torch.cuda.synchronize()
-        one = reg_ev[0].elapsed_time(reg_ev[1]) / steps
+        one = reg_ev[0].elapsed_time(reg_ev[1]) / n_one
         if R > S and not a.no_replay:
             # the round-2 replay: each stream re-reads one batch, which stays in the Infinity Cache
             region_open()
@@ -751,8 +754,8 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
                               "writes" + ("; the 64-B lookup record instead of the record" if mode == "partitioned" else ""),
             "table_probe_bytes_per_launch": probed * 128 if mode != "partitioned" else 0,
             "kernel_ms_mean": round(parse_s * 1e3, 5),
-            "kernel_launches_timed": steps if region else int(len(pk)),
-            "kernel_time_source": ("one HIP event pair on the launch stream around the same --steps launches back "
+            "kernel_launches_timed": max(steps, 100) if region else int(len(pk)),
+            "kernel_time_source": ("one HIP event pair on the launch stream around max(--steps, 100) launches back "
                                    f"to back on one stream, rotating over the {R} batch slots, right after the timed "
                                    "region: elapsed / launches = each launch alone (what rocprofv3's kernel "
                                    "trace times, plus the ~1 us dispatch gap between launches)" if region else

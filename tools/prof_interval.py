@@ -4,9 +4,9 @@
 
 bench.py's pipelined steps (--streams 2, --batches 8) enqueue: the warmup launches, then the
 `steps` launches of the timed region alternating between the streams over the rotating slots
-(roofline.pipelined), then `steps` launches back to back on one stream over the rotating batch
-slots (each launch alone: roofline.kernel_ms_mean / frac), then `steps` launches replaying one
-batch per stream (roofline.cache_resident_replay).  (Before the end of round 3 the timed region
+(roofline.pipelined), then max(`steps`, 100) launches back to back on one stream over the
+rotating batch slots (each launch alone: roofline.kernel_ms_mean / frac), then `steps` launches
+replaying one batch per stream (roofline.cache_resident_replay).  (Before the end of round 3 the timed region
 came last: --old-order.)  For those three groups of
 `steps` k_rx dispatches this prints the mean per-dispatch duration (what `--stats` averages)
 and the interval (last end - first start) / launches, which is what the bench's one event pair
@@ -25,7 +25,8 @@ def col(row, *names):
     raise KeyError(names)
 
 
-def main(path, steps, replay=True, old_order=False):
+def main(path, steps, replay=True, old_order=False, one=None):
+    one = max(steps, 100) if one is None else one  # bench.py times one launch alone over max(--steps, 100)
     ks = []
     for row in csv.DictReader(open(path)):
         name = col(row, "Kernel_Name", "Kernel-Name", "KernelName")
@@ -35,16 +36,19 @@ def main(path, steps, replay=True, old_order=False):
                    int(col(row, "End_Timestamp", "End-Timestamp", "EndNs"))))
     ks.sort()
     out = {"k_rx_dispatches": len(ks), "steps": steps}
-    g = [ks[len(ks) - (i + 1) * steps:len(ks) - i * steps] for i in range(3)]  # last, second to last, ...
     if old_order:
+        g = [ks[len(ks) - (i + 1) * steps:len(ks) - i * steps] for i in range(3)]  # last, second to last, ...
         groups = [("timed_region", g[0])]
         groups += [("cache_resident_replay", g[1]), ("one_stream", g[2])] if replay else [("one_stream", g[1])]
-    elif replay:
-        groups = [("cache_resident_replay", g[0]), ("one_stream", g[1]), ("timed_region", g[2])]
     else:
-        groups = [("one_stream", g[0]), ("timed_region", g[1])]
+        # from the end: the replay (steps), the one-stream launches (max(steps, 100)), the timed region
+        sizes = ([("cache_resident_replay", steps)] if replay else []) + [("one_stream", one), ("timed_region", steps)]
+        groups, end = [], len(ks)
+        for label, size in sizes:
+            groups.append((label, ks[max(0, end - size):end]))
+            end -= size
     for label, grp in groups:
-        if len(grp) < steps:
+        if not grp or len(grp) < min(steps, len(grp)) or (label != "one_stream" and len(grp) < steps):
             continue
         dur = sum(e - s for s, e in grp) / len(grp)
         span = max(e for _, e in grp) - min(s for s, _ in grp)
@@ -54,4 +58,6 @@ def main(path, steps, replay=True, old_order=False):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]), replay="--no-replay" not in sys.argv[3:], old_order="--old-order" in sys.argv[3:])
+    rest = sys.argv[3:]
+    one = int(rest[rest.index("--one") + 1]) if "--one" in rest else None  # traces before max(steps, 100): --one <steps>
+    main(sys.argv[1], int(sys.argv[2]), replay="--no-replay" not in rest, old_order="--old-order" in rest, one=one)
