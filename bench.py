@@ -537,9 +537,6 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         out = {"steps": reps - 1, "source_side_ms": round(src, 5), "k_rx_ms": round(k_rx_ms, 5),
                ("owner_count_scan_ms" if mode == "partitioned" else "scan_pack_ms"): round(src - k_rx_ms, 5),
                "all_to_all_ms": round(a2a, 5), "owner_lookup_ms": round(look, 5) if mode == "partitioned" else 0.0,
-               "owner_offsets": ("two-pass (EMURX_OWNER_PASS=1: " + ("k_owner_count + scan before k_rx" if mode == "partitioned"
-                                 else "scan + k_route after k_rx") + ")") if os.environ.get("EMURX_OWNER_PASS") == "1"
-                                 else "single-pass (tile tickets + decoupled look-back inside k_rx)",
                "record_bytes": rb, "bytes_to_other_ranks": moved, "payload_bytes_to_other_ranks": payload,
                "source": "HIP events on the launch stream between the phases of non-overlapped steps; k_rx by the "
                          "library's events around its launch"}

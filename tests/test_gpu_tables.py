@@ -18,7 +18,7 @@ import pytest
 
 from emurx import abi, synth
 from emurx import frames as F
-from gpu_util import frame_tuples, rec_diff, run_dev, to_dev
+from gpu_util import frame_tuples, rec_diff, run_dev
 
 pytestmark = pytest.mark.gpu
 
@@ -307,59 +307,3 @@ def test_partitioned_edge_and_fuzz_frames(rxmod):
         for k in n2:
             ns.setdefault(k, len(ns))
     partitioned_vs_oracle(rxmod, shards, lambda t: load_frame_tables([t], ns, cl), 3)
-
-
-def test_single_pass_owner_offsets_equal_two_pass(rxmod, monkeypatch):
-    """The single-pass routes (tiles by ticket, owner offsets by decoupled look-back inside
-    k_rx) against the two-pass ones (EMURX_OWNER_PASS=1: k_owner_count + scan before the
-    partitioned source; count, scan and k_route<true> after the replicated classify): send
-    regions and send counts byte for byte over consecutive batches on one handle (new epochs
-    over the same status words, the two kinds sharing them), ragged and tiny batches, and
-    overflowing regions."""
-    import torch
-    from emurx import exchange as X
-    n = 1 << 18
-    parts = 8
-    w0 = synth.config_c(n, seed=0x51A6)
-    monkeypatch.setenv("EMURX_OWNER_PASS", "1")
-    two = rxmod(0, max_ns=4096, max_clients=65536, max_frames=n)
-    monkeypatch.delenv("EMURX_OWNER_PASS")
-    one = rxmod(0, max_ns=4096, max_clients=65536, max_frames=n)
-    for h in (one, two):
-        h.register_all()
-        synth.load_tables(w0, h)
-    cases = [(n, n), (n, n), (n - 77, n), (5, n), (n, n // 16), (n, n)]
-    for k, (m, cap) in enumerate(cases):
-        w = synth.config_c(n, seed=0x51A6 + k, rank=k % parts)
-        buf, desc = to_dev(w["buf"]), to_dev(w["desc"][:m])
-        qcap = abi.queue_cap(m)
-        outs = []
-        for h in (one, two):
-            rec = torch.zeros(m * 32, dtype=torch.uint8, device="cuda")
-            ql = torch.empty(abi.NUM_QUEUES * qcap, dtype=torch.int32, device="cuda")
-            tc = torch.empty(abi.ntiles(m) * 16, dtype=torch.int32, device="cuda")
-            hi = torch.zeros(abi.HIST_SHARDS * 2 * abi.HIST_BINS, dtype=torch.int64, device="cuda")
-            sd = torch.full((parts * cap * X.LOOKUP_BYTES,), 0xEE, dtype=torch.uint8, device="cuda")
-            sc = torch.full((parts,), -1, dtype=torch.int32, device="cuda")
-            h.parse_route_dev(buf, desc, m, rec, ql, qcap, tc, hi, parts, k % parts, cap, sd, sc)
-            # the replicated route: classify + the found records' 40-B route records per owner
-            crec = torch.zeros(m * 32, dtype=torch.uint8, device="cuda")
-            rsd = torch.full((parts * cap * X.REC_BYTES,), 0xEE, dtype=torch.uint8, device="cuda")
-            rsc = torch.full((parts,), -1, dtype=torch.int32, device="cuda")
-            h.classify_route_dev(buf, desc, m, crec, ql, qcap, tc, hi, parts, k % parts, cap, rsd, rsc)
-            torch.cuda.synchronize()
-            outs.append((rec.cpu().numpy(), sc.cpu().numpy(), sd.cpu().numpy().reshape(parts, cap, X.LOOKUP_BYTES),
-                         crec.cpu().numpy(), rsc.cpu().numpy(), rsd.cpu().numpy().reshape(parts, cap, X.REC_BYTES)))
-        (r1, c1, s1, cr1, rc1, rs1), (r2, c2, s2, cr2, rc2, rs2) = outs
-        assert np.array_equal(r1, r2), k
-        assert np.array_equal(c1, c2), (k, c1, c2)
-        assert int(c1.astype(np.int64).sum()) <= m, k
-        assert np.array_equal(cr1, cr2), k
-        assert np.array_equal(rc1, rc2), (k, rc1, rc2)
-        found = int((cr1.view(abi.REC_DTYPE)["ns_id"] != abi.ID_NONE).sum())
-        assert int(rc1.astype(np.int64).sum()) == found, k
-        for p in range(parts):
-            u = min(int(c1[p]), cap)
-            assert s1[p, :u].tobytes() == s2[p, :u].tobytes(), (k, p)
-            u = min(int(rc1[p]), cap)
-            assert rs1[p, :u].tobytes() == rs2[p, :u].tobytes(), (k, p)

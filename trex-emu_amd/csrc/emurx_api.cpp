@@ -156,11 +156,8 @@ struct emurx_ctx {
         bool used = false;
         hipEvent_t done = nullptr;                      // recorded after each route on st
         DevBuf<uint32_t> cnt, grp, goff;                // grp: zero between batches
-        DevBuf<uint32_t> tick;                          // single-pass tile tickets: zero between batches
-        uint32_t epoch = 0;                             // single-pass status-word tag (k_rx owner_lookback)
         void release() {
-            cnt.release(); grp.release(); goff.release(); tick.release();
-            epoch = 0;
+            cnt.release(); grp.release(); goff.release();
             if (done) (void)hipEventDestroy(done);
             done = nullptr;
         }
@@ -180,7 +177,6 @@ struct emurx_ctx {
     DevBuf<uint32_t> d_stage_fb;  // 64 sampled tiles x 4 waves: gen << 2 | has_frames << 1 | mid
     PinBuf<uint32_t> stage_fb;    // its copy
     uint32_t stage_gen = 0, stage_mode = 0;  // 0 auto, 1 wide, 2 narrow
-    bool owner_pass = false;  // EMURX_OWNER_PASS=1: the two-pass routes (owner counts / scan launches; A/B)
     bool stage_copy = false, stage_pending = false;
     uint32_t stage_copy_gen = 0;
     hipEvent_t stage_ev = nullptr;
@@ -404,22 +400,8 @@ int route_scratch(emurx_t* h, uint32_t n, hipStream_t st, emurx_t::RouteScratch*
     if (!r->grp.p) {
         if (r->grp.alloc(gw) || !EMURX_HIP_OK(hipMemset(r->grp.p, 0, gw * sizeof(uint32_t)))) return EMURX_ENOMEM;
     }
-    uint32_t* const old_cnt = r->cnt.p;
     if (r->cnt.alloc(tiles * 16) || r->goff.alloc(gw)) return EMURX_ENOMEM;
-    // fresh status words hold no epoch's flags (owner_lookback): zero them once
-    if (r->cnt.p != old_cnt && !EMURX_HIP_OK(hipMemsetAsync(r->cnt.p, 0, r->cnt.n * sizeof(uint32_t), st)))
-        return EMURX_EDEVICE;
-    if (!r->tick.p && (r->tick.alloc(1) || !EMURX_HIP_OK(hipMemset(r->tick.p, 0, sizeof(uint32_t)))))
-        return EMURX_ENOMEM;
     *out = r;
-    return EMURX_OK;
-}
-// the next single-pass status-word tag of a scratch set (k_rx owner_lookback)
-int next_epoch(emurx_t::RouteScratch* r, hipStream_t st) {
-    if (++r->epoch > 0x3fffffffu) {  // the tag wrapped: no stale word may carry the new one
-        r->epoch = 1;
-        if (!EMURX_HIP_OK(hipMemsetAsync(r->cnt.p, 0, r->cnt.n * sizeof(uint32_t), st))) return EMURX_EDEVICE;
-    }
     return EMURX_OK;
 }
 // after a route's last launch on st: its scratch set may change hands behind this event
@@ -644,7 +626,6 @@ int emurx_open(const emurx_cfg* cfg, emurx_t** out) {
     int rc = bind(h);
     if (rc) { delete h; return rc; }
     if (!EMURX_HIP_OK(hipStreamCreate(&h->stream))) { delete h; return EMURX_EDEVICE; }
-    if (const char* e = getenv("EMURX_OWNER_PASS")) h->owner_pass = !strcmp(e, "1");
     if (const char* e = getenv("EMURX_STAGE")) h->stage_mode = !strcmp(e, "wide") ? 1 : !strcmp(e, "narrow") ? 2 : 0;
     if (h->stage_fb.alloc(256) || h->d_stage_fb.alloc(256) ||
         !EMURX_HIP_OK(hipEventCreateWithFlags(&h->stage_ev, hipEventDisableTiming)) ||
@@ -944,15 +925,6 @@ int emurx_classify_route_dev(emurx_t* h, const uint8_t* d_frames, const emurx_de
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
     emurx_t::RouteScratch* rs = nullptr;
     if ((rc = route_scratch(h, n, st, &rs))) return rc;
-    if (!h->owner_pass && n) {
-        // single pass: k_rx classifies, finds its tile's offsets by look-back and packs the
-        // found records' route records itself; the last tile writes send_count
-        if ((rc = next_epoch(rs, st))) return rc;
-        const emurx_route_args rt{n_parts, my_rank, cap, rs->cnt.p, rs->grp.p, nullptr, nullptr, rs->tick.p,
-                                  d_send_count, rs->epoch, d_send};
-        if ((rc = run_dev(h, d_frames, d_desc, n, out, st, 1, &rt))) return rc;
-        return route_done(rs, st);
-    }
     const emurx_route_args rt{n_parts, my_rank, cap, rs->cnt.p, rs->grp.p, nullptr, nullptr};
     if (n && (rc = run_dev(h, d_frames, d_desc, n, out, st, 1, &rt))) {
         // k_rx may have added its owner counts into grp before the failure; only k_route_scan
@@ -979,20 +951,11 @@ int emurx_parse_route_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc*
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
     emurx_t::RouteScratch* rs = nullptr;
     if ((rc = route_scratch(h, n, st, &rs))) return rc;
-    if (h->owner_pass || n == 0) {
-        // owner counts from the L2 headers + group scan, then k_rx packs at those offsets
-        if (emurx_launch_owner_count(d_frames, d_desc, n, n_parts, d_send_count, rs->cnt.p, rs->grp.p, rs->goff.p, st))
-            return EMURX_EDEVICE;
-        const emurx_route_args rt{n_parts, my_rank, cap, rs->cnt.p, rs->grp.p, rs->goff.p, d_send};
-        if (n && (rc = run_dev(h, d_frames, d_desc, n, out, st, 2, &rt))) return rc;
-        return route_done(rs, st);
-    }
-    // single pass: k_rx takes tiles by ticket and finds its offsets by look-back (no
-    // owner-count pass over the frames, no scan launch); the last tile writes send_count
-    if ((rc = next_epoch(rs, st))) return rc;
-    const emurx_route_args rt{n_parts, my_rank, cap, rs->cnt.p, rs->grp.p, nullptr, d_send, rs->tick.p, d_send_count,
-                              rs->epoch};
-    if ((rc = run_dev(h, d_frames, d_desc, n, out, st, 2, &rt))) return rc;
+    // owner counts from the L2 headers + group scan, then k_rx packs at those offsets
+    if (emurx_launch_owner_count(d_frames, d_desc, n, n_parts, d_send_count, rs->cnt.p, rs->grp.p, rs->goff.p, st))
+        return EMURX_EDEVICE;
+    const emurx_route_args rt{n_parts, my_rank, cap, rs->cnt.p, rs->grp.p, rs->goff.p, d_send};
+    if (n && (rc = run_dev(h, d_frames, d_desc, n, out, st, 2, &rt))) return rc;
     return route_done(rs, st);
 }
 

@@ -29,22 +29,12 @@ inline bool emurx_hip_ok(hipError_t e, const char* file, int line) {
 // per-group sums added into grp, as emurx_launch_route's first pass); kind 2 (required): the
 // owner counts cnt / group offsets goff of k_owner_count + k_route_scan, and every frame's
 // 64-byte emurx_lookup_rec (emurx_parse.h pack_lookup) packed into send[owner * cap + ..).
-// Kind 2 without goff (the single-pass source): no owner-count pass; tiles take their index
-// from the ticket counter `tick` (zero between launches) and find their offsets by decoupled
-// look-back over cnt, read as one 64-bit status word per (tile, owner) tagged with `epoch`
-// (k_rx, emurx_kernels.hip); the last tile writes send_count.  Kind 1 with tick (the
-// single-pass replicated route) packs the 40-B route records of the frames whose Namespace
-// was found straight into rsend the same way (no scan, no k_route<true> pass).
 struct emurx_route_args {
     uint32_t parts, rank, cap;
     uint32_t* cnt;
     uint32_t* grp;
     const uint32_t* goff;
     emurx_lookup_rec* send;
-    uint32_t* tick;
-    uint32_t* send_count;
-    uint32_t epoch;
-    emurx_route_rec* rsend;  // kind 1 single pass: the classified 40-B route records per owner
 };
 int emurx_launch_batch(const uint8_t* frames, const emurx_desc* desc, uint32_t n,
                        const emurx_dev_tables& T, int kind, const emurx_dev_out& out,

@@ -10,9 +10,6 @@
 //         Frames reach LDS by LDS-DMA (global_load_lds_dwordx4), with no VGPR round trip.
 // Queue q is the concatenation over tiles of qlist[q*qcap + t*TILE .. + tile_cnt[t][q]):
 // stable (frame order) without any cross-tile prefix, so no scan launch and no waiting.
-// The one exception is the single-pass partitioned source (kind 2 without an owner-count
-// pass): its owner regions are dense, so each tile waits for its predecessors' owner prefixes
-// (owner_lookback, decoupled look-back in ticket order) before it packs.
 // No MFMA: there is no dense contraction on this path; it is HBM / latency bound.
 #include <hip/hip_runtime.h>
 
@@ -130,42 +127,6 @@ struct TileLds {
     uint32_t toff[EMURX_MAX_PARTS];              // kKind 2: the tile's offset in each region
 };
 
-// Single-pass owner offsets of kind 2 (decoupled look-back, one lane per owner of wave 0,
-// after the tile barrier that made L.rcnt complete).  Status word per (tile, owner), 64 bits:
-// flag << 62 | epoch << 32 | value, flag 1 = the tile's own count, 2 = the inclusive prefix
-// through the tile.  A tile waits only on tiles with smaller tickets, which took them earlier
-// and so are resident: every wait ends (tile 0 waits on nothing).  A word of another epoch (or
-// flag 0: words a kind-1 route left, fresh memory) is not ready.  Relaxed agent-scope atomics:
-// the word carries its own value, nothing else is published with it.
-constexpr uint64_t kLbAgg = 1ull << 62, kLbInc = 2ull << 62;
-__device__ __forceinline__ void owner_lookback(const emurx_route_args& rt, uint32_t tile, uint32_t ntiles,
-                                               uint32_t lane, TileLds& L) {
-    unsigned long long* sw = reinterpret_cast<unsigned long long*>(rt.cnt);
-    const uint64_t tag = (uint64_t)(rt.epoch & 0x3fffffffu) << 32;
-    if (lane < rt.parts) {
-        const uint32_t own = L.rcnt[0][lane] + L.rcnt[1][lane] + L.rcnt[2][lane] + L.rcnt[3][lane];
-        unsigned long long* me = sw + (size_t)tile * EMURX_MAX_PARTS + lane;
-        uint32_t excl = 0;
-        if (tile > 0) {
-            __hip_atomic_store(me, kLbAgg | tag | own, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            for (uint32_t p = tile - 1;;) {
-                const uint64_t w = __hip_atomic_load(sw + (size_t)p * EMURX_MAX_PARTS + lane, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-                if ((w & (0x3fffffffull << 32)) != tag || (w >> 62) == 0) {
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                excl += (uint32_t)w;
-                if ((w >> 62) == 2 || p == 0) break;  // tile 0 publishes its inclusive word only
-                --p;
-            }
-        }
-        __hip_atomic_store(me, kLbInc | tag | (uint32_t)(excl + own), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        L.toff[lane] = excl;
-        if (tile == ntiles - 1) rt.send_count[lane] = excl + own;
-    }
-}
-
 // kKind: 0 parse only, 1 parse + classify, 2 parse + lookup keys (the partitioned source:
 // every frame's emurx_lookup_rec packed straight into its Namespace owner's send region, at
 // the offsets the owner-count pass (k_owner_count + k_route_scan) fixed; no table reads).
@@ -193,7 +154,7 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
     const uint32_t i = tile * EMURX_QUEUE_TILE + tid;
     if (lane < 16) L.wcnt[wv][lane] = 0;
     if (lane < EMURX_MAX_PARTS) L.rcnt[wv][lane] = 0;
-    if (kKind == 2 && !rt.tick && wv == 0)
+    if (kKind == 2 && wv == 0)
         tile_offsets(rt.cnt, rt.goff, rt.parts, tile, lane, L.toff, [](uint32_t v) { return wave_sum_u32(v); });
     const bool valid = (dd.y >> 24) != EMURX_DESC_HOLE;
     const uint32_t off = dd.x, len = dd.y & 0xffff, vport = (dd.y >> 16) & 0xff;
@@ -319,37 +280,12 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
     STAMP(7);
     __syncthreads();
     STAMP(8);
-    if (kKind == 1 && rt.cnt && !rt.tick && tid < 16) {
+    if (kKind == 1 && rt.cnt && tid < 16) {
         const uint32_t c = tid < rt.parts ? L.rcnt[0][tid] + L.rcnt[1][tid] + L.rcnt[2][tid] + L.rcnt[3][tid] : 0u;
         rt.cnt[(size_t)tile * 16 + tid] = c;
         if (c) atomicAdd(&rt.grp[(tile / 64) * 16 + tid], c);
     }
-    if (kKind == 1 && rt.tick) {  // single-pass route: the found records' 40-B route records
-        if (wv == 0) owner_lookback(rt, tile, (a.n + EMURX_QUEUE_TILE - 1) / EMURX_QUEUE_TILE, lane, L);
-        __syncthreads();
-        uint32_t dst = 0xffffffffu;
-        if (rd != 0xffu) {
-            uint32_t pos = L.toff[rd] + rrank;
-            for (uint32_t w = 0; w < wv; ++w) pos += L.rcnt[w][rd];
-            if (pos < rt.cap) dst = rd * rt.cap + pos;  // overflow: send_count[d] > cap tells the caller
-        }
-        // five 8-B pieces per record spread over the lanes (lane l of store k: piece (64k + l)
-        // mod 5 of record (64k + l) / 5), the 32-B record from the wave's park, as k_route<true>
-        const uint2* pk = reinterpret_cast<const uint2*>(slab) + wv * (kStage / 8);
-        const uint32_t r0 = tile * EMURX_QUEUE_TILE + wv * kWave;
-#pragma unroll
-        for (uint32_t k = 0; k < 5; ++k) {
-            const uint32_t p = k * kWave + lane, rr = p / 5, part = p - rr * 5;
-            const uint32_t to = (uint32_t)__shfl((int)dst, (int)rr);
-            if (to != 0xffffffffu)
-                reinterpret_cast<uint2*>(rt.rsend + to)[part] = part < 4 ? pk[rr * 4 + part] : make_uint2(r0 + rr, rt.rank);
-        }
-    }
     if constexpr (kKind == 2) {  // every frame's 64-byte lookup record into its owner's region
-        if (rt.tick) {  // single pass: this tile's offsets by look-back (wave 0, lane = owner)
-            if (wv == 0) owner_lookback(rt, tile, (a.n + EMURX_QUEUE_TILE - 1) / EMURX_QUEUE_TILE, lane, L);
-            __syncthreads();
-        }
         uint32_t dst = 0xffffffffu;  // the record's slot in send (record units), none on overflow
         if (rd != 0xffu) {
             uint32_t pos = L.toff[rd] + rrank;
@@ -411,18 +347,7 @@ template <int kKind, uint32_t kStage>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage == kStageNarrow ? 6 : 5))) void k_rx(const RxArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t slab[kWaves * kStage / 4];
     __shared__ TileLds L;
-    uint32_t tile = blockIdx.x;
-    const uint32_t wv = threadIdx.x / kWave;
-    if (kKind != 0 && a.rt.tick) {  // single pass: tiles in ticket order (owner_lookback)
-        if (threadIdx.x == 0) {
-            const uint32_t t = atomicAdd(a.rt.tick, 1u);
-            if (t == gridDim.x - 1) atomicExch(a.rt.tick, 0u);  // every other ticket is taken: zero for the next launch
-            L.toff[0] = t;
-        }
-        __syncthreads();
-        tile = L.toff[0];
-        __syncthreads();  // L.toff is the tile's offsets from here on
-    }
+    const uint32_t tile = blockIdx.x, wv = threadIdx.x / kWave;
 #if EMURX_STAMP
     unsigned long long pre[3];
     pre[0] = __builtin_amdgcn_s_memtime();
