@@ -136,35 +136,69 @@ __global__ __launch_bounds__(kScanThreads) void k_route_scan(uint32_t* __restric
 // ---- partitioned path -------------------------------------------------------------------
 // k_owner_count: the owner of every frame from its L2 header (l2_vlans: bytes 12..19 + the
 // length), counted per (tile, owner) and per group of 64 tiles, as k_route<false> counts
-// records; k_rx kind 2 then packs at the offsets k_route_scan derives.  8 bytes of frame +
-// the descriptor per frame.
+// records; k_rx kind 2 then packs at the offsets k_route_scan derives.  A wave whose frames'
+// byte range fits kOcStage bytes copies that range into LDS with coalesced LDS-DMA (as k_rx
+// stages) and reads each frame's bytes 12..19 there: a per-lane gather of one line per frame
+// ran at the random-line rate; wider waves gather (8 bytes of frame + the descriptor).
+constexpr uint32_t kOcStage = 6144;
 __global__ __launch_bounds__(kBlock) void k_owner_count(const uint8_t* __restrict__ frames,
                                                         const emurx_desc* __restrict__ desc, uint32_t n,
                                                         uint32_t n_parts, uint32_t* __restrict__ tile_cnt,
                                                         uint32_t* __restrict__ grp) {
     __shared__ uint32_t s_wcnt[kWaves][16];
+    // the wave's staged bytes + 32 bytes of slack for the aligned dword reads past its end
+    __shared__ __attribute__((aligned(16))) uint32_t s_stage[kWaves][(kOcStage + 32) / 4];
     const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / kWave, tile = blockIdx.x;
     const uint32_t i = tile * kBlock + tid;
     if (lane < 16) s_wcnt[wv][lane] = 0;
     const uint2 dd = i < n ? *reinterpret_cast<const uint2*>(desc + i) : make_uint2(0, EMURX_DESC_HOLE << 24);
     const bool valid = (dd.y >> 24) != EMURX_DESC_HOLE;
+    const uint32_t off = dd.x, len = dd.y & 0xffff;
+    const uint32_t lo = wave_min_u32(valid ? off : 0xffffffffu);
+    const uint32_t hi = wave_max_u32(valid ? off + len : 0u);
+    const uint32_t start = lo & ~15u, nvec = hi > lo ? (hi - start + 15) >> 4 : 0;
+    const bool staged = nvec > 0 && nvec <= kOcStage / 16;  // wave-uniform
+    if (staged) {
+        static_assert(kOcStage % (16 * kWave) == 0, "whole 1 KiB DMA rows");
+        const uint4* src = reinterpret_cast<const uint4*>(frames + start);
+        uint4* dst = reinterpret_cast<uint4*>(s_stage[wv]);
+#pragma unroll
+        for (uint32_t k = 0; k < kOcStage / 16 / kWave; ++k)
+            if (k * kWave < nvec)
+                __builtin_amdgcn_global_load_lds(src + min(lane + k * kWave, nvec - 1),
+                                                 (__attribute__((address_space(3))) void*)(dst + k * kWave), 16, 0, 2);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the wave's DMA landed
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
     uint32_t d = 0xffu;
     if (valid) {
-        const uint32_t len = dd.y & 0xffff, vport = (dd.y >> 16) & 0xff;
-        // bytes 12..19 from the three aligned dwords around them, each loaded only when it
-        // holds a byte of the frame (an aligned dword never crosses the 64-byte boundary the
-        // buffer contract guarantees past the last byte, emu_rx.h): one 12-byte load for every
-        // frame of 21 bytes or more; l2_vlans reads a word only where len says its bytes exist
-        const uintptr_t a = (uintptr_t)(frames + dd.x + 12);
-        const uint32_t sh = (uint32_t)(a & 3), lim = len + sh;  // dword k holds a frame byte iff 12 + 4k < lim
-        const void* wa = reinterpret_cast<const void*>(a & ~(uintptr_t)3);
-        uint32_t w0 = 0, w1 = 0, w2 = 0;
-        if (lim > 20) {
-            const uint3 w3 = gld12(wa);  // one 12-byte load
-            w0 = w3.x; w1 = w3.y; w2 = w3.z;
+        const uint32_t vport = (dd.y >> 16) & 0xff;
+        uint32_t w0 = 0, w1 = 0, w2 = 0, sh;
+        if (staged) {
+            // bytes past the frame are the next frame's or stale: l2_vlans reads a word only
+            // where len says its bytes exist
+            const uint32_t rel = off - start + 12;
+            sh = rel & 3;
+            const uint32_t* q = s_stage[wv] + (rel >> 2);
+            w0 = q[0]; w1 = q[1]; w2 = q[2];
         } else {
-            if (lim > 12) w0 = gld4(wa);
-            if (lim > 16) w1 = gld4(reinterpret_cast<const uint8_t*>(wa) + 4);
+            // bytes 12..19 from the three aligned dwords around them, each loaded only when it
+            // holds a byte of the frame (an aligned dword never crosses the 64-byte boundary the
+            // buffer contract guarantees past the last byte, emu_rx.h): one 12-byte load for every
+            // frame of 21 bytes or more; l2_vlans reads a word only where len says its bytes exist
+            const uintptr_t a = (uintptr_t)(frames + off + 12);
+            sh = (uint32_t)(a & 3);
+            const uint32_t lim = len + sh;  // dword k holds a frame byte iff 12 + 4k < lim
+            const void* wa = reinterpret_cast<const void*>(a & ~(uintptr_t)3);
+            if (lim > 20) {
+                const uint3 w3 = gld12(wa);  // one 12-byte load
+                w0 = w3.x; w1 = w3.y; w2 = w3.z;
+            } else {
+                if (lim > 12) w0 = gld4(wa);
+                if (lim > 16) w1 = gld4(reinterpret_cast<const uint8_t*>(wa) + 4);
+            }
         }
         const uint32_t b12 = __builtin_bswap32(__builtin_amdgcn_alignbyte(w1, w0, sh));
         const uint32_t b16 = __builtin_bswap32(__builtin_amdgcn_alignbyte(w2, w1, sh));
