@@ -383,7 +383,12 @@ int emurx_rx_stream(emurx_t* h, const uint8_t* msg, size_t len, emurx_rec* out_r
    events go ahead of it, and a whole-table or growing shipment synchronises the host with
    the stream (or the device).  Not capturable in a hipGraph: the kernel arguments carry the
    table addresses, which a later table growth reallocates; a capturing stream gets
-   EMURX_EINVAL.  Call emurx_sync first to take the shipment out of a latency-critical call. */
+   EMURX_EINVAL before anything is enqueued (the same for emurx_classify_route_dev,
+   emurx_parse_route_dev, emurx_lookup_dev and emurx_route_dev, whose scratch may be allocated
+   or change streams behind an event).  Call emurx_sync first to take the shipment out of a
+   latency-critical call.  No emurx_* call reads or clears the thread's last HIP error
+   (hipGetLastError): a launch's status is hipLaunchKernel's return value, so an error a
+   caller's earlier HIP call left pending is still pending after the call. */
 int emurx_classify_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_desc,
                        uint32_t n, const emurx_dev_out* out, void* stream);
 

@@ -307,3 +307,70 @@ def test_partitioned_edge_and_fuzz_frames(rxmod):
         for k in n2:
             ns.setdefault(k, len(ns))
     partitioned_vs_oracle(rxmod, shards, lambda t: load_frame_tables([t], ns, cl), 3)
+
+
+def test_capture_refused_before_enqueue(rxmod):
+    """Every device entry point that ships tables or takes route scratch refuses a capturing
+    stream with EMURX_EINVAL BEFORE it enqueues anything: the capture ends cleanly
+    (no foreign event waited on, no scratch allocated inside it), replaying the graph changes
+    nothing, and the same calls on the same stream work once it no longer captures."""
+    import torch
+    from emurx import exchange as X
+    from gpu_util import to_dev
+    n = 4096
+    w = synth.config_c(n)
+    rx = rxmod(0, max_ns=4096, max_clients=65536, max_frames=n)
+    rx.register_all()
+    synth.load_tables(w, rx)
+    # table edits pending at capture time: a call that shipped them would enqueue k_apply
+    c0 = int(w["clients"]["cid"][0])
+    rx.client_update_ipv4(c0, bytes([10, 9, 8, 7]))
+    buf, desc = to_dev(w["buf"]), to_dev(w["desc"])
+    qcap = abi.queue_cap(n)
+    rec = torch.full((n * 32,), 0xEE, dtype=torch.uint8, device="cuda")
+    ql = torch.full((abi.NUM_QUEUES * qcap,), -1, dtype=torch.int32, device="cuda")
+    tc = torch.full((abi.ntiles(n) * 16,), -1, dtype=torch.int32, device="cuda")
+    hist = torch.zeros(abi.HIST_SHARDS * 2 * abi.HIST_BINS, dtype=torch.int64, device="cuda")
+    cap = X.capacity(n, 2)
+    send = torch.full((2 * cap * X.LOOKUP_BYTES,), 0xEE, dtype=torch.uint8, device="cuda")
+    sc = torch.full((2,), -1, dtype=torch.int32, device="cuda")
+    out = torch.full((2 * cap * X.REC_BYTES,), 0xEE, dtype=torch.uint8, device="cuda")
+    rsend = torch.full((2 * cap * X.REC_BYTES,), 0xEE, dtype=torch.uint8, device="cuda")
+    calls = {
+        "classify_dev": lambda s: rx.classify_dev(buf, desc, n, rec, ql, qcap, tc, hist, stream=s),
+        "classify_route_dev": lambda s: rx.classify_route_dev(buf, desc, n, rec, ql, qcap, tc, hist, 2, 0, cap,
+                                                              rsend, sc, stream=s),
+        "parse_route_dev": lambda s: rx.parse_route_dev(buf, desc, n, None, ql, qcap, tc, hist, 2, 0, cap, send, sc,
+                                                        stream=s),
+        "lookup_dev": lambda s: rx.lookup_dev(send, sc, 2, cap, out, stream=s),
+        "route_dev": lambda s: rx.route_dev(rec, n, 2, 0, cap, rsend, sc, stream=s),
+    }
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    refused = {}
+    with torch.cuda.graph(g, stream=s):
+        for name, call in calls.items():
+            try:
+                call(s)
+                refused[name] = False
+            except RuntimeError as e:
+                refused[name] = "invalid argument" in str(e)
+    assert all(refused.values()), refused
+    g.replay()
+    torch.cuda.synchronize()
+    assert (rec == 0xEE).all() and (ql == -1).all() and (tc == -1).all() and (sc == -1).all()
+    assert (send == 0xEE).all() and (out == 0xEE).all() and (rsend == 0xEE).all() and (hist == 0).all()
+    # the edit is still pending and ships with the first real call; the outputs equal the oracle's
+    import pyoracle
+    from gpu_util import run_dev
+    o = pyoracle.Oracle()
+    synth.load_tables(w, o)
+    o.client_update_ipv4(c0, bytes([10, 9, 8, 7]))
+    want = o.rx_batch(w["buf"], w["desc"])[0]
+    got = run_dev(rx, w["buf"], w["desc"])[0]
+    assert got.tobytes() == want.tobytes(), rec_diff(got, want)
+    with torch.cuda.stream(s):
+        calls["parse_route_dev"](s)
+    torch.cuda.synchronize()
+    assert int(sc.sum()) == n

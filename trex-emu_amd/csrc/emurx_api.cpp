@@ -923,6 +923,8 @@ int emurx_classify_route_dev(emurx_t* h, const uint8_t* d_frames, const emurx_de
         (n && (!d_send || cap == 0)) || ((uintptr_t)d_send & 7))
         return EMURX_EINVAL;
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    // before anything is enqueued: nothing of a refused call may end up in the caller's graph
+    if ((rc = not_capturing(st))) return rc;
     emurx_t::RouteScratch* rs = nullptr;
     if ((rc = route_scratch(h, n, st, &rs))) return rc;
     const emurx_route_args rt{n_parts, my_rank, cap, rs->cnt.p, rs->grp.p, nullptr, nullptr};
@@ -949,6 +951,8 @@ int emurx_parse_route_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc*
         (n && (!d_send || cap == 0)) || ((uintptr_t)d_send & 15))
         return EMURX_EINVAL;
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    // before anything is enqueued: nothing of a refused call may end up in the caller's graph
+    if ((rc = not_capturing(st))) return rc;
     emurx_t::RouteScratch* rs = nullptr;
     if ((rc = route_scratch(h, n, st, &rs))) return rc;
     // owner counts from the L2 headers + group scan, then k_rx packs at those offsets
@@ -1112,6 +1116,8 @@ int emurx_route_dev(emurx_t* h, const emurx_rec* d_rec, uint32_t n, uint32_t n_p
     int rc = bind(h);
     if (rc) return rc;
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    // before anything is enqueued: nothing of a refused call may end up in the caller's graph
+    if ((rc = not_capturing(st))) return rc;
     emurx_t::RouteScratch* rs = nullptr;
     if ((rc = route_scratch(h, n, st, &rs))) return rc;
     if (emurx_launch_route(d_rec, n, n_parts, my_rank, cap, d_send, d_send_count, rs->cnt.p, rs->grp.p, rs->goff.p,

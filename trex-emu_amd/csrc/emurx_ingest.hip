@@ -181,23 +181,25 @@ __global__ __launch_bounds__(kBlock) void k_qpack(const uint32_t* __restrict__ q
 
 int emurx_launch_zmq_walk(const uint8_t* buf, const uint32_t* ctl, uint32_t nmsg, emurx_desc* desc,
                           uint32_t* msg_stat, hipStream_t st) {
-    (void)hipGetLastError();  // a status left by the caller's own failed HIP call is not this launch's
     using namespace emurx;
-    if (nmsg)
-        hipLaunchKernelGGL(k_zmq_walk, dim3((nmsg + kBlock - 1) / kBlock), dim3(kBlock), 0, st, buf, ctl, nmsg,
-                           desc, msg_stat);
-    return EMURX_HIP_OK(hipGetLastError()) ? 0 : -1;
+    if (!nmsg) return 0;
+    return EMURX_HIP_OK(emurx_launch(k_zmq_walk, dim3((nmsg + kBlock - 1) / kBlock), dim3(kBlock), 0, st, buf, ctl,
+                                     nmsg, desc, msg_stat))
+               ? 0
+               : -1;
 }
 
 int emurx_launch_queue_pack(const uint32_t* qlist, uint32_t qcap, const uint32_t* tile_cnt, uint32_t n,
                             uint32_t* seg_off, uint32_t* packed, uint32_t* qoff, uint64_t* hist,
                             uint64_t* hist_out, hipStream_t st) {
-    (void)hipGetLastError();  // a status left by the caller's own failed HIP call is not this launch's
     using namespace emurx;
     const uint32_t nt = (n + EMURX_QUEUE_TILE - 1) / EMURX_QUEUE_TILE;
-    hipLaunchKernelGGL(k_qscan, dim3(1), dim3(kScanLanes), 0, st, tile_cnt, nt, seg_off, qoff,
-                       reinterpret_cast<unsigned long long*>(hist), reinterpret_cast<unsigned long long*>(hist_out));
-    if (nt)
-        hipLaunchKernelGGL(k_qpack, dim3(nt), dim3(kBlock), 0, st, qlist, qcap, tile_cnt, seg_off, packed);
-    return EMURX_HIP_OK(hipGetLastError()) ? 0 : -1;
+    if (!EMURX_HIP_OK(emurx_launch(k_qscan, dim3(1), dim3(kScanLanes), 0, st, tile_cnt, nt, seg_off, qoff,
+                                   reinterpret_cast<unsigned long long*>(hist),
+                                   reinterpret_cast<unsigned long long*>(hist_out))))
+        return -1;
+    if (!nt) return 0;
+    return EMURX_HIP_OK(emurx_launch(k_qpack, dim3(nt), dim3(kBlock), 0, st, qlist, qcap, tile_cnt, seg_off, packed))
+               ? 0
+               : -1;
 }

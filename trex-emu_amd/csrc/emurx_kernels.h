@@ -4,6 +4,9 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <tuple>
+#include <type_traits>
+#include <utility>
 
 #include "../../include/emu_rx.h"
 #include "emurx_tables.h"
@@ -17,6 +20,21 @@ inline bool emurx_hip_ok(hipError_t e, const char* file, int line) {
     return false;
 }
 #define EMURX_HIP_OK(x) emurx_hip_ok((x), __FILE__, __LINE__)
+
+// One kernel launch whose status is the return value of hipLaunchKernel: the launchers never
+// read or clear the thread's last-error state, so an error a caller's own earlier HIP call
+// left pending stays pending for the caller (and is not taken for this launch's).
+template <typename... P, typename... A>
+inline hipError_t emurx_launch(void (*k)(P...), dim3 grid, dim3 block, size_t lds, hipStream_t st, A&&... a) {
+    static_assert(sizeof...(P) == sizeof...(A), "kernel argument count");
+    std::tuple<std::decay_t<P>...> args{std::forward<A>(a)...};
+    return std::apply(
+        [&](auto&... e) {
+            void* p[] = {(void*)&e...};
+            return hipLaunchKernel((const void*)k, grid, block, p, lds, st);
+        },
+        args);
+}
 
 // Enqueue one batch on `st`: a single k_rx launch, no host synchronisation (capturable in a
 // hipGraph).  ev[0..1] (optional) are recorded before and after it.  narrow: the 6 KiB

@@ -378,10 +378,9 @@ __global__ __launch_bounds__(kBlock) void k_apply(const emurx_delta* __restrict_
 }  // namespace emurx
 
 int emurx_launch_apply(const emurx_delta* d, uint32_t n, hipStream_t st) {
-    (void)hipGetLastError();  // a status left by the caller's own failed HIP call is not this launch's
     using namespace emurx;
-    if (n) hipLaunchKernelGGL(k_apply, dim3((n * 4 + kBlock - 1) / kBlock), dim3(kBlock), 0, st, d, n);
-    return EMURX_HIP_OK(hipGetLastError()) ? 0 : -1;
+    if (!n) return 0;
+    return EMURX_HIP_OK(emurx_launch(k_apply, dim3((n * 4 + kBlock - 1) / kBlock), dim3(kBlock), 0, st, d, n)) ? 0 : -1;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -391,9 +390,9 @@ int emurx_launch_batch(const uint8_t* frames, const emurx_desc* desc, uint32_t n
                        const emurx_dev_tables& T, int kind, const emurx_dev_out& out,
                        hipStream_t st, const hipEvent_t* ev, bool narrow, uint32_t* fb, uint32_t gen,
                        const emurx_route_args* rt) {
-    (void)hipGetLastError();  // a status left by the caller's own failed HIP call is not this launch's
     using namespace emurx;
-    if (ev) (void)hipEventRecord(ev[0], st);
+    hipError_t e = hipSuccess;
+    if (ev && !EMURX_HIP_OK(hipEventRecord(ev[0], st))) return -1;
     if (n) {
         const uint32_t ntiles = (n + EMURX_QUEUE_TILE - 1) / EMURX_QUEUE_TILE;
         unsigned long long* hist = reinterpret_cast<unsigned long long*>(out.hist);
@@ -403,10 +402,10 @@ int emurx_launch_batch(const uint8_t* frames, const emurx_desc* desc, uint32_t n
         auto k = kind == 1 ? (narrow ? k_rx<1, kStageNarrow> : k_rx<1, kStageWide>)
                : kind == 2 ? (narrow ? k_rx<2, kStageNarrow> : k_rx<2, kStageWide>)
                            : (narrow ? k_rx<0, kStageNarrow> : k_rx<0, kStageWide>);
-        hipLaunchKernelGGL(k, dim3(ntiles), dim3(kBlock), 0, st, args);
+        e = emurx_launch(k, dim3(ntiles), dim3(kBlock), 0, st, args);
     }
-    if (ev) (void)hipEventRecord(ev[1], st);
-    return EMURX_HIP_OK(hipGetLastError()) ? 0 : -1;
+    if (!EMURX_HIP_OK(e)) return -1;
+    return ev && !EMURX_HIP_OK(hipEventRecord(ev[1], st)) ? -1 : 0;
 }
 
 namespace emurx {
@@ -443,10 +442,10 @@ extern "C" int emurx_debug_set_stamps(void* dev_buf) {
 #endif
 
 extern "C" int emurx_copy_ceiling_dev(void* d_dst, const void* d_src, size_t bytes, void* stream) {
-    (void)hipGetLastError();  // a status left by the caller's own failed HIP call is not this launch's
     if (!d_dst || !d_src || (bytes & 15) || ((uintptr_t)d_dst & 15) || ((uintptr_t)d_src & 15)) return EMURX_EINVAL;
-    if (bytes)
-        hipLaunchKernelGGL(emurx::k_copy, dim3(emurx::kCopyGrid), dim3(emurx::kBlock), 0, (hipStream_t)stream,
-                           reinterpret_cast<uint4*>(d_dst), reinterpret_cast<const uint4*>(d_src), bytes / 16);
-    return EMURX_HIP_OK(hipGetLastError()) ? EMURX_OK : EMURX_EDEVICE;
+    if (!bytes) return EMURX_OK;
+    return EMURX_HIP_OK(emurx_launch(emurx::k_copy, dim3(emurx::kCopyGrid), dim3(emurx::kBlock), 0, (hipStream_t)stream,
+                                     reinterpret_cast<uint4*>(d_dst), reinterpret_cast<const uint4*>(d_src), bytes / 16))
+               ? EMURX_OK
+               : EMURX_EDEVICE;
 }

@@ -289,41 +289,46 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EMURX_LO
 int emurx_launch_owner_count(const uint8_t* frames, const emurx_desc* desc, uint32_t n, uint32_t n_parts,
                              uint32_t* send_count, uint32_t* tile_cnt, uint32_t* grp, uint32_t* grp_off,
                              hipStream_t st) {
-    (void)hipGetLastError();  // a status left by the caller's own failed HIP call is not this launch's
     using namespace emurx;
     const uint32_t ntiles = (n + kBlock - 1) / kBlock, ngroups = (ntiles + kGroup - 1) / kGroup;
     if (n == 0) return EMURX_HIP_OK(hipMemsetAsync(send_count, 0, n_parts * sizeof(uint32_t), st)) ? 0 : -1;
     if (ngroups > kScanThreads) return -1;
-    hipLaunchKernelGGL(k_owner_count, dim3(ntiles), dim3(kBlock), 0, st, frames, desc, n, n_parts, tile_cnt, grp);
-    hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(kScanThreads), 0, st, grp, ngroups, n_parts, grp_off, send_count);
-    return EMURX_HIP_OK(hipGetLastError()) ? 0 : -1;
+    if (!EMURX_HIP_OK(emurx_launch(k_owner_count, dim3(ntiles), dim3(kBlock), 0, st, frames, desc, n, n_parts,
+                                   tile_cnt, grp)))
+        return -1;
+    return EMURX_HIP_OK(emurx_launch(k_route_scan, dim3(1), dim3(kScanThreads), 0, st, grp, ngroups, n_parts, grp_off,
+                                     send_count))
+               ? 0
+               : -1;
 }
 
 int emurx_launch_lookup(const emurx_lookup_rec* recv, const uint32_t* recv_count, uint32_t n_parts, uint32_t cap,
                         const emurx_dev_tables& T, emurx_route_rec* out, uint32_t* flow, hipStream_t st) {
-    (void)hipGetLastError();  // a status left by the caller's own failed HIP call is not this launch's
     using namespace emurx;
-    if (n_parts && cap) {
-        if (n_parts > 65535) return -1;
-        hipLaunchKernelGGL(k_lookup, dim3((cap + kBlock - 1) / kBlock, n_parts), dim3(kBlock), 0, st, recv, recv_count,
-                           n_parts, cap, T, out, flow);
-    }
-    return EMURX_HIP_OK(hipGetLastError()) ? 0 : -1;
+    if (!n_parts || !cap) return 0;
+    if (n_parts > 65535) return -1;
+    return EMURX_HIP_OK(emurx_launch(k_lookup, dim3((cap + kBlock - 1) / kBlock, n_parts), dim3(kBlock), 0, st, recv,
+                                     recv_count, n_parts, cap, T, out, flow))
+               ? 0
+               : -1;
 }
 
 int emurx_launch_route(const emurx_rec* rec, uint32_t n, uint32_t n_parts, uint32_t my_rank, uint32_t cap,
                        emurx_route_rec* send, uint32_t* send_count, uint32_t* tile_cnt, uint32_t* grp,
                        uint32_t* grp_off, hipStream_t st, bool counted) {
-    (void)hipGetLastError();  // a status left by the caller's own failed HIP call is not this launch's
     using namespace emurx;
     const uint32_t ntiles = (n + kBlock - 1) / kBlock, ngroups = (ntiles + kGroup - 1) / kGroup;
     if (n == 0) return EMURX_HIP_OK(hipMemsetAsync(send_count, 0, n_parts * sizeof(uint32_t), st)) ? 0 : -1;
     if (ngroups > kScanThreads) return -1;
-    if (!counted)  // else k_rx counted the owners of this batch (emurx_set_route_parts)
-        hipLaunchKernelGGL(k_route<false>, dim3(ntiles), dim3(kBlock), 0, st, rec, n, n_parts, my_rank, tile_cnt,
-                           grp, (const uint32_t*)nullptr, send, cap);
-    hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(kScanThreads), 0, st, grp, ngroups, n_parts, grp_off, send_count);
-    hipLaunchKernelGGL(k_route<true>, dim3(ntiles), dim3(kBlock), 0, st, rec, n, n_parts, my_rank, tile_cnt, grp,
-                       grp_off, send, cap);
-    return EMURX_HIP_OK(hipGetLastError()) ? 0 : -1;
+    if (!counted &&  // else k_rx counted the owners of this batch (emurx_classify_route_dev)
+        !EMURX_HIP_OK(emurx_launch(k_route<false>, dim3(ntiles), dim3(kBlock), 0, st, rec, n, n_parts, my_rank,
+                                   tile_cnt, grp, (const uint32_t*)nullptr, send, cap)))
+        return -1;
+    if (!EMURX_HIP_OK(emurx_launch(k_route_scan, dim3(1), dim3(kScanThreads), 0, st, grp, ngroups, n_parts, grp_off,
+                                   send_count)))
+        return -1;
+    return EMURX_HIP_OK(emurx_launch(k_route<true>, dim3(ntiles), dim3(kBlock), 0, st, rec, n, n_parts, my_rank,
+                                     tile_cnt, grp, grp_off, send, cap))
+               ? 0
+               : -1;
 }

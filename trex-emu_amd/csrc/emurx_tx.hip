@@ -127,10 +127,10 @@ __global__ __launch_bounds__(kBlock) void k_tx_csum(uint8_t* __restrict__ frames
 
 int emurx_launch_tx_csum(uint8_t* frames, const emurx_tx_desc* desc, uint32_t n, uint8_t* status,
                          hipStream_t st) {
-    (void)hipGetLastError();  // a status left by the caller's own failed HIP call is not this launch's
     using namespace emurx;
-    if (n)
-        hipLaunchKernelGGL(k_tx_csum, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, frames, desc, n,
-                           status);
-    return EMURX_HIP_OK(hipGetLastError()) ? 0 : -1;
+    if (!n) return 0;
+    return EMURX_HIP_OK(emurx_launch(k_tx_csum, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, frames, desc, n,
+                                     status))
+               ? 0
+               : -1;
 }

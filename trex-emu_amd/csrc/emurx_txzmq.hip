@@ -319,7 +319,9 @@ __global__ __launch_bounds__(256) void k_txz_write(const uint8_t* __restrict__ f
         const unsigned long long obase = o0 & ~15ull;
         const uint32_t nrow = (uint32_t)(((o1 + 15) & ~15ull) - obase) >> 4;
         if constexpr (kStaged) {  // nsv, nrow within the budget (the test above)
-            __shared__ __attribute__((aligned(16))) uint32_t s_src[4][(kTxSrc + 16) / 4];
+            // 16 B of lead (below) + the budget + 16 B of tail: a frame ending at the budget's
+            // last byte reads the dword after it (masked out, but inside the array)
+            __shared__ __attribute__((aligned(16))) uint32_t s_src[4][(kTxSrc + 32) / 4];
             __shared__ __attribute__((aligned(16))) uint32_t s_out[4][kTxOut / 4];
             uint32_t* src = s_src[wv];
             uint32_t* o32 = s_out[wv];
@@ -506,14 +508,12 @@ size_t emurx_txz_scratch_bytes(uint32_t n) {
 
 int emurx_launch_tx_zmq(const uint8_t* frames, const emurx_desc* desc, uint32_t n, uint8_t* out, uint64_t cap,
                         uint64_t* msg_off, uint64_t* info, void* scratch, hipStream_t st) {
-    (void)hipGetLastError();  // a status left by the caller's own failed HIP call is not this launch's
     using namespace emurx;
     unsigned long long* mo = reinterpret_cast<unsigned long long*>(msg_off);
     unsigned long long* inf = reinterpret_cast<unsigned long long*>(info);
-    if (n == 0) {
-        hipLaunchKernelGGL(k_txz_finish, dim3(1), dim3(64), 0, st, nullptr, nullptr, 0u, mo, inf);
-        return EMURX_HIP_OK(hipGetLastError()) ? 0 : -1;
-    }
+    if (n == 0)
+        return EMURX_HIP_OK(emurx_launch(k_txz_finish, dim3(1), dim3(64), 0, st, nullptr, nullptr, 0u, mo, inf)) ? 0
+                                                                                                               : -1;
     struct Level {
         uint32_t units;
         uint32_t *X, *M, *E, *MB;
@@ -548,18 +548,20 @@ int emurx_launch_tx_zmq(const uint8_t* frames, const emurx_desc* desc, uint32_t 
         tl.X[k] = lv[k].X; tl.M[k] = lv[k].M; tl.E[k] = lv[k].E; tl.MB[k] = lv[k].MB;
         tl.B[k] = lv[k].B; tl.BB[k] = lv[k].BB;
     }
-    hipLaunchKernelGGL(k_txz_leaf, dim3((nt + 3) / 4), dim3(256), 0, st, desc, n, nt, lv[0].X, lv[0].M, lv[0].B);
-    for (uint32_t k = 1; k < tl.k0; ++k)
-        hipLaunchKernelGGL(k_txz_compose, dim3(lv[k].units), dim3(64), 0, st, lv[k - 1].X, lv[k - 1].M, lv[k - 1].B,
-                           lv[k - 1].units, lv[k].X, lv[k].M, lv[k].B);
-    hipLaunchKernelGGL(k_txz_top, dim3(1), dim3(kTxTopWaves * kWave), 0, st, tl);
-    for (int k = (int)tl.k0 - 1; k >= 1; --k)
-        hipLaunchKernelGGL(k_txz_descend, dim3(lv[k].units), dim3(64), 0, st, lv[k - 1].X, lv[k - 1].M,
-                           lv[k - 1].B, lv[k - 1].units, lv[k].E, lv[k].MB, lv[k].BB, lv[k - 1].E, lv[k - 1].MB,
-                           lv[k - 1].BB);
-    hipLaunchKernelGGL(k_txz_write<true>, dim3((nt + 3) / 4), dim3(256), 0, st, frames, desc, n, nt, lv[0].E,
-                       lv[0].MB, lv[0].BB, out, (unsigned long long)cap, mo, done);
-    hipLaunchKernelGGL(k_txz_write<false>, dim3((nt + 3) / 4), dim3(256), 0, st, frames, desc, n, nt, lv[0].E,
-                       lv[0].MB, lv[0].BB, out, (unsigned long long)cap, mo, done);
-    return EMURX_HIP_OK(hipGetLastError()) ? 0 : -1;
+    hipError_t e = emurx_launch(k_txz_leaf, dim3((nt + 3) / 4), dim3(256), 0, st, desc, n, nt, lv[0].X, lv[0].M,
+                                lv[0].B);
+    for (uint32_t k = 1; k < tl.k0 && e == hipSuccess; ++k)
+        e = emurx_launch(k_txz_compose, dim3(lv[k].units), dim3(64), 0, st, lv[k - 1].X, lv[k - 1].M, lv[k - 1].B,
+                         lv[k - 1].units, lv[k].X, lv[k].M, lv[k].B);
+    if (e == hipSuccess) e = emurx_launch(k_txz_top, dim3(1), dim3(kTxTopWaves * kWave), 0, st, tl);
+    for (int k = (int)tl.k0 - 1; k >= 1 && e == hipSuccess; --k)
+        e = emurx_launch(k_txz_descend, dim3(lv[k].units), dim3(64), 0, st, lv[k - 1].X, lv[k - 1].M, lv[k - 1].B,
+                         lv[k - 1].units, lv[k].E, lv[k].MB, lv[k].BB, lv[k - 1].E, lv[k - 1].MB, lv[k - 1].BB);
+    if (e == hipSuccess)
+        e = emurx_launch(k_txz_write<true>, dim3((nt + 3) / 4), dim3(256), 0, st, frames, desc, n, nt, lv[0].E,
+                         lv[0].MB, lv[0].BB, out, (unsigned long long)cap, mo, done);
+    if (e == hipSuccess)
+        e = emurx_launch(k_txz_write<false>, dim3((nt + 3) / 4), dim3(256), 0, st, frames, desc, n, nt, lv[0].E,
+                         lv[0].MB, lv[0].BB, out, (unsigned long long)cap, mo, done);
+    return EMURX_HIP_OK(e) ? 0 : -1;
 }

@@ -121,6 +121,12 @@ int Parser::dispatch(const emurx_rec& r, Mbuf* m, CTunnelKey* tun, bool memo) {
     ParserCb* cb = callback(r.proto);
     if (!cb || !*cb) throw std::runtime_error("emu: nil ParserCb");  // Go: nil func call
     CThreadCtx::Memo& mo = tctx->memo_;
+    // the memo lives exactly as long as the callback: off again on return AND when the callback
+    // throws (a Go panic), so no later lookup compares against this frame's freed Mbuf
+    struct Off {
+        CThreadCtx::Memo& m;
+        ~Off() { m.on = false; }
+    } off{mo};
     mo.on = memo;
     if (!memo) tctx->memo_stats.stale++;
     mo.tun = *tun;
@@ -131,9 +137,7 @@ int Parser::dispatch(const emurx_rec& r, Mbuf* m, CTunnelKey* tun, bool memo) {
     mo.frame = m->GetData();
     mo.len = m->PktLen();
     mo.l3 = r.l3;
-    const int rv = (*cb)(&ps);
-    mo.on = false;
-    return rv;
+    return (*cb)(&ps);
 }
 
 int Parser::ParsePacket(Mbuf* m) {
@@ -263,6 +267,7 @@ uint64_t mac48(const uint8_t* m) {
 }  // namespace
 
 int CThreadCtx::AddNs(const CTunnelKey& key, uint32_t plugins) {
+    memo_.on = false;  // an edit from inside a callback: the frame's GPU answer may be stale
     const uint32_t id = next_ns_;
     const int rc = emurx_ns_add(h_, key.b, id, plugins);
     if (rc) return rc;
@@ -271,12 +276,14 @@ int CThreadCtx::AddNs(const CTunnelKey& key, uint32_t plugins) {
     return (int)id;
 }
 int CThreadCtx::RemoveNs(const CTunnelKey& key) {
+    memo_.on = false;  // an edit from inside a callback: the frame's GPU answer may be stale
     const int rc = emurx_ns_remove(h_, key.b);
     if (rc == EMURX_OK) ns_map_.erase(key12(key));
     return rc;
 }
 int CThreadCtx::AddClient(uint32_t ns, const uint8_t mac[6], const uint8_t ipv4[4], const uint8_t ipv6[16],
                           uint32_t plugins) {
+    memo_.on = false;  // an edit from inside a callback: the frame's GPU answer may be stale
     const uint32_t id = next_client_;
     const int rc = emurx_client_add(h_, ns, id, mac, ipv4, ipv6, nullptr, plugins);
     if (rc) return rc;
@@ -288,6 +295,7 @@ int CThreadCtx::AddClient(uint32_t ns, const uint8_t mac[6], const uint8_t ipv4[
     return (int)id;
 }
 int CThreadCtx::RemoveClient(uint32_t ns, const uint8_t mac[6]) {
+    memo_.on = false;  // an edit from inside a callback: the frame's GPU answer may be stale
     const int rc = emurx_client_remove(h_, ns, mac);
     if (rc != EMURX_OK) return rc;
     auto it = mac_map_.find({ns, mac48(mac)});
@@ -300,6 +308,7 @@ int CThreadCtx::RemoveClient(uint32_t ns, const uint8_t mac[6]) {
     return rc;
 }
 int CThreadCtx::UpdateClientIpv4(uint32_t ns, uint32_t client, const uint8_t ipv4[4]) {
+    memo_.on = false;  // an edit from inside a callback: the frame's GPU answer may be stale
     const int rc = emurx_client_update_ipv4(h_, client, ipv4);
     if (rc != EMURX_OK) return rc;
     auto& ck = client_keys_[client];

@@ -361,6 +361,34 @@ void TestMemoLookups() {
     };
     tctx.veth.OnRxBatch({msgs[0]});
     if (bad || s.probes != 16 || s.hits != 0) FATALF(" other keys: bad %d probes %lu", bad, (unsigned long)s.probes);
+    // a callback that edits the maps (dhcp.go:718 updates its own client) and then looks its own
+    // frame's key up again: the edit turned the memo off, the answer comes from the maps
+    tctx.memo_stats = {};
+    tctx.parser.udp = [&](ParserPacketState* ps) {
+        CThreadCtx* t = ps->Tctx;
+        const uint8_t* dst = ps->M->GetData();
+        const int c = t->CLookupByMac((uint32_t)ns, dst);
+        if (c >= 0 && dst[5] == macs[5][5]) {
+            if (t->RemoveClient((uint32_t)ns, dst) != EMURX_OK) bad++;
+            truth.erase(dst[5]);
+            if (t->CLookupByMac((uint32_t)ns, dst) != -1) bad++;  // not the pre-edit GPU answer
+        }
+        return 0;
+    };
+    tctx.veth.OnRxBatch({msgs[0]});
+    if (bad || truth.count(macs[5][5])) FATALF(" a lookup after an edit in its own callback: bad %d", bad);
+    // a callback that throws (a Go panic): the memo does not outlive it, so a lookup made after
+    // the batch (the frame's Mbuf gone) goes to the maps
+    tctx.parser.udp = [&](ParserPacketState*) -> int { throw std::runtime_error("plugin panic"); };
+    bool threw = false;
+    try {
+        tctx.veth.OnRxBatch({msgs[1]});
+    } catch (const std::runtime_error&) {
+        threw = true;
+    }
+    tctx.memo_stats = {};
+    if (!threw || tctx.GetNs(key) != ns || s.hits != 0 || s.probes != 1)
+        FATALF(" memo after a throwing callback: threw %d hits %lu", (int)threw, (unsigned long)s.hits);
 }
 
 }  // namespace
