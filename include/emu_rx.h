@@ -220,13 +220,14 @@ typedef struct emurx_cfg {
                               generations and image queries, no device: data-path calls
                               return EMURX_EDEVICE) */
     uint32_t max_ns;       /* ns ids must be < max_ns */
-    uint32_t max_clients;  /* client ids must be < max_clients.  The device tables are sized
-                              for max_ns / max_clients and kept sparse so that a lookup
-                              almost always ends in its home bucket: about 128 B of device
-                              memory per Namespace and 1.7 KB per client (MAC, IPv4, IPv6,
-                              client info), 1/n_parts of that when partitioned; env
-                              EMURX_TABLE_SPREAD="ns,mac,ip,ci" (slots per entry, powers of
-                              two >= 2; default 8,8,16,16) trades them back */
+    uint32_t max_clients;  /* client ids must be < max_clients.  The device tables are
+                              two-choice cuckoo tables sized for max_ns / max_clients (every
+                              lookup reads its key's two candidate buckets in one round
+                              trip, whatever the load): about 48 B of device memory per
+                              Namespace and 250 B per client (MAC, IPv4, IPv6, client info),
+                              1/n_parts of that when partitioned; they grow on demand.  env
+                              EMURX_TABLE_LOAD="two,one" (starting load in percent of the
+                              two-slot and one-slot bucket tables; default 50,35) */
     uint32_t max_frames;   /* frames per batch (device scratch is sized for it) */
     uint32_t max_bytes;    /* bytes per host batch (emurx_rx_stream staging) */
 } emurx_cfg;
@@ -317,13 +318,13 @@ int emurx_server_add(emurx_t* h, uint32_t client_id, uint16_t port, uint8_t prot
 int emurx_server_remove(emurx_t* h, uint32_t client_id, uint16_t port, uint8_t proto);
 int emurx_client_set_transport(emurx_t* h, uint32_t client_id, int has_ctx);
 /* Table edits reach the device incrementally: every call above edits the slots of the
-   device table image it changes (deleted slots become tombstones) and marks the 64-byte
-   blocks it touched.  Before the next launch that reads the tables, the edited blocks are
+   device table image it changes (a cuckoo insert may move other entries to their second
+   bucket; a delete clears its slot) and marks the 64-byte blocks it touched.  Before the next launch that reads the tables, the edited blocks are
    copied to the device and scattered by one kernel on that launch's stream, ordered after
    every launch on any stream that read the tables since the previous shipment (stream
    events, no host synchronisation) and before every later reader.  A table that outgrows
-   its load factor is rebuilt larger and shipped whole (then the host waits for the device
-   once).  Streams given to the library must outlive the handle.
+   its load factor, or whose cuckoo insert found no place (rebuilt with a new hash seed), is
+   shipped whole (then the host waits for the device once).  Streams given to the library must outlive the handle.
    emurx_sync ships pending edits now, on `stream` (NULL = the handle's stream). */
 int emurx_sync(emurx_t* h, void* stream);
 /* diagnostics: 64-byte blocks shipped as deltas and whole tables uploaded since emurx_open,

@@ -29,6 +29,9 @@ for what in "${@:-all}"; do
     run bench_B_driver 600 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline; stop_on_fault $?
     run bench_C 600 python bench.py --config C --steps 100 --warmup 10 --no-cpu-baseline; stop_on_fault $?
     run bench_E 600 python bench.py --config E --steps 50 --warmup 5 --no-cpu-baseline; stop_on_fault $? ;;&
+  dclass)
+    run bench_DN 600 python bench.py --config D --tables none --no-exchange-run --steps 50 --warmup 5 --no-cpu-baseline; stop_on_fault $?
+    run bench_D 600 python bench.py --config D --no-exchange-run --steps 50 --warmup 5 --no-cpu-baseline; stop_on_fault $? ;;&
   prof|all)
     run prof_B 600 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof_B -o run --output-format csv \
         -- python bench.py --steps 50 --warmup 5 --no-cpu-baseline; stop_on_fault $?
