@@ -104,6 +104,10 @@ def parse_args():
                     help="rendezvous + max-over-ranks reduction only, no GPU (CPU test of the launch path)")
     ap.add_argument("--host-path", action="store_true",
                     help="also time the host-inclusive path (pinned H2D + kernels + D2H)")
+    ap.add_argument("--dump-exchange", default=None, metavar="DIR",
+                    help="N > 1 with an exchange: after the timed steps, run 4 more overlapped steps and write "
+                         "every rank's received and resolved records per step, and its input batches, to DIR "
+                         "(tests/test_bench_launch.py checks them against the oracle)")
     return ap.parse_args()
 
 
@@ -437,6 +441,7 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         alloc_regions()
 
         def produce(b, k):
+            b["k"] = k
             fb, fd = inputs[k % R]
             if mode == "replicated":
                 # classify + route in one call: the route's owner counts are taken inside k_rx
@@ -452,6 +457,13 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             b["pending"] = None
             if mode == "partitioned":
                 rx.lookup_dev(xch["recv"], xch["recv_count"], world, xch["cap"], b["out"], stream=stream)
+            if xch.get("dump") is not None:  # --dump-exchange: this step's owner records, as they are now
+                torch.cuda.synchronize()
+                cnt = xch["recv_count"].cpu().numpy().astype(np.int64)
+                res = (b["out"] if mode == "partitioned" else xch["recv"]).cpu().numpy()
+                res = res.reshape(world, -1)[:, : xch["cap"] * X.REC_BYTES]
+                xch["dump"].append(dict(k=b["k"], cnt=cnt, recs=np.concatenate(
+                    [res[sr, : min(int(cnt[sr]), xch["cap"]) * X.REC_BYTES] for sr in range(world)])))
 
         def step_overlapped():
             """Batch k: parse + pack, then its all-to-all starts on the collective stream while
@@ -716,6 +728,8 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
                                for b in xch["sets"]):
         raise RuntimeError("exchange region overflow in the timed region")
 
+    if a.dump_exchange and xch is not None and overlapped:
+        dump_exchange(a, xch, inputs, R, rank, world, dist, torch, step_overlapped, drain)
     phases = None
     if xch is not None:
         phases = phase_breakdown()
@@ -854,6 +868,32 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             out["exchange"]["one_stream_steps"] = {"value": out["value"], "ms_per_step": out["ms_per_step"]}
             out["value"], out["ms_per_step"] = pipelined["value"], pipelined["ms_per_step"]
     return out, rx, w
+
+
+def dump_exchange(a, xch, inputs, R, rank, world, dist, torch, step_overlapped, drain, k_steps=4):
+    """--dump-exchange: k_steps more steps of the overlapped pipeline exactly as timed (batch k's
+    all-to-all started, then the previous batch's owner lookups), each step's records saved
+    when its consume() has run; then the batch slots' frames and descriptors.  Untimed."""
+    import numpy as np
+    d = Path(a.dump_exchange)
+    d.mkdir(parents=True, exist_ok=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    xch["k"] = 0
+    xch["dump"] = []
+    for _ in range(k_steps):
+        step_overlapped()
+    drain()
+    torch.cuda.synchronize()
+    for e in xch["dump"]:
+        np.savez(d / f"rank{rank}_step{e['k']}.npz", cnt=e["cnt"], recs=e["recs"], slot=e["k"] % R,
+                 cap=xch["cap"], mode=xch["rb"])
+    for j in range(R):
+        np.savez(d / f"rank{rank}_slot{j}.npz", buf=inputs[j][0].cpu().numpy(), desc=inputs[j][1].cpu().numpy())
+    xch["dump"] = None
+    if world > 1:
+        dist.barrier()
 
 
 def table_update_cost(a, rx, w, torch, rounds=8):

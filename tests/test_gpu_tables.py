@@ -176,7 +176,7 @@ def _owners_by_key(rec, parts):
     return out
 
 
-def partitioned_vs_oracle(rxmod, shards, load, parts, flows=None):
+def partitioned_vs_oracle(rxmod, shards, load, parts, flows=None, max_ns=4096, max_clients=65536):
     """Shards through the partitioned path (one handle per partition) and through the
     replicated classify + route, against the oracle.  load(target) fills a table target;
     flows(targets, orecs) may add transport state to every target."""
@@ -188,12 +188,12 @@ def partitioned_vs_oracle(rxmod, shards, load, parts, flows=None):
     n = max(len(w["desc"]) for w in shards)
     o = pyoracle.Oracle()
     load(o)
-    full = rxmod(0, max_ns=4096, max_clients=65536, max_frames=n)
+    full = rxmod(0, max_ns=max_ns, max_clients=max_clients, max_frames=n)
     full.register_all()
     load(full)
     owners = []
     for p in range(parts):
-        h = rxmod(0, max_ns=4096, max_clients=65536, max_frames=n)
+        h = rxmod(0, max_ns=max_ns, max_clients=max_clients, max_frames=n)
         h.register_all()
         h.set_partition(parts, p)
         load(h)
@@ -264,12 +264,9 @@ def partitioned_vs_oracle(rxmod, shards, load, parts, flows=None):
     return o, orecs
 
 
-@pytest.mark.parametrize("parts", [2, 4])
-def test_partitioned_lookups_equal_replicated(rxmod, parts):
-    """Config C shards with bare SYNs, flows and listeners: records and flow decisions."""
-    n = 40000
-    shards = [synth.config_c(n, rank=s, syn=0.3) for s in range(parts)]
-
+def transport_state(shards):
+    """flows(targets, orecs) for partitioned_vs_oracle: flows for a third of shard 0's TCP / UDP
+    frames and listeners on a fifth of their destination ports, on every target."""
     def flows(targets, orecs):
         tup = frame_tuples(shards[0]["buf"], shards[0]["desc"], orecs[0])
         rng = np.random.default_rng(0xAB)
@@ -282,7 +279,16 @@ def test_partitioned_lookups_equal_replicated(rxmod, parts):
             dport = (t[10] << 8 | t[11]) if len(t) == 13 else (t[34] << 8 | t[35])
             proto = 6 if orecs[0][i]["proto"] == abi.CB_TCP else 17
             assert len({x.server_add(cid, dport, proto) for x in targets}) == 1
-    o, orecs = partitioned_vs_oracle(rxmod, shards, lambda t: synth.load_tables(shards[0], t), parts, flows)
+    return flows
+
+
+@pytest.mark.parametrize("parts", [2, 4])
+def test_partitioned_lookups_equal_replicated(rxmod, parts):
+    """Config C shards with bare SYNs, flows and listeners: records and flow decisions."""
+    n = 40000
+    shards = [synth.config_c(n, rank=s, syn=0.3) for s in range(parts)]
+    o, orecs = partitioned_vs_oracle(rxmod, shards, lambda t: synth.load_tables(shards[0], t), parts,
+                                     transport_state(shards))
     allf = o.flows(shards[0]["buf"], shards[0]["desc"], orecs[0])
     assert (allf <= abi.FLOW_ID_MAX).sum() > 1000 and (allf == abi.FLOW_NEW).sum() > 100
 
@@ -374,3 +380,17 @@ def test_capture_refused_before_enqueue(rxmod):
         calls["parse_route_dev"](s)
     torch.cuda.synchronize()
     assert int(sc.sum()) == n
+
+
+@pytest.mark.timeout(900)
+def test_partitioned_config_d_full_tables(rxmod):
+    """Config D's full tables (32,768 Namespaces, 1,048,576 clients) split over 8
+    partition handles on one GPU, as 8 ranks hold them: each of 8 shards (256K frames each, 2M
+    in all) goes through parse_route_dev, the all-to-all is played on the device, and every
+    owner's lookup_dev output -- records and flow decisions, with flows and listeners present
+    -- is bit-exact against the oracle's classification (ns_ctx.go:262-329,
+    thread_ctx.go:772-784), and its records with a Namespace equal the replicated route's."""
+    parts = 8
+    shards = [synth.config_d(1 << 18, rank=s) for s in range(parts)]
+    partitioned_vs_oracle(rxmod, shards, lambda t: synth.load_tables(shards[0], t), parts,
+                          transport_state(shards), max_ns=32768, max_clients=1 << 20)
