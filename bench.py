@@ -104,6 +104,9 @@ def parse_args():
                     help="rendezvous + max-over-ranks reduction only, no GPU (CPU test of the launch path)")
     ap.add_argument("--host-path", action="store_true",
                     help="also time the host-inclusive path (pinned H2D + kernels + D2H)")
+    ap.add_argument("--unkeyed", action="store_true",
+                    help="leave the descriptors without owner keys (EMURX_DESC_KEYED): the partitioned source's "
+                         "owner-count pass then reads every frame's L2 header instead of the descriptors alone")
     ap.add_argument("--dump-exchange", default=None, metavar="DIR",
                     help="N > 1 with an exchange: after the timed steps, run 4 more overlapped steps and write "
                          "every rank's received and resolved records per step, and its input batches, to DIR "
@@ -397,6 +400,12 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
     desc = torch.from_numpy(w["desc"].view(np.uint8).copy()).to(dev)
     inputs = [(buf, desc)] + [permuted_batch(torch, buf, w["desc"], (int(w["seed"]) << 8) + j + 1000 * rank, dev)
                               for j in range(1, R)]
+    if not a.unkeyed:
+        # the descriptors as the device framing walk hands them over (veth_zmq.go:277-320): each
+        # with its frame's Namespace-owner key (EMURX_DESC_KEYED), which the walk derives from
+        # the frame header it reads anyway; untimed, as the rest of the descriptors' making
+        for fb, fd in inputs:
+            rx.desc_keys_dev(fb, fd, n, stream=torch.cuda.current_stream(dev).cuda_stream)
     qcap = abi.queue_cap(n)
 
     def outputs():
@@ -798,6 +807,7 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             "frame_bytes_per_gpu": w["nbytes"],
             "parallelism": par,
             "tables": mode if mode != "none" else "replicated",
+            "descriptors": "unkeyed" if a.unkeyed else "keyed (EMURX_DESC_KEYED owner keys, as the device framing walk writes them)",
             "table_bytes_per_gpu": ts["table_bytes"],
             "streams": S,
             "batches": R,

@@ -151,11 +151,19 @@ typedef struct emurx_desc {
     uint32_t off;
     uint16_t len;
     uint8_t vport;
-    uint8_t pad;   /* 0, or EMURX_DESC_HOLE */
+    uint8_t pad;   /* 0, EMURX_DESC_HOLE, or the frame's owner key (EMURX_DESC_KEYED) */
 } emurx_desc;
 /* pad value of an empty descriptor slot: no frame, no record, no queue entry, not counted
    (the batched ingest leaves one for every frame a message announced but did not carry) */
 #define EMURX_DESC_HOLE 0xFFu
+/* pad = EMURX_DESC_KEYED | k (k <= 126): the frame's Namespace-owner key, a 7-bit digest of
+   the CTunnelKey its parse leaves (vport and the dot1q / QinQ words of its first 22 bytes,
+   parser.go:801-818).  The device framing walk of the batched ingest writes it with every
+   descriptor (it reads the frame's header there anyway); emurx_desc_keys_dev writes it for
+   descriptors built elsewhere; emurx_owner_key gives it for a key.  With keyed descriptors
+   emurx_parse_route_dev counts the owners from the descriptors alone instead of re-reading
+   every frame's header.  A key that does not match the frame misroutes that frame. */
+#define EMURX_DESC_KEYED 0x80u
 
 /* 32-byte record, one per frame, in frame order.  The numeric fields are exactly the
    ParserPacketState the reference hands to a ParserCb (parser.go:51-61) plus the
@@ -565,6 +573,13 @@ typedef struct emurx_route_rec {
 } emurx_route_rec;       /* 40 bytes */
 
 uint32_t emurx_ns_owner(const uint8_t key[12], uint32_t n_parts);
+/* the descriptor owner key of a CTunnelKey (EMURX_DESC_KEYED | k); emurx_ns_owner(key, n) =
+   ((k & 0x7f) * n) >> 7 for every n_parts <= EMURX_MAX_PARTS */
+uint8_t emurx_owner_key(const uint8_t key[12]);
+/* Write the owner key (EMURX_DESC_KEYED) of every frame into d_desc[i].pad, in place (holes
+   stay holes): what the device framing walk does, for descriptors built without it.  Reads
+   8 bytes of every frame.  One launch, no host synchronisation. */
+int emurx_desc_keys_dev(emurx_t* h, const uint8_t* d_frames, emurx_desc* d_desc, uint32_t n, void* stream);
 /* d_rec: the batch's records (device), n frames; d_send: [n_parts * cap] (device);
    d_send_count: [n_parts] (device).  Three kernel launches on `stream`, no host sync. */
 int emurx_route_dev(emurx_t* h, const emurx_rec* d_rec, uint32_t n, uint32_t n_parts, uint32_t my_rank,
@@ -597,8 +612,9 @@ typedef struct emurx_lookup_rec {
 /* Parse the batch (records without lookups into out->rec when non-NULL, queues, histogram as
    emurx_parse_dev) and pack the lookup record of every frame (holes excepted) into the region
    of its Namespace's owner: d_send[d * cap ..  + d_send_count[d]), frame order.  Three
-   launches: the owner counts from each frame's L2 header (8 bytes), their group scan, and
-   k_rx writing each lookup record at its final place.  Reads no table.  A region holds at
+   launches: the owner counts (from the descriptors' owner keys, EMURX_DESC_KEYED; a frame
+   without one has its L2 header read, 8 bytes), their group scan, and k_rx writing each
+   lookup record at its final place.  Reads no table.  A region holds at
    most cap records: d_send_count[d] is the true count, and a count > cap means records were
    dropped from that region.  The caller must check every count of every batch (after the
    count exchange, on every rank) and, on overflow, grow cap and route the batch again; the

@@ -122,3 +122,15 @@ def frame_tuples(buf, desc, rec):
         else:
             out.append(p[l3 + 8:l3 + 40] + p[l4:l4 + 4] + bytes([int(r["next_hdr"])]))
     return out
+
+
+def owner_keys(rec):
+    """The descriptor owner key (EMURX_DESC_KEYED | digest) of every record's CTunnelKey."""
+    from emurx import frames as F
+    from emurx.rx import owner_key
+    if len(rec) == 0:
+        return np.zeros(0, np.uint8)
+    k = np.stack([rec["vport"].astype(np.uint64), rec["vlan0"].astype(np.uint64), rec["vlan1"].astype(np.uint64)], 1)
+    uk, inv = np.unique(k, axis=0, return_inverse=True)
+    ok = np.array([owner_key(F.tunnel_key(int(a), int(b), int(c))) for a, b, c in uk], np.uint8)
+    return ok[inv.reshape(-1)]

@@ -13,7 +13,7 @@ import kat_frames as K
 from emurx import abi
 from emurx import frames as F
 from emurx import synth
-from gpu_util import frames_tables, load_frame_tables, rec_diff, run_dev
+from gpu_util import frames_tables, load_frame_tables, owner_keys, rec_diff, run_dev
 
 pytestmark = pytest.mark.gpu
 ALL = (1 << 12) - 1
@@ -677,7 +677,13 @@ def check_ingest(res, o, msgs, tab):
     for d, t in zip(want_desc, tab):
         d["off"] += t["off"]
     want_desc = np.concatenate(want_desc) if want_desc else np.zeros(0, abi.DESC_DTYPE)
-    assert res["desc"].tobytes() == want_desc.tobytes()
+    # the device walk keys every descriptor (EMURX_DESC_KEYED): the owner key of the
+    # CTunnelKey the frame's parse leaves; the host walk's descriptors carry none
+    got = res["desc"].copy()
+    keys = got["pad"].copy()
+    got["pad"] = 0
+    assert got.tobytes() == want_desc.tobytes()
+    assert np.array_equal(keys, owner_keys(rec)), "descriptor owner keys"
     assert res["counters"] == cnt
 
 

@@ -394,3 +394,48 @@ def test_partitioned_config_d_full_tables(rxmod):
     shards = [synth.config_d(1 << 18, rank=s) for s in range(parts)]
     partitioned_vs_oracle(rxmod, shards, lambda t: synth.load_tables(shards[0], t), parts,
                           transport_state(shards), max_ns=32768, max_clients=1 << 20)
+
+
+def test_keyed_descriptors_route_the_same(rxmod):
+    """Owner counts from descriptor owner keys (EMURX_DESC_KEYED, written by emurx_desc_keys_dev
+    as the device framing walk writes them) instead of every frame's L2 header: config D frames
+    routed to 8 owners give byte-equal send regions and counts with unkeyed, keyed and
+    half-keyed descriptors (holes included), and the keys equal emurx_owner_key of the
+    CTunnelKey the oracle's parse leaves."""
+    import pyoracle
+    import torch
+    from emurx import exchange as X
+    from gpu_util import owner_keys, to_dev
+    n = 1 << 17
+    w = synth.config_d(n, rank=3)
+    desc = w["desc"].copy()
+    holes = np.random.default_rng(4).random(n) < 0.01
+    desc["pad"][holes] = abi.DESC_HOLE
+    rx = rxmod(0, max_ns=4096, max_clients=65536, max_frames=n)
+    buf = to_dev(w["buf"])
+    dk = to_dev(desc)
+    rx.desc_keys_dev(buf, dk, n)
+    torch.cuda.synchronize()
+    keyed = dk.cpu().numpy()[: n * 8].view(abi.DESC_DTYPE).copy()
+    orec = pyoracle.Oracle().rx_batch(w["buf"], w["desc"])[0]
+    assert np.array_equal(keyed["pad"][holes], np.full(holes.sum(), abi.DESC_HOLE, np.uint8))
+    assert np.array_equal(keyed["pad"][~holes], owner_keys(orec[~holes]))
+    plain = keyed.copy()
+    plain["pad"][~holes] = 0
+    half = keyed.copy()
+    half["pad"][::2] = plain["pad"][::2]
+    cap = X.capacity(n, 8)
+    outs = []
+    for d in (plain, keyed, half):
+        qcap = abi.queue_cap(n)
+        ql = torch.empty(abi.NUM_QUEUES * qcap, dtype=torch.int32, device="cuda")
+        tc = torch.empty(abi.ntiles(n) * 16, dtype=torch.int32, device="cuda")
+        hi = torch.zeros(abi.HIST_SHARDS * 2 * abi.HIST_BINS, dtype=torch.int64, device="cuda")
+        sd = torch.full((8 * cap * X.LOOKUP_BYTES,), 0xEE, dtype=torch.uint8, device="cuda")
+        sc = torch.full((8,), -1, dtype=torch.int32, device="cuda")
+        rx.parse_route_dev(buf, to_dev(d), n, None, ql, qcap, tc, hi, 8, 0, cap, sd, sc)
+        torch.cuda.synchronize()
+        outs.append((sc.cpu().numpy(), sd.cpu().numpy()))
+    assert int(outs[0][0].sum()) == int((~holes).sum())
+    for c, s in outs[1:]:
+        assert np.array_equal(c, outs[0][0]) and np.array_equal(s, outs[0][1])

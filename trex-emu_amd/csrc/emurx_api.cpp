@@ -1102,6 +1102,17 @@ uint32_t emurx_ns_owner(const uint8_t key[12], uint32_t n_parts) {
     if (!key || n_parts == 0) return 0;
     return emurx_owner(emurx_tk_hash(le32(key), le32(key + 4), le32(key + 8)), n_parts);
 }
+uint8_t emurx_owner_key(const uint8_t key[12]) {
+    if (!key) return 0;
+    return (uint8_t)emurx_owner_key(emurx_tk_hash(le32(key), le32(key + 4), le32(key + 8)));
+}
+int emurx_desc_keys_dev(emurx_t* h, const uint8_t* d_frames, emurx_desc* d_desc, uint32_t n, void* stream) {
+    if (!h || (n && (!d_frames || !d_desc)) || ((uintptr_t)d_desc & 7)) return EMURX_EINVAL;
+    int rc = bind(h);
+    if (rc) return rc;
+    return emurx_launch_desc_keys(d_frames, d_desc, n, stream ? (hipStream_t)stream : h->stream) ? EMURX_EDEVICE
+                                                                                                 : EMURX_OK;
+}
 
 int emurx_route_dev(emurx_t* h, const emurx_rec* d_rec, uint32_t n, uint32_t n_parts, uint32_t my_rank,
                     uint32_t cap, emurx_route_rec* d_send, uint32_t* d_send_count, void* stream) {

@@ -5,8 +5,10 @@
 // per-callback queues and folded counters.  Around k_rx (emurx_kernels.hip) run:
 //   k_zmq_walk  one lane per message: the offset walk of VethIFZmq.OnRxStream
 //               (veth_zmq.go:277-320, uint16 running offset, abort on a header error) ->
-//               descriptors in the message's slot range; slots past the decoded frames are
-//               marked EMURX_DESC_HOLE (k_rx skips them); one status word per message
+//               descriptors in the message's slot range, each with its frame's owner key
+//               (EMURX_DESC_KEYED: bytes 12..19 of the frame, loaded beside its header);
+//               slots past the decoded frames are marked EMURX_DESC_HOLE (k_rx skips them);
+//               one status word per message
 //   k_qscan     one workgroup: exclusive offset of every (queue, tile) segment of k_rx's
 //               per-tile queue output in the packed queue-major order, qoff[14], and the
 //               histogram shards folded into one copy (shards left zero for the next batch)
@@ -67,7 +69,12 @@ __global__ __launch_bounds__(kBlock) void k_zmq_walk(const uint8_t* __restrict__
                 if (plen > EMURX_MAX_FRAME) { err = EMURX_MSG_PANIC; break; }  // MbufPoll.Alloc
                 if (e < h4) { err = EMURX_MSG_PANIC; break; }
                 if (found >= slots) { err = EMURX_MSG_PANIC; break; }  // unreachable: slots bound the walk
-                reinterpret_cast<uint2*>(desc)[base + found] = make_uint2(M.x + h4, plen | (vport << 16));
+                // the owner key from the CTunnelKey the parse will leave (l2_vlans: the frame's
+                // bytes 12..19 and its length); bytes past the frame are masked by the length
+                uint32_t v0, v1;
+                l2_vlans(plen, ld_be32(s + h4 + 12), ld_be32(s + h4 + 16), v0, v1);
+                const uint32_t key = emurx_owner_key(emurx_tk_hash(vport, v0, v1));
+                reinterpret_cast<uint2*>(desc)[base + found] = make_uint2(M.x + h4, plen | (vport << 16) | (key << 24));
                 ++found;
                 of = e;
             }

@@ -79,6 +79,8 @@ int emurx_launch_route(const emurx_rec* rec, uint32_t n, uint32_t n_parts, uint3
 int emurx_launch_owner_count(const uint8_t* frames, const emurx_desc* desc, uint32_t n, uint32_t n_parts,
                              uint32_t* send_count, uint32_t* tile_cnt, uint32_t* grp, uint32_t* grp_off,
                              hipStream_t st);
+// The owner keys of device-resident descriptors (emurx_desc_keys_dev), in place.  One launch.
+int emurx_launch_desc_keys(const uint8_t* frames, emurx_desc* desc, uint32_t n, hipStream_t st);
 // The owner side (emurx_lookup_dev): one lane per received slot, n_parts regions of cap.
 int emurx_launch_lookup(const emurx_lookup_rec* recv, const uint32_t* recv_count, uint32_t n_parts, uint32_t cap,
                         const emurx_dev_tables& T, emurx_route_rec* out, uint32_t* flow, hipStream_t st);

@@ -259,7 +259,12 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
     uint32_t rd = 0xffu;
     if ((kKind == 1 && rt.cnt) || kKind == 2) {
         const bool routed = valid && (kKind == 2 || r.ns != EMURX_ID_NONE);
-        rd = routed ? emurx_owner(emurx_tk_hash(r.vport, r.vlan0, r.vlan1), rt.parts) : 0xffu;
+        // kind 2: the owner the count pass used (a keyed descriptor's key, the same digest of
+        // the CTunnelKey the parse left: packing and counts agree by construction)
+        const uint32_t pad = dd.y >> 24;
+        rd = !routed ? 0xffu
+             : (kKind == 2 && (pad & EMURX_DESC_KEYED)) ? emurx_owner_of_key(pad, rt.parts)
+                                                        : emurx_owner(emurx_tk_hash(r.vport, r.vlan0, r.vlan1), rt.parts);
     }
     // Namespace owners (rt.parts > 0): kind 1 counts the records whose Namespace was found
     // (the first pass of emurx_route_dev, fused; k_route<false> counts them the same way,

@@ -134,12 +134,14 @@ __global__ __launch_bounds__(kScanThreads) void k_route_scan(uint32_t* __restric
 }
 
 // ---- partitioned path -------------------------------------------------------------------
-// k_owner_count: the owner of every frame from its L2 header (l2_vlans: bytes 12..19 + the
-// length), counted per (tile, owner) and per group of 64 tiles, as k_route<false> counts
-// records; k_rx kind 2 then packs at the offsets k_route_scan derives.  A wave whose frames'
-// byte range fits kOcStage bytes copies that range into LDS with coalesced LDS-DMA (as k_rx
-// stages) and reads each frame's bytes 12..19 there: a per-lane gather of one line per frame
-// ran at the random-line rate; wider waves gather (8 bytes of frame + the descriptor).
+// k_owner_count: the owner of every frame, counted per (tile, owner) and per group of 64
+// tiles, as k_route<false> counts records; k_rx kind 2 then packs at the offsets
+// k_route_scan derives.  A keyed descriptor (EMURX_DESC_KEYED, written by the device framing
+// walk or k_desc_keys) gives the owner by itself: a wave of keyed descriptors reads 512 bytes.
+// For the other frames the owner comes from the L2 header (l2_vlans: bytes 12..19 + the
+// length): a wave whose unkeyed frames' byte range fits kOcStage bytes copies that range into
+// LDS with coalesced LDS-DMA (as k_rx stages) and reads each frame's bytes 12..19 there (a
+// per-lane gather of one line per frame ran at the random-line rate); wider waves gather.
 constexpr uint32_t kOcStage = 6144;
 __global__ __launch_bounds__(kBlock) void k_owner_count(const uint8_t* __restrict__ frames,
                                                         const emurx_desc* __restrict__ desc, uint32_t n,
@@ -152,11 +154,17 @@ __global__ __launch_bounds__(kBlock) void k_owner_count(const uint8_t* __restric
     const uint32_t i = tile * kBlock + tid;
     if (lane < 16) s_wcnt[wv][lane] = 0;
     const uint2 dd = i < n ? *reinterpret_cast<const uint2*>(desc + i) : make_uint2(0, EMURX_DESC_HOLE << 24);
-    const bool valid = (dd.y >> 24) != EMURX_DESC_HOLE;
+    const uint32_t pad = dd.y >> 24;
+    const bool valid = pad != EMURX_DESC_HOLE, keyed = valid && (pad & EMURX_DESC_KEYED);
+    const bool need = valid && !keyed;  // the owner must come from the frame's bytes
     const uint32_t off = dd.x, len = dd.y & 0xffff;
-    const uint32_t lo = wave_min_u32(valid ? off : 0xffffffffu);
-    const uint32_t hi = wave_max_u32(valid ? off + len : 0u);
-    const uint32_t start = lo & ~15u, nvec = hi > lo ? (hi - start + 15) >> 4 : 0;
+    uint32_t start = 0, nvec = 0;
+    if (__ballot(need)) {  // wave-uniform: a wave of keyed descriptors reads no frame byte
+        const uint32_t lo = wave_min_u32(need ? off : 0xffffffffu);
+        const uint32_t hi = wave_max_u32(need ? off + len : 0u);
+        start = lo & ~15u;
+        nvec = hi > lo ? (hi - start + 15) >> 4 : 0;
+    }
     const bool staged = nvec > 0 && nvec <= kOcStage / 16;  // wave-uniform
     if (staged) {
         static_assert(kOcStage % (16 * kWave) == 0, "whole 1 KiB DMA rows");
@@ -172,8 +180,8 @@ __global__ __launch_bounds__(kBlock) void k_owner_count(const uint8_t* __restric
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    uint32_t d = 0xffu;
-    if (valid) {
+    uint32_t d = keyed ? emurx_owner_of_key(pad, n_parts) : 0xffu;
+    if (need) {
         const uint32_t vport = (dd.y >> 16) & 0xff;
         uint32_t w0 = 0, w1 = 0, w2 = 0, sh;
         if (staged) {
@@ -220,6 +228,28 @@ __global__ __launch_bounds__(kBlock) void k_owner_count(const uint8_t* __restric
         tile_cnt[tile * 16 + tid] = c;
         if (c) atomicAdd(&grp[(tile / kGroup) * 16 + tid], c);
     }
+}
+
+// k_desc_keys: the owner key of every frame into its descriptor's pad byte (what the device
+// framing walk writes, for descriptors built without it): one lane per descriptor, bytes
+// 12..19 of the frame by the three aligned dwords around them (each loaded only where it
+// holds a frame byte, as k_owner_count's gather).  Holes stay holes.
+__global__ __launch_bounds__(kBlock) void k_desc_keys(const uint8_t* __restrict__ frames, emurx_desc* __restrict__ desc,
+                                                      uint32_t n) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    uint2 dd = *reinterpret_cast<const uint2*>(desc + i);
+    if ((dd.y >> 24) == EMURX_DESC_HOLE) return;
+    const uint32_t off = dd.x, len = dd.y & 0xffff, vport = (dd.y >> 16) & 0xff;
+    const uintptr_t a = (uintptr_t)(frames + off + 12);
+    const uint32_t sh = (uint32_t)(a & 3), lim = len + sh;  // dword k holds a frame byte iff 12 + 4k < lim
+    const uint8_t* wa = reinterpret_cast<const uint8_t*>(a & ~(uintptr_t)3);
+    const uint32_t w0 = lim > 12 ? gld4(wa) : 0u, w1 = lim > 16 ? gld4(wa + 4) : 0u, w2 = lim > 20 ? gld4(wa + 8) : 0u;
+    uint32_t v0, v1;
+    l2_vlans(len, __builtin_bswap32(__builtin_amdgcn_alignbyte(w1, w0, sh)),
+             __builtin_bswap32(__builtin_amdgcn_alignbyte(w2, w1, sh)), v0, v1);
+    dd.y = (dd.y & 0x00ffffffu) | (emurx_owner_key(emurx_tk_hash(vport, v0, v1)) << 24);
+    reinterpret_cast<uint2*>(desc)[i] = dd;
 }
 
 // k_lookup: the owner's half — GetNs + the callback's client rule + the flow decision for
@@ -298,6 +328,14 @@ int emurx_launch_owner_count(const uint8_t* frames, const emurx_desc* desc, uint
         return -1;
     return EMURX_HIP_OK(emurx_launch(k_route_scan, dim3(1), dim3(kScanThreads), 0, st, grp, ngroups, n_parts, grp_off,
                                      send_count))
+               ? 0
+               : -1;
+}
+
+int emurx_launch_desc_keys(const uint8_t* frames, emurx_desc* desc, uint32_t n, hipStream_t st) {
+    using namespace emurx;
+    if (!n) return 0;
+    return EMURX_HIP_OK(emurx_launch(k_desc_keys, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, frames, desc, n))
                ? 0
                : -1;
 }

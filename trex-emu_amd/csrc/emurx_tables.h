@@ -122,8 +122,14 @@ struct emurx_dev_tables {
     emurx_dev_tab ft6;                    // 64-byte buckets
 };
 
-// Namespace partition of a tunnel-key hash among n_parts GPUs (multiply-high: uniform for a
-// well-mixed hash, no division)
-EMURX_HD uint32_t emurx_owner(uint32_t tk, uint32_t n_parts) {
-    return (uint32_t)(((uint64_t)tk * n_parts) >> 32);
+// Namespace partition of a tunnel-key hash among n_parts <= 8 GPUs: the top 7 bits of the
+// hash, scaled (uniform for a well-mixed hash, no division).  The owner is a function of the
+// frame's OWNER KEY, the descriptor byte 0x80 | min(tk >> 25, 126) that the device framing
+// walk writes (emurx_desc.pad, EMURX_DESC_KEYED): 126 and 127 give the same owner for every
+// n_parts <= 8, so the key never collides with EMURX_DESC_HOLE (0xFF).
+EMURX_HD uint32_t emurx_owner(uint32_t tk, uint32_t n_parts) { return ((tk >> 25) * n_parts) >> 7; }
+EMURX_HD uint32_t emurx_owner_key(uint32_t tk) {
+    const uint32_t k = tk >> 25;
+    return 0x80u | (k < 126u ? k : 126u);
 }
+EMURX_HD uint32_t emurx_owner_of_key(uint32_t key, uint32_t n_parts) { return ((key & 0x7fu) * n_parts) >> 7; }

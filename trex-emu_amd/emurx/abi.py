@@ -82,6 +82,7 @@ MAX_PARTS = 8
 DESC_DTYPE = np.dtype([("off", "<u4"), ("len", "<u2"), ("vport", "u1"), ("pad", "u1")])
 assert DESC_DTYPE.itemsize == 8
 DESC_HOLE = 0xFF   # EMURX_DESC_HOLE: an empty descriptor slot
+DESC_KEYED = 0x80  # EMURX_DESC_KEYED | k: the frame's Namespace-owner key
 INGEST_SLOTS = 2   # EMURX_INGEST_SLOTS
 MSG_OK, MSG_PARSE_ERR, MSG_PANIC = 0, 1, 2
 MSG_DTYPE = np.dtype([("off", "<u4"), ("len", "<u4")])
@@ -174,6 +175,8 @@ SIGNATURES = [
     ("emurx_last_stage", C.c_uint32, [_P]),
     ("emurx_copy_ceiling_dev", C.c_int, [_P, _P, C.c_size_t, _P]),
     ("emurx_ns_owner", C.c_uint32, [_U8P, C.c_uint32]),
+    ("emurx_owner_key", C.c_uint8, [_U8P]),
+    ("emurx_desc_keys_dev", C.c_int, [_P, _P, _P, C.c_uint32, _P]),
     ("emurx_route_dev", C.c_int, [_P, _P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P]),
     ("emurx_classify_route_dev", C.c_int, [_P, _P, _P, C.c_uint32, C.POINTER(DevOut), C.c_uint32, C.c_uint32,
                                            C.c_uint32, _P, _P, _P]),

@@ -278,6 +278,12 @@ class RxPath:
                                                         n_parts, my_rank, cap, _addr(send), _addr(send_count),
                                                         _stream(stream)), "parse_route_dev")
 
+    def desc_keys_dev(self, frames, desc, n: int, stream=None):
+        """Write every frame's owner key into its descriptor's pad byte, in place
+        (include/emu_rx.h emurx_desc_keys_dev): what the device framing walk does."""
+        return abi.check(self.lib.emurx_desc_keys_dev(self.h, _addr(frames), _addr(desc), n, _stream(stream)),
+                         "desc_keys_dev")
+
     def lookup_dev(self, recv, recv_count, n_parts: int, cap: int, out, flow=None, stream=None):
         """The owner's lookups over received LOOKUP_REC_DTYPE regions -> ROUTE_REC_DTYPE slots."""
         return abi.check(self.lib.emurx_lookup_dev(self.h, _addr(recv), _addr(recv_count), n_parts, cap,
@@ -315,6 +321,11 @@ class RxPath:
         a, b, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
         abi.check(self.lib.emurx_table_stats(self.h, C.byref(a), C.byref(b), C.byref(c)), "table_stats")
         return dict(delta_blocks=a.value, whole_tables=b.value, table_bytes=c.value)
+
+
+def owner_key(key: bytes) -> int:
+    """The descriptor owner key of a 12-byte CTunnelKey (EMURX_DESC_KEYED | 7-bit digest)."""
+    return int(abi.load().emurx_owner_key(_p(_u8(key, 12))))
 
 
 def ns_owner(key: bytes, n_parts: int) -> int:
