@@ -228,14 +228,17 @@ typedef struct emurx_cfg {
                               generations and image queries, no device: data-path calls
                               return EMURX_EDEVICE) */
     uint32_t max_ns;       /* ns ids must be < max_ns */
-    uint32_t max_clients;  /* client ids must be < max_clients.  The device tables are
-                              two-choice cuckoo tables sized for max_ns / max_clients (every
-                              lookup reads its key's two candidate buckets in one round
-                              trip, whatever the load): about 48 B of device memory per
-                              Namespace and 250 B per client (MAC, IPv4, IPv6, client info),
-                              1/n_parts of that when partitioned; they grow on demand.  env
-                              EMURX_TABLE_LOAD="two,one" (starting load in percent of the
-                              two-slot and one-slot bucket tables; default 50,35) */
+    uint32_t max_clients;  /* client ids must be < max_clients.  The device tables are sized
+                              for max_ns / max_clients and kept sparse so that a lookup
+                              almost always ends in its home bucket (one memory trip for a
+                              wave of 64 lookups): about 128 B of device memory per Namespace
+                              and 1.7 KB per client (MAC, IPv4, IPv6, client info), 1/n_parts
+                              of that when partitioned.  The memory is traded for lookup
+                              latency: a table that would pass 2 GiB, or whose device
+                              allocation fails, is built at half the spread (down to 2 slots
+                              per entry: more probe trips) instead of failing;
+                              env EMURX_TABLE_SPREAD="ns,mac,ip,ci" (slots per entry, powers of
+                              two >= 2; default 8,8,16,16) sets the spreads */
     uint32_t max_frames;   /* frames per batch (device scratch is sized for it) */
     uint32_t max_bytes;    /* bytes per host batch (emurx_rx_stream staging) */
 } emurx_cfg;
@@ -326,13 +329,13 @@ int emurx_server_add(emurx_t* h, uint32_t client_id, uint16_t port, uint8_t prot
 int emurx_server_remove(emurx_t* h, uint32_t client_id, uint16_t port, uint8_t proto);
 int emurx_client_set_transport(emurx_t* h, uint32_t client_id, int has_ctx);
 /* Table edits reach the device incrementally: every call above edits the slots of the
-   device table image it changes (a cuckoo insert may move other entries to their second
-   bucket; a delete clears its slot) and marks the 64-byte blocks it touched.  Before the next launch that reads the tables, the edited blocks are
+   device table image it changes (deleted slots become tombstones) and marks the 64-byte
+   blocks it touched.  Before the next launch that reads the tables, the edited blocks are
    copied to the device and scattered by one kernel on that launch's stream, ordered after
    every launch on any stream that read the tables since the previous shipment (stream
    events, no host synchronisation) and before every later reader.  A table that outgrows
-   its load factor, or whose cuckoo insert found no place (rebuilt with a new hash seed), is
-   shipped whole (then the host waits for the device once).  Streams given to the library must outlive the handle.
+   its load factor is rebuilt larger and shipped whole (then the host waits for the device
+   once).  Streams given to the library must outlive the handle.
    emurx_sync ships pending edits now, on `stream` (NULL = the handle's stream). */
 int emurx_sync(emurx_t* h, void* stream);
 /* diagnostics: 64-byte blocks shipped as deltas and whole tables uploaded since emurx_open,
@@ -397,7 +400,8 @@ int emurx_rx_stream(emurx_t* h, const uint8_t* msg, size_t len, emurx_rec* out_r
    or change streams behind an event).  Call emurx_sync first to take the shipment out of a
    latency-critical call.  No emurx_* call reads or clears the thread's last HIP error
    (hipGetLastError): a launch's status is hipLaunchKernel's return value, so an error a
-   caller's earlier HIP call left pending is still pending after the call. */
+   caller's earlier HIP call left pending is still pending after the call (the one exception:
+   the out-of-memory status of a table allocation the library recovered from, emurx_cfg). */
 int emurx_classify_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_desc,
                        uint32_t n, const emurx_dev_out* out, void* stream);
 

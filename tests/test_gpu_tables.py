@@ -439,3 +439,34 @@ def test_keyed_descriptors_route_the_same(rxmod):
     assert int(outs[0][0].sum()) == int((~holes).sum())
     for c, s in outs[1:]:
         assert np.array_equal(c, outs[0][0]) and np.array_equal(s, outs[0][1])
+
+
+def test_table_allocation_fallback():
+    """A device table whose allocation fails is rebuilt at half its spread and allocated again
+    (emurx_cfg) instead of failing emurx_open: with every allocation above 64 MiB
+    refused (EMURX_DEBUG_TABLE_LIMIT), config D's tables (1M clients; the IPv4 / IPv6 / client
+    info tables are 512 MiB at their default spread) still open, and a config-D batch classified
+    on them equals the oracle."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    code = (
+        "import sys; sys.path[:0] = ['tests', 'trex-emu_amd', 'oracle']\n"
+        "import numpy as np, pyoracle\n"
+        "from emurx import synth\n"
+        "from emurx.rx import RxPath\n"
+        "from gpu_util import run_dev, rec_diff\n"
+        "w = synth.config_d(1 << 16)\n"
+        "rx = RxPath(0, max_ns=32768, max_clients=1 << 20, max_frames=1 << 16); rx.register_all()\n"
+        "synth.load_tables(w, rx)\n"
+        "o = pyoracle.Oracle(); synth.load_tables(w, o)\n"
+        "want = o.rx_batch(w['buf'], w['desc'])[0]\n"
+        "got = run_dev(rx, w['buf'], w['desc'])[0]\n"
+        "assert got.tobytes() == want.tobytes(), rec_diff(got, want)\n"
+        "print('ok', rx.table_stats()['table_bytes'])\n")
+    out = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=600,
+                         env={**os.environ, "EMURX_DEBUG_TABLE_LIMIT": str(64 << 20)})
+    assert out.returncode == 0 and "ok" in out.stdout, out.stderr[-3000:]
+    assert int(out.stdout.split()[-1]) < (400 << 20)  # every table at most 64 MiB

@@ -2,9 +2,8 @@
 
 * Go map semantics: every table call returns what the oracle (the Go restatement) returns.
 * The device image: after every mutation the kernels' bucket walk over the host image
-  (emurx_image_lookup: the two candidate buckets of the key, nothing else) finds exactly the
-  live map entries -- through cuckoo evictions, deletes, reseeded rebuilds and growth -- so the
-  blocks the library ships to the device hold the tables Go would probe.
+  (emurx_image_lookup) finds exactly the live map entries -- through tombstones, rebuilds and
+  growth -- so the blocks the library ships to the device hold the tables Go would probe.
 * Partitioned images hold only the owned Namespaces and about 1/n of the bytes.
 * The mid-batch rule (include/emu_rx.h emurx_recs_stale): a record of a batch classified at
   batch start that is NOT flagged stale equals Go's classification of that frame against the
@@ -173,10 +172,9 @@ def test_image_follows_random_mutations(oracle_built):
     random_ops(rx, o, Model(), np.random.default_rng(7), 6000, _keys(300))
 
 
-def test_churn_keeps_every_key(oracle_built):
-    """Thousands of add / remove cycles on small tables (cuckoo evictions move entries between
-    their two buckets, deletes clear slots): the image keeps answering every live key from its
-    two candidate buckets, and nothing else."""
+def test_tombstone_churn_rebuilds(oracle_built):
+    """Thousands of add / remove cycles on a small table: tombstones force rebuilds at the
+    same size, and the image keeps answering every live key."""
     rx, o = host_pair(max_ns=8, max_clients=64)
     m = Model()
     key = F.tunnel_key(0, 0, 0)
@@ -345,86 +343,34 @@ def _image_bytes(max_ns, max_clients):
     return RxPath(-1, max_ns=max_ns, max_clients=max_clients, max_frames=64).table_stats()["table_bytes"]
 
 
-def _cuckoo_bytes(max_ns, max_clients, two=0.5, one=0.35):
-    """Expected image bytes of an empty handle (emurx_mirror.cpp set_partition): per table,
-    ceil(entries / (load x slots per bucket)) buckets (at least 2) of 32 B (the IPv6 flow
-    table: 64 B), rounded up to whole 64-byte blocks, plus the dense ns info."""
-    import math
-
-    def tab(entries, per, bw_bytes, load):
-        nb = max(2, math.ceil(entries / (load * per)))
-        return math.ceil(nb * bw_bytes / 64) * 64
-    return (tab(max_ns, 2, 32, two) + tab(max_clients, 2, 32, two) + 2 * tab(max_clients, 1, 32, one)
-            + tab(max_clients, 2, 32, two) + tab(8, 1, 32, one) + tab(8, 1, 64, one) + tab(16, 2, 32, two)
-            + max_ns * 16)
-
-
-def test_cuckoo_table_sizes(oracle_built):
-    """Tables start dense, at their target load for max_ns / max_clients: two-slot buckets at
-    1/2, one-slot buckets at 0.35 (about 48 B per Namespace and 250 B per client in all)."""
-    assert _image_bytes(1024, 4096) == _cuckoo_bytes(1024, 4096)
-    per_client = (_image_bytes(1024, 1 << 16) - _image_bytes(1024, 1 << 12)) / ((1 << 16) - (1 << 12))
-    assert 240 < per_client < 260, per_client
+def _sparse_bytes(max_ns, max_clients, sp):
+    """Expected image bytes of an empty handle: slots = next power of two >= spread x entries
+    (emurx_mirror.cpp set_partition), times the slot size, plus the dense ns info."""
+    def p2(v):
+        p = 16
+        while p < v:
+            p <<= 1
+        return p
+    ns, mac, ip, ci = sp
+    return (p2(ns * max_ns) * 16 + p2(mac * max_clients) * 16 + 2 * p2(ip * max_clients) * 32
+            + p2(ci * max_clients) * 32 + p2(16 * 8) * 32 + p2(32 * 8) * 64 + p2(8 * 16) * 16 + max_ns * 16)
 
 
-def test_table_load_override():
-    """EMURX_TABLE_LOAD="two,one" (percent, read once per process) sets the starting loads;
-    malformed or out-of-range values keep the defaults."""
+def test_sparse_table_sizes(oracle_built):
+    """Tables start at their target spread (slots per entry: 8 for ns / MAC, 16 for IPv4 /
+    IPv6 / client info), so that almost every key of a 64-lane wave sits in its home bucket."""
+    assert _image_bytes(1024, 4096) == _sparse_bytes(1024, 4096, (8, 8, 16, 16))
+
+
+def test_table_spread_override():
+    """EMURX_TABLE_SPREAD="ns,mac,ip,ci" (read once per process) sets the spreads; malformed
+    values keep the defaults."""
     code = ("import sys; sys.path.insert(0, 'trex-emu_amd'); from emurx.rx import RxPath; "
             "print(RxPath(-1, max_ns=1024, max_clients=4096, max_frames=64).table_stats()['table_bytes'])")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    for env, (two, one) in (("70,40", (0.7, 0.4)), ("25,20", (0.25, 0.2)), ("90,35", (0.5, 0.35)),
-                            ("junk", (0.5, 0.35))):
+    for env, sp in (("2,2,2,2", (2, 2, 2, 2)), ("4,8,32,2", (4, 8, 32, 2)), ("3,8,16,16", (8, 8, 16, 16)),
+                    ("junk", (8, 8, 16, 16))):
         out = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=120,
-                             env={**os.environ, "EMURX_TABLE_LOAD": env})
+                             env={**os.environ, "EMURX_TABLE_SPREAD": env})
         assert out.returncode == 0, out.stderr
-        assert int(out.stdout.split()[-1]) == _cuckoo_bytes(1024, 4096, two, one), env
-
-
-def _fill_at_load():
-    """(run with EMURX_TABLE_LOAD=80,45: every table starts AT its growth load) max_clients
-    clients with an IPv4, an IPv6 and a DHCPv6 address each: the MAC and client-info tables end
-    at 4/5 of their slots, the IPv4 table at 0.45 (both cuckoo thresholds' neighbourhood), the
-    IPv6 table past it (two addresses per client: it grows)."""
-    mc = 1 << 13
-    rx = RxPath(-1, max_ns=8, max_clients=mc, max_frames=64)
-    m = Model()
-    key = F.tunnel_key(0, 0, 0)
-    assert rx.ns_add(key, 0, abi.PLUG_ALL) == 0
-    m.ns[key] = 0
-    for cid in range(mc):
-        mac = bytes([2, 0, 0, cid >> 16 & 255, cid >> 8 & 255, cid & 255])
-        ip = bytes([10, cid >> 16 & 255, cid >> 8 & 255, cid & 255])
-        ip6 = bytes([0x20, 1, 0xd, 0xb8] + [0] * 10 + [cid >> 8 & 255, cid & 255])
-        d6 = bytes([0xfd] + [0] * 13 + [cid >> 8 & 255, cid & 255])
-        assert rx.client_add(0, cid, mac, ip, ip6, d6, abi.PLUG_ALL) == 0
-        m.mac[(0, mac)] = cid
-        m.ip4[(0, ip)] = cid
-        m.ip6[(0, ip6)] = cid
-        m.ip6[(0, d6)] = cid
-        m.cl[cid] = dict(ns=0, plugins=abi.PLUG_ALL)
-    m.check(rx)
-    # remove every third client and add them back: evictions over a full table
-    for cid in range(0, mc, 3):
-        mac = bytes([2, 0, 0, cid >> 16 & 255, cid >> 8 & 255, cid & 255])
-        assert rx.client_remove(0, mac) == 0
-    for cid in range(0, mc, 3):
-        mac = bytes([2, 0, 0, cid >> 16 & 255, cid >> 8 & 255, cid & 255])
-        ip = bytes([10, cid >> 16 & 255, cid >> 8 & 255, cid & 255])
-        ip6 = bytes([0x20, 1, 0xd, 0xb8] + [0] * 10 + [cid >> 8 & 255, cid & 255])
-        d6 = bytes([0xfd] + [0] * 13 + [cid >> 8 & 255, cid & 255])
-        assert rx.client_add(0, cid, mac, ip, ip6, d6, abi.PLUG_ALL) == 0
-    m.check(rx)
-    print("ok", rx.table_stats()["table_bytes"])
-
-
-def test_cuckoo_at_growth_load():
-    """Every table started at its growth load (EMURX_TABLE_LOAD=80,45) and filled: every key
-    is in one of its two buckets (evictions' random walks, reseeded rebuilds, growth of the
-    IPv6 table), through a remove / re-add third of the clients."""
-    code = ("import sys; sys.path[:0] = ['tests', 'trex-emu_amd', 'oracle']; import test_table_mirror as t; "
-            "t._fill_at_load()")
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    out = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=300,
-                         env={**os.environ, "EMURX_TABLE_LOAD": "80,45"})
-    assert out.returncode == 0 and "ok" in out.stdout, out.stderr[-3000:]
+        assert int(out.stdout.split()[-1]) == _sparse_bytes(1024, 4096, sp), env

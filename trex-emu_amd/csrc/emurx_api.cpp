@@ -189,23 +189,27 @@ struct emurx_ctx {
 
     emurx_dev_tables tables() const {
         using namespace emurx_host;
-        auto tab = [&](int k) {
-            const Hash& t = *m.hashes(k);
-            return emurx_dev_tab{d_tab[k].p, t.nb, t.seed};
-        };
         emurx_dev_tables T{};
-        T.ns = tab(kTabNs);
-        T.mac = tab(kTabMac);
-        T.ip4 = tab(kTabIp4);
-        T.ip6 = tab(kTabIp6);
-        T.ci = tab(kTabCi);
+        T.ns_tab = d_tab[kTabNs].p;
         T.ns_info = d_nsinfo.p;
+        T.mac_tab = d_tab[kTabMac].p;
+        T.ip4_tab = d_tab[kTabIp4].p;
+        T.ip6_tab = d_tab[kTabIp6].p;
+        T.ci_tab = d_tab[kTabCi].p;
+        T.ns_mask = m.ns_t.mask();
+        T.mac_mask = m.mac_t.mask();
+        T.ip4_mask = m.ip4_t.mask();
+        T.ip6_mask = m.ip6_t.mask();
+        T.ci_mask = m.ci_t.mask();
         T.max_ns = cfg.max_ns;
         T.cb_mask = cb_mask;
         T.ft_on = m.n_ctx ? 1u : 0u;
-        T.ft4 = tab(kTabFt4);
-        T.ft6 = tab(kTabFt6);
-        T.srv = tab(kTabSrv);
+        T.ft4_tab = d_tab[kTabFt4].p;
+        T.ft6_tab = d_tab[kTabFt6].p;
+        T.srv_tab = d_tab[kTabSrv].p;
+        T.ft4_mask = m.ft4_t.mask();
+        T.ft6_mask = m.ft6_t.mask();
+        T.srv_mask = m.srv_t.mask();
         return T;
     }
 };
@@ -268,9 +272,18 @@ int ship_tables(emurx_t* h, hipStream_t st) {
     if (grow && !EMURX_HIP_OK(hipDeviceSynchronize())) return EMURX_EDEVICE;
     if (whole) {
         if (!EMURX_HIP_OK(hipStreamSynchronize(st))) return EMURX_EDEVICE;
+        // a table whose device allocation fails is rebuilt at half its spread and tried again
+        // (emurx_cfg: memory traded for lookup latency, down to 2 slots per entry);
+        // EMURX_DEBUG_TABLE_LIMIT (bytes) fails every larger allocation, for tests
+        static const size_t lim = getenv("EMURX_DEBUG_TABLE_LIMIT") ? strtoull(getenv("EMURX_DEBUG_TABLE_LIMIT"), nullptr, 0)
+                                                                     : ~(size_t)0;
         for (int k = 0; k <= kNumTabs; ++k) {
             if (!img[k]->all) continue;
-            if (dev[k]->alloc(img[k]->img.size())) return EMURX_ENOMEM;
+            while (img[k]->img.size() * 4 > lim || dev[k]->alloc(img[k]->img.size())) {
+                if (k == kNumTabs || !m.shrink(k)) return EMURX_ENOMEM;
+                // the out-of-memory status our own hipMalloc left pending: recovered from here
+                if (hipPeekAtLastError() == hipErrorOutOfMemory) (void)hipGetLastError();
+            }
             if (!EMURX_HIP_OK(hipMemcpy(dev[k]->p, img[k]->img.data(), img[k]->img.size() * 4, hipMemcpyHostToDevice)))
                 return EMURX_EDEVICE;
             h->shipped_whole++;

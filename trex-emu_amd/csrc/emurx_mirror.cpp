@@ -7,13 +7,17 @@
 #include "emurx_mirror.h"
 
 #include <algorithm>
-#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 
 namespace emurx_host {
 namespace {
 
+uint32_t pow2_at_least(uint64_t v) {
+    uint64_t p = 16;
+    while (p < v) p <<= 1;
+    return (uint32_t)p;
+}
 uint32_t le32(const uint8_t* p) { return p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24); }
 bool zero(const uint8_t* p, int n) {
     for (int i = 0; i < n; ++i)
@@ -27,70 +31,36 @@ K5 key_ip6(uint32_t ns, const uint8_t* ip) { return K5{{ns, le32(ip), le32(ip + 
 
 }  // namespace
 
-// ---- cuckoo table image -----------------------------------------------------------------
-void Hash::init(uint32_t nbuckets, uint32_t w, uint32_t bucket_words, uint32_t m) {
+// ---- bucketed image ----------------------------------------------------------------------
+void Hash::init(uint32_t nbuckets, uint32_t w) {
     words = w;
-    bw = bucket_words;
-    mw = m;
-    nb = std::max<uint32_t>(nbuckets, 1);
-    resize_blocks((uint32_t)(((size_t)nb * bw + EMURX_BUCKET_WORDS - 1) / EMURX_BUCKET_WORDS));
-    for (uint32_t k = 0; k < nslots(); ++k) at(k)[mw] = EMURX_EMPTY;
-    hs.assign(nslots(), 0);
-    back.assign(nslots(), nullptr);
-    live = 0;
-    failed = false;
+    buckets = std::max<uint32_t>(nbuckets, 1);
+    resize_blocks(buckets);
+    for (size_t i = words - 1; i < img.size(); i += words) img[i] = EMURX_EMPTY;
+    live = tomb = 0;
 }
-uint32_t Hash::sized(uint64_t entries) const {
-    const double b = std::ceil((double)std::max<uint64_t>(entries, 1) / (target * per()));
-    return (uint32_t)std::min<double>(std::max(b, 2.0), (double)(1u << 31) / bw);
-}
-void Hash::place(uint32_t s, const uint32_t* e, uint32_t h, uint32_t* bp) {
-    memcpy(at(s), e, words * sizeof(uint32_t));
-    hs[s] = h;
-    back[s] = bp;
-    if (bp) *bp = s;
-    touch_slot(s);
-}
-bool Hash::put(uint32_t h, const uint32_t* e, uint32_t* bp) {
+uint32_t Hash::put(uint32_t hash, const uint32_t* e) {
     const uint32_t P = per();
-    uint32_t cur[16], ch = h, from = EMURX_EMPTY;
-    uint32_t* cb = bp;
-    memcpy(cur, e, words * sizeof(uint32_t));
-    for (int kick = 0; kick <= kMaxKicks; ++kick) {
-        const uint32_t c1 = emurx_b1(ch, nb), c2 = emurx_b2(ch, nb);
-        for (uint32_t bb : {c1, c2})
-            for (uint32_t k = 0; k < P; ++k)
-                if (is_free(bb * P + k)) {
-                    place(bb * P + k, cur, ch, cb);
-                    ++live;
-                    return true;
-                }
-        if (kick == kMaxKicks) break;
-        // both buckets full: evict a random slot of the bucket this entry did not just come from
-        const uint32_t vb = from == c1 ? c2 : from == c2 ? c1 : ((rand32() & 1) ? c2 : c1);
-        const uint32_t v = vb * P + rand32() % P;
-        uint32_t tmp[16];
-        memcpy(tmp, at(v), words * sizeof(uint32_t));
-        const uint32_t th = hs[v];
-        uint32_t* tb = back[v];
-        place(v, cur, ch, cb);
-        memcpy(cur, tmp, words * sizeof(uint32_t));
-        ch = th;
-        cb = tb;
-        from = vb;
-    }
-    if (cb) *cb = kNoSlot;  // this entry lost its slot: the table is rebuilt before it is used
-    failed = true;
-    return false;
+    for (uint32_t b = hash & mask(), n = 0; n < buckets; b = (b + 1) & mask(), ++n)
+        for (uint32_t k = 0; k < P; ++k) {
+            uint32_t* s = &img[(size_t)b * EMURX_BUCKET_WORDS + k * words];
+            const uint32_t v = s[words - 1];
+            if (v != EMURX_EMPTY && v != EMURX_TOMB) continue;
+            if (v == EMURX_TOMB) --tomb;
+            memcpy(s, e, words * sizeof(uint32_t));
+            ++live;
+            touch(b);
+            return b * P + k;
+        }
+    return kNoSlot;  // unreachable: reserve() keeps a quarter of the slots free
 }
 void Hash::del(uint32_t s) {
     uint32_t* p = at(s);
-    for (uint32_t k = 0; k < words; ++k) p[k] = 0;
-    p[mw] = EMURX_EMPTY;
-    hs[s] = 0;
-    back[s] = nullptr;
+    for (uint32_t k = 0; k + 1 < words; ++k) p[k] = 0xFFFFFFFFu;
+    p[words - 1] = EMURX_TOMB;
     --live;
-    touch_slot(s);
+    ++tomb;
+    touch(s / per());
 }
 
 // ---- sizing ------------------------------------------------------------------------------
@@ -116,33 +86,32 @@ void Mirror::clean_all() {
     for (int k = 0; k < kNumTabs; ++k) hashes(k)->clean();
 }
 
-// Table shapes (ns, mac, ip4, ip6, ci, ft4, ft6, srv): slot words, bucket words, marker word.
-// Two-slot buckets (16-byte slots) start at load 1/2 and grow past 4/5 (the two-choice,
-// two-slot cuckoo threshold is 0.897); one-slot buckets (32- and 64-byte slots) start at 0.35
-// and grow past 0.45 (threshold 1/2).  EMURX_TABLE_LOAD="two,one" (percent) overrides the
-// starting loads, for measurements.
+// Slots per entry by table (ns, mac, ip4, ip6, ci, ft4, ft6, srv).  A wave's lookups take as
+// many dependent memory trips as the longest probe chain among its 64 lanes; at load 1/2,
+// 93 % of 64-lane waves hold a key outside its 4-slot home bucket (2-slot buckets: all of
+// them), at 1/8 (1/16 for 2 slots) about 2 % (4 %).  EMURX_TABLE_SPREAD="ns,mac,ip,ci"
+// overrides the first five (the ip value for both IP tables), for measurements.
 namespace {
-constexpr uint32_t kWords[kNumTabs] = {4, 4, 8, 8, 4, 8, 16, 4};
-constexpr uint32_t kBucketWords[kNumTabs] = {8, 8, 8, 8, 8, 8, 16, 8};
-constexpr uint32_t kMarker[kNumTabs] = {3, 3, 7, 7, 0, 7, 15, 3};
-struct Loads {
-    double two = 0.5, one = 0.35;
-    Loads() {
-        const char* s = getenv("EMURX_TABLE_LOAD");
-        unsigned a = 0, b = 0;
-        if (!s || sscanf(s, "%u,%u", &a, &b) != 2) return;
-        if (a >= 10 && a <= 80) two = a / 100.0;
-        if (b >= 10 && b <= 45) one = b / 100.0;
+struct Spread {
+    uint32_t v[kNumTabs] = {8, 8, 16, 16, 16, 16, 32, 8};
+    Spread() {
+        const char* s = getenv("EMURX_TABLE_SPREAD");
+        unsigned a = 0, b = 0, c = 0, d = 0;
+        if (!s || sscanf(s, "%u,%u,%u,%u", &a, &b, &c, &d) != 4) return;
+        const unsigned w[5] = {a, b, c, c, d};
+        for (int k = 0; k < 5; ++k)
+            if (w[k] >= 2 && w[k] <= 64 && !(w[k] & (w[k] - 1))) v[k] = w[k];
     }
 };
-const Loads& table_loads() {
-    static const Loads l;
-    return l;
+const uint32_t* table_spread() {
+    static const Spread s;
+    return s.v;
 }
+constexpr uint64_t kSpreadCap = 2ull << 30;  // bytes per table
 }  // namespace
 
-// Every table starts at its target load for its share of max_ns / max_clients (the whole of
-// them with one partition, 1/n of them with n) and grows on demand.
+// Every table starts at its target load (1 / spread) for its share of max_ns / max_clients
+// (the whole of them with one partition, 1/n of them plus slack with n) and grows on demand.
 void Mirror::set_partition(uint32_t n, uint32_t p) {
     n_parts = std::max<uint32_t>(n, 1);
     part = p;
@@ -150,6 +119,8 @@ void Mirror::set_partition(uint32_t n, uint32_t p) {
         NsInfo& s = ns[kv.second.id];
         s.owned = n_parts == 1 || emurx_owner(emurx_tk_hash(kv.first.w[0], kv.first.w[1], kv.first.w[2]), n_parts) == part;
     }
+    // a partition's fair share (load <= 1/2 then; the owner hash's imbalance, a few percent,
+    // is absorbed below the 3/4 rebuild threshold, and a partition that receives far more grows)
     const uint64_t ens = std::max<uint64_t>(((uint64_t)max_ns + n_parts - 1) / n_parts, 16);
     const uint64_t ecl = std::max<uint64_t>(((uint64_t)max_clients + n_parts - 1) / n_parts, 64);
     // entries each table holds now (all of them: a rebuild re-filters by the new partition)
@@ -161,14 +132,17 @@ void Mirror::set_partition(uint32_t n, uint32_t p) {
     // IPv6: one address per client to start (a client may hold two, Ipv6 and Dhcpv6: the
     // table grows when they come)
     const uint64_t want[kNumTabs] = {ens, ecl, ecl, ecl, ecl, 8, 8, 16};
+    const uint32_t per[kNumTabs] = {4, 4, 2, 2, 2, 2, 1, 4};
+    const uint32_t* sp = table_spread();
     for (int k = 0; k < kNumTabs; ++k) {
-        Hash& t = *hashes(k);
-        t.words = kWords[k];
-        t.bw = kBucketWords[k];
-        const bool two = t.per() >= 2;
-        t.target = two ? table_loads().two : table_loads().one;
-        t.grow_at = two ? 0.8 : 0.45;
-        rebuild(k, t.sized(std::max(want[k], (need[k] + n_parts - 1) / n_parts)));
+        const uint64_t e = std::max(want[k], (need[k] + n_parts - 1) / n_parts);
+        // sparser tables cost bytes, not lookups; above kSpreadCap a table falls back towards
+        // the load of 1/2
+        uint32_t s = sp[k];
+        while (s > 2 && (uint64_t)pow2_at_least((uint64_t)s * e) * (EMURX_BUCKET_WORDS / per[k]) * 4 > kSpreadCap)
+            s >>= 1;
+        hashes(k)->spread = s;
+        rebuild(k, std::max<uint32_t>(pow2_at_least((uint64_t)s * e) / per[k], 1));
     }
     nsinfo.resize_blocks(nsinfo.nblocks());
     for (uint32_t i = 0; i < max_ns; ++i)
@@ -176,6 +150,14 @@ void Mirror::set_partition(uint32_t n, uint32_t p) {
     n_ctx = 0;
     for (uint32_t c = 0; c < max_clients; ++c)
         if (cl[c].alive && cl[c].has_ctx && owned_ns(cl[c].ns)) ++n_ctx;
+}
+
+bool Mirror::shrink(int k) {
+    Hash& t = *hashes(k);
+    if (t.spread <= 2) return false;
+    t.spread >>= 1;
+    rebuild(k, std::max<uint32_t>(t.buckets / 2, 1));
+    return true;
 }
 
 uint32_t Mirror::tk_of(uint32_t ns_id) const {
@@ -200,7 +182,8 @@ void Mirror::ns_slot_put(const K5& k, Entry& e) {
     // Namespace's plugin mask, so one probe answers GetNs + ns.PluginCtx.Get.
     if (!owned_ns(e.id) || (k.w[0] >> 16)) return;
     const uint32_t s[4] = {k.w[0] | (ns[e.id].plugins << 16), k.w[1], k.w[2], e.id};
-    ns_t.put(emurx_ns_hash(emurx_tk_hash(k.w[0], k.w[1], k.w[2]), ns_t.seed), s, &e.slot);
+    e.slot = ns_t.put(emurx_tk_hash(k.w[0], k.w[1], k.w[2]), s);
+    ns[e.id].slot = e.slot;
 }
 // the client's MAC and plugin mask ride in the MAC slot's free upper half and in the IP
 // slots' spare words: PluginCtx.Get and IsUnicastToMe need no second read
@@ -208,36 +191,33 @@ static void mac_words(const ClientInfo& c, uint32_t& lo, uint32_t& hip) {
     lo = le32(c.mac);
     hip = (uint32_t)(c.mac[4] | (c.mac[5] << 8)) | ((c.plugins & 0xffffu) << 16);
 }
-// client info word 1: plugins | has_ra << 16 | has_transport_ctx << 17 | ra prefix length << 24
-static uint32_t ci_word(const ClientInfo& c) {
-    return (c.plugins & 0xffffu) | (c.has_ra ? 1u << 16 : 0u) | (c.has_ctx ? 1u << 17 : 0u) | ((uint32_t)c.ra_plen << 24);
-}
 void Mirror::mac_slot_put(const K5& k, Entry& e) {
     e.slot = kNoSlot;
     if (!owned_ns(k.w[0])) return;
     const uint32_t s[4] = {k.w[0], k.w[1], k.w[2] | ((cl[e.id].plugins & 0xffffu) << 16), e.id};
-    mac_t.put(emurx_mac_hash(tk_of(k.w[0]), k.w[1], k.w[2], mac_t.seed), s, &e.slot);
+    e.slot = mac_t.put(emurx_mac_hash(tk_of(k.w[0]), k.w[1], k.w[2]), s);
 }
 void Mirror::ip4_slot_put(const K5& k, Entry& e) {
     e.slot = kNoSlot;
     if (!owned_ns(k.w[0])) return;
     uint32_t s[8] = {k.w[0], k.w[1], 0, 0, 0, 0, 0, e.id};
     mac_words(cl[e.id], s[2], s[3]);
-    ip4_t.put(emurx_ip4_hash(tk_of(k.w[0]), k.w[1], ip4_t.seed), s, &e.slot);
+    e.slot = ip4_t.put(emurx_ip4_hash(tk_of(k.w[0]), k.w[1]), s);
 }
 void Mirror::ip6_slot_put(const K5& k, Entry& e) {
     e.slot = kNoSlot;
     if (!owned_ns(k.w[0])) return;
     uint32_t s[8] = {k.w[0], k.w[1], k.w[2], k.w[3], k.w[4], 0, 0, e.id};
     mac_words(cl[e.id], s[5], s[6]);
-    ip6_t.put(emurx_ip6_hash(tk_of(k.w[0]), k.w[1], k.w[2], k.w[3], k.w[4], ip6_t.seed), s, &e.slot);
+    e.slot = ip6_t.put(emurx_ip6_hash(tk_of(k.w[0]), k.w[1], k.w[2], k.w[3], k.w[4]), s);
 }
 void Mirror::ci_put(uint32_t cid) {
     ClientInfo& c = cl[cid];
     c.ci_slot = kNoSlot;
     if (!c.alive || !owned_ns(c.ns)) return;
-    const uint32_t s[4] = {cid, ci_word(c), le32(c.ra_prefix), le32(c.ra_prefix + 4)};
-    ci_t.put(emurx_ci_hash(cid, ci_t.seed), s, &c.ci_slot);
+    const uint32_t s[8] = {cid, c.plugins, (c.has_ra ? 1u : 0u) | ((uint32_t)c.ra_plen << 8), le32(c.ra_prefix),
+                           le32(c.ra_prefix + 4), c.has_ctx ? 1u : 0u, 0, 0};
+    c.ci_slot = ci_t.put(emurx_ci_hash(cid), s);
 }
 void Mirror::ft_slot_put(const std::string& key, Entry& e) {
     e.slot = kNoSlot;
@@ -247,7 +227,7 @@ void Mirror::ft_slot_put(const std::string& key, Entry& e) {
     const uint8_t* t = k + 4;
     if (key.size() == 4 + 13) {
         const uint32_t s[8] = {cid, le32(t), le32(t + 4), le32(t + 8), t[12], 0, 0, e.id};
-        ft4_t.put(emurx_ft4_hash(cid, s[1], s[2], s[3], s[4], ft4_t.seed), s, &e.slot);
+        e.slot = ft4_t.put(emurx_ft4_hash(cid, s[1], s[2], s[3], s[4]), s);
     } else {
         uint32_t s[16] = {cid};
         for (int j = 0; j < 4; ++j) {
@@ -257,8 +237,7 @@ void Mirror::ft_slot_put(const std::string& key, Entry& e) {
         s[9] = le32(t + 32);
         s[10] = t[36];
         s[15] = e.id;
-        ft6_t.put(emurx_ft6_hash(cid, s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9], s[10], ft6_t.seed), s,
-                  &e.slot);
+        e.slot = ft6_t.put(emurx_ft6_hash(cid, s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9], s[10]), s);
     }
 }
 void Mirror::srv_slot_put(uint64_t k, Entry& e) {
@@ -266,54 +245,53 @@ void Mirror::srv_slot_put(uint64_t k, Entry& e) {
     const uint32_t cid = (uint32_t)(k >> 32);
     if (!owned_ns(cl[cid].ns)) return;
     const uint32_t s[4] = {cid, (uint32_t)k, 0, 1};
-    srv_t.put(emurx_srv_hash(s[0], s[1], srv_t.seed), s, &e.slot);
+    e.slot = srv_t.put(emurx_srv_hash(s[0], s[1]), s);
 }
 void Mirror::drop(Hash& t, Entry& e) {
     if (e.slot != kNoSlot) t.del(e.slot);
     e.slot = kNoSlot;
 }
 
-void Mirror::rebuild(int which, uint32_t nb, bool reseed) {
-    Hash& t = *hashes(which);
-    for (int attempt = 0;; ++attempt) {
-        if (reseed || attempt) t.seed = emurx_fmix(t.seed + 0x9E3779B9u + (uint32_t)attempt);
-        if (attempt >= 3) nb += nb / 2;  // three seeds failed at this size: more room
-        t.init(nb, kWords[which], kBucketWords[which], kMarker[which]);
-        switch (which) {
-        case kTabNs:
-            for (auto& kv : ns_map) ns_slot_put(kv.first, kv.second);
-            break;
-        case kTabMac:
-            for (auto& kv : mac_map) mac_slot_put(kv.first, kv.second);
-            break;
-        case kTabIp4:
-            for (auto& kv : ip4_map) ip4_slot_put(kv.first, kv.second);
-            break;
-        case kTabIp6:
-            for (auto& kv : ip6_map) ip6_slot_put(kv.first, kv.second);
-            break;
-        case kTabCi:
-            for (uint32_t c = 0; c < max_clients; ++c) ci_put(c);
-            break;
-        case kTabFt4:
-        case kTabFt6:
-            for (auto& kv : ft_map)
-                if ((kv.first.size() == 4 + 13) == (which == kTabFt4)) ft_slot_put(kv.first, kv.second);
-            break;
-        case kTabSrv:
-            for (auto& kv : srv_map) srv_slot_put(kv.first, kv.second);
-            break;
-        }
-        if (!t.failed) return;
+void Mirror::rebuild(int which, uint32_t nb) {
+    switch (which) {
+    case kTabNs:
+        ns_t.init(nb, 4);
+        for (auto& n : ns) n.slot = kNoSlot;
+        for (auto& kv : ns_map) ns_slot_put(kv.first, kv.second);
+        break;
+    case kTabMac:
+        mac_t.init(nb, 4);
+        for (auto& kv : mac_map) mac_slot_put(kv.first, kv.second);
+        break;
+    case kTabIp4:
+        ip4_t.init(nb, 8);
+        for (auto& kv : ip4_map) ip4_slot_put(kv.first, kv.second);
+        break;
+    case kTabIp6:
+        ip6_t.init(nb, 8);
+        for (auto& kv : ip6_map) ip6_slot_put(kv.first, kv.second);
+        break;
+    case kTabCi:
+        ci_t.init(nb, 8);
+        for (uint32_t c = 0; c < max_clients; ++c) ci_put(c);
+        break;
+    case kTabFt4:
+    case kTabFt6: {
+        Hash& t = which == kTabFt4 ? ft4_t : ft6_t;
+        t.init(nb, which == kTabFt4 ? 8 : 16);
+        for (auto& kv : ft_map)
+            if ((kv.first.size() == 4 + 13) == (which == kTabFt4)) ft_slot_put(kv.first, kv.second);
+        break;
+    }
+    case kTabSrv:
+        srv_t.init(nb, 4);
+        for (auto& kv : srv_map) srv_slot_put(kv.first, kv.second);
+        break;
     }
 }
 void Mirror::reserve(Hash& t, int which, uint32_t k) {
     if (!t.full(k)) return;
-    rebuild(which, std::max<uint32_t>(t.nb * 2, t.sized((uint64_t)t.live + k)));
-}
-void Mirror::settle() {
-    for (int k = 0; k < kNumTabs; ++k)
-        if (hashes(k)->failed) rebuild(k, hashes(k)->nb, true);
+    rebuild(which, t.next_buckets(k));
 }
 
 // ---- Go map operations ---------------------------------------------------------------------
@@ -332,7 +310,6 @@ int Mirror::ns_add(const uint8_t key[12], uint32_t id, uint32_t plugins) {
     Entry& e = ns_map[k];
     e.id = id;
     ns_slot_put(k, e);
-    settle();
     put_nsinfo(id);
     touch_ns(id);
     return EMURX_OK;
@@ -348,6 +325,7 @@ int Mirror::ns_remove(const uint8_t key[12]) {
     drop(ns_t, it->second);
     ns_map.erase(it);
     n.alive = false;
+    n.slot = kNoSlot;
     put_nsinfo(id);
     touch_ns(id);
     if (removed.size() >= (1u << 16)) {  // forget old removals: older snapshots count as stale
@@ -361,11 +339,7 @@ int Mirror::ns_set_plugins(uint32_t id, uint32_t plugins) {
     if (id >= max_ns || !ns[id].alive) return EMURX_ENOENT;
     NsInfo& n = ns[id];
     n.plugins = plugins;
-    auto it = ns_map.find(key_ns(n.key));
-    if (it != ns_map.end() && it->second.slot != kNoSlot) {
-        const uint32_t sl = it->second.slot;
-        ns_t.rewrite(sl, 0, (ns_t.at(sl)[0] & 0xffffu) | (plugins << 16));
-    }
+    if (n.slot != kNoSlot) ns_t.rewrite(n.slot, 0, (ns_t.at(n.slot)[0] & 0xffffu) | (plugins << 16));
     put_nsinfo(id);
     touch_ns(id);
     return EMURX_OK;
@@ -415,7 +389,6 @@ int Mirror::client_add(uint32_t ns_id, uint32_t cid, const uint8_t mac[6], const
     if (has6) put(ip6_map, key_ip6(ns_id, ipv6), &Mirror::ip6_slot_put);
     if (has6d) put(ip6_map, key_ip6(ns_id, dhcpv6), &Mirror::ip6_slot_put);
     ci_put(cid);
-    settle();
     ns[ns_id].order.push_back(cid);  // clientHead.AddLast
     if (ns[ns_id].order.size() == 1) put_nsinfo(ns_id);
     touch_ns(ns_id);
@@ -492,9 +465,11 @@ void Mirror::rewrite_client_slots(uint32_t cid) {
     if (!zero(c.dhcpv6, 16))
         if (Entry* e = mine(ip6_map, key_ip6(c.ns, c.dhcpv6))) ip6_t.rewrite(e->slot, 6, hip);
     if (c.ci_slot != kNoSlot) {
-        ci_t.rewrite(c.ci_slot, 1, ci_word(c));
-        ci_t.rewrite(c.ci_slot, 2, le32(c.ra_prefix));
-        ci_t.rewrite(c.ci_slot, 3, le32(c.ra_prefix + 4));
+        ci_t.rewrite(c.ci_slot, 1, c.plugins);
+        ci_t.rewrite(c.ci_slot, 2, (c.has_ra ? 1u : 0u) | ((uint32_t)c.ra_plen << 8));
+        ci_t.rewrite(c.ci_slot, 3, le32(c.ra_prefix));
+        ci_t.rewrite(c.ci_slot, 4, le32(c.ra_prefix + 4));
+        ci_t.rewrite(c.ci_slot, 5, c.has_ctx ? 1u : 0u);
     }
 }
 int Mirror::client_set_plugins(uint32_t cid, uint32_t plugins) {
@@ -535,7 +510,6 @@ int Mirror::update_addr(uint32_t cid, int which, const uint8_t* nw) {
         e.id = cid;
         if (which == 4) ip4_slot_put(key(nw), e);
         else ip6_slot_put(key(nw), e);
-        settle();
     }
     memcpy(cur, nw, n);
     return EMURX_OK;
@@ -576,7 +550,6 @@ int Mirror::flow_add(uint32_t cid, const uint8_t* tuple, uint32_t tlen, uint32_t
     Entry& e = ft_map[k];
     e.id = flow;
     ft_slot_put(k, e);
-    settle();
     client_set_transport(cid, true);
     return EMURX_OK;
 }
@@ -602,7 +575,6 @@ int Mirror::server_add(uint32_t cid, uint16_t port, uint8_t proto) {
     Entry& e = srv_map[k];
     e.id = 1;
     srv_slot_put(k, e);
-    settle();
     client_set_transport(cid, true);
     return EMURX_OK;
 }
@@ -628,37 +600,38 @@ bool Mirror::stale(const emurx_rec& r, uint64_t since) const {
     return rm != removed.end() && rm->second > since;
 }
 
-// ---- the device lookup over the host image (tests of the table maintenance) -----------------
+// ---- the device walk over the host image (tests of the table maintenance) -------------------
 int Mirror::image_lookup(uint32_t table, const uint32_t* key, uint32_t* value) {
     if (table >= kNumTabs || !key || !value) return EMURX_EINVAL;
     Hash& t = *hashes((int)table);
     uint32_t h = 0, nk = 0;
     uint32_t kw[11] = {0};
     switch (table) {
-    case kTabNs: h = emurx_ns_hash(emurx_tk_hash(key[0], key[1], key[2]), t.seed); nk = 3; break;
+    case kTabNs: h = emurx_tk_hash(key[0], key[1], key[2]); nk = 3; break;
     case kTabMac:
         if (key[0] >= max_ns || !ns[key[0]].alive) return EMURX_ENOENT;
-        h = emurx_mac_hash(tk_of(key[0]), key[1], key[2], t.seed); nk = 3; break;
+        h = emurx_mac_hash(tk_of(key[0]), key[1], key[2]); nk = 3; break;
     case kTabIp4:
         if (key[0] >= max_ns || !ns[key[0]].alive) return EMURX_ENOENT;
-        h = emurx_ip4_hash(tk_of(key[0]), key[1], t.seed); nk = 2; break;
+        h = emurx_ip4_hash(tk_of(key[0]), key[1]); nk = 2; break;
     case kTabIp6:
         if (key[0] >= max_ns || !ns[key[0]].alive) return EMURX_ENOENT;
-        h = emurx_ip6_hash(tk_of(key[0]), key[1], key[2], key[3], key[4], t.seed); nk = 5; break;
-    case kTabCi: h = emurx_ci_hash(key[0], t.seed); nk = 1; break;
-    case kTabFt4: h = emurx_ft4_hash(key[0], key[1], key[2], key[3], key[4], t.seed); nk = 5; break;
+        h = emurx_ip6_hash(tk_of(key[0]), key[1], key[2], key[3], key[4]); nk = 5; break;
+    case kTabCi: h = emurx_ci_hash(key[0]); nk = 1; break;
+    case kTabFt4: h = emurx_ft4_hash(key[0], key[1], key[2], key[3], key[4]); nk = 5; break;
     case kTabFt6:
-        h = emurx_ft6_hash(key[0], key[1], key[2], key[3], key[4], key[5], key[6], key[7], key[8], key[9], key[10],
-                           t.seed);
+        h = emurx_ft6_hash(key[0], key[1], key[2], key[3], key[4], key[5], key[6], key[7], key[8], key[9], key[10]);
         nk = 11; break;
-    case kTabSrv: h = emurx_srv_hash(key[0], key[1], t.seed); nk = 2; break;
+    case kTabSrv: h = emurx_srv_hash(key[0], key[1]); nk = 2; break;
     }
     memcpy(kw, key, nk * 4);
-    // exactly the kernels' probe: the slots of the two candidate buckets, nothing else
-    for (uint32_t b : {emurx_b1(h, t.nb), emurx_b2(h, t.nb)})
+    for (uint32_t b = h & t.mask(), n = 0; n < t.buckets; b = (b + 1) & t.mask(), ++n) {
+        bool hole = false;
         for (uint32_t k = 0; k < t.per(); ++k) {
-            const uint32_t* s = t.at(b * t.per() + k);
-            if (s[t.mw] == EMURX_EMPTY) continue;
+            const uint32_t* s = &t.img[(size_t)b * EMURX_BUCKET_WORDS + k * t.words];
+            const uint32_t v = s[t.words - 1];
+            if (v == EMURX_EMPTY) { hole = true; continue; }
+            if (v == EMURX_TOMB) continue;
             bool eq = true;
             for (uint32_t j = 0; j < nk && eq; ++j) {
                 uint32_t x = s[j];
@@ -666,10 +639,12 @@ int Mirror::image_lookup(uint32_t table, const uint32_t* key, uint32_t* value) {
                 eq = x == kw[j];
             }
             if (eq) {
-                *value = table == kTabCi ? (s[1] & 0xffffu) : s[t.mw];  // client info: its plugin mask
+                *value = table == kTabCi ? s[1] : v;  // client info: its plugin mask
                 return EMURX_OK;
             }
         }
+        if (hole) break;
+    }
     return EMURX_ENOENT;
 }
 

@@ -4,11 +4,10 @@
 // AddNs / AddClient / UpdateClient* ...) AND the image of every device table in the layout of
 // emurx_tables.h.  Each mutation edits the image slot by slot and marks the 64-byte blocks it
 // touched; emurx_api.cpp ships only those blocks to the device (emurx_delta) before the next
-// batch.  The tables are two-choice bucketized cuckoo tables: an insert takes a free slot of
-// either candidate bucket or evicts an entry to ITS other bucket (a random walk, every moved
-// entry's slot index updated through a back pointer); a delete clears its slot.  An insert
-// that finds no place within kMaxKicks rebuilds the table with a new hash seed (then larger);
-// a table past its growth load is rebuilt larger.  Rebuilt tables are shipped whole.
+// batch.  Deleted slots become tombstones (key words 0xFFFFFFFF, value EMURX_TOMB): a probe
+// walks past them and never matches them, so a chain stays intact without moving entries.
+// A table whose live + tombstone slots pass 3/4 is rebuilt (doubled when live passes 1/2)
+// and shipped whole.
 //
 // Partitioned mode (set_partition): the maps stay complete (Go semantics do not change), but
 // the device images hold only the Namespaces this partition owns (emurx_owner of their
@@ -75,44 +74,33 @@ struct Blocks {
     }
 };
 
-// A two-choice bucketized cuckoo table image (emurx_tables.h): nb buckets of bw words (8,
-// or 16 for the IPv6 flow table) holding bw / words slots; the slot's marker word mw is
-// EMURX_EMPTY when free.  Every entry sits in emurx_b1 or emurx_b2 of its table hash.
+// open addressing over 64-byte buckets (emurx_tables.h), slots of `words` words.
+// `spread` is the table's target of slots per live entry (a power of two >= 2): a lookup's
+// wave waits for the longest probe chain among its 64 lanes, so the tables are kept sparse
+// enough that almost every key sits in its home bucket (emurx_table_spread).
 struct Hash : Blocks {
-    uint32_t words = 4, bw = EMURX_CBUCKET_WORDS, mw = 3, nb = 0, live = 0, seed = 0;
-    double target = 0.5, grow_at = 0.8;  // load of a freshly sized table, load that triggers growth
-    std::vector<uint32_t> hs;     // per slot: the entry's table hash (its two buckets), for evictions
-    std::vector<uint32_t*> back;  // per slot: where the entry's owner keeps its slot index
-    bool failed = false;          // an insert found no place: rebuild (new seed) before shipping
-    uint64_t rng = 0x9E3779B97F4A7C15ull;
-    static constexpr int kMaxKicks = 512;
-    uint32_t per() const { return bw / words; }
-    uint32_t nslots() const { return nb * per(); }
-    uint32_t* at(uint32_t s) { return &img[(size_t)(s / per()) * bw + (s % per()) * words]; }
-    const uint32_t* at(uint32_t s) const { return &img[(size_t)(s / per()) * bw + (s % per()) * words]; }
-    bool is_free(uint32_t s) const { return at(s)[mw] == EMURX_EMPTY; }
-    void touch_slot(uint32_t s) { touch((uint32_t)((size_t)(s / per()) * bw / EMURX_BUCKET_WORDS)); }
-    // nbuckets buckets of bucket_words words, slots of w words with marker word m, all free
-    void init(uint32_t nbuckets, uint32_t w, uint32_t bucket_words, uint32_t m);
-    // insert entry e (its table hash h) into a free slot of its buckets, evicting along a
-    // random walk when both are full; *bp (and every moved entry's back pointer) receives the
-    // slot.  false: some entry was left without a slot (*its* back pointer = kNoSlot, failed set)
-    bool put(uint32_t h, const uint32_t* e, uint32_t* bp);
+    uint32_t words = 4, buckets = 0, live = 0, tomb = 0, spread = 2;
+    uint32_t per() const { return EMURX_BUCKET_WORDS / words; }
+    uint32_t nslots() const { return buckets * per(); }
+    uint32_t mask() const { return buckets - 1; }
+    uint32_t* at(uint32_t s) { return &img[(size_t)(s / per()) * EMURX_BUCKET_WORDS + (s % per()) * words]; }
+    void init(uint32_t nbuckets, uint32_t w);
+    // first empty or tombstone slot in bucket order from the home bucket
+    uint32_t put(uint32_t hash, const uint32_t* e);
     void del(uint32_t s);
     void rewrite(uint32_t s, uint32_t word, uint32_t v) {
         at(s)[word] = v;
-        touch_slot(s);
+        touch(s / per());
     }
-    // k more inserts would take the table past its growth load
-    bool full(uint32_t k = 1) const { return (double)(live + k) > grow_at * nslots(); }
-    // buckets for `entries` at the target load
-    uint32_t sized(uint64_t entries) const;
-
-   private:
-    void place(uint32_t s, const uint32_t* e, uint32_t h, uint32_t* bp);
-    uint32_t rand32() {
-        rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17;
-        return (uint32_t)(rng >> 16);
+    // k more inserts would take live + tombstones past 2 / spread of the slots (3/4 at
+    // spread 2): twice the target load, then a rebuild drops the tombstones
+    bool full(uint32_t k = 1) const {
+        const uint64_t used = (uint64_t)live + tomb + k;
+        return spread <= 2 ? used * 4 > (uint64_t)nslots() * 3 : used * spread > (uint64_t)nslots() * 2;
+    }
+    // bucket count for a rebuild: doubled once live would pass the target load 1 / spread
+    uint32_t next_buckets(uint32_t k = 1) const {
+        return (uint64_t)(live + k) * spread > nslots() ? buckets * 2 : buckets;
     }
 };
 
@@ -122,6 +110,7 @@ struct NsInfo {
     uint8_t key[12] = {0};
     uint32_t plugins = 0;
     std::vector<uint32_t> order;  // clientHead dlist (insertion order)
+    uint32_t slot = kNoSlot;
     uint64_t gen = 0;             // generation of the last mutation of this Namespace
 };
 struct ClientInfo {
@@ -153,6 +142,8 @@ struct Mirror {
     void open(uint32_t max_ns, uint32_t max_clients);
     // device images hold only the Namespaces with emurx_owner(key, n) == part; rebuilds all
     void set_partition(uint32_t n, uint32_t part);
+    // table k at half its spread (its device allocation failed): rebuilt; false at spread 2
+    bool shrink(int k);
     bool pending() const;  // some image has edits not shipped yet
     Hash* hashes(int k);   // the 8 hash images (k < 8), for the uploader
     const Hash* hashes(int k) const { return const_cast<Mirror*>(this)->hashes(k); }
@@ -193,11 +184,8 @@ struct Mirror {
     void ft_slot_put(const std::string& k, Entry& e);
     void srv_slot_put(uint64_t k, Entry& e);
     void drop(Hash& t, Entry& e);
-    void reserve(Hash& t, int which, uint32_t k = 1);  // rebuild `t` larger first when k more inserts would not fit
-    // refill table `which` from the maps in `buckets` buckets (a new seed, then more buckets, when
-    // an insert fails); reseed: start with a new seed
-    void rebuild(int which, uint32_t buckets, bool reseed = false);
-    void settle();  // rebuild every table an insert failed on (after each mutation)
+    void reserve(Hash& t, int which, uint32_t k = 1);  // rebuild `t` first when k more inserts would not fit
+    void rebuild(int which, uint32_t buckets);
     void rewrite_client_slots(uint32_t cid);
     void drop_transport(uint32_t cid);
 };

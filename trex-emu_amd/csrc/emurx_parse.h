@@ -770,67 +770,104 @@ __device__ __forceinline__ void coop_checksum_rows(Rec& r, const uint8_t* f, uin
 
 // ---------------------------------------------------------------------------------------
 // Namespace / Client lookups (GetNs thread_ctx.go:777-784, CLookupBy* ns_ctx.go:262-329)
-// over the two-choice cuckoo tables of emurx_tables.h.  A key lives in one of its two
-// candidate buckets, both read together (four 16-byte loads), so a lookup resolves after
-// exactly one memory round trip.  A frame's Namespace buckets and its client buckets all
-// follow from the parsed tunnel key, so classify() issues the four reads at once.
+// over the bucketed tables of emurx_tables.h.  A frame's Namespace bucket and its client
+// bucket both follow from the parsed tunnel key, so classify() issues the two 64-byte
+// bucket reads together and resolves them afterwards; overflow buckets are rare.
 // ---------------------------------------------------------------------------------------
 struct Bucket {
-    uint4 s[4];  // s[0..1]: the first candidate bucket (32 B), s[2..3]: the second
+    uint4 s[4];
 };
-__device__ __forceinline__ Bucket ld_cands(const uint32_t* tab, uint32_t b1, uint32_t b2) {
-    const uint32_t* p = tab + (size_t)b1 * EMURX_CBUCKET_WORDS;
-    const uint32_t* q = tab + (size_t)b2 * EMURX_CBUCKET_WORDS;
-    return Bucket{{gld16(p), gld16(p + 4), gld16(q), gld16(q + 4)}};
+__device__ __forceinline__ Bucket ld_bucket(const uint32_t* tab, uint32_t b) {
+    const uint32_t* p = tab + (size_t)b * EMURX_BUCKET_WORDS;
+    return Bucket{{gld16(p), gld16(p + 4), gld16(p + 8), gld16(p + 12)}};
 }
 
-// A key sits at most once in a table, so "the matching slot of either bucket" is the answer;
-// slot order is free.  Free slots carry EMURX_EMPTY in their marker word and never match.
+// Lookups stop at the first bucket holding an empty slot.  A key sits at most once in a
+// table and the host rebuilds the tables without holes (bucket_put, emurx_api.cpp), so "a
+// matching slot anywhere in the bucket" equals the in-order scan and slot order is free.
 // ns slot {vport | ns_plugins << 16, vlan0, vlan1, ns_id} -> (ns_id, ns plugin mask)
-__device__ __forceinline__ uint2 resolve_ns(const Bucket& e, uint32_t w0, uint32_t w1, uint32_t w2) {
-    uint2 hit = make_uint2(EMURX_ID_NONE, 0);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint4 x = e.s[k];
-        if (x.w != EMURX_EMPTY && (x.x & 0xffffu) == w0 && x.y == w1 && x.z == w2) hit = make_uint2(x.w, x.x >> 16);
+__device__ __forceinline__ uint2 resolve_ns(const emurx_dev_tables& T, uint32_t b, Bucket e, uint32_t w0, uint32_t w1,
+                            uint32_t w2) {
+    {  // the home bucket's first slot alone: the common hit, a uniform early exit
+        const uint4 x = e.s[0];
+        if (x.w != EMURX_EMPTY && (x.x & 0xffffu) == w0 && x.y == w1 && x.z == w2) return make_uint2(x.w, x.x >> 16);
     }
-    return hit;
+    for (uint32_t n = 0;;) {
+        bool hole = false;
+        uint2 hit = make_uint2(EMURX_ID_NONE, 0);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint4 x = e.s[k];
+            hole |= x.w == EMURX_EMPTY;
+            if (x.w != EMURX_EMPTY && (x.x & 0xffffu) == w0 && x.y == w1 && x.z == w2) hit = make_uint2(x.w, x.x >> 16);
+        }
+        if (hit.x != EMURX_ID_NONE || hole || ++n > T.ns_mask) return hit;
+        b = (b + 1) & T.ns_mask;
+        e = ld_bucket(T.ns_tab, b);
+    }
 }
 // mac slot {ns_id, mac[0..3], mac[4..5] | client_plugins << 16, client_id} -> (cid, plugins)
-__device__ __forceinline__ uint2 resolve_mac(const Bucket& e, uint32_t ns, uint32_t lo, uint32_t hi) {
-    uint2 hit = make_uint2(EMURX_ID_NONE, 0);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint4 x = e.s[k];
-        if (x.w != EMURX_EMPTY && x.x == ns && x.y == lo && (x.z & 0xffffu) == hi) hit = make_uint2(x.w, x.z >> 16);
+__device__ __forceinline__ uint2 resolve_mac(const emurx_dev_tables& T, uint32_t b, Bucket e, uint32_t ns, uint32_t lo,
+                             uint32_t hi) {
+    {
+        const uint4 x = e.s[0];
+        if (x.w != EMURX_EMPTY && x.x == ns && x.y == lo && (x.z & 0xffffu) == hi) return make_uint2(x.w, x.z >> 16);
     }
-    return hit;
+    for (uint32_t n = 0;;) {
+        bool hole = false;
+        uint2 hit = make_uint2(EMURX_ID_NONE, 0);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint4 x = e.s[k];
+            hole |= x.w == EMURX_EMPTY;
+            if (x.w != EMURX_EMPTY && x.x == ns && x.y == lo && (x.z & 0xffffu) == hi) hit = make_uint2(x.w, x.z >> 16);
+        }
+        if (hit.x != EMURX_ID_NONE || hole || ++n > T.mac_mask) return hit;
+        b = (b + 1) & T.mac_mask;
+        e = ld_bucket(T.mac_tab, b);
+    }
 }
 // IP slots carry the client's MAC and plugin mask: {cid, mac_lo, mac_hi | plugins << 16}
 struct IpHit {
     uint32_t cid, mlo, mhip;
 };
-// ip4 slot {ns_id, ip, mac_lo, mac_hi | plugins << 16} {0, 0, 0, client_id}, one per bucket
-__device__ __forceinline__ IpHit resolve_ip4(const Bucket& e, uint32_t ns, uint32_t ip) {
-    IpHit hit{EMURX_ID_NONE, 0, 0};
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const uint4 x = e.s[2 * k], y = e.s[2 * k + 1];
-        if (y.w != EMURX_EMPTY && x.x == ns && x.y == ip) hit = IpHit{y.w, x.z, x.w};
+// ip4 slot {ns_id, ip, mac_lo, mac_hi | plugins << 16} {0, 0, 0, client_id}, 2 per bucket
+__device__ __forceinline__ IpHit resolve_ip4(const emurx_dev_tables& T, uint32_t b, Bucket e, uint32_t ns, uint32_t ip) {
+    {
+        const uint4 x = e.s[0], y = e.s[1];
+        if (y.w != EMURX_EMPTY && x.x == ns && x.y == ip) return IpHit{y.w, x.z, x.w};
     }
-    return hit;
+    for (uint32_t n = 0;;) {
+        bool hole = false;
+        IpHit hit{EMURX_ID_NONE, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const uint4 x = e.s[2 * k], y = e.s[2 * k + 1];
+            hole |= y.w == EMURX_EMPTY;
+            if (y.w != EMURX_EMPTY && x.x == ns && x.y == ip) hit = IpHit{y.w, x.z, x.w};
+        }
+        if (hit.cid != EMURX_ID_NONE || hole || ++n > T.ip4_mask) return hit;
+        b = (b + 1) & T.ip4_mask;
+        e = ld_bucket(T.ip4_tab, b);
+    }
 }
 // ip6 slot {ns_id, ip[0..3], ip[4..7], ip[8..11]} {ip[12..15], mac_lo, mac_hi | plugins << 16,
-// client_id}, one per bucket
-__device__ __forceinline__ IpHit resolve_ip6(const Bucket& e, uint32_t ns, const uint32_t w[4]) {
-    IpHit hit{EMURX_ID_NONE, 0, 0};
+// client_id}, 2 per bucket
+__device__ __forceinline__ IpHit resolve_ip6(const emurx_dev_tables& T, uint32_t b, Bucket e, uint32_t ns, const uint32_t w[4]) {
+    for (uint32_t n = 0;;) {
+        bool hole = false;
+        IpHit hit{EMURX_ID_NONE, 0, 0};
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const uint4 x = e.s[2 * k], y = e.s[2 * k + 1];
-        if (y.w != EMURX_EMPTY && x.x == ns && x.y == w[0] && x.z == w[1] && x.w == w[2] && y.x == w[3])
-            hit = IpHit{y.w, y.y, y.z};
+        for (int k = 0; k < 2; ++k) {
+            const uint4 x = e.s[2 * k], y = e.s[2 * k + 1];
+            hole |= y.w == EMURX_EMPTY;
+            if (y.w != EMURX_EMPTY && x.x == ns && x.y == w[0] && x.z == w[1] && x.w == w[2] && y.x == w[3])
+                hit = IpHit{y.w, y.y, y.z};
+        }
+        if (hit.cid != EMURX_ID_NONE || hole || ++n > T.ip6_mask) return hit;
+        b = (b + 1) & T.ip6_mask;
+        e = ld_bucket(T.ip6_tab, b);
     }
-    return hit;
 }
 
 __device__ __forceinline__ void set_lk(Rec& r, uint32_t lk) {
@@ -844,22 +881,24 @@ __device__ __forceinline__ void client_result(Rec& r, uint32_t cid, uint32_t cpl
     if (check && !(cplugins & (1u << plug))) { set_lk(r, EMURX_LK_CLIENT_NO_PLUGIN); return; }
     set_lk(r, EMURX_LK_CLIENT);
 }
-// client info slot {cid, plugins | has_ra << 16 | has_ctx << 17 | ra_len << 24, ra_prefix[0..3],
-// ra_prefix[4..7]} of a client id (emurx_tables.h ci table, two per bucket); zeros when absent.
-// ra: bit 0 has_ra, bits 8..15 the prefix length
+// client info slot {cid, plugins, ra, ra_prefix[0..3], ra_prefix[4..7], has_ctx, 0, 0} of a
+// client id (emurx_tables.h ci table, 2 per bucket); zeros when absent
 struct CInfo {
     uint32_t plugins, ra, ra0, ra1, ctx;
 };
 __device__ __forceinline__ CInfo client_info(const emurx_dev_tables& T, uint32_t cid) {
     CInfo c{0, 0, 0, 0, 0};
     if (cid == EMURX_ID_NONE) return c;
-    const uint32_t h = emurx_ci_hash(cid, T.ci.seed);
-    const Bucket e = ld_cands(T.ci.p, emurx_b1(h, T.ci.nb), emurx_b2(h, T.ci.nb));
+    for (uint32_t b = emurx_ci_hash(cid) & T.ci_mask, n = 0; n <= T.ci_mask; b = (b + 1) & T.ci_mask, ++n) {
+        const Bucket e = ld_bucket(T.ci_tab, b);
+        bool hole = false;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint4 x = e.s[k];
-        if (x.x == cid)
-            c = CInfo{x.y & 0xffffu, ((x.y >> 16) & 1u) | ((x.y >> 24) << 8), x.z, x.w, (x.y >> 17) & 1u};
+        for (int k = 0; k < 2; ++k) {
+            const uint4 x = e.s[2 * k], y = e.s[2 * k + 1];
+            hole |= y.w == EMURX_EMPTY;
+            if (y.w != EMURX_EMPTY && x.x == cid) return CInfo{x.y, x.z, x.w, y.x, y.y};
+        }
+        if (hole) break;
     }
     return c;
 }
@@ -942,46 +981,45 @@ __device__ __forceinline__ Tuple get_tuple(const S& s, uint32_t len, const Rec& 
 // else the new-flow checks of handleRxTcpNewFlow / handleRxUdpNewFlow (:829-904) up to OnAccept
 __device__ __forceinline__ uint32_t flow_probe(const emurx_dev_tables& T, const Tuple& t, uint32_t cid) {
     const uint32_t proto = t.proto, ports = t.ports;
-    if (!t.v6) {  // ft4: one 32-byte slot per bucket
+    if (!t.v6) {
         const uint32_t src = t.a[0], dst = t.d[0];
-        const uint32_t h = emurx_ft4_hash(cid, src, dst, ports, proto, T.ft4.seed);
-        const Bucket e = ld_cands(T.ft4.p, emurx_b1(h, T.ft4.nb), emurx_b2(h, T.ft4.nb));
-        uint32_t hit = EMURX_EMPTY;
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const uint4 x = e.s[2 * k], y = e.s[2 * k + 1];
-            if (y.w != EMURX_EMPTY && x.x == cid && x.y == src && x.z == dst && x.w == ports && y.x == proto) hit = y.w;
+        for (uint32_t b = emurx_ft4_hash(cid, src, dst, ports, proto) & T.ft4_mask, k = 0; k <= T.ft4_mask;
+             ++k, b = (b + 1) & T.ft4_mask) {
+            const Bucket e = ld_bucket(T.ft4_tab, b);
+            const uint4 x0 = e.s[0], x1 = e.s[1], y0 = e.s[2], y1 = e.s[3];
+            if (x0.x == cid && x0.y == src && x0.z == dst && x0.w == ports && x1.x == proto && x1.w != EMURX_EMPTY)
+                return x1.w;
+            if (y0.x == cid && y0.y == src && y0.z == dst && y0.w == ports && y1.x == proto && y1.w != EMURX_EMPTY)
+                return y1.w;
+            if (x1.w == EMURX_EMPTY || y1.w == EMURX_EMPTY) break;
         }
-        if (hit != EMURX_EMPTY) return hit;
-    } else {  // ft6: one 64-byte slot per 64-byte bucket
-        const uint32_t h = emurx_ft6_hash(cid, t.a[0], t.a[1], t.a[2], t.a[3], t.d[0], t.d[1], t.d[2], t.d[3], ports,
-                                          proto, T.ft6.seed);
-        const uint32_t bk[2] = {emurx_b1(h, T.ft6.nb), emurx_b2(h, T.ft6.nb)};
-        uint4 s[2][4];
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const uint32_t* p = T.ft6.p + (size_t)bk[k] * 16;
-            s[k][0] = gld16(p); s[k][1] = gld16(p + 4); s[k][2] = gld16(p + 8); s[k][3] = gld16(p + 12);
+    } else {
+        for (uint32_t b = emurx_ft6_hash(cid, t.a[0], t.a[1], t.a[2], t.a[3], t.d[0], t.d[1], t.d[2], t.d[3], ports,
+                                         proto) & T.ft6_mask, k = 0;
+             k <= T.ft6_mask; ++k, b = (b + 1) & T.ft6_mask) {
+            const Bucket e = ld_bucket(T.ft6_tab, b);
+            if (e.s[3].w == EMURX_EMPTY) break;
+            if (e.s[0].x == cid && e.s[0].y == t.a[0] && e.s[0].z == t.a[1] && e.s[0].w == t.a[2] &&
+                e.s[1].x == t.a[3] && e.s[1].y == t.d[0] && e.s[1].z == t.d[1] && e.s[1].w == t.d[2] &&
+                e.s[2].x == t.d[3] && e.s[2].y == ports && e.s[2].z == proto)
+                return e.s[3].w;
         }
-        uint32_t hit = EMURX_EMPTY;
-#pragma unroll
-        for (int k = 0; k < 2; ++k)
-            if (s[k][3].w != EMURX_EMPTY && s[k][0].x == cid && s[k][0].y == t.a[0] && s[k][0].z == t.a[1] &&
-                s[k][0].w == t.a[2] && s[k][1].x == t.a[3] && s[k][1].y == t.d[0] && s[k][1].z == t.d[1] &&
-                s[k][1].w == t.d[2] && s[k][2].x == t.d[3] && s[k][2].y == ports && s[k][2].z == proto)
-                hit = s[k][3].w;
-        if (hit != EMURX_EMPTY) return hit;
     }
     // a new flow: handleRxTcpNewFlow needs a bare SYN (GetFlags() & 0x3F == 0x2)
     if (proto == 6 && (t.flags & 0x3f) != 0x2) return EMURX_FLOW_NO_SYN;
     const uint32_t dport = ((ports >> 16) & 0xff) << 8 | (ports >> 24);
     const uint32_t key = dport | ((proto == 6 ? 6u : 17u) << 16);  // lookupServerPort(dst, TCP|UDP)
-    const uint32_t h = emurx_srv_hash(cid, key, T.srv.seed);
-    const Bucket e = ld_cands(T.srv.p, emurx_b1(h, T.srv.nb), emurx_b2(h, T.srv.nb));
-    bool found = false;
+    for (uint32_t b = emurx_srv_hash(cid, key) & T.srv_mask, k = 0; k <= T.srv_mask; ++k, b = (b + 1) & T.srv_mask) {
+        const Bucket e = ld_bucket(T.srv_tab, b);
+        bool hole = false;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) found |= e.s[j].w != EMURX_EMPTY && e.s[j].x == cid && e.s[j].y == key;
-    return found ? EMURX_FLOW_NEW : EMURX_FLOW_NO_SERVER;
+        for (int j = 0; j < 4; ++j) {
+            hole |= e.s[j].w == EMURX_EMPTY;
+            if (e.s[j].w != EMURX_EMPTY && e.s[j].x == cid && e.s[j].y == key) return EMURX_FLOW_NEW;
+        }
+        if (hole) break;
+    }
+    return EMURX_FLOW_NO_SERVER;
 }
 
 // the plugin whose PluginCtx each callback checks, a nibble per callback in one immediate (a
@@ -1078,10 +1116,10 @@ __device__ __forceinline__ LKey make_key(const S& s, uint32_t len, const Rec& r)
     return k;
 }
 
-// The reads of a frame's lookups, issued together: the two candidate buckets of its
-// Namespace (loaded here) and of its client key (ctab == nullptr: the rule reads none).
+// The two bucket reads of a frame's lookups, issued together: its Namespace bucket (loaded
+// here) and the first bucket of its client table (ctab == nullptr: the rule reads none).
 struct Probe {
-    uint32_t cb1, cb2, mlo, mhi;  // mlo / mhi: the MAC probed for kMac / kEui
+    uint32_t nb, cbk, mlo, mhi;  // mlo / mhi: the MAC probed for kMac / kEui
     const uint32_t* ctab;
     Bucket ne;
 };
@@ -1096,43 +1134,37 @@ __device__ __forceinline__ Probe probe_issue(const emurx_dev_tables& T, const Re
         p.mhi = ((k.kw[3] >> 16) & 0xff) | ((k.kw[3] >> 24) << 8);
     }
     const uint32_t tk = emurx_tk_hash(r.vport, r.vlan0, r.vlan1);  // CTunnelKey words
-    const uint32_t hn = emurx_ns_hash(tk, T.ns.seed);
-    p.ne = ld_cands(T.ns.p, emurx_b1(hn, T.ns.nb), emurx_b2(hn, T.ns.nb));
-    p.cb1 = p.cb2 = 0;
+    p.nb = tk & T.ns_mask;
+    p.ne = ld_bucket(T.ns_tab, p.nb);
+    p.cbk = 0;
     p.ctab = nullptr;
     // The three table bases as SGPR values selected per lane: left to itself the compiler
     // turns "this lane's table pointer" into a vector load from the kernarg segment at a
-    // per-lane offset, one more dependent memory trip before the client buckets' addresses
-    uintptr_t tm = (uintptr_t)T.mac.p, t4 = (uintptr_t)T.ip4.p, t6 = (uintptr_t)T.ip6.p;
+    // per-lane offset, one more dependent memory trip before the client bucket's address
+    uintptr_t tm = (uintptr_t)T.mac_tab, t4 = (uintptr_t)T.ip4_tab, t6 = (uintptr_t)T.ip6_tab;
     asm volatile("" : "+s"(tm), "+s"(t4), "+s"(t6));
-    uint32_t h = 0, nb = 0;
     if (key == kMac || key == kEui) {
-        h = emurx_mac_hash(tk, p.mlo, p.mhi, T.mac.seed);
-        nb = T.mac.nb;
+        p.cbk = emurx_mac_hash(tk, p.mlo, p.mhi) & T.mac_mask;
         p.ctab = reinterpret_cast<const uint32_t*>(tm);
     } else if (key == kIp4) {
-        h = emurx_ip4_hash(tk, k.kw[0], T.ip4.seed);
-        nb = T.ip4.nb;
+        p.cbk = emurx_ip4_hash(tk, k.kw[0]) & T.ip4_mask;
         p.ctab = reinterpret_cast<const uint32_t*>(t4);
     } else if (key == kIp6) {
-        h = emurx_ip6_hash(tk, k.kw[0], k.kw[1], k.kw[2], k.kw[3], T.ip6.seed);
-        nb = T.ip6.nb;
+        p.cbk = emurx_ip6_hash(tk, k.kw[0], k.kw[1], k.kw[2], k.kw[3]) & T.ip6_mask;
         p.ctab = reinterpret_cast<const uint32_t*>(t6);
     }
-    p.cb1 = emurx_b1(h, nb);
-    p.cb2 = emurx_b2(h, nb);
     return p;
 }
 
-// GetNs + the callback's client rule, given the Namespace and client candidate buckets.  `flow(cid)` gives the transport
+// GetNs + the callback's client rule, given the two buckets.  `flow(cid)` gives the transport
 // flow decision of a tcp/udp frame whose client was found with the transport plugin.
 template <class Flow>
 __device__ __forceinline__ void resolve_done(const emurx_dev_tables& T, Rec& r, const LKey& k, const Probe& p,
                                              const Bucket& ce, Flow flow) {
     const uint32_t cb = r.proto, plug = cb_plugin(cb);
-    const uint32_t key = k.key, mlo = p.mlo, mhi = p.mhi;
+    const uint32_t key = k.key, cbk = p.cbk, mlo = p.mlo, mhi = p.mhi;
     // ---- GetNs + ns.PluginCtx.Get(plugin) ----
-    const uint2 nsr = resolve_ns(p.ne, r.vport, r.vlan0, r.vlan1);
+    const uint2 nsr = resolve_ns(T, p.nb, p.ne, r.vport, r.vlan0, r.vlan1);
     const uint32_t ns = nsr.x;
     if (ns == EMURX_ID_NONE) { set_lk(r, EMURX_LK_NO_NS); return; }
     r.ns = ns;
@@ -1152,7 +1184,7 @@ __device__ __forceinline__ void resolve_done(const emurx_dev_tables& T, Rec& r, 
         return;
     }
     case kIp4: {
-        const IpHit h = resolve_ip4(ce, ns, k.kw[0]);
+        const IpHit h = resolve_ip4(T, cbk, ce, ns, k.kw[0]);
         if (cb == EMURX_CB_ARP) {
             client_result(r, h.cid, h.mhip >> 16, plug, true);
         } else {  // icmp: IsUnicastToMe against the MAC in the slot
@@ -1165,7 +1197,7 @@ __device__ __forceinline__ void resolve_done(const emurx_dev_tables& T, Rec& r, 
     case kIp6: {  // icmpv6 echo request
         uint32_t cid, clo, chi;  // the client and its MAC (IsUnicastToMe)
         if (key == kEui) {
-            cid = resolve_mac(ce, ns, mlo, mhi).x;
+            cid = resolve_mac(T, cbk, ce, ns, mlo, mhi).x;
             clo = mlo;  // the MAC table's key is the client's MAC
             chi = mhi;
             // CClient.IsValidPrefix client_ctx.go:279-295
@@ -1175,7 +1207,7 @@ __device__ __forceinline__ void resolve_done(const emurx_dev_tables& T, Rec& r, 
                     cid = EMURX_ID_NONE;
             }
         } else {
-            const IpHit h = resolve_ip6(ce, ns, k.kw);
+            const IpHit h = resolve_ip6(T, cbk, ce, ns, k.kw);
             cid = h.cid;
             clo = h.mlo;
             chi = h.mhip & 0xffffu;
@@ -1186,7 +1218,7 @@ __device__ __forceinline__ void resolve_done(const emurx_dev_tables& T, Rec& r, 
         return;
     }
     default: {  // kMac
-        const uint2 c = resolve_mac(ce, ns, mlo, mhi);
+        const uint2 c = resolve_mac(T, cbk, ce, ns, mlo, mhi);
         client_result(r, c.x, c.y, plug, true);
         // transport: the client's TransportCtx decides (plugin_transport.go:109-114, :73-80)
         if ((cb == EMURX_CB_TCP || cb == EMURX_CB_UDP) &&
@@ -1205,7 +1237,7 @@ template <class Flow>
 __device__ __forceinline__ void resolve(const emurx_dev_tables& T, Rec& r, const LKey& k, Flow flow) {
     const Probe p = probe_issue(T, r, k);
     Bucket ce{};
-    if (p.ctab) ce = ld_cands(p.ctab, p.cb1, p.cb2);
+    if (p.ctab) ce = ld_bucket(p.ctab, p.cbk);
     resolve_done(T, r, k, p, ce, flow);
 }
 
