@@ -289,11 +289,20 @@ def main():
         out["table_updates"] = table_update_cost(a, rx, w, torch)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(w, a.cpu_seconds)
+        if "host_inclusive" in out and a.config == "B":
+            out["host_inclusive"]["crossover"] = crossover(out["host_inclusive"], out["cpu_baseline"]["value"])
     if rank == 0:
         print(json.dumps(out), flush=True)
     rx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def progress(rank, msg):
+    """A progress line on stderr (rank 0): a long run shows it is alive, and a log shows where
+    a run that was stopped had got to (the JSON line comes only at the end)."""
+    if rank == 0:
+        print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
 def exchange_block(xo):
@@ -382,6 +391,8 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
     import numpy as np
     from emurx import abi
     from emurx.rx import RxPath
+    t_start = time.perf_counter()
+    progress(rank, f"measure config {cfg}, {n} frames per GPU, tables {mode}, {world} rank(s)")
     w = workload(cfg, n, rank)
     max_ns = max(4096, len(w["ns"]))
     max_cl = max(65536, len(w["clients"]["cid"]) + (8192 if a.table_updates else 0))  # spare ids
@@ -649,6 +660,7 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
     # leaves the GPU idle long enough for its clocks to drop, which a 20-step region would time
     warm_s = warm_for_time()
 
+    progress(rank, f"config {cfg} {mode}: tables and batches ready, warmed up ({time.perf_counter() - t_start:.1f} s)")
     region = xch is None and a.kernel_timing == "region"
     if xch is not None or a.kernel_timing == "launch":
         rx.set_timing(steps + 8, a.time_stride)
@@ -1086,20 +1098,48 @@ def host_path_rate(rx, w, per_msg=64, budget_s=3.0):
     out["mpkts_prefilled"] = round(k * n / el / 1e6, 2)
     out["gbs_in_prefilled"] = round(k * total / el / 1e9, 2)
     # latency of one batch by its size in messages (one slot, nothing else in flight): submit
-    # (H2D of the staged messages + framing walk + k_rx + queue packing + D2H) until wait returns
-    lat = {}
-    for nm in (1, 16, 256, 1024, 4096, len(msgs)):
-        if nm > len(msgs):
+    # (batches that fit it: the one-launch path k_ingest_small, zero-copy in and out; larger
+    # ones: H2D + framing walk + k_rx + queue packing + D2H) until wait returns; raw C calls
+    # (no Python-side views), the staging already filled.  And the rate of such batches with
+    # both slots alternating (one submitted while the other is in flight)
+    import ctypes as C
+    from emurx import abi
+    lib, h = rx.lib, rx.h
+    res = abi.IngestResult()
+    mt = np.ascontiguousarray(np.asarray(msgs)).view(np.uint32).reshape(-1, 2)
+    np.copyto(bufs[0], stream)
+    np.copyto(bufs[1], stream)
+    lat, thr = {}, {}
+    for nm in (1, 2, 4, 8, 16, 32, 64, 256, 1024, 4096, len(msgs)):
+        if nm > len(msgs) or str(nm) in lat:
             continue
-        sub_msgs = msgs[:nm]
+        tab = np.ascontiguousarray(mt[:nm])
+        ptr = tab.ctypes.data
         ts = []
-        for rep in range(7):
+        for rep in range(25 if nm <= 1024 else 7):
             t0 = time.perf_counter()
-            rx.ingest_submit(0, sub_msgs)
-            rx.ingest_wait(0, copy=False)
+            abi.check(lib.emurx_ingest_submit(h, 0, ptr, nm), "ingest_submit")
+            abi.check(lib.emurx_ingest_wait(h, 0, C.byref(res)), "ingest_wait")
             ts.append(time.perf_counter() - t0)
-        lat[str(nm)] = {"frames": nm * per_msg, "us_median": round(float(np.median(ts[2:])) * 1e6, 1)}
+        ts = np.array(ts[3:]) * 1e6
+        lat[str(nm)] = {"frames": nm * per_msg, "us_median": round(float(np.median(ts)), 1),
+                        "us_p10": round(float(np.percentile(ts, 10)), 1),
+                        "mpkts": round(nm * per_msg / float(np.median(ts)), 3)}
+        if nm <= 1024:  # two slots in flight
+            k, t0 = 0, time.perf_counter()
+            while k < 400 and (k < 8 or time.perf_counter() - t0 < 0.5):
+                sl = k & 1
+                if k >= 2:
+                    abi.check(lib.emurx_ingest_wait(h, sl, C.byref(res)), "ingest_wait")
+                abi.check(lib.emurx_ingest_submit(h, sl, ptr, nm), "ingest_submit")
+                k += 1
+            for sl in range(2):
+                abi.check(lib.emurx_ingest_wait(h, sl, C.byref(res)), "ingest_wait")
+            el = time.perf_counter() - t0
+            thr[str(nm)] = {"frames": nm * per_msg, "mpkts": round(k * nm * per_msg / el / 1e6, 3),
+                            "us_per_batch": round(el / k * 1e6, 1)}
     out["batch_latency_by_msgs"] = lat
+    out["two_slot_rate_by_msgs"] = thr
     # one ZMQ message per call (the unbatched OnRxStream shape)
     one = [stream[m["off"]:m["off"] + m["len"]].tobytes() for m in msgs[:300]]
     rx.on_rx_stream(one[0])
@@ -1108,6 +1148,21 @@ def host_path_rate(rx, w, per_msg=64, budget_s=3.0):
         rx.on_rx_stream(m, cap=per_msg)
     out["mpkts_one_msg_per_call"] = round(len(one) * per_msg / (time.perf_counter() - t0) / 1e6, 4)
     return out
+
+
+def crossover(hp, cpu_mpkts):
+    """The smallest batch (frames) at which the host-inclusive ingest beats one core of the CPU
+    restatement on the same frames: by latency (frames / the batch's submit-to-wait time) and
+    by rate with both slots in flight."""
+    def first(table):
+        for k in sorted(table, key=lambda x: table[x]["frames"]):
+            if table[k]["mpkts"] >= cpu_mpkts:
+                return table[k]["frames"]
+        return None
+    return {"cpu_one_core_mpkts": cpu_mpkts, "frames_by_latency": first(hp["batch_latency_by_msgs"]),
+            "frames_by_two_slot_rate": first(hp["two_slot_rate_by_msgs"]),
+            "note": "smallest batch whose GPU path (pinned staging -> results in pinned memory) processes frames "
+                    "at least as fast as one host core running the oracle's rx_batch"}
 
 
 def tx_zmq_rate(rx, w, torch, reps=50):

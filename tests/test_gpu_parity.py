@@ -708,6 +708,38 @@ def test_ingest_messages(rxmod):
     check_ingest(res, o, msgs, tab)
 
 
+@pytest.mark.parametrize("small", ["1", "0"])
+def test_ingest_small_batches(rxmod, small, monkeypatch):
+    """Batches that fit the one-launch path (k_ingest_small: <= 16 tiles, <= 256 messages, each
+    tile's messages within its LDS budget) and, with EMURX_INGEST_SMALL=0, the same batches
+    through the multi-launch pipeline: records, descriptors (owner keys included), queues,
+    per-message frame counts and status, and every counter equal the oracle's OnRxStream per
+    message.  1 to 64 messages of config C frames and hostile messages (truncated, corrupted,
+    over-announcing, empty), so that messages span tiles, some carry no slot and the last
+    tile's status words include the trailing empty messages."""
+    import test_abi
+    monkeypatch.setenv("EMURX_INGEST_SMALL", small)
+    rng = np.random.default_rng(0x5A11 + int(small))
+    w = synth.config_c(8192, seed=0xC0DE)
+    frames = [w["buf"][d["off"]:d["off"] + d["len"]].tobytes() for d in w["desc"]]
+    rx, o = new_pair(rxmod)
+    for t in (rx, o):
+        synth.load_tables(w, t)
+    k = 0
+    for nm in (1, 2, 3, 5, 16, 17, 40, 64):
+        msgs = []
+        for j in range(nm):
+            per = int(rng.integers(1, 65))
+            msgs.append(F.zmq_pack(frames[k:k + per], list(w["desc"]["vport"][k:k + per])))
+            k = (k + per) % (len(frames) - 64)
+        msgs += test_abi._rand_msgs(rng, 4)[:4] + [b""]
+        msgs = [msgs[i] for i in rng.permutation(len(msgs))]
+        tab = place_messages(rx, 0, msgs, rng)
+        rx.ingest_submit(0, tab)
+        res = rx.ingest_wait(0)
+        check_ingest(res, o, msgs, tab)
+
+
 def test_ingest_two_slots_pipelined(rxmod):
     """Config C frames as 64-frame messages, three batches over the two slots with one batch
     always in flight while the next is staged; each equals the oracle."""

@@ -92,9 +92,13 @@ struct IngestSlot {
     DevBuf<emurx_desc> d_desc;
     DevBuf<emurx_rec> d_rec;
     DevBuf<uint64_t> d_hist, d_hist_out;  // d_hist: zero between batches (k_qscan clears it)
+    // the fused small-batch path's scratch (k_ingest_small), zero between batches
+    DevBuf<uint32_t> d_qseg, d_tcnt, d_ticket;
+    DevBuf<uint64_t> d_hsmall;
     std::vector<uint32_t> remap;          // slot -> frame index, only when a message fell short
     void release() {
         if (st) (void)hipStreamSynchronize(st);
+        d_qseg.release(); d_tcnt.release(); d_ticket.release(); d_hsmall.release();
         h_buf.release(); h_ctl.release(); h_stat.release(); h_qlist.release(); h_qoff.release();
         h_mframes.release(); h_mstatus.release(); h_rec.release(); h_desc.release(); h_hist.release();
         d_buf.release(); d_ctl.release(); d_stat.release(); d_qlist.release(); d_tile_cnt.release();
@@ -144,6 +148,7 @@ struct emurx_ctx {
 
     // batched host ingest: EMURX_INGEST_SLOTS public slots + one private to emurx_rx_stream
     IngestSlot ing[EMURX_INGEST_SLOTS + 1];
+    bool ingest_small = true;  // small batches in one launch (k_ingest_small); EMURX_INGEST_SMALL=0: never
 
     // tx ZMQ framing scratch (emurx_tx_zmq_dev): per-level chain transfer tables
     DevBuf<uint8_t> d_txz;
@@ -467,6 +472,32 @@ int ingest_buffer(emurx_t* h, uint32_t slot, size_t bytes, uint8_t** buf) {
     return EMURX_OK;
 }
 
+// Does a batch fit the one-launch path (k_ingest_small)?  At most EMURX_SMALL_MSGS messages and
+// EMURX_SMALL_TILES tiles of descriptor slots, and every tile's messages (those with slots in
+// it, and those whose status word it writes: tile min(base / 256, tiles - 1)) within the
+// kernel's LDS budget, counted exactly as the kernel stages them: 16-byte vectors from the
+// message's aligned start, plus two of slack.
+bool small_fits(const uint32_t* ctl, uint32_t nmsg, uint32_t n) {
+    if (nmsg > EMURX_SMALL_MSGS || n > (uint32_t)EMURX_SMALL_TILES * EMURX_QUEUE_TILE) return false;
+    const uint32_t nt = std::max<uint32_t>(ntiles(n), 1);
+    const uint32_t* base = ctl + 2 * (size_t)nmsg;
+    uint64_t vec[EMURX_SMALL_TILES] = {0};
+    for (uint32_t m = 0; m < nmsg; ++m) {
+        const uint32_t off = ctl[2 * m], len = ctl[2 * m + 1];
+        const uint64_t v = len ? (((off & 15u) + (uint64_t)len + 15) >> 4) + 2 : 0;
+        const uint32_t b0 = base[m], b1 = base[m + 1], ts = std::min(b0 / EMURX_QUEUE_TILE, nt - 1);
+        uint32_t t0 = ts, t1 = ts;
+        if (b1 > b0) {
+            t0 = std::min(t0, b0 / EMURX_QUEUE_TILE);
+            t1 = std::max(t1, std::min((b1 - 1) / EMURX_QUEUE_TILE, nt - 1));
+        }
+        for (uint32_t t = t0; t <= t1; ++t) vec[t] += v;
+    }
+    for (uint32_t t = 0; t < nt; ++t)
+        if (vec[t] * 16 > EMURX_SMALL_LDS) return false;
+    return true;
+}
+
 int ingest_submit(emurx_t* h, uint32_t slot, const emurx_msg* msgs, uint32_t nmsg) {
     IngestSlot& s = h->ing[slot];
     if (s.pending || (nmsg && (!msgs || !s.h_buf.p))) return EMURX_EINVAL;
@@ -509,10 +540,32 @@ int ingest_submit(emurx_t* h, uint32_t slot, const emurx_msg* msgs, uint32_t nms
         return EMURX_ENOMEM;
     hipStream_t st = s.st;
     if ((rc = prepare_read(h, st))) return rc;  // table deltas ordered against every reader
+    // the pipeline's histogram shards start zeroed (k_qscan leaves them zero)
+    if (fresh_hist && !EMURX_HIP_OK(hipMemsetAsync(s.d_hist.p, 0, hw * sizeof(uint64_t), st))) return EMURX_EDEVICE;
+    if (h->ingest_small && small_fits(ctl, nmsg, n)) {
+        // one launch: control words and messages read from the pinned buffers, every result
+        // written into the pinned result buffers (no copies)
+        if (!s.d_ticket.p) {
+            if (s.d_qseg.alloc((size_t)EMURX_SMALL_TILES * EMURX_NUM_QUEUES * EMURX_QUEUE_TILE) ||
+                s.d_tcnt.alloc((size_t)EMURX_SMALL_TILES * 16) || s.d_hsmall.alloc(2 * EMURX_HIST_BINS) ||
+                s.d_ticket.alloc(1))
+                return EMURX_ENOMEM;
+            if (!EMURX_HIP_OK(hipMemsetAsync(s.d_hsmall.p, 0, 2 * EMURX_HIST_BINS * sizeof(uint64_t), st)) ||
+                !EMURX_HIP_OK(hipMemsetAsync(s.d_ticket.p, 0, sizeof(uint32_t), st)))
+                return EMURX_EDEVICE;
+        }
+        if (emurx_launch_ingest_small(s.h_buf.p, ctl, nmsg, n, h->tables(), s.h_rec.p, s.h_desc.p, s.h_qlist.p,
+                                      s.h_stat.p, s.h_qoff.p, s.h_hist.p, s.d_qseg.p, s.d_tcnt.p, s.d_hsmall.p,
+                                      s.d_ticket.p, st) ||
+            !EMURX_HIP_OK(hipEventRecord(s.done, st)))
+            return EMURX_EDEVICE;
+        s.pending = true;
+        s.nmsg = nmsg;
+        s.slots = n;
+        return EMURX_OK;
+    }
     const auto H2D = hipMemcpyHostToDevice, D2H = hipMemcpyDeviceToHost;
-    bool ok = true;
-    if (fresh_hist) ok = ok && EMURX_HIP_OK(hipMemsetAsync(s.d_hist.p, 0, hw * sizeof(uint64_t), st));
-    ok = ok && EMURX_HIP_OK(hipMemcpyAsync(s.d_ctl.p, ctl, ((size_t)3 * nmsg + 1) * 4, H2D, st));
+    bool ok = EMURX_HIP_OK(hipMemcpyAsync(s.d_ctl.p, ctl, ((size_t)3 * nmsg + 1) * 4, H2D, st));
     if (end) ok = ok && EMURX_HIP_OK(hipMemcpyAsync(s.d_buf.p, s.h_buf.p, end, H2D, st));
     if (!ok) return EMURX_EDEVICE;
     if (emurx_launch_zmq_walk(s.d_buf.p, s.d_ctl.p, nmsg, s.d_desc.p, s.d_stat.p, st)) return EMURX_EDEVICE;
@@ -636,6 +689,7 @@ int emurx_open(const emurx_cfg* cfg, emurx_t** out) {
     if (rc) { delete h; return rc; }
     if (!EMURX_HIP_OK(hipStreamCreate(&h->stream))) { delete h; return EMURX_EDEVICE; }
     if (const char* e = getenv("EMURX_STAGE")) h->stage_mode = !strcmp(e, "wide") ? 1 : !strcmp(e, "narrow") ? 2 : 0;
+    if (const char* e = getenv("EMURX_INGEST_SMALL")) h->ingest_small = strcmp(e, "0") != 0;
     if (h->stage_fb.alloc(256) || h->d_stage_fb.alloc(256) ||
         !EMURX_HIP_OK(hipEventCreateWithFlags(&h->stage_ev, hipEventDisableTiming)) ||
         !EMURX_HIP_OK(hipEventCreateWithFlags(&h->ship_ev, hipEventDisableTiming)) ||

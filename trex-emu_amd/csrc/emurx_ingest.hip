@@ -184,6 +184,253 @@ __global__ __launch_bounds__(kBlock) void k_qpack(const uint32_t* __restrict__ q
     }
 }
 
+// ---- small batches: the whole ingest in ONE launch (emurx_ingest_submit's latency path) --------
+// For a batch of at most kSmallTiles tiles whose every tile's messages fit kSmallLds bytes of
+// LDS, one launch replaces the two H2D copies, the four kernels and the six D2H copies of the
+// pipeline above: the kernel reads the control words and the messages straight from the slot's
+// pinned host buffers and writes every result straight into the slot's pinned result buffers.
+// Workgroup t owns descriptor slots [256 t, 256 t + 256):
+//   1. the messages with slots in the tile (and those whose status word the tile writes) are
+//      copied host -> LDS (16-byte loads, all in flight), each at an LDS offset congruent to
+//      its buffer offset mod 16;
+//   2. one lane per message walks it in LDS exactly as k_zmq_walk does (owner keys included),
+//      keeping the descriptors of the tile's slots;
+//   3. one lane per slot parses + classifies its frame from LDS (parse_flat / classify, as
+//      k_rx's staged path), writes its record and descriptor, ranks it in its queue (ballots);
+//      the tile's queue segments and counts go to device scratch with write-through stores;
+//   4. the workgroup that arrives last (one agent-scope atomic per workgroup, after a release
+//      fence; MI355X_MICROARCH.md's hand-off table, row 1) packs the queues in queue-major
+//      order, writes qoff and the folded histogram, and clears the scratch for the next batch.
+// The results are the pipeline's, slot for slot (tests/test_gpu_parity.py runs both paths).
+constexpr uint32_t kSmallLds = EMURX_SMALL_LDS;        // staged message bytes per tile
+constexpr uint32_t kSmallMsgs = EMURX_SMALL_MSGS;      // messages per batch
+struct SmallArgs {
+    const uint8_t* buf;          // pinned host: the slot's messages
+    const uint32_t* ctl;         // pinned host: emurx_msg[nmsg], slot_base[nmsg + 1]
+    uint32_t nmsg, n, nt;        // messages, descriptor slots, tiles
+    emurx_dev_tables T;
+    emurx_rec* rec;              // pinned host results
+    emurx_desc* desc;
+    uint32_t* qlist;
+    uint32_t* stat;
+    uint32_t* qoff;
+    unsigned long long* hist_out;
+    uint32_t* qseg;              // device scratch: [EMURX_SMALL_TILES][EMURX_NUM_QUEUES][256]
+    uint32_t* tcnt;              // [EMURX_SMALL_TILES][16]
+    unsigned long long* hist;    // [2 * EMURX_HIST_BINS], zero between batches
+    uint32_t* ticket;            // zero between batches
+};
+
+__device__ __forceinline__ void st_agent(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // write-through (sc1)
+}
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
+    return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// 4 bytes at an LDS byte index as a big-endian word (the staged message has 32 bytes of slack)
+__device__ __forceinline__ uint32_t lds_be32(const uint32_t* w, uint32_t a) {
+    return __builtin_bswap32(__builtin_amdgcn_alignbyte(w[(a >> 2) + 1], w[a >> 2], a & 3));
+}
+
+__global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t s_msg[kSmallLds / 4];
+    __shared__ uint32_t s_lo[kSmallMsgs + 1];   // LDS byte offset of each staged message (prefix)
+    __shared__ uint32_t s_vec[kSmallMsgs + 1];  // 16-byte vectors before each staged message (prefix)
+    __shared__ uint2 s_desc[kBlock];            // the tile's descriptors: LDS frame offset, len | vport | key
+    __shared__ uint32_t s_wcnt[kWaves][16];
+    __shared__ uint32_t s_hp[EMURX_HIST_BINS], s_hb[EMURX_HIST_BINS];
+    __shared__ uint32_t s_m0, s_m1, s_last;
+    const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / kWave, t = blockIdx.x;
+    const uint32_t* base = a.ctl + 2 * a.nmsg;
+    const uint32_t s0 = t * kBlock, s1 = s0 + kBlock;
+    if (tid == 0) { s_m0 = 0xffffffffu; s_m1 = 0; }
+    if (tid < 16) for (uint32_t w = 0; w < kWaves; ++w) s_wcnt[w][tid] = 0;
+    if (tid < EMURX_HIST_BINS) { s_hp[tid] = 0; s_hb[tid] = 0; }
+    s_desc[tid] = make_uint2(0, EMURX_DESC_HOLE << 24);
+    __syncthreads();
+    // 1. this tile's messages: slots overlapping [s0, s1), or the message's status word is ours
+    //    (tile min(base / 256, nt - 1)): a contiguous range, base being monotonic
+    const bool inm = tid < a.nmsg;
+    const uint32_t b0 = inm ? base[tid] : 0u, b1 = inm ? base[tid + 1] : 0u;
+    const bool mine = inm && ((b0 < s1 && b1 > s0) || min(b0 / kBlock, a.nt - 1) == t);
+    if (mine) { atomicMin(&s_m0, tid); atomicMax(&s_m1, tid); }
+    __syncthreads();
+    const uint32_t m0 = s_m0, nm = s_m0 == 0xffffffffu ? 0u : s_m1 - s_m0 + 1;
+    // staged layout: message k of the range at LDS byte s_lo[k] (+ its offset mod 16), its
+    // vectors [s_vec[k], s_vec[k + 1]) of the range's flat vector list
+    if (wv == 0) {
+        uint32_t vb = 0, nv = 0;
+        for (uint32_t c = 0; c < nm; c += kWave) {  // exclusive prefix over the range, 64 at a time
+            const uint32_t k = c + lane;
+            uint32_t v = 0;
+            if (k < nm) {
+                const uint2 mk = reinterpret_cast<const uint2*>(a.ctl)[m0 + k];
+                v = mk.y ? (((mk.x & 15u) + mk.y + 15u) >> 4) + 2u : 0u;  // + 32 B of slack
+            }
+            uint32_t incl = v;
+#pragma unroll
+            for (uint32_t o = 1; o < kWave; o <<= 1) {
+                const uint32_t up = (uint32_t)__shfl_up((int)incl, o);
+                if (lane >= o) incl += up;
+            }
+            if (k < nm) { s_vec[k] = vb + incl - v; s_lo[k] = (vb + incl - v) * 16; }
+            vb += (uint32_t)__shfl((int)incl, kWave - 1);
+            nv = vb;
+        }
+        if (lane == 0) { s_vec[nm] = nv; s_lo[nm] = nv * 16; }
+    }
+    __syncthreads();
+    // host -> LDS, every vector of the range's messages in flight before the barrier (a binary
+    // search over s_vec finds a vector's message)
+    const uint32_t nvec = min(s_vec[nm], kSmallLds / 16);  // the host admits only batches that fit
+    for (uint32_t v = tid; v < nvec; v += kBlock) {
+        uint32_t lo = 0, hi = nm;  // last k with s_vec[k] <= v
+        while (hi - lo > 1) {
+            const uint32_t md = (lo + hi) >> 1;
+            if (s_vec[md] <= v) lo = md; else hi = md;
+        }
+        const uint2 mk = reinterpret_cast<const uint2*>(a.ctl)[m0 + lo];
+        const uint32_t j = v - s_vec[lo];
+        const uint8_t* src = a.buf + (mk.x & ~15u) + 16u * j;
+        uint4 x = make_uint4(0, 0, 0, 0);
+        if (16u * j < (mk.x & 15u) + mk.y) x = *reinterpret_cast<const uint4*>(src);
+        reinterpret_cast<uint4*>(s_msg)[v] = x;
+    }
+    __syncthreads();
+    // 2. the walk of OnRxStream (veth_zmq.go:277-320), in LDS: one lane per message of the range
+    if (tid < nm) {
+        const uint32_t m = m0 + tid;
+        const uint2 mk = reinterpret_cast<const uint2*>(a.ctl)[m];
+        const uint32_t bm = base[m], slots = base[m + 1] - bm;
+        const uint32_t L0 = s_lo[tid] + (mk.x & 15u);  // LDS byte of message byte 0
+        const uint32_t blen = mk.y;
+        uint32_t found = 0, err = 0;
+        if (blen < 4) {
+            err = EMURX_MSG_PARSE_ERR;
+        } else {
+            uint32_t header = lds_be32(s_msg, L0);
+            if ((header >> 16) != EMURX_ZMQ_MAGIC) {
+                err = EMURX_MSG_PARSE_ERR;
+            } else {
+                const uint32_t pkts = header & 0xffff;
+                uint32_t of = 4;
+                for (uint32_t i = 0; i < pkts; ++i) {
+                    const uint32_t h4 = (of + 4) & 0xffff;
+                    if (blen < h4) { err = EMURX_MSG_PARSE_ERR; break; }
+                    if (h4 < of) { err = EMURX_MSG_PANIC; break; }
+                    header = lds_be32(s_msg, L0 + of);
+                    if ((header & 0xff000000u) != 0xAA000000u) { err = EMURX_MSG_PARSE_ERR; break; }
+                    const uint32_t vport = (header >> 16) & 0xff, plen = header & 0xffff;
+                    const uint32_t e = (of + 4 + plen) & 0xffff;
+                    if (blen < e) { err = EMURX_MSG_PARSE_ERR; break; }
+                    if (plen > EMURX_MAX_FRAME) { err = EMURX_MSG_PANIC; break; }
+                    if (e < h4) { err = EMURX_MSG_PANIC; break; }
+                    if (found >= slots) { err = EMURX_MSG_PANIC; break; }
+                    const uint32_t sl = bm + found;
+                    if (sl >= s0 && sl < s1) {
+                        uint32_t v0, v1;
+                        l2_vlans(plen, lds_be32(s_msg, L0 + h4 + 12), lds_be32(s_msg, L0 + h4 + 16), v0, v1);
+                        const uint32_t key = emurx_owner_key(emurx_tk_hash(vport, v0, v1));
+                        s_desc[sl - s0] = make_uint2(L0 + h4, plen | (vport << 16) | (key << 24));
+                        reinterpret_cast<uint2*>(a.desc)[sl] = make_uint2(mk.x + h4, plen | (vport << 16) | (key << 24));
+                    }
+                    ++found;
+                    of = e;
+                }
+            }
+        }
+        for (uint32_t k = max(bm + found, s0); k < min(bm + slots, s1); ++k)
+            reinterpret_cast<uint2*>(a.desc)[k] = make_uint2(0, EMURX_DESC_HOLE << 24);
+        if (min(bm / kBlock, a.nt - 1) == t) a.stat[m] = found | (err << 24);
+    }
+    __syncthreads();
+    // 3. one lane per slot: parse + classify from LDS, record, queue rank, histogram
+    const uint32_t sl = s0 + tid;
+    const uint2 dd = s_desc[tid];
+    const bool valid = sl < a.n && (dd.y >> 24) != EMURX_DESC_HOLE;
+    const uint32_t len = dd.y & 0xffff, vport = (dd.y >> 16) & 0xff;
+    Rec r;
+    r.dlen = 0;
+    if (valid) {
+        LdsSrc src{reinterpret_cast<const uint8_t*>(s_msg), s_msg, dd.x};
+        parse_flat(src, len, vport, a.T.cb_mask, r);
+        classify(src, len, a.T, r);
+    }
+    if (sl < a.n) {
+        uint4* o = reinterpret_cast<uint4*>(a.rec + sl);
+        o[0] = valid ? make_uint4(r.ns, r.cl, r.vlan0, r.vlan1) : make_uint4(EMURX_ID_NONE, EMURX_ID_NONE, 0, 0);
+        o[1] = valid ? make_uint4(r.vport | (r.l3 << 16), r.l4 | (r.l7 << 16), r.l7len | (r.nh << 16) | (r.proto << 24),
+                                  r.status | (r.flags << 8))
+                     : make_uint4(0, 0, (uint32_t)EMURX_CB_NONE << 24, EMURX_ST_HOLE);
+    }
+    const uint32_t q = valid ? (r.status == EMURX_ST_OK ? r.proto : EMURX_Q_DROP) : 0xffu;
+    if (valid) {
+        const uint32_t bin = EMURX_HIST_BIN(r.status, r.proto);
+        atomicAdd(&s_hp[bin], 1u);
+        atomicAdd(&s_hb[bin], len);
+    }
+    uint32_t rank = 0;
+    uint64_t left = __ballot(q != 0xffu);
+    while (left) {
+        const uint32_t lead = (uint32_t)__ffsll((long long)left) - 1;
+        const uint32_t qq = (uint32_t)__builtin_amdgcn_readlane((int)q, (int)lead);
+        const uint64_t m = __ballot(q == qq);
+        if (q == qq) rank = mbcnt(m);
+        if (lane == lead) s_wcnt[wv][qq] = (uint32_t)__popcll(m);
+        left &= ~m;
+    }
+    __syncthreads();
+    if (q != 0xffu) {
+        uint32_t pos = rank;
+        for (uint32_t w = 0; w < wv; ++w) pos += s_wcnt[w][q];
+        st_agent(a.qseg + ((size_t)t * EMURX_NUM_QUEUES + q) * kBlock + pos, sl);
+    }
+    if (tid < 16) st_agent(a.tcnt + t * 16 + tid, s_wcnt[0][tid] + s_wcnt[1][tid] + s_wcnt[2][tid] + s_wcnt[3][tid]);
+    if (tid < EMURX_HIST_BINS && s_hp[tid]) {
+        atomicAdd(&a.hist[2 * tid], (unsigned long long)s_hp[tid]);
+        atomicAdd(&a.hist[2 * tid + 1], (unsigned long long)s_hb[tid]);
+    }
+    // 4. arrival: the workgroup whose ticket is last packs every tile's queues.  Every wave's
+    // write-through stores have completed (vmcnt 0) before the barrier; then one lane releases
+    // and takes a ticket (MI355X_MICROARCH.md, the hand-off table's first row)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        __atomic_thread_fence(__ATOMIC_RELEASE);  // every wave's stores are behind the barrier
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        s_last = atomicAdd(a.ticket, 1u) == a.nt - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    // queue-major offsets of every (queue, tile) segment; lane tid < 13 * nt owns one
+    __shared__ uint32_t s_cnt[EMURX_SMALL_TILES * EMURX_NUM_QUEUES], s_off[EMURX_SMALL_TILES * EMURX_NUM_QUEUES + 1];
+    const uint32_t nseg = a.nt * EMURX_NUM_QUEUES;  // segment k = (q = k / nt, t = k % nt)
+    for (uint32_t k = tid; k < nseg; k += kBlock) s_cnt[k] = ld_agent(a.tcnt + (k % a.nt) * 16 + k / a.nt);
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t at = 0;
+        for (uint32_t k = 0; k < nseg; ++k) {
+            if (k % a.nt == 0) a.qoff[k / a.nt] = at;
+            s_off[k] = at;
+            at += s_cnt[k];
+        }
+        a.qoff[EMURX_NUM_QUEUES] = at;
+    }
+    __syncthreads();
+    for (uint32_t k = wv; k < nseg; k += kWaves) {  // a wave per segment
+        const uint32_t c = s_cnt[k], qq = k / a.nt, tt = k % a.nt;
+        for (uint32_t j = lane; j < c; j += kWave)
+            a.qlist[s_off[k] + j] = ld_agent(a.qseg + ((size_t)tt * EMURX_NUM_QUEUES + qq) * kBlock + j);
+    }
+    if (tid < 2 * EMURX_HIST_BINS) {
+        unsigned long long* hp = a.hist + tid;
+        a.hist_out[tid] = __hip_atomic_load(hp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(hp, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (tid == 0) __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace emurx
 
 int emurx_launch_zmq_walk(const uint8_t* buf, const uint32_t* ctl, uint32_t nmsg, emurx_desc* desc,
@@ -194,6 +441,19 @@ int emurx_launch_zmq_walk(const uint8_t* buf, const uint32_t* ctl, uint32_t nmsg
                                      nmsg, desc, msg_stat))
                ? 0
                : -1;
+}
+
+int emurx_launch_ingest_small(const uint8_t* h_buf, const uint32_t* h_ctl, uint32_t nmsg, uint32_t n,
+                              const emurx_dev_tables& T, emurx_rec* h_rec, emurx_desc* h_desc, uint32_t* h_qlist,
+                              uint32_t* h_stat, uint32_t* h_qoff, uint64_t* h_hist, uint32_t* d_qseg, uint32_t* d_tcnt,
+                              uint64_t* d_hist, uint32_t* d_ticket, hipStream_t st) {
+    using namespace emurx;
+    const uint32_t nt = std::max<uint32_t>((n + kBlock - 1) / kBlock, 1);
+    if (nt > EMURX_SMALL_TILES || nmsg > kSmallMsgs) return -1;
+    const SmallArgs args{h_buf, h_ctl, nmsg, n, nt, T, h_rec, h_desc, h_qlist, h_stat, h_qoff,
+                         reinterpret_cast<unsigned long long*>(h_hist), d_qseg, d_tcnt,
+                         reinterpret_cast<unsigned long long*>(d_hist), d_ticket};
+    return EMURX_HIP_OK(emurx_launch(k_ingest_small, dim3(nt), dim3(kBlock), 0, st, args)) ? 0 : -1;
 }
 
 int emurx_launch_queue_pack(const uint32_t* qlist, uint32_t qcap, const uint32_t* tile_cnt, uint32_t n,
