@@ -730,7 +730,7 @@ def test_ingest_small_batches(rxmod, small, monkeypatch):
         msgs = []
         for j in range(nm):
             per = int(rng.integers(1, 65))
-            msgs.append(F.zmq_pack(frames[k:k + per], list(w["desc"]["vport"][k:k + per])))
+            msgs.append(F.zmq_pack(frames[k:k + per], [int(v) for v in w["desc"]["vport"][k:k + per]]))
             k = (k + per) % (len(frames) - 64)
         msgs += test_abi._rand_msgs(rng, 4)[:4] + [b""]
         msgs = [msgs[i] for i in rng.permutation(len(msgs))]
