@@ -445,14 +445,20 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         rb = X.LOOKUP_BYTES if mode == "partitioned" else X.REC_BYTES
         xch = dict(cap=X.capacity(n, world, slack=1.06), ev=[], timing=False, k=0, rb=rb)
 
-        # two buffer sets when the timed steps overlap batch k's exchange with batch k+1's parse
+        # two buffer sets when the timed steps overlap batch k's exchange with batch k+1's parse,
+        # each on its own compute stream (as the N = 1 pipelined steps): batch k+1's parse runs
+        # beside batch k's all-to-all AND beside batch k-1's owner lookups
         nsets = 2 if world > 1 and not a.no_overlap else 1
+        side = torch.cuda.Stream(dev) if nsets > 1 else None
 
         def alloc_regions():
             xch["sets"] = []
-            for _ in range(nsets):
+            for j in range(nsets):
                 b = dict(send=torch.empty(world * xch["cap"] * rb, dtype=torch.uint8, device=dev),
-                         send_count=torch.zeros(world, dtype=torch.int32, device=dev), pending=None)
+                         send_count=torch.zeros(world, dtype=torch.int32, device=dev), pending=None,
+                         st=stream if j == 0 else side, ev=None)
+                # set 0 writes the handle's record / queue buffers (the sanity checks read them)
+                b["rec"], b["qlist"], b["tile_cnt"] = (rec, qlist, tile_cnt) if j == 0 else outputs()
                 if mode == "partitioned":
                     b["out"] = torch.empty(world * xch["cap"] * X.REC_BYTES, dtype=torch.uint8, device=dev)
                 xch["sets"].append(b)
@@ -465,18 +471,19 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             fb, fd = inputs[k % R]
             if mode == "replicated":
                 # classify + route in one call: the route's owner counts are taken inside k_rx
-                rx.classify_route_dev(fb, fd, n, rec, qlist, qcap, tile_cnt, hist, world, rank, xch["cap"],
-                                      b["send"], b["send_count"], stream=stream)
+                rx.classify_route_dev(fb, fd, n, b["rec"], b["qlist"], qcap, b["tile_cnt"], hist, world, rank,
+                                      xch["cap"], b["send"], b["send_count"], stream=b["st"])
             else:
                 # no source records: every frame's lookup record carries its parse to the owner
-                rx.parse_route_dev(fb, fd, n, None, qlist, qcap, tile_cnt, hist, world, rank, xch["cap"],
-                                   b["send"], b["send_count"], stream=stream)
+                rx.parse_route_dev(fb, fd, n, None, b["qlist"], qcap, b["tile_cnt"], hist, world, rank, xch["cap"],
+                                   b["send"], b["send_count"], stream=b["st"])
 
         def consume(b):
-            xch["recv"], xch["recv_count"] = X.exchange_finish(b["pending"])
+            with torch.cuda.stream(b["st"]):  # the set's stream waits for its all-to-all
+                xch["recv"], xch["recv_count"] = X.exchange_finish(b["pending"])
             b["pending"] = None
             if mode == "partitioned":
-                rx.lookup_dev(xch["recv"], xch["recv_count"], world, xch["cap"], b["out"], stream=stream)
+                rx.lookup_dev(xch["recv"], xch["recv_count"], world, xch["cap"], b["out"], stream=b["st"])
             if xch.get("dump") is not None:  # --dump-exchange: this step's owner records, as they are now
                 torch.cuda.synchronize()
                 cnt = xch["recv_count"].cpu().numpy().astype(np.int64)
@@ -486,28 +493,35 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
                     [res[sr, : min(int(cnt[sr]), xch["cap"]) * X.REC_BYTES] for sr in range(world)])))
 
         def step_overlapped():
-            """Batch k: parse + pack, then its all-to-all starts on the collective stream while
-            the previous batch's owner lookups (behind its own all-to-all) and the next batch's
-            parse queue up on this stream."""
+            """Batch k on set k mod 2's stream: parse + pack, then its all-to-all starts on the
+            collective stream (behind that parse); then the previous batch's owner lookups are
+            queued on ITS stream behind its own all-to-all.  So batch k's parse, batch k-1's
+            transfer and batch k-2's lookups overlap.  Events time a batch from its parse to its
+            lookups' end, on its stream."""
             k = xch["k"]
             xch["k"] += 1
             b, prev = xch["sets"][k % 2], xch["sets"][(k + 1) % 2]
-            ev = None
             if xch["timing"] and k % a.time_stride == 0 and xch["pool"]:
-                ev = xch["pool"].pop()
-                ev[0].record(stream)
+                b["ev"] = xch["pool"].pop()
+                b["ev"][0].record(b["st"])
             produce(b, k)
-            b["pending"] = X.exchange_start(b["send"], b["send_count"], xch["cap"], rec_bytes=rb)
+            with torch.cuda.stream(b["st"]):  # the collective waits for this set's stream
+                b["pending"] = X.exchange_start(b["send"], b["send_count"], xch["cap"], rec_bytes=rb)
             if prev["pending"] is not None:
                 consume(prev)
-            if ev is not None:
-                ev[1].record(stream)
-                xch["ev"].append(ev)
+                if prev["ev"] is not None:
+                    prev["ev"][1].record(prev["st"])
+                    xch["ev"].append(prev["ev"])
+                    prev["ev"] = None
 
         def drain():
-            for b in xch["sets"]:
+            for b in sorted(xch["sets"], key=lambda x: x.get("k", 0)):
                 if b["pending"] is not None:
                     consume(b)
+                    if b["ev"] is not None:
+                        b["ev"][1].record(b["st"])
+                        xch["ev"].append(b["ev"])
+                        b["ev"] = None
 
     kk = [0]
 
