@@ -71,6 +71,11 @@ __device__ __forceinline__ uint2 load_desc(const emurx_desc* __restrict__ desc, 
     return i < n ? *reinterpret_cast<const uint2*>(desc + i) : make_uint2(0, EMURX_DESC_HOLE << 24);
 }
 
+// EMURX_WIN_NT (build variant, A/B): non-temporal window loads (with EMURX_WSKIP the
+// cooperative pass reads no window byte again)
+#ifndef EMURX_WIN_NT
+#define EMURX_WIN_NT 0
+#endif
 // The wave's staging of its 64 frames into its slab (wslab: the wave's kStage bytes):
 // the byte range [lo, hi) of the wave's frames copied HBM -> LDS by LDS-DMA
 // (global_load_lds_dwordx4, no VGPR round trip) when it fits the slab, else a window of each
@@ -106,7 +111,7 @@ __device__ __forceinline__ Stage stage_issue(const uint8_t* __restrict__ frames,
         const uint32_t nv = valid ? (uint32_t)(((fa & 15) + len + 15) >> 4) : 0;  // vectors of the frame
 #pragma unroll
         for (uint32_t k = 0; k < kWinVec; ++k)
-            if (k < nv) glds16<false>(src + k, wslab + k * kWave);  // the span past it is read again
+            if (k < nv) glds16<EMURX_WIN_NT != 0>(src + k, wslab + k * kWave);  // the span past it is read again
     }
     return sg;
 }

@@ -305,13 +305,26 @@ template <class S>
 __device__ __forceinline__ bool csum_l4(const S& s, Rec& r, uint32_t at, uint32_t n, uint32_t pcs, uint32_t fail_st) {
     return csum(s, at, n, pcs);
 }
+// EMURX_WSKIP (build variant, A/B): the span's bytes inside the window are summed from LDS
+// here and folded into the deferred pseudo sum (the byte-pair sum is linear mod 0xffff, and
+// be_domain with the span's own start parity orients both parts alike), so the cooperative
+// pass reads only the bytes past the window: every span byte crosses HBM once
+#ifndef EMURX_WSKIP
+#define EMURX_WSKIP 0
+#endif
 template <>
 __device__ __forceinline__ bool csum_l4<WinSrc>(const WinSrc& s, Rec& r, uint32_t at, uint32_t n, uint32_t pcs,
                                                 uint32_t fail_st) {
     if (at + n <= s.wlim || n == 0) return csum(s, at, n, pcs);
-    r.dstart = at;
-    r.dlen = n;
-    r.dpcs = pcs;
+    uint32_t st = at, pw = pcs;
+    if (EMURX_WSKIP && at < s.wlim) {
+        const uint32_t tw = dword_sum(WinDw{s.b32 + (s.wbase >> 2)}, s.head + at, s.wlim - at);
+        pw = pcs + be_domain(tw, s.at(at));  // tw == 0 leaves pcs as it was (Go's all-zero case)
+        st = s.wlim;
+    }
+    r.dstart = st;
+    r.dlen = at + n - st;
+    r.dpcs = pw;
     r.dfail = fail_st | ((s.at(at) & 1u) << 16);  // the span's start parity (csum_ok's a_start)
     return true;
 }
@@ -705,6 +718,9 @@ __device__ __forceinline__ uint32_t dpp_row_sum(uint32_t v) {
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);  // row_shr:8
     return v;  // lane 15 of each row: the row's total
 }
+#ifndef EMURX_COOP_NT
+#define EMURX_COOP_NT 0
+#endif
 __device__ __forceinline__ void coop_checksum_rows(Rec& r, const uint8_t* f, uint32_t* wsum) {
     constexpr uint32_t kRound = 16 * kCoopVec;  // vectors of one span per row round
     const uint32_t lane = lane_id(), l16 = lane & 15, row = lane >> 4;
@@ -745,7 +761,16 @@ __device__ __forceinline__ void coop_checksum_rows(Rec& r, const uint8_t* f, uin
 #pragma unroll
         for (uint32_t k = 0; k < kCoopVec; ++k) {
             const uint32_t v = c * kRound + k * 16 + l16;
+#if EMURX_COOP_NT  // build variant (A/B): the span bytes are read once, never again
+            if (v < nvj) {
+                const emurx_v4u y = __builtin_nontemporal_load((const __attribute__((address_space(1))) emurx_v4u*)(src + 16 * v));
+                x[k] = make_uint4(y.x, y.y, y.z, y.w);
+            } else {
+                x[k] = make_uint4(0, 0, 0, 0);
+            }
+#else
             x[k] = v < nvj ? gld16(src + 16 * v) : make_uint4(0, 0, 0, 0);
+#endif
         }
         uint32_t part = 0;
 #pragma unroll
