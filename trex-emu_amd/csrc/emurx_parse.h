@@ -1257,13 +1257,117 @@ __device__ __forceinline__ void resolve_done(const emurx_dev_tables& T, Rec& r, 
     }
 }
 
+// The same outcome as resolve_done with far fewer divergent branches (EMURX_FLATRES, build
+// variant for A/B): every table kind's answer from the first buckets by straight-line selects
+// (the client bucket read as MAC, IPv4 and IPv6 slots at once: the lane's key kind picks one),
+// probe chains past the first bucket behind one wave-uniform test (the sparse tables make them
+// rare), the rule's outcome by selects, and the rules that read memory again (GetFirstClient,
+// the EUI-64 RA-prefix check, the transport flow) behind wave-uniform "any lane" tests.  The
+// divergent switch over key kinds in resolve_done costs its wave exec-mask bookkeeping for
+// every kind present, which mixed traffic (config C) pays on every wave.
+#ifndef EMURX_FLATRES
+#define EMURX_FLATRES 0
+#endif
+__device__ __forceinline__ bool any_lane(bool c) { return __ballot(c) != 0; }
+template <class Flow>
+__device__ __forceinline__ void resolve_done_flat(const emurx_dev_tables& T, Rec& r, const LKey& k, const Probe& p,
+                                                  const Bucket& ce, Flow flow) {
+    const uint32_t cb = r.proto, plug = cb_plugin(cb), key = k.key;
+    const uint32_t w0 = r.vport, w1 = r.vlan0, w2 = r.vlan1;
+    // ---- first buckets, every view at once ----
+    uint2 nsr = make_uint2(EMURX_ID_NONE, 0), mc = make_uint2(EMURX_ID_NONE, 0);
+    IpHit i4{EMURX_ID_NONE, 0, 0}, i6{EMURX_ID_NONE, 0, 0};
+    bool nhole = false, mhole = false, h4 = false, h6 = false;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint4 x = p.ne.s[j];
+        nhole |= x.w == EMURX_EMPTY;
+        if (x.w != EMURX_EMPTY && (x.x & 0xffffu) == w0 && x.y == w1 && x.z == w2) nsr = make_uint2(x.w, x.x >> 16);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // the client views compare the Namespace id found above
+        const uint4 y = ce.s[j];
+        mhole |= y.w == EMURX_EMPTY;
+        if (y.w != EMURX_EMPTY && y.x == nsr.x && y.y == p.mlo && (y.z & 0xffffu) == p.mhi) mc = make_uint2(y.w, y.z >> 16);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const uint4 x = ce.s[2 * j], y = ce.s[2 * j + 1];
+        h4 |= y.w == EMURX_EMPTY;
+        h6 |= y.w == EMURX_EMPTY;
+        if (y.w != EMURX_EMPTY && x.x == nsr.x && x.y == k.kw[0]) i4 = IpHit{y.w, x.z, x.w};
+        if (y.w != EMURX_EMPTY && x.x == nsr.x && x.y == k.kw[0] && x.z == k.kw[1] && x.w == k.kw[2] && y.x == k.kw[3])
+            i6 = IpHit{y.w, y.y, y.z};
+    }
+    const bool isMac = key == kMac || key == kEui, isIp4 = key == kIp4, isIp6 = key == kIp6;
+    // ---- chains past the first buckets (wave-uniform test; the loop resolvers walk on) ----
+    const bool ns_more = nsr.x == EMURX_ID_NONE && !nhole;
+    if (any_lane(ns_more) && ns_more) {
+        const uint32_t b = (p.nb + 1) & T.ns_mask;
+        nsr = resolve_ns(T, b, ld_bucket(T.ns_tab, b), w0, w1, w2);
+    }
+    const uint32_t ns = nsr.x;
+    // the client probe needs the Namespace id: a lane whose Namespace came from its chain, or
+    // whose client key lies past the first bucket, resolves its client from the start again
+    const bool c_more = ns != EMURX_ID_NONE && (nsr.y & (1u << plug)) &&
+                        (ns_more || (isMac && mc.x == EMURX_ID_NONE && !mhole) ||
+                         (isIp4 && i4.cid == EMURX_ID_NONE && !h4) || (isIp6 && i6.cid == EMURX_ID_NONE && !h6));
+    if (any_lane(c_more) && c_more) {
+        if (isMac) mc = resolve_mac(T, p.cbk, ce, ns, p.mlo, p.mhi);
+        else if (isIp4) i4 = resolve_ip4(T, p.cbk, ce, ns, k.kw[0]);
+        else if (isIp6) i6 = resolve_ip6(T, p.cbk, ce, ns, k.kw);
+    }
+    // ---- the rule's client, by selects ----
+    uint32_t cid = EMURX_ID_NONE, cpl = 0, clo = 0, chi = 0;
+    bool check = true;
+    if (isMac) { cid = mc.x; cpl = mc.y; clo = p.mlo; chi = p.mhi; }
+    if (isIp4) { cid = i4.cid; cpl = i4.mhip >> 16; clo = i4.mlo; chi = i4.mhip & 0xffffu; }
+    if (isIp6) { cid = i6.cid; clo = i6.mlo; chi = i6.mhip & 0xffffu; }
+    const bool icmp4 = isIp4 && cb != EMURX_CB_ARP;
+    if (icmp4 && !(clo == k.dlo && chi == k.dhi)) cid = EMURX_ID_NONE;  // IsUnicastToMe
+    check = !(icmp4 || key == kEui || isIp6);
+    const bool ns_ok = ns != EMURX_ID_NONE && (nsr.y & (1u << plug));
+    // GetFirstClient (dhcpsrv / eapol) and the EUI-64 RA-prefix check read client info
+    const bool first = ns_ok && key == kFirst;
+    const bool eui = ns_ok && key == kEui && cid != EMURX_ID_NONE && !(k.kw[0] == 0x000080feu && k.kw[1] == 0);
+    if (any_lane(first || eui)) {
+        if (first) cid = gld4(T.ns_info + 4 * ns + 1);
+        if (first || eui) {
+            const CInfo c = client_info(T, cid);
+            cpl = c.plugins;
+            if (eui && !((c.ra & 1u) && ((c.ra >> 8) & 0xff) == 64 && c.ra0 == k.kw[0] && c.ra1 == k.kw[1]))
+                cid = EMURX_ID_NONE;
+        }
+    }
+    if ((key == kEui || isIp6) && cid != EMURX_ID_NONE && (!(clo == k.dlo && chi == k.dhi) || k.mc6)) cid = EMURX_ID_NONE;
+    // ---- the outcome ----
+    uint32_t lk = cid == EMURX_ID_NONE ? EMURX_LK_NO_CLIENT
+                  : (check && !(cpl & (1u << plug))) ? EMURX_LK_CLIENT_NO_PLUGIN : EMURX_LK_CLIENT;
+    if (key == kNsLevel) lk = EMURX_LK_NS_LEVEL;
+    if (key == kNoClient) lk = EMURX_LK_NO_CLIENT;
+    if (!(nsr.y & (1u << plug))) lk = EMURX_LK_NS_NO_PLUGIN;
+    if (ns == EMURX_ID_NONE) lk = EMURX_LK_NO_NS;
+    if (ns != EMURX_ID_NONE) r.ns = ns;
+    const bool client_kind = ns_ok && key != kNsLevel && key != kNoClient;
+    if (client_kind && cid != EMURX_ID_NONE) r.cl = cid;
+    set_lk(r, lk);
+    // transport: the client's TransportCtx decides (plugin_transport.go:109-114, :73-80)
+    const bool trans = key == kMac && (cb == EMURX_CB_TCP || cb == EMURX_CB_UDP) && lk == EMURX_LK_CLIENT;
+    if (trans) r.flow = EMURX_FLOW_NO_CTX;
+    if (T.ft_on && any_lane(trans) && trans && (client_info(T, cid).ctx & 1u)) r.flow = flow(cid);
+}
+
 // GetNs + the callback's client rule against the tables (both bucket reads in flight together)
 template <class Flow>
 __device__ __forceinline__ void resolve(const emurx_dev_tables& T, Rec& r, const LKey& k, Flow flow) {
     const Probe p = probe_issue(T, r, k);
     Bucket ce{};
     if (p.ctab) ce = ld_bucket(p.ctab, p.cbk);
+#if EMURX_FLATRES
+    resolve_done_flat(T, r, k, p, ce, flow);
+#else
     resolve_done(T, r, k, p, ce, flow);
+#endif
 }
 
 // parse state -> Namespace / Client ids, lookup outcome, flow decision (replicated tables:
