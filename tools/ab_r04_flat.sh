@@ -1,6 +1,7 @@
 #!/bin/bash
-# Round-4 A/B of the flat resolver (EMURX_FLATRES=1, emurx_parse.h resolve_done_flat) against
-# the in-tree build: GPU parity of the variant first, then configs C / B / D (replicated)
+# Round-4 A/B of the flat resolver (EMURX_FLATRES=1, emurx_parse.h resolve_done_flat) and of it
+# with ballot-per-bit ranking (flatm: + EMURX_MATCHRANK=1, emurx_kernels.hip match_lanes) against
+# the in-tree build: GPU parity of flatm first, then configs C / B / D (replicated)
 # interleaved on one box, then SQ instruction counts of k_rx on config C for both.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -8,13 +9,13 @@ export TMPDIR=/tmp
 out=gpurun_out/ab4f
 mkdir -p $out
 L=$PWD/trex-emu_amd/lib
-EMURX_LIB=$L/libemurx_flat.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_tables.py \
+EMURX_LIB=$L/libemurx_flatm.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_tables.py \
   -m gpu -x -q -p no:cacheprovider --timeout 200 --timeout-method thread > $out/pytest_flat.log 2>&1
-rc=$?; echo "flat parity rc=$rc"; tail -n 3 $out/pytest_flat.log
+rc=$?; echo "flatm parity rc=$rc"; tail -n 3 $out/pytest_flat.log
 [ $rc -eq 0 ] || exit $rc
 for rep in 1 2; do
   for cfg in "C" "B" "D --tables none"; do
-    for v in default flat; do
+    for v in default flat flatm; do
       lib=$L/libemurx.so; [ $v != default ] && lib=$L/libemurx_$v.so
       tag=$(echo "$cfg" | tr -d ' -')_${v}_$rep
       EMURX_LIB=$lib timeout -k 10 300 python bench.py --config $cfg --steps 100 --warmup 10 --no-cpu-baseline \
@@ -23,7 +24,7 @@ for rep in 1 2; do
     done
   done
 done
-for v in default flat; do
+for v in default flat flatm; do
   lib=$L/libemurx.so; [ $v != default ] && lib=$L/libemurx_$v.so
   EMURX_LIB=$lib timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_BRANCH SQ_WAVE_CYCLES \
     -T --kernel-include-regex k_rx -d $out/sq_$v -o run --output-format csv \

@@ -124,6 +124,24 @@ __device__ __forceinline__ void stage_wait() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// EMURX_MATCHRANK (build variant, A/B): rank the lanes of a queue / an owner by one ballot
+// per bit of its id (the lanes holding the same id, as match_any) instead of one loop
+// iteration of scalar bookkeeping per distinct id present in the wave
+#ifndef EMURX_MATCHRANK
+#define EMURX_MATCHRANK 0
+#endif
+template <int kBits>
+__device__ __forceinline__ uint64_t match_lanes(uint32_t v, uint64_t act) {
+    uint64_t m = act;
+#pragma unroll
+    for (int b = 0; b < kBits; ++b) {
+        const bool bit = (v >> b) & 1u;
+        const uint64_t x = __ballot(bit);
+        m &= bit ? x : ~x;
+    }
+    return m;
+}
+
 // The workgroup's small LDS arrays of one tile
 struct TileLds {
     uint32_t wcnt[kWaves][16];                   // queue counts per wave
@@ -218,6 +236,13 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
     const uint32_t q = valid ? (r.status == EMURX_ST_OK ? r.proto : EMURX_Q_DROP) : 0xffu;
     // rank inside (wave, queue): one ballot per distinct queue present in the wave
     uint32_t rank = 0;
+#if EMURX_MATCHRANK
+    {
+        const uint64_t m = match_lanes<4>(q, __ballot(valid));
+        rank = mbcnt(m);
+        if (valid && rank == 0) L.wcnt[wv][q] = (uint32_t)__popcll(m);
+    }
+#else
     uint64_t left = __ballot(valid);
     while (left) {
         const uint32_t lead = (uint32_t)__ffsll((long long)left) - 1;
@@ -227,6 +252,7 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
         if (lane == lead) L.wcnt[wv][qq] = (uint32_t)__popcll(m);
         left &= ~m;
     }
+#endif
     STAMP(5);
     STAMP(6);
     typedef unsigned v4u __attribute__((ext_vector_type(4)));
@@ -277,6 +303,11 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
     // ranked by ballots like the queues
     uint32_t rrank = 0;
     if ((kKind == 1 && rt.cnt) || kKind == 2) {
+#if EMURX_MATCHRANK
+        const uint64_t m = match_lanes<3>(rd, __ballot(rd != 0xffu));
+        rrank = mbcnt(m);
+        if (rd != 0xffu && rrank == 0) L.rcnt[wv][rd] = (uint32_t)__popcll(m);
+#else
         uint64_t rl = __ballot(rd != 0xffu);
         while (rl) {
             const uint32_t lead = (uint32_t)__ffsll((long long)rl) - 1;
@@ -286,6 +317,7 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
             if (lane == lead) L.rcnt[wv][dd2] = (uint32_t)__popcll(m);
             rl &= ~m;
         }
+#endif
     }
     STAMP(7);
     __syncthreads();
