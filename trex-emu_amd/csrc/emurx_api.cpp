@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <array>
 #include <cstdio>
 #include <cstdlib>
@@ -95,10 +97,13 @@ struct IngestSlot {
     // the fused small-batch path's scratch (k_ingest_small), zero between batches
     DevBuf<uint32_t> d_qseg, d_tcnt, d_ticket;
     DevBuf<uint64_t> d_hsmall;
+    PinBuf<uint32_t> h_done;  // the small path's completion word: the batch's seq, written last
+    uint32_t seq = 0;
+    bool small = false;       // the batch in flight took the small path
     std::vector<uint32_t> remap;          // slot -> frame index, only when a message fell short
     void release() {
         if (st) (void)hipStreamSynchronize(st);
-        d_qseg.release(); d_tcnt.release(); d_ticket.release(); d_hsmall.release();
+        d_qseg.release(); d_tcnt.release(); d_ticket.release(); d_hsmall.release(); h_done.release();
         h_buf.release(); h_ctl.release(); h_stat.release(); h_qlist.release(); h_qoff.release();
         h_mframes.release(); h_mstatus.release(); h_rec.release(); h_desc.release(); h_hist.release();
         d_buf.release(); d_ctl.release(); d_stat.release(); d_qlist.release(); d_tile_cnt.release();
@@ -548,17 +553,20 @@ int ingest_submit(emurx_t* h, uint32_t slot, const emurx_msg* msgs, uint32_t nms
         if (!s.d_ticket.p) {
             if (s.d_qseg.alloc((size_t)EMURX_SMALL_TILES * EMURX_NUM_QUEUES * EMURX_QUEUE_TILE) ||
                 s.d_tcnt.alloc((size_t)EMURX_SMALL_TILES * 16) || s.d_hsmall.alloc(2 * EMURX_HIST_BINS) ||
-                s.d_ticket.alloc(1))
+                s.h_done.alloc(1) || s.d_ticket.alloc(1))
                 return EMURX_ENOMEM;
+            *(volatile uint32_t*)s.h_done.p = s.seq;
             if (!EMURX_HIP_OK(hipMemsetAsync(s.d_hsmall.p, 0, 2 * EMURX_HIST_BINS * sizeof(uint64_t), st)) ||
                 !EMURX_HIP_OK(hipMemsetAsync(s.d_ticket.p, 0, sizeof(uint32_t), st)))
                 return EMURX_EDEVICE;
         }
         if (emurx_launch_ingest_small(s.h_buf.p, ctl, nmsg, n, h->tables(), s.h_rec.p, s.h_desc.p, s.h_qlist.p,
                                       s.h_stat.p, s.h_qoff.p, s.h_hist.p, s.d_qseg.p, s.d_tcnt.p, s.d_hsmall.p,
-                                      s.d_ticket.p, st) ||
+                                      s.d_ticket.p, s.h_done.p, s.seq + 1, st) ||
             !EMURX_HIP_OK(hipEventRecord(s.done, st)))
             return EMURX_EDEVICE;
+        ++s.seq;
+        s.small = true;
         s.pending = true;
         s.nmsg = nmsg;
         s.slots = n;
@@ -589,10 +597,29 @@ int ingest_submit(emurx_t* h, uint32_t slot, const emurx_msg* msgs, uint32_t nms
          EMURX_HIP_OK(hipMemcpyAsync(s.h_hist.p, s.d_hist_out.p, 2 * EMURX_HIST_BINS * 8, D2H, st)) &&
          EMURX_HIP_OK(hipEventRecord(s.done, st));
     if (!ok) return EMURX_EDEVICE;
+    s.small = false;
     s.pending = true;
     s.nmsg = nmsg;
     s.slots = n;
     return EMURX_OK;
+}
+
+// The small path's completion: spin on the pinned word k_ingest_small writes after every result
+// (a few microseconds sooner than the end-of-kernel signal hipEventSynchronize waits for).
+// Bounded: after 2 ms the caller waits on the event, which also reports a failed kernel.
+bool spin_done(const uint32_t* word, uint32_t seq) {
+    const volatile uint32_t* w = word;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t k = 1;; ++k) {
+        if (*w == seq) {
+            std::atomic_thread_fence(std::memory_order_acquire);
+            return true;
+        }
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+        if ((k & 255) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) return false;
+    }
 }
 
 int ingest_wait(emurx_t* h, uint32_t slot, emurx_ingest_result* res) {
@@ -601,7 +628,8 @@ int ingest_wait(emurx_t* h, uint32_t slot, emurx_ingest_result* res) {
     int rc = bind(h);
     if (rc) return rc;
     s.pending = false;
-    if (!EMURX_HIP_OK(hipEventSynchronize(s.done))) return EMURX_EDEVICE;
+    if (!(s.small && spin_done(s.h_done.p, s.seq)) && !EMURX_HIP_OK(hipEventSynchronize(s.done)))
+        return EMURX_EDEVICE;
     memset(res, 0, sizeof(*res));
     emurx_counters& d = res->delta;
     d.rx_batch = s.nmsg;  // one OnRxStream per message, veth_zmq.go:278

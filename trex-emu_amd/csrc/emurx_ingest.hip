@@ -219,6 +219,8 @@ struct SmallArgs {
     uint32_t* tcnt;              // [EMURX_SMALL_TILES][16]
     unsigned long long* hist;    // [2 * EMURX_HIST_BINS], zero between batches
     uint32_t* ticket;            // zero between batches
+    uint32_t* done;              // pinned host: the batch's sequence number, written last
+    uint32_t seq;
 };
 
 __device__ __forceinline__ void st_agent(uint32_t* p, uint32_t v) {
@@ -240,8 +242,10 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
     __shared__ uint32_t s_wcnt[kWaves][16];
     __shared__ uint32_t s_hp[EMURX_HIST_BINS], s_hb[EMURX_HIST_BINS];
     __shared__ uint32_t s_m0, s_m1, s_last;
+    __shared__ uint32_t s_ctl[3 * kSmallMsgs + 1];  // the control words, read from the host once
     const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / kWave, t = blockIdx.x;
-    const uint32_t* base = a.ctl + 2 * a.nmsg;
+    for (uint32_t k = tid; k < 3 * a.nmsg + 1; k += kBlock) s_ctl[k] = a.ctl[k];  // one bus round trip
+    const uint32_t* base = s_ctl + 2 * a.nmsg;
     const uint32_t s0 = t * kBlock, s1 = s0 + kBlock;
     if (tid == 0) { s_m0 = 0xffffffffu; s_m1 = 0; }
     if (tid < 16) for (uint32_t w = 0; w < kWaves; ++w) s_wcnt[w][tid] = 0;
@@ -264,7 +268,7 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
             const uint32_t k = c + lane;
             uint32_t v = 0;
             if (k < nm) {
-                const uint2 mk = reinterpret_cast<const uint2*>(a.ctl)[m0 + k];
+                const uint2 mk = make_uint2(s_ctl[2 * (m0 + k)], s_ctl[2 * (m0 + k) + 1]);
                 v = mk.y ? (((mk.x & 15u) + mk.y + 15u) >> 4) + 2u : 0u;  // + 32 B of slack
             }
             uint32_t incl = v;
@@ -289,7 +293,7 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
             const uint32_t md = (lo + hi) >> 1;
             if (s_vec[md] <= v) lo = md; else hi = md;
         }
-        const uint2 mk = reinterpret_cast<const uint2*>(a.ctl)[m0 + lo];
+        const uint2 mk = make_uint2(s_ctl[2 * (m0 + lo)], s_ctl[2 * (m0 + lo) + 1]);
         const uint32_t j = v - s_vec[lo];
         const uint8_t* src = a.buf + (mk.x & ~15u) + 16u * j;
         uint4 x = make_uint4(0, 0, 0, 0);
@@ -300,7 +304,7 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
     // 2. the walk of OnRxStream (veth_zmq.go:277-320), in LDS: one lane per message of the range
     if (tid < nm) {
         const uint32_t m = m0 + tid;
-        const uint2 mk = reinterpret_cast<const uint2*>(a.ctl)[m];
+        const uint2 mk = make_uint2(s_ctl[2 * m], s_ctl[2 * m + 1]);
         const uint32_t bm = base[m], slots = base[m + 1] - bm;
         const uint32_t L0 = s_lo[tid] + (mk.x & 15u);  // LDS byte of message byte 0
         const uint32_t blen = mk.y;
@@ -429,6 +433,16 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
         __hip_atomic_store(hp, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (tid == 0) __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // 5. the host's completion word, after every result store of this workgroup has completed
+    // and a system-scope release (the other workgroups' results are ordered before their
+    // tickets, which this one acquired): emurx_ingest_wait spins on it instead of waiting for
+    // the kernel's end-of-dispatch signal
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        __atomic_thread_fence(__ATOMIC_RELEASE);
+        __hip_atomic_store(a.done, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 }  // namespace emurx
@@ -446,13 +460,14 @@ int emurx_launch_zmq_walk(const uint8_t* buf, const uint32_t* ctl, uint32_t nmsg
 int emurx_launch_ingest_small(const uint8_t* h_buf, const uint32_t* h_ctl, uint32_t nmsg, uint32_t n,
                               const emurx_dev_tables& T, emurx_rec* h_rec, emurx_desc* h_desc, uint32_t* h_qlist,
                               uint32_t* h_stat, uint32_t* h_qoff, uint64_t* h_hist, uint32_t* d_qseg, uint32_t* d_tcnt,
-                              uint64_t* d_hist, uint32_t* d_ticket, hipStream_t st) {
+                              uint64_t* d_hist, uint32_t* d_ticket, uint32_t* h_done, uint32_t seq,
+                              hipStream_t st) {
     using namespace emurx;
     const uint32_t nt = std::max<uint32_t>((n + kBlock - 1) / kBlock, 1);
     if (nt > EMURX_SMALL_TILES || nmsg > kSmallMsgs) return -1;
     const SmallArgs args{h_buf, h_ctl, nmsg, n, nt, T, h_rec, h_desc, h_qlist, h_stat, h_qoff,
                          reinterpret_cast<unsigned long long*>(h_hist), d_qseg, d_tcnt,
-                         reinterpret_cast<unsigned long long*>(d_hist), d_ticket};
+                         reinterpret_cast<unsigned long long*>(d_hist), d_ticket, h_done, seq};
     return EMURX_HIP_OK(emurx_launch(k_ingest_small, dim3(nt), dim3(kBlock), 0, st, args)) ? 0 : -1;
 }
 

@@ -95,14 +95,16 @@ int emurx_launch_zmq_walk(const uint8_t* buf, const uint32_t* ctl, uint32_t nmsg
 // from pinned host memory, walk + parse + classify + queue packing, every result written into
 // pinned host memory (h_*: the layout of the pipeline's D2H copies).  Device scratch: d_qseg
 // [EMURX_SMALL_TILES * 13 * 256], d_tcnt [EMURX_SMALL_TILES * 16], d_hist [128] and d_ticket,
-// zero before the first launch (each launch leaves them zero).
+// zero before the first launch (each launch leaves them zero).  h_done (pinned host): seq is
+// written there after every result (the host may spin on it instead of the stream).
 #define EMURX_SMALL_TILES 16
 #define EMURX_SMALL_LDS 40960
 #define EMURX_SMALL_MSGS 256
 int emurx_launch_ingest_small(const uint8_t* h_buf, const uint32_t* h_ctl, uint32_t nmsg, uint32_t n,
                               const emurx_dev_tables& T, emurx_rec* h_rec, emurx_desc* h_desc, uint32_t* h_qlist,
                               uint32_t* h_stat, uint32_t* h_qoff, uint64_t* h_hist, uint32_t* d_qseg, uint32_t* d_tcnt,
-                              uint64_t* d_hist, uint32_t* d_ticket, hipStream_t st);
+                              uint64_t* d_hist, uint32_t* d_ticket, uint32_t* h_done, uint32_t seq,
+                              hipStream_t st);
 // Concatenate k_rx's per-tile queue segments (queue-major, frame order) into `packed`, write
 // qoff[EMURX_NUM_QUEUES + 1], fold the histogram shards into hist_out[2 * EMURX_HIST_BINS] and
 // clear the shards.  Scratch seg_off: [ceil(n / 256) * 16].  Two launches.
