@@ -154,6 +154,7 @@ struct emurx_ctx {
     // batched host ingest: EMURX_INGEST_SLOTS public slots + one private to emurx_rx_stream
     IngestSlot ing[EMURX_INGEST_SLOTS + 1];
     bool ingest_small = true;  // small batches in one launch (k_ingest_small); EMURX_INGEST_SMALL=0: never
+    bool ingest_spin = true;   // wait for them on their completion word; EMURX_INGEST_SPIN=0: on the event
 
     // tx ZMQ framing scratch (emurx_tx_zmq_dev): per-level chain transfer tables
     DevBuf<uint8_t> d_txz;
@@ -628,7 +629,7 @@ int ingest_wait(emurx_t* h, uint32_t slot, emurx_ingest_result* res) {
     int rc = bind(h);
     if (rc) return rc;
     s.pending = false;
-    if (!(s.small && spin_done(s.h_done.p, s.seq)) && !EMURX_HIP_OK(hipEventSynchronize(s.done)))
+    if (!(s.small && h->ingest_spin && spin_done(s.h_done.p, s.seq)) && !EMURX_HIP_OK(hipEventSynchronize(s.done)))
         return EMURX_EDEVICE;
     memset(res, 0, sizeof(*res));
     emurx_counters& d = res->delta;
@@ -718,6 +719,7 @@ int emurx_open(const emurx_cfg* cfg, emurx_t** out) {
     if (!EMURX_HIP_OK(hipStreamCreate(&h->stream))) { delete h; return EMURX_EDEVICE; }
     if (const char* e = getenv("EMURX_STAGE")) h->stage_mode = !strcmp(e, "wide") ? 1 : !strcmp(e, "narrow") ? 2 : 0;
     if (const char* e = getenv("EMURX_INGEST_SMALL")) h->ingest_small = strcmp(e, "0") != 0;
+    if (const char* e = getenv("EMURX_INGEST_SPIN")) h->ingest_spin = strcmp(e, "0") != 0;
     if (h->stage_fb.alloc(256) || h->d_stage_fb.alloc(256) ||
         !EMURX_HIP_OK(hipEventCreateWithFlags(&h->stage_ev, hipEventDisableTiming)) ||
         !EMURX_HIP_OK(hipEventCreateWithFlags(&h->ship_ev, hipEventDisableTiming)) ||

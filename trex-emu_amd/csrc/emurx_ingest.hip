@@ -223,6 +223,23 @@ struct SmallArgs {
     uint32_t seq;
 };
 
+// EMURX_SMALL_STAMP=1 (diagnostic build, tools/lat_probe.py): the wall clock (100 MHz) at the
+// phases of k_ingest_small, per workgroup, read back by emurx_debug_small_stamps
+#ifndef EMURX_SMALL_STAMP
+#define EMURX_SMALL_STAMP 0
+#endif
+#if EMURX_SMALL_STAMP
+__device__ unsigned long long g_small_stamp[EMURX_SMALL_TILES * 10];
+#define SSTAMP(k)                                                 \
+    do {                                                          \
+        if (tid == 0) g_small_stamp[t * 10 + (k)] = wall_clock64(); \
+    } while (0)
+#else
+#define SSTAMP(k) \
+    do {          \
+    } while (0)
+#endif
+
 __device__ __forceinline__ void st_agent(uint32_t* p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // write-through (sc1)
 }
@@ -238,7 +255,8 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t s_msg[kSmallLds / 4];
     __shared__ uint32_t s_lo[kSmallMsgs + 1];   // LDS byte offset of each staged message (prefix)
     __shared__ uint32_t s_vec[kSmallMsgs + 1];  // 16-byte vectors before each staged message (prefix)
-    __shared__ uint2 s_desc[kBlock];            // the tile's descriptors: LDS frame offset, len | vport | key
+    __shared__ uint2 s_desc[kBlock + 1];        // the tile's descriptors: LDS frame offset, len | vport | key
+    __shared__ uint32_t s_hoff[kBlock + 1];     // and their frames' offsets in the host buffer (+ a spare)
     __shared__ uint32_t s_wcnt[kWaves][16];
     __shared__ uint32_t s_hp[EMURX_HIST_BINS], s_hb[EMURX_HIST_BINS];
     __shared__ uint32_t s_m0, s_m1, s_last;
@@ -246,6 +264,7 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
     const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / kWave, t = blockIdx.x;
     for (uint32_t k = tid; k < 3 * a.nmsg + 1; k += kBlock) s_ctl[k] = a.ctl[k];  // one bus round trip
     const uint32_t* base = s_ctl + 2 * a.nmsg;
+    SSTAMP(0);
     const uint32_t s0 = t * kBlock, s1 = s0 + kBlock;
     if (tid == 0) { s_m0 = 0xffffffffu; s_m1 = 0; }
     if (tid < 16) for (uint32_t w = 0; w < kWaves; ++w) s_wcnt[w][tid] = 0;
@@ -259,6 +278,7 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
     const bool mine = inm && ((b0 < s1 && b1 > s0) || min(b0 / kBlock, a.nt - 1) == t);
     if (mine) { atomicMin(&s_m0, tid); atomicMax(&s_m1, tid); }
     __syncthreads();
+    SSTAMP(1);
     const uint32_t m0 = s_m0, nm = s_m0 == 0xffffffffu ? 0u : s_m1 - s_m0 + 1;
     // staged layout: message k of the range at LDS byte s_lo[k] (+ its offset mod 16), its
     // vectors [s_vec[k], s_vec[k + 1]) of the range's flat vector list
@@ -284,6 +304,7 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
         if (lane == 0) { s_vec[nm] = nv; s_lo[nm] = nv * 16; }
     }
     __syncthreads();
+    SSTAMP(2);
     // host -> LDS, every vector of the range's messages in flight before the barrier (a binary
     // search over s_vec finds a vector's message)
     const uint32_t nvec = min(s_vec[nm], kSmallLds / 16);  // the host admits only batches that fit
@@ -301,7 +322,11 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
         reinterpret_cast<uint4*>(s_msg)[v] = x;
     }
     __syncthreads();
+    SSTAMP(3);
     // 2. the walk of OnRxStream (veth_zmq.go:277-320), in LDS: one lane per message of the range
+    //    follows the offset chain alone (a frame's header word, the checks, its LDS offset and
+    //    host offset noted); the owner keys and the descriptor stores come after, one lane per
+    //    slot, off the serial chain
     if (tid < nm) {
         const uint32_t m = m0 + tid;
         const uint2 mk = make_uint2(s_ctl[2 * m], s_ctl[2 * m + 1]);
@@ -316,38 +341,54 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
             if ((header >> 16) != EMURX_ZMQ_MAGIC) {
                 err = EMURX_MSG_PARSE_ERR;
             } else {
+                // the chain step with one exit test: the loop's checks in OnRxStream's order
+                // become one select chain (a branch per check cost its exec-mask bookkeeping on
+                // every frame of this single-lane loop); the header word is read at a clamped
+                // offset, so the read stays inside the message before the checks reject it
                 const uint32_t pkts = header & 0xffff;
                 uint32_t of = 4;
-                for (uint32_t i = 0; i < pkts; ++i) {
+                for (; found < pkts; ++found) {
                     const uint32_t h4 = (of + 4) & 0xffff;
-                    if (blen < h4) { err = EMURX_MSG_PARSE_ERR; break; }
-                    if (h4 < of) { err = EMURX_MSG_PANIC; break; }
-                    header = lds_be32(s_msg, L0 + of);
-                    if ((header & 0xff000000u) != 0xAA000000u) { err = EMURX_MSG_PARSE_ERR; break; }
-                    const uint32_t vport = (header >> 16) & 0xff, plen = header & 0xffff;
+                    header = lds_be32(s_msg, L0 + min(of, blen));
+                    const uint32_t plen = header & 0xffff;
                     const uint32_t e = (of + 4 + plen) & 0xffff;
-                    if (blen < e) { err = EMURX_MSG_PARSE_ERR; break; }
-                    if (plen > EMURX_MAX_FRAME) { err = EMURX_MSG_PANIC; break; }
-                    if (e < h4) { err = EMURX_MSG_PANIC; break; }
-                    if (found >= slots) { err = EMURX_MSG_PANIC; break; }
-                    const uint32_t sl = bm + found;
-                    if (sl >= s0 && sl < s1) {
-                        uint32_t v0, v1;
-                        l2_vlans(plen, lds_be32(s_msg, L0 + h4 + 12), lds_be32(s_msg, L0 + h4 + 16), v0, v1);
-                        const uint32_t key = emurx_owner_key(emurx_tk_hash(vport, v0, v1));
-                        s_desc[sl - s0] = make_uint2(L0 + h4, plen | (vport << 16) | (key << 24));
-                        reinterpret_cast<uint2*>(a.desc)[sl] = make_uint2(mk.x + h4, plen | (vport << 16) | (key << 24));
-                    }
-                    ++found;
+                    // the first failing check decides: selects applied last-check-first
+                    uint32_t bad = found >= slots ? EMURX_MSG_PANIC : 0u;
+                    bad = e < h4 ? EMURX_MSG_PANIC : bad;
+                    bad = plen > EMURX_MAX_FRAME ? EMURX_MSG_PANIC : bad;
+                    bad = blen < e ? EMURX_MSG_PARSE_ERR : bad;
+                    bad = (header & 0xff000000u) != 0xAA000000u ? EMURX_MSG_PARSE_ERR : bad;
+                    bad = h4 < of ? EMURX_MSG_PANIC : bad;
+                    bad = blen < h4 ? EMURX_MSG_PARSE_ERR : bad;
+                    if (bad) { err = bad; break; }
+                    // slots of other tiles land in the spare entry past the tile's (no branch)
+                    const uint32_t sl = bm + found, k = sl >= s0 && sl < s1 ? sl - s0 : kBlock;
+                    s_desc[k] = make_uint2(L0 + h4, header & 0x00ffffffu);  // key byte: below
+                    s_hoff[k] = mk.x + h4;
                     of = e;
                 }
             }
         }
-        for (uint32_t k = max(bm + found, s0); k < min(bm + slots, s1); ++k)
-            reinterpret_cast<uint2*>(a.desc)[k] = make_uint2(0, EMURX_DESC_HOLE << 24);
         if (min(bm / kBlock, a.nt - 1) == t) a.stat[m] = found | (err << 24);
     }
     __syncthreads();
+    SSTAMP(4);
+    {  // one lane per slot of the tile: owner key, descriptor (holes stay holes)
+        const uint32_t sl = s0 + tid;
+        uint2 dd = s_desc[tid];
+        if ((dd.y >> 24) != EMURX_DESC_HOLE) {
+            const uint32_t plen = dd.y & 0xffff, vport = (dd.y >> 16) & 0xff;
+            uint32_t v0, v1;
+            l2_vlans(plen, lds_be32(s_msg, dd.x + 12), lds_be32(s_msg, dd.x + 16), v0, v1);
+            dd.y |= emurx_owner_key(emurx_tk_hash(vport, v0, v1)) << 24;
+            s_desc[tid] = dd;
+        }
+        if (sl < a.n)
+            reinterpret_cast<uint2*>(a.desc)[sl] =
+                (dd.y >> 24) != EMURX_DESC_HOLE ? make_uint2(s_hoff[tid], dd.y) : make_uint2(0, EMURX_DESC_HOLE << 24);
+    }
+    __syncthreads();
+    SSTAMP(5);
     // 3. one lane per slot: parse + classify from LDS, record, queue rank, histogram
     const uint32_t sl = s0 + tid;
     const uint2 dd = s_desc[tid];
@@ -360,6 +401,7 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
         parse_flat(src, len, vport, a.T.cb_mask, r);
         classify(src, len, a.T, r);
     }
+    SSTAMP(6);
     if (sl < a.n) {
         uint4* o = reinterpret_cast<uint4*>(a.rec + sl);
         o[0] = valid ? make_uint4(r.ns, r.cl, r.vlan0, r.vlan1) : make_uint4(EMURX_ID_NONE, EMURX_ID_NONE, 0, 0);
@@ -402,9 +444,10 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
     if (tid == 0) {
         __atomic_thread_fence(__ATOMIC_RELEASE);  // every wave's stores are behind the barrier
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        s_last = atomicAdd(a.ticket, 1u) == a.nt - 1;
+        s_last = a.nt == 1 || atomicAdd(a.ticket, 1u) == a.nt - 1;  // one tile: no ticket
     }
     __syncthreads();
+    SSTAMP(7);
     if (!s_last) return;
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
     // queue-major offsets of every (queue, tile) segment; lane tid < 13 * nt owns one
@@ -433,6 +476,7 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
         __hip_atomic_store(hp, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (tid == 0) __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    SSTAMP(8);
     // 5. the host's completion word, after every result store of this workgroup has completed
     // and a system-scope release (the other workgroups' results are ordered before their
     // tickets, which this one acquired): emurx_ingest_wait spins on it instead of waiting for
@@ -443,6 +487,7 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
         __atomic_thread_fence(__ATOMIC_RELEASE);
         __hip_atomic_store(a.done, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    SSTAMP(9);
 }
 
 }  // namespace emurx
@@ -470,6 +515,12 @@ int emurx_launch_ingest_small(const uint8_t* h_buf, const uint32_t* h_ctl, uint3
                          reinterpret_cast<unsigned long long*>(d_hist), d_ticket, h_done, seq};
     return EMURX_HIP_OK(emurx_launch(k_ingest_small, dim3(nt), dim3(kBlock), 0, st, args)) ? 0 : -1;
 }
+
+#if EMURX_SMALL_STAMP
+extern "C" int emurx_debug_small_stamps(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(emurx::g_small_stamp), sizeof(emurx::g_small_stamp)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 int emurx_launch_queue_pack(const uint32_t* qlist, uint32_t qcap, const uint32_t* tile_cnt, uint32_t n,
                             uint32_t* seg_off, uint32_t* packed, uint32_t* qoff, uint64_t* hist,
