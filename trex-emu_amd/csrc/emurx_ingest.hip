@@ -255,8 +255,9 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t s_msg[kSmallLds / 4];
     __shared__ uint32_t s_lo[kSmallMsgs + 1];   // LDS byte offset of each staged message (prefix)
     __shared__ uint32_t s_vec[kSmallMsgs + 1];  // 16-byte vectors before each staged message (prefix)
-    __shared__ uint2 s_desc[kBlock + 1];        // the tile's descriptors: LDS frame offset, len | vport | key
-    __shared__ uint32_t s_hoff[kBlock + 1];     // and their frames' offsets in the host buffer (+ a spare)
+    __shared__ uint2 s_desc[kBlock];            // the tile's descriptors: LDS frame offset, len | vport | key
+    __shared__ uint32_t s_fpos[kBlock + 1];     // the walk: LDS byte of each slot's frame header (0: none)
+    __shared__ uint32_t s_hoff[kBlock + 1];     // and its offset in the host buffer (+ a spare entry)
     __shared__ uint32_t s_wcnt[kWaves][16];
     __shared__ uint32_t s_hp[EMURX_HIST_BINS], s_hb[EMURX_HIST_BINS];
     __shared__ uint32_t s_m0, s_m1, s_last;
@@ -269,7 +270,7 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
     if (tid == 0) { s_m0 = 0xffffffffu; s_m1 = 0; }
     if (tid < 16) for (uint32_t w = 0; w < kWaves; ++w) s_wcnt[w][tid] = 0;
     if (tid < EMURX_HIST_BINS) { s_hp[tid] = 0; s_hb[tid] = 0; }
-    s_desc[tid] = make_uint2(0, EMURX_DESC_HOLE << 24);
+    s_fpos[tid] = 0;
     __syncthreads();
     // 1. this tile's messages: slots overlapping [s0, s1), or the message's status word is ours
     //    (tile min(base / 256, nt - 1)): a contiguous range, base being monotonic
@@ -341,31 +342,33 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
             if ((header >> 16) != EMURX_ZMQ_MAGIC) {
                 err = EMURX_MSG_PARSE_ERR;
             } else {
-                // the chain step with one exit test: the loop's checks in OnRxStream's order
-                // become one select chain (a branch per check cost its exec-mask bookkeeping on
-                // every frame of this single-lane loop); the header word is read at a clamped
-                // offset, so the read stays inside the message before the checks reject it
+                // the chain alone: a step continues while every check of OnRxStream passes,
+                // which with the message inside the LDS budget (< 64 KiB, so no 16-bit wrap of
+                // an accepted step) is magic && plen <= MAX && of + 4 + plen <= blen && a slot
+                // is left; the first failing step's error is then decided once, below, with
+                // the checks in their Go order.  The frame's header position is all a step notes.
                 const uint32_t pkts = header & 0xffff;
                 uint32_t of = 4;
                 for (; found < pkts; ++found) {
+                    header = lds_be32(s_msg, L0 + of);  // of <= blen: inside the staged message
+                    const uint32_t plen = header & 0xffff, e = of + 4 + plen;
+                    if (!((header >> 24) == 0xAAu && plen <= EMURX_MAX_FRAME && e <= blen && found < slots)) break;
+                    const uint32_t d = bm + found - s0, k = d < (uint32_t)kBlock ? d : (uint32_t)kBlock;  // else: the spare
+                    s_fpos[k] = L0 + of;
+                    s_hoff[k] = mk.x + of;
+                    of = e;
+                }
+                if (found < pkts) {  // the failing step: the first of Go's checks that fails
                     const uint32_t h4 = (of + 4) & 0xffff;
                     header = lds_be32(s_msg, L0 + min(of, blen));
-                    const uint32_t plen = header & 0xffff;
-                    const uint32_t e = (of + 4 + plen) & 0xffff;
-                    // the first failing check decides: selects applied last-check-first
-                    uint32_t bad = found >= slots ? EMURX_MSG_PANIC : 0u;
-                    bad = e < h4 ? EMURX_MSG_PANIC : bad;
-                    bad = plen > EMURX_MAX_FRAME ? EMURX_MSG_PANIC : bad;
-                    bad = blen < e ? EMURX_MSG_PARSE_ERR : bad;
-                    bad = (header & 0xff000000u) != 0xAA000000u ? EMURX_MSG_PARSE_ERR : bad;
-                    bad = h4 < of ? EMURX_MSG_PANIC : bad;
-                    bad = blen < h4 ? EMURX_MSG_PARSE_ERR : bad;
-                    if (bad) { err = bad; break; }
-                    // slots of other tiles land in the spare entry past the tile's (no branch)
-                    const uint32_t sl = bm + found, k = sl >= s0 && sl < s1 ? sl - s0 : kBlock;
-                    s_desc[k] = make_uint2(L0 + h4, header & 0x00ffffffu);  // key byte: below
-                    s_hoff[k] = mk.x + h4;
-                    of = e;
+                    const uint32_t plen = header & 0xffff, e = (of + 4 + plen) & 0xffff;
+                    err = blen < h4                                 ? EMURX_MSG_PARSE_ERR
+                          : h4 < of                                 ? EMURX_MSG_PANIC
+                          : (header & 0xff000000u) != 0xAA000000u   ? EMURX_MSG_PARSE_ERR
+                          : blen < e                                ? EMURX_MSG_PARSE_ERR
+                          : plen > EMURX_MAX_FRAME                  ? EMURX_MSG_PANIC
+                          : e < h4                                  ? EMURX_MSG_PANIC
+                                                                    : EMURX_MSG_PANIC;  // found >= slots
                 }
             }
         }
@@ -373,19 +376,18 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
     }
     __syncthreads();
     SSTAMP(4);
-    {  // one lane per slot of the tile: owner key, descriptor (holes stay holes)
-        const uint32_t sl = s0 + tid;
-        uint2 dd = s_desc[tid];
-        if ((dd.y >> 24) != EMURX_DESC_HOLE) {
-            const uint32_t plen = dd.y & 0xffff, vport = (dd.y >> 16) & 0xff;
+    {  // one lane per slot of the tile: the frame's header word, owner key, descriptor (holes stay holes)
+        const uint32_t sl = s0 + tid, fp = s_fpos[tid];
+        uint2 dd = make_uint2(0, EMURX_DESC_HOLE << 24);
+        if (fp) {  // a header is never at LDS byte 0 (it follows the message's own 4-byte header)
+            const uint32_t hd = lds_be32(s_msg, fp), plen = hd & 0xffff, vport = (hd >> 16) & 0xff;
             uint32_t v0, v1;
-            l2_vlans(plen, lds_be32(s_msg, dd.x + 12), lds_be32(s_msg, dd.x + 16), v0, v1);
-            dd.y |= emurx_owner_key(emurx_tk_hash(vport, v0, v1)) << 24;
-            s_desc[tid] = dd;
+            l2_vlans(plen, lds_be32(s_msg, fp + 16), lds_be32(s_msg, fp + 20), v0, v1);
+            dd = make_uint2(fp + 4, plen | (vport << 16) | (emurx_owner_key(emurx_tk_hash(vport, v0, v1)) << 24));
         }
+        s_desc[tid] = dd;
         if (sl < a.n)
-            reinterpret_cast<uint2*>(a.desc)[sl] =
-                (dd.y >> 24) != EMURX_DESC_HOLE ? make_uint2(s_hoff[tid], dd.y) : make_uint2(0, EMURX_DESC_HOLE << 24);
+            reinterpret_cast<uint2*>(a.desc)[sl] = fp ? make_uint2(s_hoff[tid] + 4, dd.y) : make_uint2(0, EMURX_DESC_HOLE << 24);
     }
     __syncthreads();
     SSTAMP(5);
@@ -426,6 +428,41 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
         left &= ~m;
     }
     __syncthreads();
+    if (a.nt == 1) {
+        // one tile: queues, qoff and the histogram straight from LDS into the host buffers, no
+        // device scratch and no ticket; then the completion word after every store and a
+        // system-scope release
+        __shared__ uint32_t s_qo[EMURX_NUM_QUEUES];
+        if (tid == 0) {
+            uint32_t at = 0;
+            for (uint32_t k = 0; k < EMURX_NUM_QUEUES; ++k) {
+                s_qo[k] = at;
+                a.qoff[k] = at;
+                at += s_wcnt[0][k] + s_wcnt[1][k] + s_wcnt[2][k] + s_wcnt[3][k];
+            }
+            a.qoff[EMURX_NUM_QUEUES] = at;
+        }
+        __syncthreads();
+        if (q != 0xffu) {
+            uint32_t pos = s_qo[q] + rank;
+            for (uint32_t w = 0; w < wv; ++w) pos += s_wcnt[w][q];
+            a.qlist[pos] = sl;
+        }
+        if (tid < EMURX_HIST_BINS) {
+            a.hist_out[2 * tid] = s_hp[tid];
+            a.hist_out[2 * tid + 1] = s_hb[tid];
+        }
+        SSTAMP(7);
+        SSTAMP(8);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            __atomic_thread_fence(__ATOMIC_RELEASE);
+            __hip_atomic_store(a.done, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        SSTAMP(9);
+        return;
+    }
     if (q != 0xffu) {
         uint32_t pos = rank;
         for (uint32_t w = 0; w < wv; ++w) pos += s_wcnt[w][q];
@@ -444,7 +481,7 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
     if (tid == 0) {
         __atomic_thread_fence(__ATOMIC_RELEASE);  // every wave's stores are behind the barrier
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        s_last = a.nt == 1 || atomicAdd(a.ticket, 1u) == a.nt - 1;  // one tile: no ticket
+        s_last = atomicAdd(a.ticket, 1u) == a.nt - 1;
     }
     __syncthreads();
     SSTAMP(7);
