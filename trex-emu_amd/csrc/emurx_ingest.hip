@@ -306,22 +306,27 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
     }
     __syncthreads();
     SSTAMP(2);
-    // host -> LDS, every vector of the range's messages in flight before the barrier (a binary
-    // search over s_vec finds a vector's message)
+    // host -> LDS by LDS-DMA (global_load_lds_dwordx4: no VGPR round trip, every row of every
+    // wave in flight before one wait): a wave per 64-vector row of the flat list, a lane's
+    // message found by a binary search over s_vec.  The vectors past a message's end (its 32
+    // bytes of slack) hold the host buffer's next bytes (the slot keeps 64 bytes of padding
+    // past the last message): the parse reads no byte past a frame's length
     const uint32_t nvec = min(s_vec[nm], kSmallLds / 16);  // the host admits only batches that fit
-    for (uint32_t v = tid; v < nvec; v += kBlock) {
+    static_assert(kSmallLds % (16 * kWave) == 0, "whole 1 KiB DMA rows");
+    for (uint32_t c = wv * kWave; c < nvec; c += kBlock) {
+        const uint32_t v = min(c + lane, nvec - 1);  // the row's tail repeats its last vector
         uint32_t lo = 0, hi = nm;  // last k with s_vec[k] <= v
         while (hi - lo > 1) {
             const uint32_t md = (lo + hi) >> 1;
             if (s_vec[md] <= v) lo = md; else hi = md;
         }
-        const uint2 mk = make_uint2(s_ctl[2 * (m0 + lo)], s_ctl[2 * (m0 + lo) + 1]);
-        const uint32_t j = v - s_vec[lo];
-        const uint8_t* src = a.buf + (mk.x & ~15u) + 16u * j;
-        uint4 x = make_uint4(0, 0, 0, 0);
-        if (16u * j < (mk.x & 15u) + mk.y) x = *reinterpret_cast<const uint4*>(src);
-        reinterpret_cast<uint4*>(s_msg)[v] = x;
+        const uint32_t off = s_ctl[2 * (m0 + lo)];
+        const uint8_t* src = a.buf + (off & ~15u) + 16u * (v - s_vec[lo]);
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint4*>(src),
+                                         (__attribute__((address_space(3))) void*)(reinterpret_cast<uint4*>(s_msg) + c),
+                                         16, 0, 0);
     }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's rows landed
     __syncthreads();
     SSTAMP(3);
     // 2. the walk of OnRxStream (veth_zmq.go:277-320), in LDS: one lane per message of the range
