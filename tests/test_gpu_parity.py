@@ -738,6 +738,38 @@ def test_ingest_small_batches(rxmod, small, monkeypatch):
         rx.ingest_submit(0, tab)
         res = rx.ingest_wait(0)
         check_ingest(res, o, msgs, tab)
+    # runs of equal-sized frames (the walk speculates one stride per round): whole runs, a run
+    # broken by one other size, a corrupted header mid-run, a length past the message, an
+    # over-announcing header, a run longer than a wave's 64 guesses
+    by_len = {}
+    for f in frames:
+        by_len.setdefault(len(f), []).append(f)
+    runs = sorted(by_len.values(), key=len, reverse=True)
+    vp = lambda c: [int(rng.integers(0, 4)) for _ in range(c)]
+    for nm in (1, 2, 4, 8):
+        msgs = []
+        for j in range(nm):
+            run = runs[j % 3]
+            per = int(rng.integers(1, 65)) if j % 2 else 64
+            fr = [run[i % len(run)] for i in range(per)]
+            kind = (j + nm) % 6
+            if kind == 1 and per > 3:
+                fr[per // 2] = runs[(j + 1) % 3][0]
+            m = bytearray(F.zmq_pack(fr, vp(len(fr))))
+            at = 4 + sum(4 + len(x) for x in fr[: len(fr) // 2])
+            if kind == 2:
+                m[at] = 0x00                                  # magic of the middle frame
+            elif kind == 3:
+                m[at + 2:at + 4] = (0xFFF0).to_bytes(2, "big")  # a length past the message
+            elif kind == 4:
+                m[2:4] = (len(fr) + 7).to_bytes(2, "big")      # announces more than it carries
+            msgs.append(bytes(m))
+        if nm == 8:
+            run = runs[0]
+            msgs.append(F.zmq_pack([run[i % len(run)] for i in range(150)], vp(150)))
+        tab = place_messages(rx, 0, msgs, rng)
+        rx.ingest_submit(0, tab)
+        check_ingest(rx.ingest_wait(0), o, msgs, tab)
 
 
 def test_ingest_two_slots_pipelined(rxmod):

@@ -329,11 +329,72 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's rows landed
     __syncthreads();
     SSTAMP(3);
-    // 2. the walk of OnRxStream (veth_zmq.go:277-320), in LDS: one lane per message of the range
-    //    follows the offset chain alone (a frame's header word, the checks, its LDS offset and
-    //    host offset noted); the owner keys and the descriptor stores come after, one lane per
-    //    slot, off the serial chain
-    if (tid < nm) {
+    // 2. the walk of OnRxStream (veth_zmq.go:277-320), in LDS.  A frame's step notes only its
+    //    header position (LDS and host offset); owner keys and descriptors come after, one lane
+    //    per slot.  A step continues while every check of OnRxStream passes, which with the
+    //    message inside the LDS budget (< 64 KiB, so no 16-bit wrap of an accepted step) is
+    //    magic && plen <= MAX && of + 4 + plen <= blen && a slot is left; the first failing
+    //    step's error is then decided once with the checks in their Go order (go_error).
+    //    Few messages (the latency case): a wave per message, 64 steps speculated per round
+    //    (lane j guesses the header at P + j * s, s the stride of the frame at P) and the prefix
+    //    whose guesses chain up accepted, so a message of equal-sized frames takes one round
+    //    and any message at least one frame per round.  Many messages: one lane per message
+    //    follows its chain serially, every message in parallel.
+    auto go_error = [&](uint32_t L0, uint32_t blen, uint32_t of) {  // the failing step at of
+        const uint32_t h4 = (of + 4) & 0xffff;
+        const uint32_t hd = lds_be32(s_msg, L0 + min(of, blen));
+        const uint32_t plen = hd & 0xffff, e = (of + 4 + plen) & 0xffff;
+        return blen < h4                             ? (uint32_t)EMURX_MSG_PARSE_ERR
+               : h4 < of                             ? (uint32_t)EMURX_MSG_PANIC
+               : (hd & 0xff000000u) != 0xAA000000u   ? (uint32_t)EMURX_MSG_PARSE_ERR
+               : blen < e                            ? (uint32_t)EMURX_MSG_PARSE_ERR
+               : plen > EMURX_MAX_FRAME              ? (uint32_t)EMURX_MSG_PANIC
+               : e < h4                              ? (uint32_t)EMURX_MSG_PANIC
+                                                     : (uint32_t)EMURX_MSG_PANIC;  // no slot left
+    };
+    auto note = [&](uint32_t sl, uint32_t pos, uint32_t host) {  // a frame of slot sl; other tiles': the spare
+        const uint32_t d = sl - s0, k = d < (uint32_t)kBlock ? d : (uint32_t)kBlock;
+        s_fpos[k] = pos;
+        s_hoff[k] = host;
+    };
+    if (nm <= 2 * kWaves) {
+        for (uint32_t mi = wv; mi < nm; mi += kWaves) {  // wave-uniform
+            const uint32_t m = m0 + mi;
+            const uint2 mk = make_uint2(s_ctl[2 * m], s_ctl[2 * m + 1]);
+            const uint32_t bm = base[m], slots = base[m + 1] - bm;
+            const uint32_t L0 = s_lo[mi] + (mk.x & 15u), blen = mk.y;
+            uint32_t f = 0, err = 0;
+            if (blen < 4) {
+                err = EMURX_MSG_PARSE_ERR;
+            } else if ((lds_be32(s_msg, L0) >> 16) != EMURX_ZMQ_MAGIC) {
+                err = EMURX_MSG_PARSE_ERR;
+            } else {
+                const uint32_t pkts = lds_be32(s_msg, L0) & 0xffff;
+                uint32_t P = 4;
+                while (f < pkts) {
+                    const uint32_t st = 4 + (lds_be32(s_msg, L0 + min(P, blen)) & 0xffff);
+                    const uint32_t g = P + lane * st;
+                    const uint32_t hd = lds_be32(s_msg, L0 + min(g, blen));
+                    const uint32_t plen = hd & 0xffff, e = g + 4 + plen;
+                    const bool ok = (hd >> 24) == 0xAAu && plen <= EMURX_MAX_FRAME && e <= blen && f + lane < slots;
+                    const uint64_t brk = __ballot(!(ok && e == g + st));
+                    const uint32_t first = brk ? (uint32_t)__ffsll((long long)brk) - 1 : kWave;
+                    const uint32_t fl = first < kWave ? first : kWave - 1;
+                    const bool okf = first == kWave || __builtin_amdgcn_readlane((int)ok, (int)fl) != 0;
+                    const uint32_t acc = min(first + (okf && first < kWave ? 1u : 0u), pkts - f);
+                    if (lane < acc) note(bm + f + lane, L0 + g, mk.x + g);
+                    if (!okf && f + first < pkts) {
+                        err = go_error(L0, blen, (uint32_t)__builtin_amdgcn_readlane((int)g, (int)first));
+                        f += acc;
+                        break;
+                    }
+                    f += acc;
+                    P = (uint32_t)__builtin_amdgcn_readlane((int)e, (int)fl);
+                }
+            }
+            if (lane == 0 && min(bm / kBlock, a.nt - 1) == t) a.stat[m] = f | (err << 24);
+        }
+    } else if (tid < nm) {
         const uint32_t m = m0 + tid;
         const uint2 mk = make_uint2(s_ctl[2 * m], s_ctl[2 * m + 1]);
         const uint32_t bm = base[m], slots = base[m + 1] - bm;
@@ -347,34 +408,16 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
             if ((header >> 16) != EMURX_ZMQ_MAGIC) {
                 err = EMURX_MSG_PARSE_ERR;
             } else {
-                // the chain alone: a step continues while every check of OnRxStream passes,
-                // which with the message inside the LDS budget (< 64 KiB, so no 16-bit wrap of
-                // an accepted step) is magic && plen <= MAX && of + 4 + plen <= blen && a slot
-                // is left; the first failing step's error is then decided once, below, with
-                // the checks in their Go order.  The frame's header position is all a step notes.
                 const uint32_t pkts = header & 0xffff;
                 uint32_t of = 4;
                 for (; found < pkts; ++found) {
                     header = lds_be32(s_msg, L0 + of);  // of <= blen: inside the staged message
                     const uint32_t plen = header & 0xffff, e = of + 4 + plen;
                     if (!((header >> 24) == 0xAAu && plen <= EMURX_MAX_FRAME && e <= blen && found < slots)) break;
-                    const uint32_t d = bm + found - s0, k = d < (uint32_t)kBlock ? d : (uint32_t)kBlock;  // else: the spare
-                    s_fpos[k] = L0 + of;
-                    s_hoff[k] = mk.x + of;
+                    note(bm + found, L0 + of, mk.x + of);
                     of = e;
                 }
-                if (found < pkts) {  // the failing step: the first of Go's checks that fails
-                    const uint32_t h4 = (of + 4) & 0xffff;
-                    header = lds_be32(s_msg, L0 + min(of, blen));
-                    const uint32_t plen = header & 0xffff, e = (of + 4 + plen) & 0xffff;
-                    err = blen < h4                                 ? EMURX_MSG_PARSE_ERR
-                          : h4 < of                                 ? EMURX_MSG_PANIC
-                          : (header & 0xff000000u) != 0xAA000000u   ? EMURX_MSG_PARSE_ERR
-                          : blen < e                                ? EMURX_MSG_PARSE_ERR
-                          : plen > EMURX_MAX_FRAME                  ? EMURX_MSG_PANIC
-                          : e < h4                                  ? EMURX_MSG_PANIC
-                                                                    : EMURX_MSG_PANIC;  // found >= slots
-                }
+                if (found < pkts) err = go_error(L0, blen, of);
             }
         }
         if (min(bm / kBlock, a.nt - 1) == t) a.stat[m] = found | (err << 24);
