@@ -2,7 +2,9 @@
 # Round-4 A/B of config E (IMIX, window path): the in-tree build against the window-skip
 # variants (EMURX_WSKIP: the cooperative checksum reads only the span bytes past each lane's
 # header window; + EMURX_WIN_NT: non-temporal window loads; + EMURX_COOP_NT: non-temporal
-# cooperative loads), interleaved on one box, then FETCH_SIZE of k_rx for each.
+# cooperative loads), interleaved on one box, then FETCH_SIZE of k_rx for each.  Built by
+# tools/build_variant.sh wskip "-DEMURX_WSKIP=1"; wskipnt "... -DEMURX_WIN_NT=1"; wskipnt2
+# "... -DEMURX_WIN_NT=1 -DEMURX_COOP_NT=1".
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp

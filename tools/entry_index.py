@@ -38,7 +38,7 @@ GROUPS = [
       "emurx_hist_to_counters", "emurx_hist_fold"],
      "`HandleRxPacket` `thread_ctx.go:365-375`, `ParsePacket` `parser.go:583-959`, `ParserStats`"),
     ("Several GPUs", ["emurx_set_partition", "emurx_route_dev", "emurx_classify_route_dev", "emurx_parse_route_dev",
-                      "emurx_lookup_dev"],
+                      "emurx_lookup_dev", "emurx_owner_key", "emurx_desc_keys_dev"],
      "`GetNs` `thread_ctx.go:772-784` on the Namespace owner (SURVEY §8e)"),
     ("Tx path", ["emurx_tx_checksum_dev", "emurx_tx_zmq_dev"],
      "gopacket checksum updates; `VethIFZmq.Send/FlushTx` `veth_zmq.go:149-200`"),

@@ -237,7 +237,12 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
     // rank inside (wave, queue): one ballot per distinct queue present in the wave
     uint32_t rank = 0;
 #if EMURX_MATCHRANK
-    {
+    if (EMURX_MATCHRANK == 2 && __ballot(valid && q != (uint32_t)__builtin_amdgcn_readfirstlane((int)q)) == 0) {
+        // hybrid: one queue in the wave (or none)
+        const uint64_t vm = __ballot(valid);
+        rank = mbcnt(vm);
+        if (valid && rank == 0) L.wcnt[wv][q] = (uint32_t)__popcll(vm);
+    } else {
         const uint64_t m = match_lanes<4>(q, __ballot(valid));
         rank = mbcnt(m);
         if (valid && rank == 0) L.wcnt[wv][q] = (uint32_t)__popcll(m);

@@ -1363,7 +1363,13 @@ __device__ __forceinline__ void resolve(const emurx_dev_tables& T, Rec& r, const
     const Probe p = probe_issue(T, r, k);
     Bucket ce{};
     if (p.ctab) ce = ld_bucket(p.ctab, p.cbk);
-#if EMURX_FLATRES
+#if EMURX_FLATRES == 2
+    // hybrid: a wave whose lanes share one key kind takes the switch without divergence
+    if (__ballot(k.key != (uint32_t)__builtin_amdgcn_readfirstlane((int)k.key)) == 0)
+        resolve_done(T, r, k, p, ce, flow);
+    else
+        resolve_done_flat(T, r, k, p, ce, flow);
+#elif EMURX_FLATRES
     resolve_done_flat(T, r, k, p, ce, flow);
 #else
     resolve_done(T, r, k, p, ce, flow);
