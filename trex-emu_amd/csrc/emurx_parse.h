@@ -305,12 +305,12 @@ template <class S>
 __device__ __forceinline__ bool csum_l4(const S& s, Rec& r, uint32_t at, uint32_t n, uint32_t pcs, uint32_t fail_st) {
     return csum(s, at, n, pcs);
 }
-// EMURX_WSKIP (build variant, A/B): the span's bytes inside the window are summed from LDS
+// EMURX_WSKIP (default since round 4; =0 the round-3 re-read): the span's bytes inside the window are summed from LDS
 // here and folded into the deferred pseudo sum (the byte-pair sum is linear mod 0xffff, and
 // be_domain with the span's own start parity orients both parts alike), so the cooperative
 // pass reads only the bytes past the window: every span byte crosses HBM once
 #ifndef EMURX_WSKIP
-#define EMURX_WSKIP 0
+#define EMURX_WSKIP 1
 #endif
 template <>
 __device__ __forceinline__ bool csum_l4<WinSrc>(const WinSrc& s, Rec& r, uint32_t at, uint32_t n, uint32_t pcs,
@@ -1284,22 +1284,28 @@ __device__ __forceinline__ void resolve_done_flat(const emurx_dev_tables& T, Rec
         nhole |= x.w == EMURX_EMPTY;
         if (x.w != EMURX_EMPTY && (x.x & 0xffffu) == w0 && x.y == w1 && x.z == w2) nsr = make_uint2(x.w, x.x >> 16);
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {  // the client views compare the Namespace id found above
-        const uint4 y = ce.s[j];
-        mhole |= y.w == EMURX_EMPTY;
-        if (y.w != EMURX_EMPTY && y.x == nsr.x && y.y == p.mlo && (y.z & 0xffffu) == p.mhi) mc = make_uint2(y.w, y.z >> 16);
-    }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const uint4 x = ce.s[2 * j], y = ce.s[2 * j + 1];
-        h4 |= y.w == EMURX_EMPTY;
-        h6 |= y.w == EMURX_EMPTY;
-        if (y.w != EMURX_EMPTY && x.x == nsr.x && x.y == k.kw[0]) i4 = IpHit{y.w, x.z, x.w};
-        if (y.w != EMURX_EMPTY && x.x == nsr.x && x.y == k.kw[0] && x.z == k.kw[1] && x.w == k.kw[2] && y.x == k.kw[3])
-            i6 = IpHit{y.w, y.y, y.z};
-    }
     const bool isMac = key == kMac || key == kEui, isIp4 = key == kIp4, isIp6 = key == kIp6;
+    // the client views compare the Namespace id found above; a view no lane of the wave needs
+    // is skipped (wave-uniform tests: a wave of one key kind computes one view)
+    if (any_lane(isMac)) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint4 y = ce.s[j];
+            mhole |= y.w == EMURX_EMPTY;
+            if (y.w != EMURX_EMPTY && y.x == nsr.x && y.y == p.mlo && (y.z & 0xffffu) == p.mhi) mc = make_uint2(y.w, y.z >> 16);
+        }
+    }
+    if (any_lane(isIp4 || isIp6)) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const uint4 x = ce.s[2 * j], y = ce.s[2 * j + 1];
+            h4 |= y.w == EMURX_EMPTY;
+            h6 |= y.w == EMURX_EMPTY;
+            if (y.w != EMURX_EMPTY && x.x == nsr.x && x.y == k.kw[0]) i4 = IpHit{y.w, x.z, x.w};
+            if (y.w != EMURX_EMPTY && x.x == nsr.x && x.y == k.kw[0] && x.z == k.kw[1] && x.w == k.kw[2] && y.x == k.kw[3])
+                i6 = IpHit{y.w, y.y, y.z};
+        }
+    }
     // ---- chains past the first buckets (wave-uniform test; the loop resolvers walk on) ----
     const bool ns_more = nsr.x == EMURX_ID_NONE && !nhole;
     if (any_lane(ns_more) && ns_more) {
