@@ -714,7 +714,7 @@ def test_ingest_small_batches(rxmod, small, monkeypatch):
     tile's messages within its LDS budget) and, with EMURX_INGEST_SMALL=0, the same batches
     through the multi-launch pipeline: records, descriptors (owner keys included), queues,
     per-message frame counts and status, and every counter equal the oracle's OnRxStream per
-    message.  1 to 64 messages of config C frames and hostile messages (truncated, corrupted,
+    message.  1 to 300 messages of config C frames and hostile messages (truncated, corrupted,
     over-announcing, empty), so that messages span tiles, some carry no slot and the last
     tile's status words include the trailing empty messages."""
     import test_abi
@@ -726,10 +726,10 @@ def test_ingest_small_batches(rxmod, small, monkeypatch):
     for t in (rx, o):
         synth.load_tables(w, t)
     k = 0
-    for nm in (1, 2, 3, 5, 16, 17, 40, 64):
+    for nm in (1, 2, 3, 5, 16, 17, 40, 64, 300):
         msgs = []
         for j in range(nm):
-            per = int(rng.integers(1, 65))
+            per = int(rng.integers(1, 65 if nm < 300 else 24))
             msgs.append(F.zmq_pack(frames[k:k + per], [int(v) for v in w["desc"]["vport"][k:k + per]]))
             k = (k + per) % (len(frames) - 64)
         msgs += test_abi._rand_msgs(rng, 4)[:4] + [b""]

@@ -483,11 +483,13 @@ int ingest_buffer(emurx_t* h, uint32_t slot, size_t bytes, uint8_t** buf) {
 // it, and those whose status word it writes: tile min(base / 256, tiles - 1)) within the
 // kernel's LDS budget, counted exactly as the kernel stages them: 16-byte vectors from the
 // message's aligned start, plus two of slack.
-bool small_fits(const uint32_t* ctl, uint32_t nmsg, uint32_t n) {
+bool small_fits(const uint32_t* ctl, uint32_t nmsg, uint32_t n, uint32_t trange[EMURX_SMALL_TILES]) {
     if (nmsg > EMURX_SMALL_MSGS || n > (uint32_t)EMURX_SMALL_TILES * EMURX_QUEUE_TILE) return false;
     const uint32_t nt = std::max<uint32_t>(ntiles(n), 1);
     const uint32_t* base = ctl + 2 * (size_t)nmsg;
     uint64_t vec[EMURX_SMALL_TILES] = {0};
+    uint32_t lo[EMURX_SMALL_TILES], hi[EMURX_SMALL_TILES];
+    for (uint32_t t = 0; t < nt; ++t) lo[t] = UINT32_MAX, hi[t] = 0;
     for (uint32_t m = 0; m < nmsg; ++m) {
         const uint32_t off = ctl[2 * m], len = ctl[2 * m + 1];
         const uint64_t v = len ? (((off & 15u) + (uint64_t)len + 15) >> 4) + 2 : 0;
@@ -497,10 +499,16 @@ bool small_fits(const uint32_t* ctl, uint32_t nmsg, uint32_t n) {
             t0 = std::min(t0, b0 / EMURX_QUEUE_TILE);
             t1 = std::max(t1, std::min((b1 - 1) / EMURX_QUEUE_TILE, nt - 1));
         }
-        for (uint32_t t = t0; t <= t1; ++t) vec[t] += v;
+        for (uint32_t t = t0; t <= t1; ++t) {
+            vec[t] += v;
+            lo[t] = std::min(lo[t], m);
+            hi[t] = std::max(hi[t], m);
+        }
     }
-    for (uint32_t t = 0; t < nt; ++t)
+    for (uint32_t t = 0; t < nt; ++t) {
         if (vec[t] * 16 > EMURX_SMALL_LDS) return false;
+        trange[t] = lo[t] == UINT32_MAX ? 0u : lo[t] | ((hi[t] - lo[t] + 1) << 16);
+    }
     return true;
 }
 
@@ -548,7 +556,8 @@ int ingest_submit(emurx_t* h, uint32_t slot, const emurx_msg* msgs, uint32_t nms
     if ((rc = prepare_read(h, st))) return rc;  // table deltas ordered against every reader
     // the pipeline's histogram shards start zeroed (k_qscan leaves them zero)
     if (fresh_hist && !EMURX_HIP_OK(hipMemsetAsync(s.d_hist.p, 0, hw * sizeof(uint64_t), st))) return EMURX_EDEVICE;
-    if (h->ingest_small && small_fits(ctl, nmsg, n)) {
+    uint32_t trange[EMURX_SMALL_TILES];
+    if (h->ingest_small && small_fits(ctl, nmsg, n, trange)) {
         // one launch: control words and messages read from the pinned buffers, every result
         // written into the pinned result buffers (no copies)
         if (!s.d_ticket.p) {
@@ -563,7 +572,7 @@ int ingest_submit(emurx_t* h, uint32_t slot, const emurx_msg* msgs, uint32_t nms
         }
         if (emurx_launch_ingest_small(s.h_buf.p, ctl, nmsg, n, h->tables(), s.h_rec.p, s.h_desc.p, s.h_qlist.p,
                                       s.h_stat.p, s.h_qoff.p, s.h_hist.p, s.d_qseg.p, s.d_tcnt.p, s.d_hsmall.p,
-                                      s.d_ticket.p, s.h_done.p, s.seq + 1, st) ||
+                                      s.d_ticket.p, s.h_done.p, s.seq + 1, trange, st) ||
             !EMURX_HIP_OK(hipEventRecord(s.done, st)))
             return EMURX_EDEVICE;
         ++s.seq;

@@ -221,6 +221,7 @@ struct SmallArgs {
     uint32_t* ticket;            // zero between batches
     uint32_t* done;              // pinned host: the batch's sequence number, written last
     uint32_t seq;
+    uint32_t trange[EMURX_SMALL_TILES];  // per tile: its first message | message count << 16
 };
 
 // EMURX_SMALL_STAMP=1 (diagnostic build, tools/lat_probe.py): the wall clock (100 MHz) at the
@@ -253,34 +254,31 @@ __device__ __forceinline__ uint32_t lds_be32(const uint32_t* w, uint32_t a) {
 
 __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t s_msg[kSmallLds / 4];
-    __shared__ uint32_t s_lo[kSmallMsgs + 1];   // LDS byte offset of each staged message (prefix)
     __shared__ uint32_t s_vec[kSmallMsgs + 1];  // 16-byte vectors before each staged message (prefix)
     __shared__ uint2 s_desc[kBlock];            // the tile's descriptors: LDS frame offset, len | vport | key
     __shared__ uint32_t s_fpos[kBlock + 1];     // the walk: LDS byte of each slot's frame header (0: none)
     __shared__ uint32_t s_hoff[kBlock + 1];     // and its offset in the host buffer (+ a spare entry)
     __shared__ uint32_t s_wcnt[kWaves][16];
     __shared__ uint32_t s_hp[EMURX_HIST_BINS], s_hb[EMURX_HIST_BINS];
-    __shared__ uint32_t s_m0, s_m1, s_last;
-    __shared__ uint32_t s_ctl[3 * kSmallMsgs + 1];  // the control words, read from the host once
+    __shared__ uint32_t s_last;
+    __shared__ uint2 s_mk[kSmallMsgs];          // the tile's messages {offset, length}, read from the host once
+    __shared__ uint32_t s_base[kSmallMsgs + 1];  // and their first descriptor slots
     const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / kWave, t = blockIdx.x;
-    for (uint32_t k = tid; k < 3 * a.nmsg + 1; k += kBlock) s_ctl[k] = a.ctl[k];  // one bus round trip
-    const uint32_t* base = s_ctl + 2 * a.nmsg;
+    // 1. this tile's messages (the host's trange: slots overlapping [s0, s1), or the message's
+    //    status word is ours, tile min(base / 256, nt - 1); a contiguous range, base being
+    //    monotonic): their control words in one bus round trip
+    const uint32_t m0 = a.trange[t] & 0xffffu, nm = a.trange[t] >> 16;
+    for (uint32_t k = tid; k < 2 * nm + 1; k += kBlock) {
+        if (k < 2 * nm) reinterpret_cast<uint32_t*>(s_mk)[k] = a.ctl[2 * m0 + k];
+        if (k <= nm) s_base[k] = a.ctl[2 * a.nmsg + m0 + k];
+    }
     SSTAMP(0);
-    const uint32_t s0 = t * kBlock, s1 = s0 + kBlock;
-    if (tid == 0) { s_m0 = 0xffffffffu; s_m1 = 0; }
+    const uint32_t s0 = t * kBlock;
     if (tid < 16) for (uint32_t w = 0; w < kWaves; ++w) s_wcnt[w][tid] = 0;
     if (tid < EMURX_HIST_BINS) { s_hp[tid] = 0; s_hb[tid] = 0; }
     s_fpos[tid] = 0;
     __syncthreads();
-    // 1. this tile's messages: slots overlapping [s0, s1), or the message's status word is ours
-    //    (tile min(base / 256, nt - 1)): a contiguous range, base being monotonic
-    const bool inm = tid < a.nmsg;
-    const uint32_t b0 = inm ? base[tid] : 0u, b1 = inm ? base[tid + 1] : 0u;
-    const bool mine = inm && ((b0 < s1 && b1 > s0) || min(b0 / kBlock, a.nt - 1) == t);
-    if (mine) { atomicMin(&s_m0, tid); atomicMax(&s_m1, tid); }
-    __syncthreads();
     SSTAMP(1);
-    const uint32_t m0 = s_m0, nm = s_m0 == 0xffffffffu ? 0u : s_m1 - s_m0 + 1;
     // staged layout: message k of the range at LDS byte s_lo[k] (+ its offset mod 16), its
     // vectors [s_vec[k], s_vec[k + 1]) of the range's flat vector list
     if (wv == 0) {
@@ -289,7 +287,7 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
             const uint32_t k = c + lane;
             uint32_t v = 0;
             if (k < nm) {
-                const uint2 mk = make_uint2(s_ctl[2 * (m0 + k)], s_ctl[2 * (m0 + k) + 1]);
+                const uint2 mk = s_mk[k];
                 v = mk.y ? (((mk.x & 15u) + mk.y + 15u) >> 4) + 2u : 0u;  // + 32 B of slack
             }
             uint32_t incl = v;
@@ -298,11 +296,11 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
                 const uint32_t up = (uint32_t)__shfl_up((int)incl, o);
                 if (lane >= o) incl += up;
             }
-            if (k < nm) { s_vec[k] = vb + incl - v; s_lo[k] = (vb + incl - v) * 16; }
+            if (k < nm) s_vec[k] = vb + incl - v;
             vb += (uint32_t)__shfl((int)incl, kWave - 1);
             nv = vb;
         }
-        if (lane == 0) { s_vec[nm] = nv; s_lo[nm] = nv * 16; }
+        if (lane == 0) s_vec[nm] = nv;
     }
     __syncthreads();
     SSTAMP(2);
@@ -320,7 +318,7 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
             const uint32_t md = (lo + hi) >> 1;
             if (s_vec[md] <= v) lo = md; else hi = md;
         }
-        const uint32_t off = s_ctl[2 * (m0 + lo)];
+        const uint32_t off = s_mk[lo].x;
         const uint8_t* src = a.buf + (off & ~15u) + 16u * (v - s_vec[lo]);
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint4*>(src),
                                          (__attribute__((address_space(3))) void*)(reinterpret_cast<uint4*>(s_msg) + c),
@@ -360,9 +358,9 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
     if (nm <= 2 * kWaves) {
         for (uint32_t mi = wv; mi < nm; mi += kWaves) {  // wave-uniform
             const uint32_t m = m0 + mi;
-            const uint2 mk = make_uint2(s_ctl[2 * m], s_ctl[2 * m + 1]);
-            const uint32_t bm = base[m], slots = base[m + 1] - bm;
-            const uint32_t L0 = s_lo[mi] + (mk.x & 15u), blen = mk.y;
+            const uint2 mk = s_mk[mi];
+            const uint32_t bm = s_base[mi], slots = s_base[mi + 1] - bm;
+            const uint32_t L0 = s_vec[mi] * 16 + (mk.x & 15u), blen = mk.y;
             uint32_t f = 0, err = 0;
             if (blen < 4) {
                 err = EMURX_MSG_PARSE_ERR;
@@ -394,33 +392,35 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
             }
             if (lane == 0 && min(bm / kBlock, a.nt - 1) == t) a.stat[m] = f | (err << 24);
         }
-    } else if (tid < nm) {
-        const uint32_t m = m0 + tid;
-        const uint2 mk = make_uint2(s_ctl[2 * m], s_ctl[2 * m + 1]);
-        const uint32_t bm = base[m], slots = base[m + 1] - bm;
-        const uint32_t L0 = s_lo[tid] + (mk.x & 15u);  // LDS byte of message byte 0
-        const uint32_t blen = mk.y;
-        uint32_t found = 0, err = 0;
-        if (blen < 4) {
-            err = EMURX_MSG_PARSE_ERR;
-        } else {
-            uint32_t header = lds_be32(s_msg, L0);
-            if ((header >> 16) != EMURX_ZMQ_MAGIC) {
+    } else {
+        for (uint32_t mi = tid; mi < nm; mi += kBlock) {  // more messages than lanes: in turns
+            const uint32_t m = m0 + mi;
+            const uint2 mk = s_mk[mi];
+            const uint32_t bm = s_base[mi], slots = s_base[mi + 1] - bm;
+            const uint32_t L0 = s_vec[mi] * 16 + (mk.x & 15u);  // LDS byte of message byte 0
+            const uint32_t blen = mk.y;
+            uint32_t found = 0, err = 0;
+            if (blen < 4) {
                 err = EMURX_MSG_PARSE_ERR;
             } else {
-                const uint32_t pkts = header & 0xffff;
-                uint32_t of = 4;
-                for (; found < pkts; ++found) {
-                    header = lds_be32(s_msg, L0 + of);  // of <= blen: inside the staged message
-                    const uint32_t plen = header & 0xffff, e = of + 4 + plen;
-                    if (!((header >> 24) == 0xAAu && plen <= EMURX_MAX_FRAME && e <= blen && found < slots)) break;
-                    note(bm + found, L0 + of, mk.x + of);
-                    of = e;
+                uint32_t header = lds_be32(s_msg, L0);
+                if ((header >> 16) != EMURX_ZMQ_MAGIC) {
+                    err = EMURX_MSG_PARSE_ERR;
+                } else {
+                    const uint32_t pkts = header & 0xffff;
+                    uint32_t of = 4;
+                    for (; found < pkts; ++found) {
+                        header = lds_be32(s_msg, L0 + of);  // of <= blen: inside the staged message
+                        const uint32_t plen = header & 0xffff, e = of + 4 + plen;
+                        if (!((header >> 24) == 0xAAu && plen <= EMURX_MAX_FRAME && e <= blen && found < slots)) break;
+                        note(bm + found, L0 + of, mk.x + of);
+                        of = e;
+                    }
+                    if (found < pkts) err = go_error(L0, blen, of);
                 }
-                if (found < pkts) err = go_error(L0, blen, of);
             }
+            if (min(bm / kBlock, a.nt - 1) == t) a.stat[m] = found | (err << 24);
         }
-        if (min(bm / kBlock, a.nt - 1) == t) a.stat[m] = found | (err << 24);
     }
     __syncthreads();
     SSTAMP(4);
@@ -591,13 +591,14 @@ int emurx_launch_ingest_small(const uint8_t* h_buf, const uint32_t* h_ctl, uint3
                               const emurx_dev_tables& T, emurx_rec* h_rec, emurx_desc* h_desc, uint32_t* h_qlist,
                               uint32_t* h_stat, uint32_t* h_qoff, uint64_t* h_hist, uint32_t* d_qseg, uint32_t* d_tcnt,
                               uint64_t* d_hist, uint32_t* d_ticket, uint32_t* h_done, uint32_t seq,
-                              hipStream_t st) {
+                              const uint32_t* trange, hipStream_t st) {
     using namespace emurx;
     const uint32_t nt = std::max<uint32_t>((n + kBlock - 1) / kBlock, 1);
     if (nt > EMURX_SMALL_TILES || nmsg > kSmallMsgs) return -1;
-    const SmallArgs args{h_buf, h_ctl, nmsg, n, nt, T, h_rec, h_desc, h_qlist, h_stat, h_qoff,
-                         reinterpret_cast<unsigned long long*>(h_hist), d_qseg, d_tcnt,
-                         reinterpret_cast<unsigned long long*>(d_hist), d_ticket, h_done, seq};
+    SmallArgs args{h_buf, h_ctl, nmsg, n, nt, T, h_rec, h_desc, h_qlist, h_stat, h_qoff,
+                   reinterpret_cast<unsigned long long*>(h_hist), d_qseg, d_tcnt,
+                   reinterpret_cast<unsigned long long*>(d_hist), d_ticket, h_done, seq, {}};
+    for (uint32_t t = 0; t < nt; ++t) args.trange[t] = trange[t];
     return EMURX_HIP_OK(emurx_launch(k_ingest_small, dim3(nt), dim3(kBlock), 0, st, args)) ? 0 : -1;
 }
 

@@ -90,21 +90,22 @@ int emurx_launch_lookup(const emurx_lookup_rec* recv, const uint32_t* recv_count
 // msg_stat[m] = frames | EMURX_MSG_* << 24.  The buffer must be readable 8 bytes past every message.
 int emurx_launch_zmq_walk(const uint8_t* buf, const uint32_t* ctl, uint32_t nmsg, emurx_desc* desc,
                           uint32_t* msg_stat, hipStream_t st);
-// A small batch (at most EMURX_SMALL_TILES tiles, 256 messages, every tile's messages within the
+// A small batch (at most EMURX_SMALL_TILES tiles, EMURX_SMALL_MSGS messages, every tile's messages within the
 // kernel's LDS budget: emurx_ingest_small_fits) in ONE launch: messages and control words read
 // from pinned host memory, walk + parse + classify + queue packing, every result written into
 // pinned host memory (h_*: the layout of the pipeline's D2H copies).  Device scratch: d_qseg
 // [EMURX_SMALL_TILES * 13 * 256], d_tcnt [EMURX_SMALL_TILES * 16], d_hist [128] and d_ticket,
 // zero before the first launch (each launch leaves them zero).  h_done (pinned host): seq is
-// written there after every result (the host may spin on it instead of the stream).
-#define EMURX_SMALL_TILES 16
+// written there after every result (the host may spin on it instead of the stream).  trange[t]
+// (emurx_ingest_tile_ranges): tile t's first message | its message count << 16.
+#define EMURX_SMALL_TILES 64
 #define EMURX_SMALL_LDS 40960
-#define EMURX_SMALL_MSGS 256
+#define EMURX_SMALL_MSGS 1024
 int emurx_launch_ingest_small(const uint8_t* h_buf, const uint32_t* h_ctl, uint32_t nmsg, uint32_t n,
                               const emurx_dev_tables& T, emurx_rec* h_rec, emurx_desc* h_desc, uint32_t* h_qlist,
                               uint32_t* h_stat, uint32_t* h_qoff, uint64_t* h_hist, uint32_t* d_qseg, uint32_t* d_tcnt,
                               uint64_t* d_hist, uint32_t* d_ticket, uint32_t* h_done, uint32_t seq,
-                              hipStream_t st);
+                              const uint32_t* trange, hipStream_t st);
 // Concatenate k_rx's per-tile queue segments (queue-major, frame order) into `packed`, write
 // qoff[EMURX_NUM_QUEUES + 1], fold the histogram shards into hist_out[2 * EMURX_HIST_BINS] and
 // clear the shards.  Scratch seg_off: [ceil(n / 256) * 16].  Two launches.
