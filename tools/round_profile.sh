@@ -50,9 +50,10 @@ for ph in $phases; do
       pmc)
         for k in FETCH_SIZE WRITE_SIZE; do
           step pmc_${c}_$k 180 rocprofv3 --pmc $k -T --kernel-include-regex k_rx -d $out/pmc_${c}/pmc_$k -o run \
-            --output-format csv -- python bench.py $(args $c) --steps 40 --warmup 8 --no-cpu-baseline --no-check --no-replay
+            --output-format csv -- python bench.py $(args $c) --steps 40 --warmup 8 --no-cpu-baseline --no-check --no-replay \
+            --no-exchange-run
         done
-        xs=""; [ "$c" = E ] && xs="--excess-streamed"  # E's excess: long spans read again (window path)
+        xs=""  # E's excess is probe lines since the window-skip checksum (round 4); --excess-streamed before
         python tools/pmc_summary.py $out/pmc_${c} $xs > $out/pmc_config$c.json 2>&1; cat $out/pmc_config$c.json ;;
     esac
   done

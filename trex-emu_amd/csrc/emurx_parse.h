@@ -134,12 +134,29 @@ __device__ __forceinline__ bool csum_ok(uint32_t T, uint32_t a_start, uint32_t p
 }
 // sum over the bytes [a, a + n) of a dword sequence w[k] (byte a at dword a >> 2):
 // head / body / tail masks, body unmasked
+#ifndef EMURX_SHORTSUM
+#define EMURX_SHORTSUM 0
+#endif
 template <class A>
 __device__ __forceinline__ uint32_t dword_sum(const A& w, uint32_t a, uint32_t n) {
     if (n == 0) return 0;
     const uint32_t e = a + n, k0 = a >> 2, k1 = (e - 1) >> 2;
     const uint32_t hm = 0xffffffffu << (8 * (a & 3));
     const uint32_t tm = 0xffffffffu >> (8 * ((0u - e) & 3));
+#if EMURX_SHORTSUM
+    // a span of at most 64 bytes (17 dwords): every dword read at once, the ones past the span
+    // masked to nothing (one LDS round trip instead of one per four dwords); wave-uniform test
+    if (__builtin_amdgcn_ballot_w64(k1 - k0 > 16) == 0) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (uint32_t j = 0; j <= 16; ++j) {
+            const uint32_t k = k0 + j;
+            const uint32_t m = k > k1 ? 0u : (j == 0 ? hm : 0xffffffffu) & (k == k1 ? tm : 0xffffffffu);
+            acc = sad16(w[k] & m, acc);  // read unconditionally: a dword past the span is in LDS
+        }
+        return acc;
+    }
+#endif
     const uint32_t w0 = w[k0] & hm;
     if (k0 == k1) return sad16(w0 & tm, 0);
     uint32_t acc = sad16(w0, 0), k = k0 + 1;
