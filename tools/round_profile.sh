@@ -41,7 +41,7 @@ for ph in $phases; do
         step bench_$c 600 python bench.py $(args $c) $extra ;;
       prof)
         step prof_$c 300 rocprofv3 --kernel-trace --stats -d $out/prof_$c -o run --output-format csv \
-          -- python bench.py $(args $c) --no-cpu-baseline
+          -- python bench.py $(args $c) --no-cpu-baseline --no-exchange-run
         f=$(ls $out/prof_$c/*/run_kernel_stats.csv $out/prof_$c/run_kernel_stats.csv 2>/dev/null | head -n 1)
         [ -n "$f" ] && cut -d, -f1-4 "$f" | head -n 12
         t=$(ls $out/prof_$c/*/run_kernel_trace.csv $out/prof_$c/run_kernel_trace.csv 2>/dev/null | head -n 1)

@@ -76,7 +76,15 @@ struct PinBuf {
     }
 };
 
+// a typed place inside a slot's result block (IngestSlot::h_res / d_res)
+template <class T>
+struct View {
+    T* p = nullptr;
+};
 // One in-flight batch of the batched ZMQ ingest: pinned staging + device scratch + results.
+// The results (records, descriptors, packed queues, message status, qoff, folded histogram)
+// share one device block and one pinned block of the same layout (set_results): the pipeline
+// copies them back with one D2H, and the one-launch path writes the pinned block directly.
 struct IngestSlot {
     hipStream_t st = nullptr;
     hipEvent_t done = nullptr;
@@ -84,16 +92,22 @@ struct IngestSlot {
     uint32_t nmsg = 0, slots = 0;  // messages and descriptor slots of the batch in flight
     PinBuf<uint8_t> h_buf;         // messages, written by the caller (+64 B pad)
     PinBuf<uint32_t> h_ctl;        // emurx_msg[nmsg], slot_base[nmsg + 1]
-    PinBuf<uint32_t> h_stat, h_qlist, h_qoff, h_mframes;
+    PinBuf<uint32_t> h_mframes;
     PinBuf<uint8_t> h_mstatus;
-    PinBuf<emurx_rec> h_rec;
-    PinBuf<emurx_desc> h_desc;
-    PinBuf<uint64_t> h_hist;
+    PinBuf<uint8_t> h_res;                 // the result block, pinned
+    View<uint32_t> h_stat, h_qlist, h_qoff;
+    View<emurx_rec> h_rec;
+    View<emurx_desc> h_desc;
+    View<uint64_t> h_hist;
     DevBuf<uint8_t> d_buf;
-    DevBuf<uint32_t> d_ctl, d_stat, d_qlist, d_tile_cnt, d_seg_off, d_packed, d_qoff;
-    DevBuf<emurx_desc> d_desc;
-    DevBuf<emurx_rec> d_rec;
-    DevBuf<uint64_t> d_hist, d_hist_out;  // d_hist: zero between batches (k_qscan clears it)
+    DevBuf<uint32_t> d_ctl, d_qlist, d_tile_cnt, d_seg_off;
+    DevBuf<uint64_t> d_hist;               // zero between batches (k_qscan clears it)
+    DevBuf<uint8_t> d_res;                 // the result block, device
+    View<uint32_t> d_stat, d_packed, d_qoff;
+    View<emurx_desc> d_desc;
+    View<emurx_rec> d_rec;
+    View<uint64_t> d_hist_out;
+    size_t res_bytes = 0;                  // the current batch's result block
     // the fused small-batch path's scratch (k_ingest_small), zero between batches
     DevBuf<uint32_t> d_qseg, d_tcnt, d_ticket;
     DevBuf<uint64_t> d_hsmall;
@@ -104,11 +118,9 @@ struct IngestSlot {
     void release() {
         if (st) (void)hipStreamSynchronize(st);
         d_qseg.release(); d_tcnt.release(); d_ticket.release(); d_hsmall.release(); h_done.release();
-        h_buf.release(); h_ctl.release(); h_stat.release(); h_qlist.release(); h_qoff.release();
-        h_mframes.release(); h_mstatus.release(); h_rec.release(); h_desc.release(); h_hist.release();
-        d_buf.release(); d_ctl.release(); d_stat.release(); d_qlist.release(); d_tile_cnt.release();
-        d_seg_off.release(); d_packed.release(); d_qoff.release(); d_desc.release(); d_rec.release();
-        d_hist.release(); d_hist_out.release();
+        h_buf.release(); h_ctl.release(); h_mframes.release(); h_mstatus.release(); h_res.release();
+        d_buf.release(); d_ctl.release(); d_qlist.release(); d_tile_cnt.release(); d_seg_off.release();
+        d_hist.release(); d_res.release();
         if (done) (void)hipEventDestroy(done);
         if (st) (void)hipStreamDestroy(st);
         done = nullptr;
@@ -512,6 +524,32 @@ bool small_fits(const uint32_t* ctl, uint32_t nmsg, uint32_t n, uint32_t trange[
     return true;
 }
 
+// the result block of a batch of n descriptor slots and nmsg messages (256-byte aligned parts):
+// allocates both copies and points the views into them
+int set_results(IngestSlot& s, uint32_t n, uint32_t nmsg) {
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t o_desc = al((size_t)n * sizeof(emurx_rec)), o_q = o_desc + al((size_t)n * sizeof(emurx_desc));
+    const size_t o_stat = o_q + al((size_t)n * 4), o_qoff = o_stat + al((size_t)nmsg * 4), o_hist = o_qoff + 256;
+    const size_t total = o_hist + 2 * EMURX_HIST_BINS * sizeof(uint64_t);
+    if (s.h_res.alloc(total) || s.d_res.alloc(total)) return EMURX_ENOMEM;
+    uint8_t* hb = s.h_res.p;
+    uint8_t* db = s.d_res.p;
+    s.h_rec.p = reinterpret_cast<emurx_rec*>(hb);
+    s.h_desc.p = reinterpret_cast<emurx_desc*>(hb + o_desc);
+    s.h_qlist.p = reinterpret_cast<uint32_t*>(hb + o_q);
+    s.h_stat.p = reinterpret_cast<uint32_t*>(hb + o_stat);
+    s.h_qoff.p = reinterpret_cast<uint32_t*>(hb + o_qoff);
+    s.h_hist.p = reinterpret_cast<uint64_t*>(hb + o_hist);
+    s.d_rec.p = reinterpret_cast<emurx_rec*>(db);
+    s.d_desc.p = reinterpret_cast<emurx_desc*>(db + o_desc);
+    s.d_packed.p = reinterpret_cast<uint32_t*>(db + o_q);
+    s.d_stat.p = reinterpret_cast<uint32_t*>(db + o_stat);
+    s.d_qoff.p = reinterpret_cast<uint32_t*>(db + o_qoff);
+    s.d_hist_out.p = reinterpret_cast<uint64_t*>(db + o_hist);
+    s.res_bytes = total;
+    return EMURX_OK;
+}
+
 int ingest_submit(emurx_t* h, uint32_t slot, const emurx_msg* msgs, uint32_t nmsg) {
     IngestSlot& s = h->ing[slot];
     if (s.pending || (nmsg && (!msgs || !s.h_buf.p))) return EMURX_EINVAL;
@@ -545,12 +583,10 @@ int ingest_submit(emurx_t* h, uint32_t slot, const emurx_msg* msgs, uint32_t nms
     const size_t qcap = std::max<size_t>(queue_cap(n), EMURX_QUEUE_TILE);
     const size_t hw = (size_t)EMURX_HIST_SHARDS * 2 * EMURX_HIST_BINS;
     const bool fresh_hist = !s.d_hist.p;
-    if (s.d_ctl.alloc((size_t)3 * nmsg + 1) || s.d_stat.alloc(nmsg) || s.d_desc.alloc(n) || s.d_rec.alloc(n) ||
-        s.d_qlist.alloc(EMURX_NUM_QUEUES * qcap) || s.d_tile_cnt.alloc((size_t)std::max<uint32_t>(nt, 1) * 16) ||
-        s.d_seg_off.alloc((size_t)std::max<uint32_t>(nt, 1) * 16) || s.d_packed.alloc(n) || s.d_qoff.alloc(16) ||
-        s.d_hist.alloc(hw) || s.d_hist_out.alloc(2 * EMURX_HIST_BINS) || s.h_stat.alloc(nmsg) ||
-        s.h_rec.alloc(n) || s.h_desc.alloc(n) || s.h_qlist.alloc(n) || s.h_qoff.alloc(16) ||
-        s.h_hist.alloc(2 * EMURX_HIST_BINS) || s.h_mframes.alloc(nmsg) || s.h_mstatus.alloc(nmsg))
+    if (s.d_ctl.alloc((size_t)3 * nmsg + 1) || s.d_qlist.alloc(EMURX_NUM_QUEUES * qcap) ||
+        s.d_tile_cnt.alloc((size_t)std::max<uint32_t>(nt, 1) * 16) ||
+        s.d_seg_off.alloc((size_t)std::max<uint32_t>(nt, 1) * 16) || s.d_hist.alloc(hw) || set_results(s, n, nmsg) ||
+        s.h_mframes.alloc(nmsg) || s.h_mstatus.alloc(nmsg))
         return EMURX_ENOMEM;
     hipStream_t st = s.st;
     if ((rc = prepare_read(h, st))) return rc;  // table deltas ordered against every reader
@@ -598,13 +634,8 @@ int ingest_submit(emurx_t* h, uint32_t slot, const emurx_msg* msgs, uint32_t nms
     if (emurx_launch_queue_pack(s.d_qlist.p, (uint32_t)qcap, s.d_tile_cnt.p, n, s.d_seg_off.p, s.d_packed.p,
                                 s.d_qoff.p, s.d_hist.p, s.d_hist_out.p, st))
         return EMURX_EDEVICE;
-    if (n)
-        ok = EMURX_HIP_OK(hipMemcpyAsync(s.h_rec.p, s.d_rec.p, (size_t)n * sizeof(emurx_rec), D2H, st)) &&
-             EMURX_HIP_OK(hipMemcpyAsync(s.h_desc.p, s.d_desc.p, (size_t)n * sizeof(emurx_desc), D2H, st)) &&
-             EMURX_HIP_OK(hipMemcpyAsync(s.h_qlist.p, s.d_packed.p, (size_t)n * 4, D2H, st));
-    if (nmsg) ok = ok && EMURX_HIP_OK(hipMemcpyAsync(s.h_stat.p, s.d_stat.p, (size_t)nmsg * 4, D2H, st));
-    ok = ok && EMURX_HIP_OK(hipMemcpyAsync(s.h_qoff.p, s.d_qoff.p, (EMURX_NUM_QUEUES + 1) * 4, D2H, st)) &&
-         EMURX_HIP_OK(hipMemcpyAsync(s.h_hist.p, s.d_hist_out.p, 2 * EMURX_HIST_BINS * 8, D2H, st)) &&
+    // every result in one copy: records, descriptors, packed queues, status, qoff, histogram
+    ok = EMURX_HIP_OK(hipMemcpyAsync(s.h_res.p, s.d_res.p, s.res_bytes, D2H, st)) &&
          EMURX_HIP_OK(hipEventRecord(s.done, st));
     if (!ok) return EMURX_EDEVICE;
     s.small = false;

@@ -1165,6 +1165,9 @@ struct Probe {
     const uint32_t* ctab;
     Bucket ne;
 };
+#ifndef EMURX_UNIHASH
+#define EMURX_UNIHASH 0
+#endif
 __device__ __forceinline__ Probe probe_issue(const emurx_dev_tables& T, const Rec& r, const LKey& k) {
     Probe p;
     const uint32_t key = k.key;
@@ -1175,7 +1178,19 @@ __device__ __forceinline__ Probe probe_issue(const emurx_dev_tables& T, const Re
                 (((k.kw[3] >> 8) & 0xff) << 24);
         p.mhi = ((k.kw[3] >> 16) & 0xff) | ((k.kw[3] >> 24) << 8);
     }
+#if EMURX_UNIHASH
+    // a wave whose frames share one CTunnelKey (one port's untagged or one-VLAN traffic) or
+    // one MAC key hashes it once, on the scalar unit (build variant for A/B)
+    const uint32_t u0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.vport),
+                   u1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.vlan0),
+                   u2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.vlan1);
+    const bool tku = __ballot(r.vport != u0 || r.vlan0 != u1 || r.vlan1 != u2) == 0;
+    uint32_t tk;
+    if (tku) tk = emurx_tk_hash(u0, u1, u2);  // wave-uniform branch: scalar arithmetic
+    else tk = emurx_tk_hash(r.vport, r.vlan0, r.vlan1);
+#else
     const uint32_t tk = emurx_tk_hash(r.vport, r.vlan0, r.vlan1);  // CTunnelKey words
+#endif
     p.nb = tk & T.ns_mask;
     p.ne = ld_bucket(T.ns_tab, p.nb);
     p.cbk = 0;
@@ -1186,7 +1201,15 @@ __device__ __forceinline__ Probe probe_issue(const emurx_dev_tables& T, const Re
     uintptr_t tm = (uintptr_t)T.mac_tab, t4 = (uintptr_t)T.ip4_tab, t6 = (uintptr_t)T.ip6_tab;
     asm volatile("" : "+s"(tm), "+s"(t4), "+s"(t6));
     if (key == kMac || key == kEui) {
+#if EMURX_UNIHASH
+        const uint32_t m0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.mlo),
+                       m1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.mhi);
+        const bool mu = tku && __ballot(p.mlo != m0 || p.mhi != m1) == 0;
+        if (mu) p.cbk = emurx_mac_hash((uint32_t)__builtin_amdgcn_readfirstlane((int)tk), m0, m1) & T.mac_mask;
+        else p.cbk = emurx_mac_hash(tk, p.mlo, p.mhi) & T.mac_mask;
+#else
         p.cbk = emurx_mac_hash(tk, p.mlo, p.mhi) & T.mac_mask;
+#endif
         p.ctab = reinterpret_cast<const uint32_t*>(tm);
     } else if (key == kIp4) {
         p.cbk = emurx_ip4_hash(tk, k.kw[0]) & T.ip4_mask;
