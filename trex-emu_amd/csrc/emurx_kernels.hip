@@ -142,11 +142,6 @@ __device__ __forceinline__ uint64_t match_lanes(uint32_t v, uint64_t act) {
     return m;
 }
 
-// EMURX_EARLYPF (build variant, A/B): touch each frame's MAC-table bucket before the parse
-#ifndef EMURX_EARLYPF
-#define EMURX_EARLYPF 0
-#endif
-
 // The workgroup's small LDS arrays of one tile
 struct TileLds {
     uint32_t wcnt[kWaves][16];                   // queue counts per wave
@@ -204,26 +199,10 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
     if (sg.staged) {  // wave-uniform branch
         if (valid) {
             LdsSrc s{reinterpret_cast<const uint8_t*>(slab), slab, wv * kStage + (off - sg.start)};
-#if EMURX_EARLYPF
-            // the frame's MAC-table bucket touched before the parse (the CTunnelKey and the
-            // destination MAC are in the L2 header), so the lookup after it finds the line in
-            // L2; only when the MAC table is larger than the caches hold (wave-uniform)
-            uint32_t touch = 0;
-            if (kClassify && T.mac_mask >= (1u << 16)) {  // >= 4 MiB: one XCD's L2
-                uint32_t v0, v1;
-                l2_vlans(len, be32(s, 12), be32(s, 16), v0, v1);
-                const uint32_t tk = emurx_tk_hash(vport, v0, v1);
-                const uint32_t b = emurx_mac_hash(tk, le32(s, 0), s.u8(4) | (s.u8(5) << 8)) & T.mac_mask;
-                touch = gld4(T.mac_tab + (size_t)b * EMURX_BUCKET_WORDS);
-            }
-#endif
             parse_flat(s, len, vport, T.cb_mask, r);
             STAMP(3);
             if (kClassify) classify(s, len, T, r);
             if (kKind == 2) pack_lookup(s, len, r, i, r.status == EMURX_ST_OK, lrec);
-#if EMURX_EARLYPF
-            asm volatile("" ::"v"(touch));  // keeps the touch load (its value is not needed)
-#endif
         }
     } else {
         const uint32_t head = (uint32_t)((uintptr_t)(a.frames + off) & 15);
