@@ -285,6 +285,7 @@ def main():
         out["host_inclusive"] = host_path_rate(rx, w)
     if a.tx_path:
         out["tx_zmq"] = tx_zmq_rate(rx, w, torch)
+        out["tx_checksum"] = tx_csum_rate(rx, w, torch)
     if a.table_updates and rank == 0:
         out["table_updates"] = table_update_cost(a, rx, w, torch)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -1212,6 +1213,58 @@ def tx_zmq_rate(rx, w, torch, reps=50):
     return {"frames": n, "msgs": nm, "bytes_out": total, "ms_per_call": round(ms, 4),
             "mpkts": round(n / ms / 1e3, 1), "gbs_moved": round(moved / ms / 1e6, 1),
             "note": "launch sequence: leaf + compose/descend per level + finish + write"}
+
+
+def tx_csum_rate(rx, w, torch, reps=50):
+    """Device tx checksum generation (emurx_tx_checksum_dev: the IPv4 header checksum and the
+    L4 checksum of TCP / UDP / ICMP over IPv4 and IPv6, as the plugins' send paths rewrite
+    them) over the batch's frames, in place on a device copy, device-resident in and out; the
+    tx descriptors come from the library's own parse of the same frames (its records' L3 / L4
+    offsets and next header).  CUDA events on torch's stream around `reps` calls.  Bytes per
+    call: the frames read (every byte of a checksummed frame) + the 16-byte descriptors."""
+    import numpy as np
+    from emurx import abi
+    n = len(w["desc"])
+    buf = torch.from_numpy(np.ascontiguousarray(w["buf"]).view(np.uint8).copy()).to("cuda")
+    desc = torch.from_numpy(np.ascontiguousarray(w["desc"]).view(np.uint8).copy()).to("cuda")
+    rec = torch.empty(n * abi.REC_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    qcap = abi.queue_cap(n)
+    ql = torch.empty(abi.NUM_QUEUES * qcap, dtype=torch.int32, device="cuda")
+    tc = torch.empty(((n + 255) // 256) * 16, dtype=torch.int32, device="cuda")
+    hist = torch.zeros(abi.HIST_SHARDS * 2 * abi.HIST_BINS, dtype=torch.int64, device="cuda")
+    rx.classify_dev(buf, desc, n, rec, ql, qcap, tc, hist, classify=False)
+    torch.cuda.synchronize()
+    r = rec.cpu().numpy().view(abi.REC_DTYPE)
+    d = w["desc"]
+    ok = (r["status"] == 0) & (r["l3"] > 0) & (r["l4"] > 0)
+    ver = np.asarray(w["buf"])[d["off"].astype(np.int64) + r["l3"].astype(np.int64)] >> 4
+    nh = r["next_hdr"].astype(np.int64)
+    v4, v6 = ok & (ver == 4), ok & (ver == 6)
+    kind = np.zeros(n, np.int64)
+    kind[v4 & (nh == 6)], kind[v4 & (nh == 17)], kind[v4 & (nh == 1)] = abi.TX_L4_TCP4, abi.TX_L4_UDP4, abi.TX_L4_ICMP4
+    kind[v6 & (nh == 6)], kind[v6 & (nh == 17)], kind[v6 & (nh == 58)] = abi.TX_L4_TCP6, abi.TX_L4_UDP6, abi.TX_L4_ICMP6
+    sel = np.nonzero(kind > 0)[0]
+    td = np.zeros(len(sel), abi.TX_DESC_DTYPE)
+    td["off"], td["len"] = d["off"][sel], d["len"][sel]
+    td["l3"], td["l4"] = r["l3"][sel], r["l4"][sel]
+    td["osize"] = np.where(v6[sel], r["l4"][sel].astype(np.int64) - r["l3"][sel] - 40, 0)
+    td["ops"] = (kind[sel] << abi.TX_L4_SHIFT) | np.where(v4[sel], abi.TX_IPV4_HDR, 0)
+    m = len(sel)
+    tdd = torch.from_numpy(td.view(np.uint8).copy()).to("cuda")
+    st = torch.cuda.current_stream()
+    for _ in range(3):
+        rx.tx_checksum_dev(buf, tdd, m, stream=st.cuda_stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        rx.tx_checksum_dev(buf, tdd, m, stream=st.cuda_stream)
+    e1.record(st)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    moved = int(d["len"][sel].astype(np.int64).sum()) + 16 * m
+    return {"frames": m, "ms_per_call": round(ms, 4), "mpkts": round(m / ms / 1e3, 1),
+            "gbs_moved": round(moved / ms / 1e6, 1), "frac_of_8tbs": round(moved / ms / 1e6 / 8000.0, 4),
+            "note": "one k_tx_csum launch per call, in place; descriptors from the library's parse"}
 
 
 if __name__ == "__main__":
