@@ -738,13 +738,16 @@ __device__ __forceinline__ uint32_t dpp_row_sum(uint32_t v) {
 #ifndef EMURX_COOP_NT
 #define EMURX_COOP_NT 0
 #endif
-__device__ __forceinline__ void coop_checksum_rows(Rec& r, const uint8_t* f, uint32_t* wsum) {
+// The wave's spans [span, span + n) (lanes with mine set) summed by its four 16-lane rows in
+// the dword form of glb_sum (sad of 16-bit halves, bytes outside the span masked): returns this
+// lane's sum (0 when not mine).  wsum: kWave words of LDS owned by the wave.  Called converged.
+__device__ __forceinline__ uint32_t coop_span_sum(const uint8_t* span, uint32_t n, bool mine, uint32_t* wsum) {
     constexpr uint32_t kRound = 16 * kCoopVec;  // vectors of one span per row round
     const uint32_t lane = lane_id(), l16 = lane & 15, row = lane >> 4;
-    const bool mine = r.dlen != 0;
+    mine = mine && n != 0;
     const uint64_t mm = __ballot(mine);
-    if (!mm) return;
-    const uintptr_t a = (uintptr_t)(f + r.dstart), e = a + r.dlen;
+    if (!mm) return 0;
+    const uintptr_t a = (uintptr_t)span, e = a + n;
     const uint32_t nv = mine ? (uint32_t)((((e + 15) & ~(uintptr_t)15) - (a & ~(uintptr_t)15)) >> 4) : 0u;
     const uint32_t rounds = (nv + kRound - 1) / kRound;
     uint32_t incl = rounds;
@@ -804,8 +807,15 @@ __device__ __forceinline__ void coop_checksum_rows(Rec& r, const uint8_t* f, uin
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return mine ? wsum[lane] : 0u;
+}
+// the rx window path's deferred L4 checksums (r.dstart / r.dlen of each lane's frame f)
+__device__ __forceinline__ void coop_checksum_rows(Rec& r, const uint8_t* f, uint32_t* wsum) {
+    const bool mine = r.dlen != 0;
+    if (!__ballot(mine)) return;
+    const uint32_t T = coop_span_sum(f + r.dstart, r.dlen, mine, wsum);
     if (mine) {
-        settle_deferred(r, csum_ok(wsum[lane], r.dfail >> 16, r.dpcs));  // parity of the span's start
+        settle_deferred(r, csum_ok(T, r.dfail >> 16, r.dpcs));  // parity of the span's start
         r.dlen = 0;
     }
 }

@@ -35,13 +35,17 @@ __device__ __forceinline__ void put_be16(uint8_t* p, uint32_t v) {
     p[1] = (uint8_t)v;
 }
 
-// the bytes of one frame: global memory (a lane's own frame, the fallback) or the wave's LDS
+// the bytes of one frame: global memory (a lane's own frame, the wide path) or the wave's LDS
 // slab (the wave's frames staged by LDS-DMA; an LDS byte index is the global address mod 16
 // plus a multiple of 16, so every parity the sums depend on is the same)
-struct TxGlb {
+// the global source with the L4 span's sum taken beforehand by the wave's rows (coop_span_sum)
+struct TxGlbPre {
     const uint8_t* p;
+    uint32_t s0, n, pre;  // sum(s0, n) == pre
     __device__ __forceinline__ uint32_t u8(uint32_t a) const { return gld1(p + a); }
-    __device__ __forceinline__ uint32_t sum(uint32_t a, uint32_t n) const { return glb_sum(p + a, n); }
+    __device__ __forceinline__ uint32_t sum(uint32_t a, uint32_t m) const {
+        return a == s0 && m == n ? pre : glb_sum(p + a, m);
+    }
     __device__ __forceinline__ uint32_t at(uint32_t a) const { return (uint32_t)(uintptr_t)(p + a); }
 };
 struct TxLds {
@@ -138,7 +142,8 @@ __device__ __forceinline__ bool tx_sums(const S& s, uint32_t len, uint32_t l3, u
 
 // One frame per lane.  A wave whose frames' byte range fits its 6 KiB LDS slab copies the
 // range in by LDS-DMA (1 KiB rows, coalesced, as k_rx stages) and sums from LDS; a wider wave
-// sums each lane's frame from global memory.  The only stores are the checksum fields.
+// sums its L4 spans cooperatively (coop_span_sum, the rx window path's rows) and the rest of
+// each frame from global memory.  The only stores are the checksum fields.
 constexpr uint32_t kTxSlab = 6144;
 __global__ __launch_bounds__(kBlock) void k_tx_csum(uint8_t* __restrict__ frames,
                                                     const emurx_tx_desc* __restrict__ desc, uint32_t n,
@@ -171,7 +176,12 @@ __global__ __launch_bounds__(kBlock) void k_tx_csum(uint8_t* __restrict__ frames
         const TxLds s{reinterpret_cast<const uint8_t*>(s_slab[wv]), s_slab[wv], d.x - start};
         ok = live && tx_sums(s, len, l3, l4, osize, ops, nhx, hcs, lcs, fo);
     } else {
-        ok = live && tx_sums(TxGlb{frames + d.x}, len, l3, l4, osize, ops, nhx, hcs, lcs, fo);
+        // frames too wide to stage (long L4 spans): the spans summed cooperatively, 16 lanes per
+        // span and 1 KiB per row round, the rest of each frame's work per lane
+        const bool want = live && (ops >> EMURX_TX_L4_SHIFT) != 0 && l4 < len;
+        const uint32_t pre = coop_span_sum(frames + d.x + l4, want ? len - l4 : 0u, want, s_slab[wv]);
+        ok = live && tx_sums(TxGlbPre{frames + d.x, l4, want ? len - l4 : 0u, pre}, len, l3, l4, osize, ops, nhx, hcs,
+                             lcs, fo);
     }
     if (!live) return;
     if (status) status[i] = ok ? EMURX_TX_OK : EMURX_TX_RANGE;
