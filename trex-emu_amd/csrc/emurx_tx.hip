@@ -38,15 +38,15 @@ __device__ __forceinline__ void put_be16(uint8_t* p, uint32_t v) {
 // the bytes of one frame: global memory (a lane's own frame, the wide path) or the wave's LDS
 // slab (the wave's frames staged by LDS-DMA; an LDS byte index is the global address mod 16
 // plus a multiple of 16, so every parity the sums depend on is the same)
-// the global source with the L4 span's sum taken beforehand by the wave's rows (coop_span_sum)
-struct TxGlbPre {
-    const uint8_t* p;
+// a wide wave's frame: its first bytes in the lane's LDS window (the rx window path's WinSrc:
+// headers read there, the rest from global memory), the L4 span's sum taken beforehand by
+// the wave's rows (coop_span_sum)
+struct TxWinPre {
+    WinSrc w;
     uint32_t s0, n, pre;  // sum(s0, n) == pre
-    __device__ __forceinline__ uint32_t u8(uint32_t a) const { return gld1(p + a); }
-    __device__ __forceinline__ uint32_t sum(uint32_t a, uint32_t m) const {
-        return a == s0 && m == n ? pre : glb_sum(p + a, m);
-    }
-    __device__ __forceinline__ uint32_t at(uint32_t a) const { return (uint32_t)(uintptr_t)(p + a); }
+    __device__ __forceinline__ uint32_t u8(uint32_t a) const { return w.u8(a); }
+    __device__ __forceinline__ uint32_t sum(uint32_t a, uint32_t m) const { return a == s0 && m == n ? pre : w.sum(a, m); }
+    __device__ __forceinline__ uint32_t at(uint32_t a) const { return w.at(a); }
 };
 struct TxLds {
     const uint8_t* b8;
@@ -142,13 +142,14 @@ __device__ __forceinline__ bool tx_sums(const S& s, uint32_t len, uint32_t l3, u
 
 // One frame per lane.  A wave whose frames' byte range fits its 6 KiB LDS slab copies the
 // range in by LDS-DMA (1 KiB rows, coalesced, as k_rx stages) and sums from LDS; a wider wave
-// sums its L4 spans cooperatively (coop_span_sum, the rx window path's rows) and the rest of
-// each frame from global memory.  The only stores are the checksum fields.
+// stages a header window per lane and sums its L4 spans cooperatively (coop_span_sum, the rx
+// window path's rows).  The only stores are the checksum fields.
 constexpr uint32_t kTxSlab = 6144;
 __global__ __launch_bounds__(kBlock) void k_tx_csum(uint8_t* __restrict__ frames,
                                                     const emurx_tx_desc* __restrict__ desc, uint32_t n,
                                                     uint8_t* __restrict__ status) {
     __shared__ __attribute__((aligned(16))) uint32_t s_slab[kWaves][(kTxSlab + 32) / 4];
+    __shared__ uint32_t s_wsum[kWaves][kWave];  // coop_span_sum's per-span sums
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x, lane = lane_id(), wv = threadIdx.x / kWave;
     const bool live = i < n;
     const uint4 d = live ? gld16(desc + i) : make_uint4(0, 0, 0, 0);  // {off} {len | l3} {l4 | osize} {ops | nh}
@@ -176,12 +177,28 @@ __global__ __launch_bounds__(kBlock) void k_tx_csum(uint8_t* __restrict__ frames
         const TxLds s{reinterpret_cast<const uint8_t*>(s_slab[wv]), s_slab[wv], d.x - start};
         ok = live && tx_sums(s, len, l3, l4, osize, ops, nhx, hcs, lcs, fo);
     } else {
-        // frames too wide to stage (long L4 spans): the spans summed cooperatively, 16 lanes per
-        // span and 1 KiB per row round, the rest of each frame's work per lane
+        // frames too wide to stage whole (long L4 spans): each lane's first kTxWinVec vectors in
+        // the slab (vector k of lane l at byte k * 1 KiB + l * 16, one DMA row per k), the L4
+        // spans summed cooperatively (16 lanes per span, 1 KiB per row round)
+        constexpr uint32_t kTxWinVec = kTxSlab / 16 / kWave;
+        const uintptr_t fa = (uintptr_t)(frames + d.x);
+        const uint4* src = reinterpret_cast<const uint4*>(fa & ~(uintptr_t)15);
+        const uint32_t head = (uint32_t)(fa & 15), nv = live && len ? (head + len + 15) >> 4 : 0u;
+        uint4* dst = reinterpret_cast<uint4*>(s_slab[wv]);
+#pragma unroll
+        for (uint32_t k = 0; k < kTxWinVec; ++k)
+            if (k < nv)
+                __builtin_amdgcn_global_load_lds(src + k, (__attribute__((address_space(3))) void*)(dst + k * kWave), 16, 0,
+                                                 0);
         const bool want = live && (ops >> EMURX_TX_L4_SHIFT) != 0 && l4 < len;
-        const uint32_t pre = coop_span_sum(frames + d.x + l4, want ? len - l4 : 0u, want, s_slab[wv]);
-        ok = live && tx_sums(TxGlbPre{frames + d.x, l4, want ? len - l4 : 0u, pre}, len, l3, l4, osize, ops, nhx, hcs,
-                             lcs, fo);
+        const uint32_t pre = coop_span_sum(frames + d.x + l4, want ? len - l4 : 0u, want, s_wsum[wv]);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the windows landed
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const WinSrc w{reinterpret_cast<const uint8_t*>(s_slab[wv]), s_slab[wv], lane * 16, head,
+                       min(kTxWinVec * 16 - head, len), frames + d.x};
+        ok = live && tx_sums(TxWinPre{w, l4, want ? len - l4 : 0u, pre}, len, l3, l4, osize, ops, nhx, hcs, lcs, fo);
     }
     if (!live) return;
     if (status) status[i] = ok ? EMURX_TX_OK : EMURX_TX_RANGE;
