@@ -187,14 +187,18 @@ void Mirror::ns_slot_put(const K5& k, Entry& e) {
 }
 // the client's MAC and plugin mask ride in the MAC slot's free upper half and in the IP
 // slots' spare words: PluginCtx.Get and IsUnicastToMe need no second read
+// the upper half of a client slot's MAC word: the plugin mask and, in its top bit
+// (EMURX_CPL_CTX), whether the client has a TransportCtx (the transport flow rule reads it
+// from the MAC slot it has already loaded instead of the client-info table)
+static uint32_t slot_half(const ClientInfo& c) { return (c.plugins & 0x7fffu) | (c.has_ctx ? EMURX_CPL_CTX : 0u); }
 static void mac_words(const ClientInfo& c, uint32_t& lo, uint32_t& hip) {
     lo = le32(c.mac);
-    hip = (uint32_t)(c.mac[4] | (c.mac[5] << 8)) | ((c.plugins & 0xffffu) << 16);
+    hip = (uint32_t)(c.mac[4] | (c.mac[5] << 8)) | (slot_half(c) << 16);
 }
 void Mirror::mac_slot_put(const K5& k, Entry& e) {
     e.slot = kNoSlot;
     if (!owned_ns(k.w[0])) return;
-    const uint32_t s[4] = {k.w[0], k.w[1], k.w[2] | ((cl[e.id].plugins & 0xffffu) << 16), e.id};
+    const uint32_t s[4] = {k.w[0], k.w[1], k.w[2] | (slot_half(cl[e.id]) << 16), e.id};
     e.slot = mac_t.put(emurx_mac_hash(tk_of(k.w[0]), k.w[1], k.w[2]), s);
 }
 void Mirror::ip4_slot_put(const K5& k, Entry& e) {

@@ -1299,8 +1299,8 @@ __device__ __forceinline__ void resolve_done(const emurx_dev_tables& T, Rec& r, 
         if ((cb == EMURX_CB_TCP || cb == EMURX_CB_UDP) &&
             ((r.flags & EMURX_FLAG_LK_MASK) >> EMURX_FLAG_LK_SHIFT) == EMURX_LK_CLIENT) {
             // GetTransportCtx() == nil -> the handler returns -1 (PluginTransClient :73-80);
-            // with no TransportCtx on these tables (ft_on 0) no client info is read
-            r.flow = T.ft_on && (client_info(T, c.x).ctx & 1u) ? flow(c.x) : EMURX_FLOW_NO_CTX;
+            // the MAC slot carries the client's TransportCtx bit, so no client info is read
+            r.flow = T.ft_on && (c.y & EMURX_CPL_CTX) ? flow(c.x) : EMURX_FLOW_NO_CTX;  // the MAC slot's ctx bit
         }
         return;
     }
@@ -1410,7 +1410,7 @@ __device__ __forceinline__ void resolve_done_flat(const emurx_dev_tables& T, Rec
     // transport: the client's TransportCtx decides (plugin_transport.go:109-114, :73-80)
     const bool trans = key == kMac && (cb == EMURX_CB_TCP || cb == EMURX_CB_UDP) && lk == EMURX_LK_CLIENT;
     if (trans) r.flow = EMURX_FLOW_NO_CTX;
-    if (T.ft_on && any_lane(trans) && trans && (client_info(T, cid).ctx & 1u)) r.flow = flow(cid);
+    if (T.ft_on && any_lane(trans) && trans && (cpl & EMURX_CPL_CTX)) r.flow = flow(cid);
 }
 
 // GetNs + the callback's client rule against the tables (both bucket reads in flight together)

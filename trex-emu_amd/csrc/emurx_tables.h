@@ -33,6 +33,7 @@
 // it and only a bucket with an EMPTY slot ends a chain
 #define EMURX_TOMB 0xFFFFFFFEu
 #define EMURX_BUCKET_WORDS 16u  // 64 B
+#define EMURX_CPL_CTX 0x8000u   // client slot plugin half: the client has a TransportCtx
 
 // 32-bit mix of up to five key words (murmur3 finaliser over a multiplicative combine).
 EMURX_HD uint32_t emurx_fmix(uint32_t h) {
@@ -56,7 +57,8 @@ EMURX_HD uint32_t emurx_hash(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uin
 //  ip4  [8]: ns_id, ipv4 bytes LE, mac[0..3], mac[4..5] | client_plugins << 16, 0, 0, 0, client_id
 //  ip6  [8]: ns_id, ip[0..3], ip[4..7], ip[8..11], ip[12..15], mac[0..3], mac[4..5] | client_plugins << 16,
 //            client_id
-//  (the client's MAC and plugin mask in the IP slots answer IsUnicastToMe / PluginCtx.Get)
+//  (the client's MAC and plugin mask in the IP slots answer IsUnicastToMe / PluginCtx.Get;
+//  the mask's top bit, EMURX_CPL_CTX, is set when the client has a TransportCtx)
 //  ns_info   [4]: plugin_mask, first_client, 0, 0            (dense, indexed by ns id)
 //  ci   [8]: client_id, plugin_mask, ra (bit0 has_ra, bits 8..15 prefix_len), ra_prefix[0..3],
 //            ra_prefix[4..7], has_transport_ctx, 0, 0      (hashed by client id, 2 per bucket)
