@@ -111,12 +111,17 @@ __device__ __forceinline__ void tx_wave_sync() {
 __device__ __forceinline__ uint32_t tx_load_children(const uint32_t* __restrict__ Xc, const uint32_t* __restrict__ Mc,
                                                      const unsigned long long* __restrict__ Bc, uint32_t nc, uint32_t p,
                                                      TxUnitLds& S) {
+    // the children's rows straight into LDS by LDS-DMA (one 256-byte row per instruction, all
+    // in flight before one wait) instead of a load and a store per row and lane
     const uint32_t lane = lane_id(), c0 = p * 64, cn = min(nc - c0, 64u);
     for (uint32_t c = 0; c < cn; ++c) {
-        S.sx[c][lane] = Xc[(size_t)(c0 + c) * kWave + lane];
-        S.sm[c][lane] = Mc[(size_t)(c0 + c) * kWave + lane];
+        __builtin_amdgcn_global_load_lds(Xc + (size_t)(c0 + c) * kWave + lane,
+                                         (__attribute__((address_space(3))) void*)&S.sx[c][0], 4, 0, 0);
+        __builtin_amdgcn_global_load_lds(Mc + (size_t)(c0 + c) * kWave + lane,
+                                         (__attribute__((address_space(3))) void*)&S.sm[c][0], 4, 0, 0);
     }
     S.sb[lane] = lane < cn ? Bc[c0 + lane] : 0ull;
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the rows landed
     tx_wave_sync();
     return cn;
 }
