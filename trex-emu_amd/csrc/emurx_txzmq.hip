@@ -102,7 +102,6 @@ struct TxUnitLds {
     unsigned long long sb[64];
     uint32_t se[64], smb[64];
     unsigned long long sbb[64];
-    uint32_t bx[8][kWave], bm[8][kWave];  // the 8 blocks of 8 children, composed (tx_blocks)
 };
 __device__ __forceinline__ void tx_wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -126,41 +125,16 @@ __device__ __forceinline__ uint32_t tx_load_children(const uint32_t* __restrict_
     tx_wave_sync();
     return cn;
 }
-// the children in blocks of 8 (lane = entry): each block's 8 functions composed, the 8 blocks'
-// chains interleaved (8 dependent LDS steps instead of 64) -> S.bx / S.bm; returns the blocks
-__device__ __forceinline__ uint32_t tx_blocks(uint32_t cn, TxUnitLds& S) {
-    const uint32_t lane = lane_id(), nb = (cn + 7) / 8;
-    uint32_t e[8], m[8];
-#pragma unroll
-    for (uint32_t b = 0; b < 8; ++b) e[b] = lane, m[b] = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < 8; ++j)
-#pragma unroll
-        for (uint32_t b = 0; b < 8; ++b) {
-            const uint32_t c = b * 8 + j;
-            if (c < cn) {
-                m[b] += S.sm[c][e[b]];
-                e[b] = S.sx[c][e[b]];
-            }
-        }
-#pragma unroll
-    for (uint32_t b = 0; b < 8; ++b)
-        if (b < nb) S.bx[b][lane] = e[b], S.bm[b][lane] = m[b];
-    tx_wave_sync();
-    return nb;
-}
-// 64 children -> parent p (one wave): X/M composed along the chain for every entry (the block
-// functions, then the 8 blocks), B summed
+// 64 children -> parent p (one wave): X/M composed along the chain for every entry, B summed
 __device__ __forceinline__ void tx_compose(const uint32_t* __restrict__ Xc, const uint32_t* __restrict__ Mc,
                                            const unsigned long long* __restrict__ Bc, uint32_t nc, uint32_t p,
                                            uint32_t* __restrict__ Xp, uint32_t* __restrict__ Mp,
                                            unsigned long long* __restrict__ Bp, TxUnitLds& S) {
     const uint32_t lane = lane_id(), cn = tx_load_children(Xc, Mc, Bc, nc, p, S);
-    const uint32_t nb = tx_blocks(cn, S);
     uint32_t e = lane, m = 0;
-    for (uint32_t b = 0; b < nb; ++b) {
-        m += S.bm[b][e];
-        e = S.bx[b][e];
+    for (uint32_t c = 0; c < cn; ++c) {
+        m += S.sm[c][e];
+        e = S.sx[c][e];
     }
     Xp[(size_t)p * kWave + lane] = e;
     Mp[(size_t)p * kWave + lane] = m;
@@ -170,10 +144,9 @@ __device__ __forceinline__ void tx_compose(const uint32_t* __restrict__ Xc, cons
         Bp[p] = b;
     }
 }
-// parent p -> its 64 children (one wave): actual entry, message base, byte base of each child
-// (the block functions, lane 0 through the 8 blocks, then each lane through at most 7 children
-// of its block).  info != nullptr: p is the root (entry 0, bases 0), and its message count and
-// total size go to info and msg_off[n_msgs]
+// parent p -> its 64 children (one wave): actual entry, message base, byte base of each child.
+// info != nullptr: p is the root (entry 0, bases 0), and its message count and total size go to
+// info and msg_off[n_msgs]
 __device__ __forceinline__ void tx_descend(const uint32_t* __restrict__ Xc, const uint32_t* __restrict__ Mc,
                                            const unsigned long long* __restrict__ Bc, uint32_t nc, uint32_t p,
                                            const uint32_t* __restrict__ Ep, const uint32_t* __restrict__ MBp,
@@ -189,31 +162,22 @@ __device__ __forceinline__ void tx_descend(const uint32_t* __restrict__ Xc, cons
         info[1] = total;
         msg_off[nm] = total;
     }
-    const uint32_t nb = tx_blocks(cn, S);
-    if (lane == 0) {  // each block's entry and message base; each child's byte base
+    if (lane == 0) {
         uint32_t e = Ep ? Ep[p] : 0u, mb = MBp ? MBp[p] : 0u;
-        for (uint32_t b = 0; b < nb; ++b) {
-            S.se[b] = e;
-            S.smb[b] = mb;
-            mb += S.bm[b][e];
-            e = S.bx[b][e];
-        }
         unsigned long long bb = BBp ? BBp[p] : 0ull;
         for (uint32_t c = 0; c < cn; ++c) {
+            S.se[c] = e;
+            S.smb[c] = mb;
             S.sbb[c] = bb;
+            mb += S.sm[c][e];
+            e = S.sx[c][e];
             bb += S.sb[c];
         }
     }
     tx_wave_sync();
     if (lane < cn) {
-        const uint32_t b = lane / 8;
-        uint32_t e = S.se[b], mb = S.smb[b];
-        for (uint32_t c = b * 8; c < lane; ++c) {
-            mb += S.sm[c][e];
-            e = S.sx[c][e];
-        }
-        Ec[c0 + lane] = e;
-        MBc[c0 + lane] = mb;
+        Ec[c0 + lane] = S.se[lane];
+        MBc[c0 + lane] = S.smb[lane];
         BBc[c0 + lane] = S.sbb[lane];
     }
 }
