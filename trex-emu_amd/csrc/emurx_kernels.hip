@@ -439,6 +439,9 @@ int emurx_launch_batch(const uint8_t* frames, const emurx_desc* desc, uint32_t n
                        const emurx_route_args* rt) {
     using namespace emurx;
     hipError_t e = hipSuccess;
+#ifndef EMURX_RX_LDS_PAD  // measurement builds only: unused LDS per workgroup, to cap k_rx's occupancy
+#define EMURX_RX_LDS_PAD 0
+#endif
     if (ev && !EMURX_HIP_OK(hipEventRecord(ev[0], st))) return -1;
     if (n) {
         const uint32_t ntiles = (n + EMURX_QUEUE_TILE - 1) / EMURX_QUEUE_TILE;
@@ -449,7 +452,7 @@ int emurx_launch_batch(const uint8_t* frames, const emurx_desc* desc, uint32_t n
         auto k = kind == 1 ? (narrow ? k_rx<1, kStageNarrow> : k_rx<1, kStageWide>)
                : kind == 2 ? (narrow ? k_rx<2, kStageNarrow> : k_rx<2, kStageWide>)
                            : (narrow ? k_rx<0, kStageNarrow> : k_rx<0, kStageWide>);
-        e = emurx_launch(k, dim3(ntiles), dim3(kBlock), 0, st, args);
+        e = emurx_launch(k, dim3(ntiles), dim3(kBlock), EMURX_RX_LDS_PAD, st, args);
     }
     if (!EMURX_HIP_OK(e)) return -1;
     return ev && !EMURX_HIP_OK(hipEventRecord(ev[1], st)) ? -1 : 0;

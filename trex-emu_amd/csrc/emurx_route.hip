@@ -345,7 +345,15 @@ int emurx_launch_lookup(const emurx_lookup_rec* recv, const uint32_t* recv_count
     using namespace emurx;
     if (!n_parts || !cap) return 0;
     if (n_parts > 65535) return -1;
-    return EMURX_HIP_OK(emurx_launch(k_lookup, dim3((cap + kBlock - 1) / kBlock, n_parts), dim3(kBlock), 0, st, recv,
+// k_lookup's occupancy is capped at 4 workgroups (16 waves) per CU by unused LDS: its 16 KiB of
+// record rows + 24 KiB = 40 KiB of the CU's 160 KiB.  Its probes are random table lines; more
+// waves in flight only queue more of them, and beside the next batch's k_rx<2> on the other
+// stream the freed slots serve that kernel (6 workgroups 98.4 us per 2M records,
+// 4: 96.9 us, the pipelined partitioned step +3-4.5 %; at an owner of 8, 74.3 -> 72.3 us)
+#ifndef EMURX_LOOKUP_LDS_PAD
+#define EMURX_LOOKUP_LDS_PAD (24 * 1024)
+#endif
+    return EMURX_HIP_OK(emurx_launch(k_lookup, dim3((cap + kBlock - 1) / kBlock, n_parts), dim3(kBlock), EMURX_LOOKUP_LDS_PAD, st, recv,
                                      recv_count, n_parts, cap, T, out, flow))
                ? 0
                : -1;
