@@ -142,7 +142,14 @@ __global__ __launch_bounds__(kScanThreads) void k_route_scan(uint32_t* __restric
 // length): a wave whose unkeyed frames' byte range fits kOcStage bytes copies that range into
 // LDS with coalesced LDS-DMA (as k_rx stages) and reads each frame's bytes 12..19 there (a
 // per-lane gather of one line per frame ran at the random-line rate); wider waves gather.
-constexpr uint32_t kOcStage = 6144;
+// 2 KiB per wave: 8 workgroups per CU (the wave limit) instead of 6 with 6 KiB. Keyed
+// descriptors (the production path: the device framing walk keys them) read no frame byte, and
+// the kernel falls 10.7 -> 8.0 us per 2M frames; unkeyed waves wider than 2 KiB gather instead
+// (config D unkeyed: 39.2 -> 46.6 us; DESIGN.md §6 round 4, profiles/r04/ab_owner_count/)
+#ifndef EMURX_OC_STAGE
+#define EMURX_OC_STAGE 2048
+#endif
+constexpr uint32_t kOcStage = EMURX_OC_STAGE;
 __global__ __launch_bounds__(kBlock) void k_owner_count(const uint8_t* __restrict__ frames,
                                                         const emurx_desc* __restrict__ desc, uint32_t n,
                                                         uint32_t n_parts, uint32_t* __restrict__ tile_cnt,
