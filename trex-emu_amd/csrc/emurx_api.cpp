@@ -192,7 +192,7 @@ struct emurx_ctx {
     // k_rx staging slab per launch (emurx_launch_batch): the narrow 6 KiB slab runs 6
     // workgroups per CU instead of 5, but a wave whose frames span 6-7 KiB then takes the
     // slower window path.  Sampled tiles report how many of their waves fall in that band
-    // into device words; the first launch and then at most every 8th copies them to pinned
+    // into device words; the first launch and then at most every `stage_every`-th copies them to pinned
     // memory behind itself (stream order, an event, no synchronisation), and the first
     // launch after the copy has landed decides.  The kernel
     // writing host memory directly was tried: host reads of lines the GPU keeps writing made
@@ -202,6 +202,11 @@ struct emurx_ctx {
     uint32_t stage_gen = 0, stage_mode = 0;  // 0 auto, 1 wide, 2 narrow
     bool stage_copy = false, stage_pending = false;
     uint32_t stage_copy_gen = 0;
+    // launches between copy-backs: 8, doubled after each decision that repeats the one before
+    // it (from the second in a row), up to 256; back to 8 when a decision changes the slab.  A
+    // copy-back is a blit between two k_rx launches on the caller's stream (it breaks the
+    // overlap with the next launch): config B's 20-step command ran 2-3 % slower with one per 8
+    uint32_t stage_every = 8, stage_same = 0;
     hipEvent_t stage_ev = nullptr;
     bool stage_narrow = false;
     uint32_t last_stage = 0;
@@ -387,10 +392,20 @@ bool choose_stage_(emurx_t* h) {
         // a wave in the 6-7 KiB band costs several staged waves on the window path; below
         // 1% of the sampled waves the extra workgroup per CU wins (configs B, E), above it
         // loses (C)
-        if (waves) h->stage_narrow = mid * 100 <= waves;
+        if (waves) {
+            const bool narrow = mid * 100 <= waves;
+            if (narrow != h->stage_narrow) {
+                h->stage_same = 0;
+                h->stage_every = 8;
+            } else if (++h->stage_same >= 2 && h->stage_every < 256) {
+                h->stage_every *= 2;
+            }
+            h->stage_narrow = narrow;
+        }
     }
-    // the first launch and then at most every 8th copies its samples back
-    if (!h->stage_pending && (!h->stage_copy_gen || ((h->stage_gen - h->stage_copy_gen) & 0x3fffffffu) >= 8))
+    // the first launch and then at most every stage_every-th copies its samples back
+    if (!h->stage_pending &&
+        (!h->stage_copy_gen || ((h->stage_gen - h->stage_copy_gen) & 0x3fffffffu) >= h->stage_every))
         h->stage_copy = true;
     return h->stage_narrow;
 }
