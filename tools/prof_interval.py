@@ -11,7 +11,9 @@ came last: --old-order.)  For those three groups of
 `steps` k_rx dispatches this prints the mean per-dispatch duration (what `--stats` averages)
 and the interval (last end - first start) / launches, which is what the bench's one event pair
 around a group measures.  With --batches <= --streams there is no replay group: pass
-`--no-replay` as the third argument.
+`--no-replay` as the third argument.  `--kernel <text>` keeps only the k_rx dispatches whose name
+holds <text> (the default command also runs config D's exchange after the headline: pass
+`--kernel "k_rx<1, 6144u>"` for config B's narrow-slab launches).
 """
 import csv
 import json
@@ -25,12 +27,12 @@ def col(row, *names):
     raise KeyError(names)
 
 
-def main(path, steps, replay=True, old_order=False, one=None):
+def main(path, steps, replay=True, old_order=False, one=None, kernel="k_rx"):
     one = max(steps, 100) if one is None else one  # bench.py times one launch alone over max(--steps, 100)
     ks = []
     for row in csv.DictReader(open(path)):
         name = col(row, "Kernel_Name", "Kernel-Name", "KernelName")
-        if "k_rx" not in name:
+        if "k_rx" not in name or kernel not in name:
             continue
         ks.append((int(col(row, "Start_Timestamp", "Start-Timestamp", "BeginNs")),
                    int(col(row, "End_Timestamp", "End-Timestamp", "EndNs"))))
@@ -60,4 +62,6 @@ def main(path, steps, replay=True, old_order=False, one=None):
 if __name__ == "__main__":
     rest = sys.argv[3:]
     one = int(rest[rest.index("--one") + 1]) if "--one" in rest else None  # traces before max(steps, 100): --one <steps>
-    main(sys.argv[1], int(sys.argv[2]), replay="--no-replay" not in rest, old_order="--old-order" in rest, one=one)
+    kernel = rest[rest.index("--kernel") + 1] if "--kernel" in rest else "k_rx"
+    main(sys.argv[1], int(sys.argv[2]), replay="--no-replay" not in rest, old_order="--old-order" in rest, one=one,
+         kernel=kernel)
