@@ -102,6 +102,8 @@ def parse_args():
                     help="also time the device tx ZMQ framing (emurx_tx_zmq_dev) over the same frames")
     ap.add_argument("--launch-check", action="store_true",
                     help="rendezvous + max-over-ranks reduction only, no GPU (CPU test of the launch path)")
+    ap.add_argument("--no-host-inclusive", action="store_true",
+                    help="skip the default line's bounded host-inclusive block (every N)")
     ap.add_argument("--host-path", action="store_true",
                     help="also time the host-inclusive path (pinned H2D + kernels + D2H)")
     ap.add_argument("--unkeyed", action="store_true",
@@ -207,20 +209,47 @@ def spawn_ranks(a):
                                       start_new_session=True))
     rc = 0
     live = list(procs)
-    while live:
-        time.sleep(0.2)
-        for p in list(live):
-            c = p.poll()
-            if c is None:
-                continue
-            live.remove(p)
-            if c != 0 and rc == 0:
-                rc = c
-                for q in live:  # a failed rank leaves the others waiting in a collective
-                    try:
-                        os.killpg(q.pid, signal.SIGTERM)
-                    except OSError:
-                        pass
+
+    def stop_all(sig=signal.SIGTERM):
+        for q in live:  # each rank leads its own session: signal its whole process group
+            try:
+                os.killpg(q.pid, sig)
+            except OSError:
+                pass
+
+    # SIGINT / SIGTERM to this launcher reach the ranks too (they are in sessions of their own
+    # and would otherwise keep their GPUs, waiting in a collective)
+    class Stopped(Exception):
+        pass
+
+    def on_signal(signum, frame):
+        raise Stopped(signum)
+    old = {sg: signal.signal(sg, on_signal) for sg in (signal.SIGINT, signal.SIGTERM)}
+    try:
+        while live:
+            time.sleep(0.2)
+            for p in list(live):
+                c = p.poll()
+                if c is None:
+                    continue
+                live.remove(p)
+                if c != 0 and rc == 0:
+                    rc = c
+                    stop_all()  # a failed rank leaves the others waiting in a collective
+    except Stopped as e:
+        rc = 128 + int(e.args[0])
+    finally:
+        if live:  # interrupted (or an error here): end every rank still running, then reap them
+            stop_all()
+            deadline = time.time() + 10
+            for q in live:
+                try:
+                    q.wait(max(0.1, deadline - time.time()))
+                except subprocess.TimeoutExpired:
+                    stop_all(signal.SIGKILL)
+                    q.wait()
+        for sg, h in old.items():
+            signal.signal(sg, h)
     return rc
 
 
@@ -248,6 +277,15 @@ def main():
         else:
             dist.init_process_group("gloo")
     out, rx, w = measure(a, a.config, a.frames, mode, a.steps, a.warmup, rank, world, local, dist, torch)
+    if a.config == "B" and not a.no_host_inclusive and not a.host_path:
+        # the north star's host-in / host-out rate, at every N (each rank through its own two
+        # ingest slots, the node's aggregate): bounded to ~2 s, on the headline's handle
+        try:
+            out["host_inclusive"] = host_inclusive_block(rx, w, rank, world, dist, torch, a.backend)
+        except Exception as e:  # noqa: BLE001 - report, keep the headline line
+            out["host_inclusive"] = {"error": repr(e)[:300]}
+    if a.host_path:
+        out["host_inclusive"] = host_path_rate(rx, w)
     if a.config == "D" and not a.no_exchange_run:
         # SURVEY.md §8e asks for both: the Namespace-partitioned lookups (the headline of D)
         # and the "replicas only" alternative (every GPU holds every table)
@@ -281,8 +319,6 @@ def main():
             "the north star's >= 6x-at-8-GPUs target after the xGMI Namespace all-to-all is judged on "
             "namespace_exchange (config D, 2M frames per GPU, partitioned tables), measured at every N with the "
             "same steps and warmup")
-    if a.host_path:
-        out["host_inclusive"] = host_path_rate(rx, w)
     if a.tx_path:
         out["tx_zmq"] = tx_zmq_rate(rx, w, torch)
         out["tx_checksum"] = tx_csum_rate(rx, w, torch)
@@ -290,7 +326,7 @@ def main():
         out["table_updates"] = table_update_cost(a, rx, w, torch)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(w, a.cpu_seconds)
-        if "host_inclusive" in out and a.config == "B":
+        if "host_inclusive" in out and a.config == "B" and "batch_latency_by_msgs" in out["host_inclusive"]:
             out["host_inclusive"]["crossover"] = crossover(out["host_inclusive"], out["cpu_baseline"]["value"])
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -343,6 +379,8 @@ def launch_check(a, rank, world, dist, torch):
     barrier, the max-over-ranks time reduction, rank 0's JSON line."""
     if os.environ.get("EMURX_BENCH_FAIL_RANK") == str(rank):
         return 3  # test hook: a rank that dies before the rendezvous completes
+    if os.environ.get("EMURX_BENCH_HANG"):
+        time.sleep(600)  # test hook: every rank stuck (as in a collective whose peer is gone)
     if world > 1:
         dist.init_process_group("gloo")
         dist.barrier()
@@ -444,7 +482,12 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
     if mode != "none":
         from emurx import exchange as X
         rb = X.LOOKUP_BYTES if mode == "partitioned" else X.REC_BYTES
-        xch = dict(cap=X.capacity(n, world, slack=1.06), ev=[], timing=False, k=0, rb=rb)
+        cap0 = X.capacity(n, world, slack=1.06)
+        # partitioned: 32-byte lookup heads + tail shards per region, two counts per region
+        # (heads, tail overflow); replicated: 40-byte classified records, one count
+        xch = dict(cap=cap0, tcap=abi.tail_capacity(cap0) if mode == "partitioned" else None, ev=[], timing=False,
+                   k=0, rb=rb, cs=2 if mode == "partitioned" else 1)
+        xch["region"] = X.region_bytes(xch["cap"], xch["tcap"])
 
         # two buffer sets when the timed steps overlap batch k's exchange with batch k+1's parse,
         # each on its own compute stream (as the N = 1 pipelined steps): batch k+1's parse runs
@@ -455,8 +498,8 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         def alloc_regions():
             xch["sets"] = []
             for j in range(nsets):
-                b = dict(send=torch.empty(world * xch["cap"] * rb, dtype=torch.uint8, device=dev),
-                         send_count=torch.zeros(world, dtype=torch.int32, device=dev), pending=None,
+                b = dict(send=torch.empty(world * xch["region"], dtype=torch.uint8, device=dev),
+                         send_count=torch.zeros(world * xch["cs"], dtype=torch.int32, device=dev), pending=None,
                          st=stream if j == 0 else side, ev=None)
                 # set 0 writes the handle's record / queue buffers (the sanity checks read them)
                 b["rec"], b["qlist"], b["tile_cnt"] = (rec, qlist, tile_cnt) if j == 0 else outputs()
@@ -477,19 +520,20 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             else:
                 # no source records: every frame's lookup record carries its parse to the owner
                 rx.parse_route_dev(fb, fd, n, None, b["qlist"], qcap, b["tile_cnt"], hist, world, rank, xch["cap"],
-                                   b["send"], b["send_count"], stream=b["st"])
+                                   b["send"], b["send_count"], stream=b["st"], tail_cap=xch["tcap"])
 
         def consume(b):
             with torch.cuda.stream(b["st"]):  # the set's stream waits for its all-to-all
                 xch["recv"], xch["recv_count"] = X.exchange_finish(b["pending"])
             b["pending"] = None
             if mode == "partitioned":
-                rx.lookup_dev(xch["recv"], xch["recv_count"], world, xch["cap"], b["out"], stream=b["st"])
+                rx.lookup_dev(xch["recv"], xch["recv_count"], world, xch["cap"], b["out"], stream=b["st"],
+                              tail_cap=xch["tcap"])
             if xch.get("dump") is not None:  # --dump-exchange: this step's owner records, as they are now
                 torch.cuda.synchronize()
-                cnt = xch["recv_count"].cpu().numpy().astype(np.int64)
+                cnt = xch["recv_count"].cpu().numpy().astype(np.int64)[0::xch["cs"]]
                 res = (b["out"] if mode == "partitioned" else xch["recv"]).cpu().numpy()
-                res = res.reshape(world, -1)[:, : xch["cap"] * X.REC_BYTES]
+                res = res.reshape(world, -1)[:, : xch["cap"] * X.REC_BYTES]  # owner outputs: cap route records
                 xch["dump"].append(dict(k=b["k"], cnt=cnt, recs=np.concatenate(
                     [res[sr, : min(int(cnt[sr]), xch["cap"]) * X.REC_BYTES] for sr in range(world)])))
 
@@ -507,7 +551,7 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
                 b["ev"][0].record(b["st"])
             produce(b, k)
             with torch.cuda.stream(b["st"]):  # the collective waits for this set's stream
-                b["pending"] = X.exchange_start(b["send"], b["send_count"], xch["cap"], rec_bytes=rb)
+                b["pending"] = X.exchange_start(b["send"], b["send_count"], xch["region"])
             if prev["pending"] is not None:
                 consume(prev)
                 if prev["ev"] is not None:
@@ -546,8 +590,8 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
                                       b["send"], b["send_count"], stream=b["st"])
             else:
                 rx.parse_route_dev(fb, fd, n, None, b["q"], qcap, b["t"], hist, 1, 0, xch["cap"],
-                                   b["send"], b["send_count"], stream=b["st"])
-                rx.lookup_dev(b["send"], b["send_count"], 1, xch["cap"], b["out"], stream=b["st"])
+                                   b["send"], b["send_count"], stream=b["st"], tail_cap=xch["tcap"])
+                rx.lookup_dev(b["send"], b["send_count"], 1, xch["cap"], b["out"], stream=b["st"], tail_cap=xch["tcap"])
         for k in range(2 * len(sets)):
             one(sets[k % len(sets)], k)
         torch.cuda.synchronize()
@@ -573,11 +617,12 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         xch["k"] += 1
         produce(xch["sets"][0], k)
         if world > 1:
-            xch["recv"], xch["recv_count"] = X.exchange(xch["send"], xch["send_count"], xch["cap"], rec_bytes=rb)
+            xch["recv"], xch["recv_count"] = X.exchange(xch["send"], xch["send_count"], xch["region"])
         else:
             xch["recv"], xch["recv_count"] = xch["send"], xch["send_count"]
         if mode == "partitioned":
-            rx.lookup_dev(xch["recv"], xch["recv_count"], world, xch["cap"], xch["out"], stream=stream)
+            rx.lookup_dev(xch["recv"], xch["recv_count"], world, xch["cap"], xch["out"], stream=stream,
+                          tail_cap=xch["tcap"])
         if ev is not None:
             ev[1].record(stream)
             xch["ev"].append(ev)
@@ -588,7 +633,8 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         (owner counts + group scan + k_rx packing the lookup records, or k_rx + scan + route
         packing), k_rx alone (the library's events around its launch), the all-to-all (counts +
         regions; RCCL's stream joined back into the launch stream), the owner's k_lookup; and
-        the bytes that crossed to other ranks (whole regions: the all-to-all is equal-split)."""
+        the bytes that crossed to other ranks (whole regions: the all-to-all is equal-split) and
+        the payload among them (heads + tail units, or routed records)."""
         reps = reps or max(4, min(steps, 30))
         ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(reps)]
         rx.set_timing(reps + 8, 1)
@@ -606,12 +652,12 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             produce(b, k)
             e[1].record(stream)
             if world > 1:
-                recv, rc = X.exchange(b["send"], b["send_count"], xch["cap"], rec_bytes=rb)
+                recv, rc = X.exchange(b["send"], b["send_count"], xch["region"])
             else:
                 recv, rc = b["send"], b["send_count"]
             e[2].record(stream)
             if mode == "partitioned":
-                rx.lookup_dev(recv, rc, world, xch["cap"], b["out"], stream=stream)
+                rx.lookup_dev(recv, rc, world, xch["cap"], b["out"], stream=stream, tail_cap=xch["tcap"])
             e[3].record(stream)
         torch.cuda.synchronize()
         krx = rx.kernel_times()
@@ -619,14 +665,27 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         ms = np.array([[e[j].elapsed_time(e[j + 1]) for j in range(3)] for e in ev[1:]])  # the first: warm
         src, a2a, look = (float(np.mean(ms[:, j])) for j in range(3))
         k_rx_ms = float(np.mean(krx[1:])) if len(krx) > 1 else float("nan")
-        sc = b["send_count"].cpu().numpy().astype(np.int64)
+        sc = b["send_count"].cpu().numpy().astype(np.int64)[0::xch["cs"]]
         others = [d for d in range(world) if d != rank]
-        moved = len(others) * xch["cap"] * rb + 4 * len(others)
-        payload = int(sum(int(sc[d]) for d in others)) * rb
+        moved = len(others) * (xch["region"] + 4 * xch["cs"])
+        # payload per region: the heads (or routed records) and, partitioned, their tail units
+        units = [0] * world
+        if mode == "partitioned":
+            sb = b["send"].cpu().numpy().reshape(world, -1)
+            for d in range(world):
+                hd = sb[d, : int(min(sc[d], xch["cap"])) * rb].view(abi.LOOKUP_REC_DTYPE)
+                units[d] = int(X.tail_units(hd["w4"]).sum())
+        payload = int(sum(int(sc[d]) * rb + 16 * units[d] for d in others))
+        to_others = int(sum(int(sc[d]) for d in others))
         out = {"steps": reps - 1, "source_side_ms": round(src, 5), "k_rx_ms": round(k_rx_ms, 5),
                ("owner_count_scan_ms" if mode == "partitioned" else "scan_pack_ms"): round(src - k_rx_ms, 5),
                "all_to_all_ms": round(a2a, 5), "owner_lookup_ms": round(look, 5) if mode == "partitioned" else 0.0,
-               "record_bytes": rb, "bytes_to_other_ranks": moved, "payload_bytes_to_other_ranks": payload,
+               "record_bytes": rb, "tail_units_per_shard": xch["tcap"], "region_bytes": xch["region"],
+               "tail_bytes_per_frame": round(16 * sum(units) / max(int(sc.sum()), 1), 3),
+               "bytes_to_other_ranks": moved, "payload_bytes_to_other_ranks": payload,
+               "frames_to_other_ranks": to_others,
+               "bytes_per_frame_to_other_ranks": round(moved / to_others, 2) if to_others else None,
+               "payload_bytes_per_frame_to_other_ranks": round(payload / to_others, 2) if to_others else None,
                "source": "HIP events on the launch stream between the phases of non-overlapped steps; k_rx by the "
                          "library's events around its launch"}
         if world > 1 and a2a > 0:
@@ -656,8 +715,10 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         torch.cuda.synchronize()
         if xch is None or not exchange_overflow(xch, world, dist, torch, dev):
             break
-        # a region overflowed (send_count > cap): grow every rank's regions and redo
-        xch["cap"] = grow_cap(xch, world, dist, torch, dev)
+        # a region overflowed (send_count > cap, or a tail shard > tcap): grow every rank's
+        # regions and redo
+        xch["cap"], xch["tcap"] = grow_cap(xch, world, dist, torch, dev)
+        xch["region"] = X.region_bytes(xch["cap"], xch["tcap"])
         alloc_regions()
         hist.zero_()
     def sanity():
@@ -782,10 +843,11 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
 
     # roofline of the dominant kernel (k_rx): algorithmic bytes / its mean launch duration.
     # Per frame: the frame, its 8-B descriptor and the 32-B record (104 B for a
-    # 64-B frame), plus the 4-B queue entry k_rx also writes (the 64-B lookup record instead of
-    # the record in the partitioned mode's k_rx)
-    per_frame = 8 + 4 + (64 if mode == "partitioned" else 32)
-    alg_bytes = w["nbytes"] + per_frame * n
+    # 64-B frame), plus the 4-B queue entry k_rx also writes (the 32-B lookup head and the
+    # batch's tail units instead of the record in the partitioned mode's k_rx)
+    per_frame = 8 + 4 + 32
+    tail_bytes = int(round((phases or {}).get("tail_bytes_per_frame", 0.0) * n)) if mode == "partitioned" else 0
+    alg_bytes = w["nbytes"] + per_frame * n + tail_bytes
     parse_s = float(np.mean(pk)) * 1e-3 if len(pk) else float("nan")
     achieved = alg_bytes / parse_s / 1e9
     traffic, pmc_src = None, None
@@ -855,7 +917,8 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             "alg_bytes_per_launch": alg_bytes,
             "alg_bytes_per_frame": round(alg_bytes / n, 2),
             "alg_bytes_note": "frame + 8-B descriptor + 32-B record (SURVEY.md §8d) + the 4-B queue entry k_rx also "
-                              "writes" + ("; the 64-B lookup record instead of the record" if mode == "partitioned" else ""),
+                              "writes" + ("; the 32-B lookup head (+ the batch's 16-B tail units) instead of the record"
+                                          if mode == "partitioned" else ""),
             "table_probe_bytes_per_launch": probed * 128 if mode != "partitioned" else 0,
             "kernel_ms_mean": round(parse_s * 1e3, 5),
             "kernel_launches_timed": max(steps, 100) if region else int(len(pk)),
@@ -892,6 +955,8 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             "steps_timed": len(xm),
             "records_per_region_cap": xch["cap"],
             "record_bytes": xch["rb"],
+            "tail_units_per_shard": xch["tcap"],
+            "region_bytes": xch["region"],
             "collective": f"all_to_all_single x2 ({a.backend})" if world > 1 else "none (1 rank)",
             "overlapped": overlapped,  # batch k's all-to-all beside batch k+1's parse (two buffer sets)
             "includes": ("k_rx + group scan + pack" + (" + all-to-all" if world > 1 else "") +
@@ -904,7 +969,64 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             out["exchange"]["pipelined"] = pipelined
             out["exchange"]["one_stream_steps"] = {"value": out["value"], "ms_per_step": out["ms_per_step"]}
             out["value"], out["ms_per_step"] = pipelined["value"], pipelined["ms_per_step"]
+        if mode == "partitioned" and not a.unkeyed:
+            # the owner keys the timed steps read from the descriptors are derived by the device
+            # framing walk: what that derivation costs the walk is added to every step (VERDICT
+            # r04 item 2), so the value covers every byte of parse work the step depends on
+            kd = key_derivation(rx, w, torch, dev, stream, inputs[0][1])
+            t = torch.tensor([kd["key_ms"]], dtype=torch.float64)
+            if world > 1:
+                t = t.to(dev) if a.backend == "nccl" else t
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            key_ms = float(t.cpu().item())
+            kd["key_ms_max_over_ranks"] = round(key_ms, 5)
+            out["exchange"]["key_derivation"] = kd
+            out["exchange"]["without_key_derivation"] = {"value": out["value"], "ms_per_step": out["ms_per_step"]}
+            ms = out["ms_per_step"] + key_ms
+            out["value"], out["ms_per_step"] = round(n * world / (ms * 1e-3) / 1e6, 2), round(ms, 4)
     return out, rx, w
+
+
+def key_derivation(rx, w, torch, dev, stream, keyed_desc, per_msg=64, reps=30):
+    """Device time the Namespace-owner keys add to the framing walk (k_zmq_walk, emurx_zmq_walk_dev)
+    on this batch packed as ZMQ messages of `per_msg` frames (veth_zmq.go:36-37,277-320): the walk
+    with the keys and without (EMURX_WALK_NO_KEYS), alternated, `reps` launches each, each timed
+    by its own event pair on the launch stream; key_ms = the difference of the medians (>= 0).
+    The keyed descriptors are checked against the untimed emurx_desc_keys_dev ones."""
+    import numpy as np
+    from emurx import abi
+    from emurx import frames as F
+    n = len(w["desc"])
+    zs, msgs = F.zmq_messages(w["buf"], w["desc"], per_msg)
+    nmsg = len(msgs)
+    per = np.minimum(per_msg, n - per_msg * np.arange(nmsg)).astype(np.uint32)
+    base = np.zeros(nmsg + 1, np.uint32)
+    base[1:] = np.cumsum(per)
+    ctl = np.concatenate([np.ascontiguousarray(msgs).view(np.uint32).reshape(-1), base])
+    d_buf = torch.from_numpy(np.concatenate([zs, np.zeros(64, np.uint8)])).to(dev)
+    d_ctl = torch.from_numpy(ctl.view(np.int32)).to(dev)
+    d_desc = torch.empty(n * 8, dtype=torch.uint8, device=dev)
+    d_stat = torch.empty(nmsg, dtype=torch.int32, device=dev)
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(2 * reps)]
+    sc = stream.cuda_stream
+    for k in range(6):
+        rx.zmq_walk_dev(d_buf, d_ctl, nmsg, d_desc, d_stat, keys=bool(k & 1), stream=sc)
+    for k in range(2 * reps):
+        ev[k][0].record(stream)
+        rx.zmq_walk_dev(d_buf, d_ctl, nmsg, d_desc, d_stat, keys=bool(k & 1), stream=sc)
+        ev[k][1].record(stream)
+    torch.cuda.synchronize()
+    ms = np.array([e0.elapsed_time(e1) for e0, e1 in ev])
+    plain, keyed = float(np.median(ms[0::2])), float(np.median(ms[1::2]))
+    got = d_desc.cpu().numpy().view(abi.DESC_DTYPE)
+    st = d_stat.cpu().numpy()
+    assert (st >> 24 == 0).all() and int((st & 0xFFFFFF).sum()) == n, "framing walk of the bench batch"
+    want = keyed_desc.cpu().numpy()[: n * 8].view(abi.DESC_DTYPE)  # emurx_desc_keys_dev's keys
+    assert np.array_equal(got["pad"], want["pad"]), "the walk's owner keys equal emurx_desc_keys_dev's"
+    return {"key_ms": round(max(0.0, keyed - plain), 5), "walk_keyed_ms": round(keyed, 5),
+            "walk_plain_ms": round(plain, 5), "messages": nmsg, "frames_per_msg": per_msg,
+            "source": "k_zmq_walk (emurx_zmq_walk_dev) on this batch as ZMQ messages, with and without the owner "
+                      f"keys, medians of {reps} launches each (HIP events); key_ms is added to every timed step"}
 
 
 def dump_exchange(a, xch, inputs, R, rank, world, dist, torch, step_overlapped, drain, k_steps=4):
@@ -925,7 +1047,7 @@ def dump_exchange(a, xch, inputs, R, rank, world, dist, torch, step_overlapped, 
     torch.cuda.synchronize()
     for e in xch["dump"]:
         np.savez(d / f"rank{rank}_step{e['k']}.npz", cnt=e["cnt"], recs=e["recs"], slot=e["k"] % R,
-                 cap=xch["cap"], mode=xch["rb"])
+                 cap=xch["cap"], mode=xch["rb"], tcap=xch["tcap"] or 0)
     for j in range(R):
         np.savez(d / f"rank{rank}_slot{j}.npz", buf=inputs[j][0].cpu().numpy(), desc=inputs[j][1].cpu().numpy())
     xch["dump"] = None
@@ -1031,9 +1153,13 @@ def copy_ceiling(torch, dev, stream, mib=1024, reps=8):
 
 
 def exchange_overflow(xch, world, dist, torch, dev):
-    """Did any rank's region overflow (send_count > cap) in the last step? (every step routes
-    the same batch, so the last step's counts are every step's)"""
-    over = torch.tensor([int((xch["send_count"].cpu() > xch["cap"]).any())], dtype=torch.int64)
+    """Did any rank's region overflow (send_count > cap, or a tail shard past tcap) in the last
+    step? (every step routes the same batch, so the last step's counts are every step's)"""
+    c = xch["send_count"].cpu()
+    over = (c[0::xch["cs"]] > xch["cap"]).any()
+    if xch["cs"] == 2:
+        over = over or (c[1::2] > xch["tcap"]).any()
+    over = torch.tensor([int(over)], dtype=torch.int64)
     if world > 1:
         over = over.to(dev) if dist.get_backend() == "nccl" else over
         dist.all_reduce(over, op=dist.ReduceOp.MAX)
@@ -1041,12 +1167,16 @@ def exchange_overflow(xch, world, dist, torch, dev):
 
 
 def grow_cap(xch, world, dist, torch, dev):
+    """(cap, tcap) after an overflow, the same on every rank."""
     from emurx import exchange as X
-    m = torch.tensor([int(xch["send_count"].cpu().max())], dtype=torch.int64)
+    c = xch["send_count"].cpu()
+    m = torch.tensor([int(c[0::xch["cs"]].max()), int(c[1::2].max()) if xch["cs"] == 2 else 0], dtype=torch.int64)
     if world > 1:
         m = m.to(dev) if dist.get_backend() == "nccl" else m
         dist.all_reduce(m, op=dist.ReduceOp.MAX)
-    return X.grow(xch["cap"], [int(m.cpu().item())])
+    m = m.cpu().tolist()
+    tcap = X.grow_tail(xch["tcap"], [m[1]]) if xch["cs"] == 2 else None
+    return X.grow(xch["cap"], [m[0]]), tcap
 
 
 def xcheck(xch, rec, n, world, rank, dist, torch, dev, mode):
@@ -1055,7 +1185,7 @@ def xcheck(xch, rec, n, world, rank, dist, torch, dev, mode):
     every frame's lookup record)."""
     import numpy as np
     from emurx import abi
-    cnt = xch["recv_count"].cpu().numpy().astype(np.int64)
+    cnt = xch["recv_count"].cpu().numpy().astype(np.int64)[0::xch["cs"]]
     assert (cnt <= xch["cap"]).all(), f"exchange overflow {cnt} > {xch['cap']}"
     sent = (rec.cpu().numpy().view(abi.REC_DTYPE)["ns_id"] != abi.ID_NONE).sum() if mode == "replicated" else n
     routed = torch.tensor([int(sent), int(cnt.sum())], dtype=torch.int64)
@@ -1064,6 +1194,67 @@ def xcheck(xch, rec, n, world, rank, dist, torch, dev, mode):
         dist.all_reduce(routed)
     routed = routed.cpu().numpy()
     assert routed[0] == routed[1], f"sent {routed[0]} != received {routed[1]}"
+
+
+def host_inclusive_block(rx, w, rank, world, dist, torch, backend, per_msg=64, budget_s=1.0):
+    """The host-inclusive rate of the default line, at every N: the
+    headline batch as ZMQ messages of `per_msg` frames (veth_zmq.go:36-37,132-143,277-320)
+    through the batched ingest (emurx_ingest_*), both slots alternating: pinned staging -> H2D
+    -> framing walk -> k_rx -> queue packing -> D2H of records, descriptors, queues and
+    counters.  Two passes of `budget_s` each, every rank at once after a barrier: with the copy
+    of the messages into the slot's pinned staging (the receive copy the caller makes anyway),
+    and with the staging prefilled (PCIe + GPU only).  Per pass the node's aggregate = all
+    ranks' frames / the slowest rank's time (max over ranks, as the headline)."""
+    import numpy as np
+    from emurx import frames as F
+    zs, msgs = F.zmq_messages(w["buf"], w["desc"], per_msg)
+    n, total = len(w["desc"]), len(zs)
+    bufs = [rx.ingest_buffer(s, total) for s in range(2)]
+    for s in range(2):  # warm both slots
+        np.copyto(bufs[s], zs)
+        rx.ingest_submit(s, msgs)
+        assert rx.ingest_wait(s, copy=False)["n"] == n
+    out = {"frames_per_batch": n, "frames_per_msg": per_msg, "msgs_per_batch": len(msgs), "bytes_per_batch": total,
+           "budget_s_per_pass": budget_s}
+
+    def one_pass(copy):
+        if world > 1:
+            dist.barrier()
+        pending, k, t0 = [False, False], 0, time.perf_counter()
+        while True:
+            s = k & 1
+            if pending[s]:
+                rx.ingest_wait(s, copy=False)
+            if copy:
+                np.copyto(bufs[s], zs)
+            rx.ingest_submit(s, msgs)
+            pending[s] = True
+            k += 1
+            if time.perf_counter() - t0 > budget_s and k >= 4:
+                break
+        for s in range(2):
+            if pending[s]:
+                rx.ingest_wait(s, copy=False)
+        el = time.perf_counter() - t0
+        t = torch.tensor([el, float(k * n), float(k * total)], dtype=torch.float64)
+        per_rank = k * n / el / 1e6
+        if world > 1:
+            dev = torch.device("cuda", torch.cuda.current_device())
+            mx = t[:1].clone().to(dev) if backend == "nccl" else t[:1].clone()
+            sm = t[1:].clone().to(dev) if backend == "nccl" else t[1:].clone()
+            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+            dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+            t = torch.cat([mx.cpu(), sm.cpu()])
+        el_max, frames, nbytes = (float(x) for x in t)
+        return {"mpkts": round(frames / el_max / 1e6, 2), "gbs_in": round(nbytes / el_max / 1e9, 2),
+                "rank0_mpkts": round(per_rank, 2), "batches_rank0": k}
+
+    out["with_host_copy"] = one_pass(True)
+    out["prefilled"] = one_pass(False)
+    out["n_gpus"] = world
+    out["source"] = ("emurx_ingest_submit/wait on both slots of every rank, wall clock per rank after a barrier; "
+                     "node aggregate = all ranks' frames / the slowest rank's time")
+    return out
 
 
 def host_path_rate(rx, w, per_msg=64, budget_s=3.0):

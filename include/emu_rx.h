@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define EMURX_ABI_VERSION 4
+#define EMURX_ABI_VERSION 5
 
 /* ---- return codes -------------------------------------------------------------------- */
 #define EMURX_OK 0
@@ -461,6 +461,19 @@ int emurx_ingest_buffer(emurx_t* h, uint32_t slot, size_t bytes, uint8_t** buf);
 int emurx_ingest_submit(emurx_t* h, uint32_t slot, const emurx_msg* msgs, uint32_t nmsg);
 /* Wait for the slot's batch and point `res` at its results (library-owned pinned memory). */
 int emurx_ingest_wait(emurx_t* h, uint32_t slot, emurx_ingest_result* res);
+/* The framing walk alone on messages already in device memory (the first stage of the
+   batched ingest, k_zmq_walk): one lane per message follows OnRxStream's offset chain
+   (veth_zmq.go:277-320) and writes the descriptors of its frames, each with its Namespace-owner
+   key (EMURX_DESC_KEYED, from the frame's bytes 12..19: what emurx_parse_route_dev's owner
+   count reads instead of the frame), and msg_stat[m] = frames | EMURX_MSG_* << 24.  d_ctl:
+   emurx_msg[nmsg] then slot_base[nmsg + 1] (message m's descriptor slots are
+   [slot_base[m], slot_base[m + 1]); slots a message announced but did not carry become
+   EMURX_DESC_HOLE).  The buffer must be readable 8 bytes past every message.  flags:
+   EMURX_WALK_NO_KEYS leaves the pad byte 0 (for the measurement of what the keys cost; the
+   bench folds the difference into the exchange's rate).  One launch, no host sync. */
+#define EMURX_WALK_NO_KEYS 1u
+int emurx_zmq_walk_dev(emurx_t* h, const uint8_t* d_buf, const uint32_t* d_ctl, uint32_t nmsg, emurx_desc* d_desc,
+                       uint32_t* d_msg_stat, uint32_t flags, void* stream);
 /* The slot's HIP stream (hipStream_t, created on first use), so that a caller can order its
    own work with the slot's batches: make the next batch wait for a device-side producer
    (hipStreamWaitEvent before emurx_ingest_submit), or chain a consumer after the D2H. */
@@ -546,6 +559,11 @@ void emurx_hist_fold(const uint64_t* shards, uint64_t out[2 * EMURX_HIST_BINS]);
 int emurx_set_timing(emurx_t* h, uint32_t slots, uint32_t stride);
 int emurx_kernel_times(emurx_t* h, float* batch_ms, uint32_t cap, uint32_t* n_out);
 
+/* The source tree this library was built from: the first 16 hex digits of the sha1 of its
+   sources, headers and Makefile (trex-emu_amd/Makefile SRC_ID).  No ABI replacement: build
+   provenance, printed by the Python binding when it loads the library. */
+const char* emurx_build_id(void);
+
 /* LDS staging slab (bytes per wave) of the most recent k_rx launch: 7168 or 6144 (0 before
    the first).  Chosen per launch from sampled feedback of earlier launches (a wave whose
    frames span 6-7 KiB fits only the wider slab); EMURX_STAGE=wide|narrow in the environment
@@ -600,41 +618,68 @@ int emurx_classify_route_dev(emurx_t* h, const uint8_t* d_frames, const emurx_de
 /* ---- owner-partitioned classification ---------------------------------
    With partitioned tables (emurx_set_partition) the lookups run on the GPU that owns the
    frame's Namespace.  The receiving GPU parses its shard and derives each frame's lookup key
-   (emurx_parse_route_dev); every frame travels, as a 64-byte emurx_lookup_rec, to the owner
-   of its CTunnelKey (an equal-split all-to-all, as for emurx_route_rec); the owner resolves
-   Namespace, Client and flow against its partition for the frames that reached a callback
-   (emurx_lookup_dev) and keeps the records of the others as parsed.  The owner's output for a
-   frame equals emurx_classify_dev's record for it on replicated tables, bit for bit. */
+   (emurx_parse_route_dev); every frame travels to the owner of its CTunnelKey as a 32-byte
+   emurx_lookup_rec head, plus a tail of 16-byte units for the few classes whose key does not
+   fit the head (an equal-split all-to-all of one region per owner, as for emurx_route_rec);
+   the owner resolves Namespace, Client and flow against its partition for the frames that
+   reached a callback (emurx_lookup_dev) and keeps the records of the others as parsed.  The
+   owner's output for a frame equals emurx_classify_dev's record for it on replicated tables,
+   bit for bit (the MapNsT / MapClient* maps thread_ctx.go:139, ns_ctx.go:110-112 split by
+   owner).
+
+   Region of one owner (EMURX_LOOKUP_REGION_BYTES(cap, tail_cap) bytes, 16-byte aligned):
+     [0, 32 cap)                        heads, frame order: head j of the `count` valid ones
+     [32 cap, + 16 EMURX_TAIL_SHARDS tail_cap)   tails: EMURX_TAIL_SHARDS shards of tail_cap
+                                        16-byte units; a head's `x` names its tail's first unit
+   Tails (the head's key kind / tuple bit say which):
+     ICMPv6 echo, CLookupByIPv6 / LocalGlobal key (ns_ctx.go:288-329): 1 unit, the IPv6
+       destination; the head carries the client-table hash of the key in place of L7 / L7Len
+       (both 0 for ICMPv6, parser.go:684-717), so the owner issues the client probe without
+       waiting for the tail
+     tcp / udp while some client has a TransportCtx (client_ctx.go:46,78, the c5tuplekey):
+       1 unit over IPv4 {ports, src, dst, 0}, 3 over IPv6 {ports, src[4], dst[4], 0, 0, 0}
+   Every other frame is its head alone: config D's traffic averages 32.8 bytes per frame
+   against the 64 of ABI version 4.  Tail units are taken per (wave, owner) by atomics on one
+   of EMURX_TAIL_SHARDS cursors (spread so that no address serialises), so the ORDER of the
+   tail units in a shard is not deterministic; what each head's tail holds is. */
+#define EMURX_TAIL_SHARDS 64u
+#define EMURX_TAIL_CURSOR_STRIDE 64u  /* words between two tail cursors: one per 256-byte line */
+#define EMURX_LOOKUP_REGION_BYTES(cap, tail_cap) \
+    ((uint64_t)(cap) * 32u + (uint64_t)EMURX_TAIL_SHARDS * (uint64_t)(tail_cap) * 16u)
+#define EMURX_TAIL_NONE 0xFFFFFFFFu   /* head.x of a record whose tail did not fit its shard */
 typedef struct emurx_lookup_rec {
     uint32_t frame;    /* source frame index (the source rank is the region it arrives in)  */
-    uint32_t w[7];     /* the parse packed: CTunnelKey VLAN words (14-bit codes), vport, l3,
-                          next header, l4, l7, l7_len, proto, status, RTALERT; the key kind;
-                          the destination MAC, TCP flags and the ports (emurx_parse.h)      */
-    uint32_t key[8];   /* the callback rule's key: client key (MAC / IPv4 / IPv6 / EUI-64 /
-                          chaddr) or, for tcp/udp, the c5tuplekey's addresses              */
-} emurx_lookup_rec;    /* 64 bytes */
+    uint32_t w[6];     /* the parse packed: CTunnelKey VLAN words (14-bit codes), vport, l3,
+                          next header, l4, l7, l7_len, proto, status, RTALERT; the key kind,
+                          the tuple bit; the destination MAC and TCP flags (emurx_parse.h)  */
+    uint32_t x;        /* MAC key bytes 0..3 / IPv4 key, or the first tail unit's index     */
+} emurx_lookup_rec;    /* 32 bytes */
 /* Parse the batch (records without lookups into out->rec when non-NULL, queues, histogram as
    emurx_parse_dev) and pack the lookup record of every frame (holes excepted) into the region
-   of its Namespace's owner: d_send[d * cap ..  + d_send_count[d]), frame order.  Three
-   launches: the owner counts (from the descriptors' owner keys, EMURX_DESC_KEYED; a frame
-   without one has its L2 header read, 8 bytes), their group scan, and k_rx writing each
-   lookup record at its final place.  Reads no table.  A region holds at
-   most cap records: d_send_count[d] is the true count, and a count > cap means records were
-   dropped from that region.  The caller must check every count of every batch (after the
-   count exchange, on every rank) and, on overflow, grow cap and route the batch again; the
-   library raises no error of its own on the device path. */
+   of its Namespace's owner: region d of d_send (EMURX_LOOKUP_REGION_BYTES(cap, tail_cap)
+   bytes each) gets d_send_count[2 d] heads in frame order.  Three launches: the owner counts
+   (from the descriptors' owner keys, EMURX_DESC_KEYED; a frame without one has its L2 header
+   read, 8 bytes), their group scan (which also clears the tail cursors), and k_rx writing
+   each head at its final place and each tail at the units its wave took.  Reads no table.
+   d_send_count: [2 n_parts]; d_send_count[2 d] is the true head count (> cap: heads past cap
+   were dropped); d_send_count[2 d + 1] is 0, or, when a tail did not fit its shard, the units
+   the fullest shard of region d needed (> tail_cap; that head's x is EMURX_TAIL_NONE).  The
+   caller must check both of every batch (after the count exchange, on every rank) and, on
+   overflow, grow cap / tail_cap and route the batch again; the library raises no error of its
+   own on the device path. */
 int emurx_parse_route_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_desc, uint32_t n,
                           const emurx_dev_out* out, uint32_t n_parts, uint32_t my_rank, uint32_t cap,
-                          emurx_lookup_rec* d_send, uint32_t* d_send_count, void* stream);
-/* The owner's half: d_recv holds n_parts regions of cap lookup records (the all-to-all's
-   receive buffer), d_recv_count[s] of them valid in region s.  Writes d_out[s * cap + j] (the
-   classified record + source index / rank, emurx_route_rec) and d_flow (optional, the
-   transport flow decision) for every valid slot.  One launch, no host synchronisation.
-   d_recv_count[s] must be <= cap (the counts the sources reported; a larger count is an
-   overflow the sources must resolve first, emurx_parse_route_dev): slots past cap are not
-   read. */
+                          uint32_t tail_cap, emurx_lookup_rec* d_send, uint32_t* d_send_count, void* stream);
+/* The owner's half: d_recv holds n_parts regions (EMURX_LOOKUP_REGION_BYTES(cap, tail_cap)
+   bytes each, the all-to-all's receive buffer), d_recv_count[2 s] heads of them valid in region
+   s.  Writes d_out[s * cap + j] (the classified record + source index / rank, emurx_route_rec)
+   and d_flow (optional, the transport flow decision) for every valid slot.  One launch, no
+   host synchronisation.  Counts must not exceed the capacities (the counts the sources
+   reported; an overflow is for the sources to resolve first, emurx_parse_route_dev): slots past
+   cap are not read, and a tail index past the shards is not read either. */
 int emurx_lookup_dev(emurx_t* h, const emurx_lookup_rec* d_recv, const uint32_t* d_recv_count,
-                     uint32_t n_parts, uint32_t cap, emurx_route_rec* d_out, uint32_t* d_flow, void* stream);
+                     uint32_t n_parts, uint32_t cap, uint32_t tail_cap, emurx_route_rec* d_out,
+                     uint32_t* d_flow, void* stream);
 
 #ifdef __cplusplus
 }

@@ -31,12 +31,18 @@ def test_exports_every_declared_symbol(lib):
 
 
 def test_abi_version(lib):
-    assert lib.emurx_abi_version() == 4
+    assert lib.emurx_abi_version() == 5  # 5: 32-byte lookup heads + tail shards (emurx_parse_route_dev)
+
+
+def test_build_id_is_this_tree(lib):
+    """The library says which source tree built it (emurx_build_id, the Makefile's SRC_ID), and
+    that is this tree: a stale libemurx.so (sources edited, not rebuilt) fails here."""
+    assert lib.emurx_build_id().decode() == abi.source_id()
 
 
 def test_layouts():
     import pyoracle
-    assert abi.REC_DTYPE.itemsize == 32 and abi.DESC_DTYPE.itemsize == 8
+    assert abi.REC_DTYPE.itemsize == 32 and abi.DESC_DTYPE.itemsize == 8 and abi.LOOKUP_REC_DTYPE.itemsize == 32
     assert abi.REC_DTYPE == pyoracle.REC_DTYPE and abi.DESC_DTYPE == pyoracle.DESC_DTYPE
     assert C.sizeof(abi.Counters) == 8 * (abi.NUM_PARSER_COUNTERS + 5)
     # field offsets as emu_rx.h lays emurx_rec out

@@ -39,6 +39,31 @@ def test_failed_rank_ends_the_run():
     assert p.returncode == 3, (p.returncode, p.stderr[-2000:])
 
 
+@pytest.mark.timeout(120)
+def test_signalled_launcher_ends_its_ranks():
+    """SIGTERM to `bench.py --gpus 2` (the ranks run in sessions of their own) ends every rank
+    too, instead of leaving them holding their GPUs; the launcher exits 128 + 15."""
+    import os
+    import signal
+    import time
+    import psutil
+    p = subprocess.Popen([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--backend", "gloo",
+                          "--launch-check"], env=dict(os.environ, EMURX_BENCH_HANG="1"),
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    kids = []
+    for _ in range(100):
+        time.sleep(0.1)
+        kids = psutil.Process(p.pid).children(recursive=True)
+        if len(kids) >= 2:
+            break
+    assert len(kids) >= 2, kids
+    time.sleep(1.0)
+    p.send_signal(signal.SIGTERM)
+    assert p.wait(timeout=30) == 128 + signal.SIGTERM
+    gone, alive = psutil.wait_procs(kids, timeout=15)
+    assert not alive, alive
+
+
 @pytest.mark.gpu
 @pytest.mark.timeout(600)
 def test_two_rank_exchange_fields(gpu_ok):
@@ -58,8 +83,12 @@ def test_two_rank_exchange_fields(gpu_ok):
     ph = x["exchange"]["phases"]
     for k in ("source_side_ms", "k_rx_ms", "owner_count_scan_ms", "all_to_all_ms", "owner_lookup_ms"):
         assert ph[k] > 0, (k, ph)
-    assert ph["record_bytes"] == 64
+    # 32-byte heads + tail units (<= 40 bytes per frame crossing to another
+    # rank, padding and tail shards included, from 64 + 6 % in round 4)
+    assert ph["record_bytes"] == 32
     assert ph["bytes_to_other_ranks"] > ph["payload_bytes_to_other_ranks"] > 0
+    assert ph["bytes_per_frame_to_other_ranks"] <= 40, ph
+    assert 32 < ph["payload_bytes_per_frame_to_other_ranks"] < 34, ph  # config D: 5 % one-unit tails
     assert ph["xgmi_gbs"] > 0
     # its N = 1 twin, measured in the same job on rank 0: the ratio the >= 6x target is judged by
     t = x["exchange_scaling_target"]

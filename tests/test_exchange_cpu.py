@@ -55,7 +55,7 @@ def _worker(rank, world, port, out_dir):
             send[d, : len(rr)] = rr
         cnt = np.array([len(rr) for rr in regions], np.int32)
         recv, recv_count = X.exchange(torch.from_numpy(send.view(np.uint8).reshape(-1).copy()),
-                                      torch.from_numpy(cnt), cap)
+                                      torch.from_numpy(cnt), cap * X.REC_BYTES)
         got = X.received(recv.numpy(), recv_count.numpy(), cap)
         want = np.concatenate([route_ref.route(recs[s], world, s)[rank] for s in range(world)])
         ok = got.tobytes() == want.tobytes() and len(got) > 0
@@ -65,8 +65,8 @@ def _worker(rank, world, port, out_dir):
         # finished B then A; A equals the blocking exchange, B (no records) delivers none
         send_t = torch.from_numpy(send.view(np.uint8).reshape(-1).copy())
         junk = torch.from_numpy(np.random.default_rng(rank).integers(0, 256, send_t.numel(), dtype=np.uint8))
-        pa = X.exchange_start(send_t, torch.from_numpy(cnt), cap)
-        pb = X.exchange_start(junk, torch.zeros(world, dtype=torch.int32), cap)
+        pa = X.exchange_start(send_t, torch.from_numpy(cnt), cap * X.REC_BYTES)
+        pb = X.exchange_start(junk, torch.zeros(world, dtype=torch.int32), cap * X.REC_BYTES)
         rb, cb = X.exchange_finish(pb)
         ra, ca = X.exchange_finish(pa)
         ok = ok and bool((cb == 0).all()) and torch.equal(ca, recv_count)
@@ -90,25 +90,46 @@ def test_exchange_gloo_world2(oracle_built, tmp_path):
     assert total == routed
 
 
-def lookup_regions(rec, world, rank):
-    """Host stand-in for emurx_parse_route_dev's send regions: every frame's 64-byte lookup record
+def lookup_regions(rec, world, rank, cap, tcap):
+    """Host stand-in for emurx_parse_route_dev's send regions: every frame's 32-byte lookup head
     (the frame index; the other words a function of frame and rank) in the region of the owner
-    of its CTunnelKey, frame order."""
+    of its CTunnelKey, frame order; every 5th head an ICMPv6-key head (kIp6) with a one-unit
+    tail, every 7th a tcp head with an IPv6 tuple (three units), the tails spread over the
+    shards in reverse order (the device's order within a shard is not deterministic).  Returns
+    (regions [world] bytes, counts [2 * world], the canonical records per region)."""
+    from emurx import exchange as X
     from test_gpu_tables import _owners_by_key
     own = _owners_by_key(rec, world)
-    out = []
+    rb = abi.lookup_region_bytes(cap, tcap)
+    out, cnt, canon = np.zeros((world, rb), np.uint8), np.zeros(2 * world, np.int32), []
     for d in range(world):
         idx = np.nonzero(own == d)[0]
-        lk = np.zeros(len(idx), abi.LOOKUP_REC_DTYPE)
-        lk["frame"] = idx
-        lk["vlans"], lk["w2"] = rec["vlan0"][idx] & 0xfff, rec["vport"][idx].astype(np.uint32) | (rank << 24)
-        lk["key"] = (idx[:, None] * 8 + np.arange(8)[None, :]).astype(np.uint32)
-        out.append(lk)
-    return out
+        hd = np.zeros(len(idx), abi.LOOKUP_REC_DTYPE)
+        hd["frame"] = idx
+        hd["vlans"], hd["w2"] = rec["vlan0"][idx] & 0xfff, rec["vport"][idx].astype(np.uint32) | (rank << 24)
+        hd["x"] = idx * 3 + rank
+        ip6 = (idx % 5) == 0
+        tup = ((idx % 7) == 0) & ~ip6
+        hd["w4"] = np.where(ip6, 6 << 28, np.where(tup, (3 << 28) | (1 << 31) | (1 << 26), 0)).astype(np.uint32)
+        tails = out[d, cap * 32:].view("<u4").reshape(-1, 4)
+        nxt = [0] * abi.TAIL_SHARDS
+        for j in np.nonzero(ip6 | tup)[0][::-1]:
+            u = 1 if ip6[j] else 3
+            sh = int(idx[j]) % abi.TAIL_SHARDS
+            x = sh * tcap + nxt[sh]
+            nxt[sh] += u
+            assert nxt[sh] <= tcap
+            tails[x: x + u] = (int(idx[j]) * 16 + np.arange(4 * u, dtype=np.uint32)).reshape(u, 4)
+            hd["x"][j] = x
+        out[d, : len(idx) * 32] = hd.view(np.uint8)
+        cnt[2 * d] = len(idx)
+        canon.append(X.lookup_records(out[d], len(idx), cap, tcap))
+    return out, cnt, canon
 
 
 def _worker_partitioned(rank, world, port, out_dir):
-    """The partitioned protocol over gloo: 64-byte lookup records to the Namespace owners,
+    """The partitioned protocol over gloo: lookup regions (32-byte heads + tail shards) to the
+    Namespace owners, two counts per region, the records with their tails intact at the owner;
     and this rank's device-table bytes (host-only handle, emurx_set_partition) ~ 1/world."""
     sys.path[:0] = [str(ROOT / "tests"), str(ROOT / "trex-emu_amd"), str(ROOT / "oracle")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -120,18 +141,16 @@ def _worker_partitioned(rank, world, port, out_dir):
     try:
         recs = [shard_records(r) for r in range(world)]
         cap = X.capacity(N_FRAMES, world)
-        regions = lookup_regions(recs[rank], world, rank)
-        send = np.zeros((world, cap), abi.LOOKUP_REC_DTYPE)
-        for d, rr in enumerate(regions):
-            send[d, : len(rr)] = rr
-        cnt = np.array([len(rr) for rr in regions], np.int32)
-        recv, recv_count = X.exchange(torch.from_numpy(send.view(np.uint8).reshape(-1).copy()),
-                                      torch.from_numpy(cnt), cap, rec_bytes=X.LOOKUP_BYTES)
-        r = recv.numpy().view(abi.LOOKUP_REC_DTYPE).reshape(world, cap)
+        tcap = 3 * (N_FRAMES // abi.TAIL_SHARDS + 1)
+        rb = abi.lookup_region_bytes(cap, tcap)
+        send, cnt, _ = lookup_regions(recs[rank], world, rank, cap, tcap)
+        recv, recv_count = X.exchange(torch.from_numpy(send.reshape(-1).copy()), torch.from_numpy(cnt), rb)
+        r = recv.numpy().reshape(world, rb)
         c = recv_count.numpy()
-        got = np.concatenate([r[s, : c[s]] for s in range(world)])
-        want = np.concatenate([lookup_regions(recs[s], world, s)[rank] for s in range(world)])
-        ok = got.tobytes() == want.tobytes() and len(got) > 0
+        got = np.concatenate([X.lookup_records(r[s], int(c[2 * s]), cap, tcap) for s in range(world)])
+        want = np.concatenate([lookup_regions(recs[s], world, s, cap, tcap)[2][rank] for s in range(world)])
+        ok = got.tobytes() == want.tobytes() and len(got) > 0 and (c[1::2] == 0).all()
+        ok = ok and int((X.tail_units(got["head"]["w4"]) > 0).sum()) > 0
         w = synth.config_c(N_FRAMES)
         full = RxPath(-1, max_ns=4096, max_clients=65536, max_frames=64)
         part = RxPath(-1, max_ns=4096, max_clients=65536, max_frames=64)

@@ -687,6 +687,69 @@ def check_ingest(res, o, msgs, tab):
     assert res["counters"] == cnt
 
 
+def test_zmq_walk_dev(rxmod):
+    """The framing walk alone on device-resident messages (emurx_zmq_walk_dev): valid, truncated,
+    corrupted, over-announcing, oversized and > 64 KiB messages at unaligned offsets give, slot
+    for slot, the host walk's descriptors (holes where a message announced more than it
+    carried), its per-message frame counts and status, and the owner key of the CTunnelKey
+    each frame's parse leaves; EMURX_WALK_NO_KEYS leaves the pad byte 0 and changes nothing
+    else (OnRxStream veth_zmq.go:277-320)."""
+    import pyoracle
+    import test_abi
+    import torch
+    from gpu_util import to_dev
+    rng = np.random.default_rng(0x3A1C)
+    frames = [c[1] for c in E.cases()] + corpus_frames()[:2000]
+    msgs = test_abi._rand_msgs(rng, 150)
+    for i in range(0, len(frames), 64):
+        msgs.append(F.zmq_pack(frames[i:i + 64], list(rng.integers(0, 4, len(frames[i:i + 64])))))
+    msgs = [msgs[i] for i in rng.permutation(len(msgs))]
+    gaps = rng.integers(0, 8, len(msgs))
+    buf = np.zeros(sum(len(m) for m in msgs) + int(gaps.sum()) + 64, np.uint8)
+    tab = np.zeros(len(msgs), abi.MSG_DTYPE)
+    base = [0]
+    at = 0
+    for i, (m, g) in enumerate(zip(msgs, gaps)):
+        at += int(g)
+        buf[at:at + len(m)] = np.frombuffer(m, np.uint8)
+        tab[i] = (at, len(m))
+        at += len(m)
+        ann = (int.from_bytes(m[2:4], "big") if len(m) >= 4 and m[:2] == b"\xbe\xef" else 0)
+        base.append(base[-1] + min(ann, (min(len(m), 65536) - 4) // 4 if len(m) >= 4 else 0))
+    nmsg, ns = len(msgs), base[-1]
+    ctl = np.concatenate([tab.view(np.uint32).reshape(-1), np.array(base, np.uint32)])
+    d_buf, d_ctl = to_dev(buf), to_dev(ctl)
+    out = {}
+    for keys in (True, False):
+        d_desc = torch.full((ns * 8,), 0x5A, dtype=torch.uint8, device="cuda")
+        d_stat = torch.full((nmsg,), -1, dtype=torch.int32, device="cuda")
+        rx = rxmod(0, max_ns=16, max_clients=16, max_frames=max(ns, 1))
+        rx.zmq_walk_dev(d_buf, d_ctl, nmsg, d_desc, d_stat, keys=keys)
+        torch.cuda.synchronize()
+        out[keys] = (d_desc.cpu().numpy().view(abi.DESC_DTYPE), d_stat.cpu().numpy().view(np.uint32))
+        rx.close()
+    o = pyoracle.Oracle()
+    for m in range(nmsg):
+        _, want, err = pyoracle.zmq_descriptors(msgs[m])
+        want = want.copy()
+        want["off"] += tab[m]["off"]
+        for keys in (True, False):
+            d, st = out[keys]
+            seg = d[base[m]:base[m + 1]]
+            nf = int(st[m] & 0xFFFFFF)
+            assert nf == len(want) and int(st[m] >> 24) == err, (m, nf, len(want), st[m] >> 24, err)
+            got = seg[:nf].copy()
+            k = got["pad"].copy()
+            got["pad"] = 0
+            assert got.tobytes() == want.tobytes(), m
+            if keys:
+                recs = o.rx_stream(msgs[m])[0]
+                assert np.array_equal(k, owner_keys(recs)), m
+            else:
+                assert (k == 0).all(), m
+            assert (seg["pad"][nf:] == abi.DESC_HOLE).all(), m
+
+
 def test_ingest_messages(rxmod):
     """Valid, truncated, corrupted, over-announcing, oversized and > 64 KiB messages in one
     batch at unaligned offsets: records, descriptors, queues, per-message frame counts and
@@ -822,14 +885,18 @@ def test_ingest_limits(rxmod):
 
 
 # ---- tx-side checksum generation (emurx_tx_checksum_dev) ---------------------------------
-def run_tx(rx, buf, d):
+def run_tx(rx, buf, d, skew=0):
+    """tx checksums of frames `buf` on the device; skew: d_frames `skew` bytes past a 16-byte
+    boundary (the C-ABI takes any frames pointer)."""
     import torch
     from gpu_util import to_dev
-    tb, td = to_dev(buf), to_dev(d)
+    tb, td = to_dev(np.concatenate([np.full(skew, 0x77, np.uint8), buf])), to_dev(d)
     st = torch.full((max(len(d), 1),), 0xEE, dtype=torch.uint8, device="cuda")
-    rx.tx_checksum_dev(tb, td, len(d), st)
+    rx.tx_checksum_dev(tb[skew:], td, len(d), st)
     torch.cuda.synchronize()
-    return tb.cpu().numpy()[: len(buf)], st.cpu().numpy()[: len(d)]
+    out = tb.cpu().numpy()
+    assert (out[:skew] == 0x77).all()
+    return out[skew: skew + len(buf)], st.cpu().numpy()[: len(d)]
 
 
 def test_tx_checksum_reference_captures(rxmod):
@@ -842,6 +909,19 @@ def test_tx_checksum_reference_captures(rxmod):
     got, st = run_tx(rx, zeroed, d)
     assert (st == abi.TX_OK).all()
     assert got.tobytes() == want.tobytes()
+
+
+def test_tx_checksum_unaligned_frames(rxmod):
+    """d_frames at every offset past a 16-byte boundary (the staged path aligned
+    its LDS rows relative to d_frames, not to the absolute address): the checksums of the
+    reference captures are byte-identical for each, and nothing before d_frames is written."""
+    import tx_util
+    buf, d, want, zeroed = tx_util.corpus_tx_cases()
+    rx, _ = new_pair(rxmod)
+    for skew in (1, 2, 3, 5, 8, 13, 15):
+        got, st = run_tx(rx, zeroed, d, skew)
+        assert (st == abi.TX_OK).all(), skew
+        assert got.tobytes() == want.tobytes(), skew
 
 
 def test_tx_checksum_fuzz_vs_oracle(rxmod):

@@ -206,6 +206,8 @@ def partitioned_vs_oracle(rxmod, shards, load, parts, flows=None, max_ns=4096, m
     assert max(h.table_stats()["table_bytes"] for h in owners) <= 2 * ts_full / parts + (1 << 16)
 
     cap = n  # no region can overflow (the edge / corpus frames share few tunnel keys)
+    tcap = tail_cap_max(n)  # nor any tail shard (with flows, most tcp / udp heads carry a tuple)
+    rb = abi.lookup_region_bytes(cap, tcap)
     send, cnt, rep_send, rep_cnt = [], [], [], []
     for s, w in enumerate(shards):
         m = len(w["desc"])
@@ -216,9 +218,9 @@ def partitioned_vs_oracle(rxmod, shards, load, parts, flows=None, max_ns=4096, m
                       torch.empty(abi.ntiles(m) * 16, dtype=torch.int32, device="cuda"),
                       torch.zeros(abi.HIST_SHARDS * 2 * abi.HIST_BINS, dtype=torch.int64, device="cuda"))
         rec, ql, tc, hi = mk()
-        sd = torch.full((parts * cap * X.LOOKUP_BYTES,), 0xEE, dtype=torch.uint8, device="cuda")
-        sc = torch.full((parts,), -1, dtype=torch.int32, device="cuda")
-        owners[s % parts].parse_route_dev(buf, desc, m, rec, ql, qcap, tc, hi, parts, s, cap, sd, sc)
+        sd = torch.full((parts * rb,), 0xEE, dtype=torch.uint8, device="cuda")
+        sc = torch.full((2 * parts,), -1, dtype=torch.int32, device="cuda")
+        owners[s % parts].parse_route_dev(buf, desc, m, rec, ql, qcap, tc, hi, parts, s, cap, sd, sc, tail_cap=tcap)
         rrec, rql, rtc, rhi = mk()
         rsd = torch.full((parts * cap * X.REC_BYTES,), 0xEE, dtype=torch.uint8, device="cuda")
         rsc = torch.full((parts,), -1, dtype=torch.int32, device="cuda")
@@ -230,18 +232,19 @@ def partitioned_vs_oracle(rxmod, shards, load, parts, flows=None, max_ns=4096, m
         assert np.array_equal(pr["status"], orecs[s]["status"]) and np.array_equal(pr["l4"], orecs[s]["l4"])
         send.append(sd)
         cnt.append(sc.cpu().numpy())
+        assert (cnt[-1][1::2] == 0).all(), cnt[-1]  # no tail shard overflowed
         rep_send.append(rsd)
         rep_cnt.append(rsc.cpu().numpy())
     for p in range(parts):
         # the all-to-all, played on the device: region s of owner p's receive buffer = region p of s
-        recv = torch.empty(parts * cap * X.LOOKUP_BYTES, dtype=torch.uint8, device="cuda")
-        rc = torch.tensor([int(cnt[s][p]) for s in range(parts)], dtype=torch.int32, device="cuda")
+        recv = torch.empty(parts * rb, dtype=torch.uint8, device="cuda")
+        rc = torch.tensor([int(cnt[s][2 * p + k]) for s in range(parts) for k in range(2)], dtype=torch.int32,
+                          device="cuda")
         for s in range(parts):
-            recv[s * cap * X.LOOKUP_BYTES:(s + 1) * cap * X.LOOKUP_BYTES] = \
-                send[s][p * cap * X.LOOKUP_BYTES:(p + 1) * cap * X.LOOKUP_BYTES]
+            recv[s * rb:(s + 1) * rb] = send[s][p * rb:(p + 1) * rb]
         out = torch.full((parts * cap * X.REC_BYTES,), 0xEE, dtype=torch.uint8, device="cuda")
         flow = torch.full((parts * cap,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
-        owners[p].lookup_dev(recv, rc, parts, cap, out, flow)
+        owners[p].lookup_dev(recv, rc, parts, cap, out, flow, tail_cap=tcap)
         torch.cuda.synchronize()
         got = out.cpu().numpy().view(abi.ROUTE_REC_DTYPE).reshape(parts, cap)
         fl = flow.cpu().numpy().view(np.uint32).reshape(parts, cap)
@@ -250,7 +253,7 @@ def partitioned_vs_oracle(rxmod, shards, load, parts, flows=None, max_ns=4096, m
         for s in range(parts):
             own = _owners_by_key(orecs[s], parts)
             sel = np.nonzero(own == p)[0]
-            assert cnt[s][p] == len(sel)
+            assert cnt[s][2 * p] == len(sel)
             want = np.zeros(len(sel), abi.ROUTE_REC_DTYPE)
             want["rec"], want["src_index"], want["src_rank"] = orecs[s][sel], sel, s
             g = got[s, : len(sel)]
@@ -262,6 +265,12 @@ def partitioned_vs_oracle(rxmod, shards, load, parts, flows=None, max_ns=4096, m
             wf = o.flows(shards[s]["buf"], shards[s]["desc"][sel], orecs[s][sel])
             assert np.array_equal(fl[s, : len(sel)], wf), (s, p)
     return o, orecs
+
+
+def tail_cap_max(n):
+    """Tail units per shard that no batch of n frames can overflow: every frame of every tile
+    of the fullest shard with a 3-unit tail (an IPv6 c5tuplekey)."""
+    return 768 * -(-abi.ntiles(n) // abi.TAIL_SHARDS)
 
 
 def transport_state(shards):
@@ -338,18 +347,20 @@ def test_capture_refused_before_enqueue(rxmod):
     tc = torch.full((abi.ntiles(n) * 16,), -1, dtype=torch.int32, device="cuda")
     hist = torch.zeros(abi.HIST_SHARDS * 2 * abi.HIST_BINS, dtype=torch.int64, device="cuda")
     cap = X.capacity(n, 2)
-    send = torch.full((2 * cap * X.LOOKUP_BYTES,), 0xEE, dtype=torch.uint8, device="cuda")
-    sc = torch.full((2,), -1, dtype=torch.int32, device="cuda")
+    send = torch.full((2 * abi.lookup_region_bytes(cap, abi.tail_capacity(cap)),), 0xEE, dtype=torch.uint8,
+                      device="cuda")
+    sc = torch.full((4,), -1, dtype=torch.int32, device="cuda")
+    rsc = torch.full((2,), -1, dtype=torch.int32, device="cuda")
     out = torch.full((2 * cap * X.REC_BYTES,), 0xEE, dtype=torch.uint8, device="cuda")
     rsend = torch.full((2 * cap * X.REC_BYTES,), 0xEE, dtype=torch.uint8, device="cuda")
     calls = {
         "classify_dev": lambda s: rx.classify_dev(buf, desc, n, rec, ql, qcap, tc, hist, stream=s),
         "classify_route_dev": lambda s: rx.classify_route_dev(buf, desc, n, rec, ql, qcap, tc, hist, 2, 0, cap,
-                                                              rsend, sc, stream=s),
+                                                              rsend, rsc, stream=s),
         "parse_route_dev": lambda s: rx.parse_route_dev(buf, desc, n, None, ql, qcap, tc, hist, 2, 0, cap, send, sc,
                                                         stream=s),
         "lookup_dev": lambda s: rx.lookup_dev(send, sc, 2, cap, out, stream=s),
-        "route_dev": lambda s: rx.route_dev(rec, n, 2, 0, cap, rsend, sc, stream=s),
+        "route_dev": lambda s: rx.route_dev(rec, n, 2, 0, cap, rsend, rsc, stream=s),
     }
     torch.cuda.synchronize()
     s = torch.cuda.Stream()
@@ -365,7 +376,7 @@ def test_capture_refused_before_enqueue(rxmod):
     assert all(refused.values()), refused
     g.replay()
     torch.cuda.synchronize()
-    assert (rec == 0xEE).all() and (ql == -1).all() and (tc == -1).all() and (sc == -1).all()
+    assert (rec == 0xEE).all() and (ql == -1).all() and (tc == -1).all() and (sc == -1).all() and (rsc == -1).all()
     assert (send == 0xEE).all() and (out == 0xEE).all() and (rsend == 0xEE).all() and (hist == 0).all()
     # the edit is still pending and ships with the first real call; the outputs equal the oracle's
     import pyoracle
@@ -379,7 +390,7 @@ def test_capture_refused_before_enqueue(rxmod):
     with torch.cuda.stream(s):
         calls["parse_route_dev"](s)
     torch.cuda.synchronize()
-    assert int(sc.sum()) == n
+    assert int(sc[0::2].sum()) == n and int(sc[1::2].sum()) == 0
 
 
 @pytest.mark.timeout(900)
@@ -425,20 +436,84 @@ def test_keyed_descriptors_route_the_same(rxmod):
     half = keyed.copy()
     half["pad"][::2] = plain["pad"][::2]
     cap = X.capacity(n, 8)
+    tcap = abi.tail_capacity(cap)
+    rb = abi.lookup_region_bytes(cap, tcap)
     outs = []
     for d in (plain, keyed, half):
         qcap = abi.queue_cap(n)
         ql = torch.empty(abi.NUM_QUEUES * qcap, dtype=torch.int32, device="cuda")
         tc = torch.empty(abi.ntiles(n) * 16, dtype=torch.int32, device="cuda")
         hi = torch.zeros(abi.HIST_SHARDS * 2 * abi.HIST_BINS, dtype=torch.int64, device="cuda")
-        sd = torch.full((8 * cap * X.LOOKUP_BYTES,), 0xEE, dtype=torch.uint8, device="cuda")
-        sc = torch.full((8,), -1, dtype=torch.int32, device="cuda")
-        rx.parse_route_dev(buf, to_dev(d), n, None, ql, qcap, tc, hi, 8, 0, cap, sd, sc)
+        sd = torch.full((8 * rb,), 0xEE, dtype=torch.uint8, device="cuda")
+        sc = torch.full((16,), -1, dtype=torch.int32, device="cuda")
+        rx.parse_route_dev(buf, to_dev(d), n, None, ql, qcap, tc, hi, 8, 0, cap, sd, sc, tail_cap=tcap)
         torch.cuda.synchronize()
-        outs.append((sc.cpu().numpy(), sd.cpu().numpy()))
-    assert int(outs[0][0].sum()) == int((~holes).sum())
+        c, b = sc.cpu().numpy(), sd.cpu().numpy().reshape(8, rb)
+        # the regions' records with their tails (the tail units' order within a shard is not
+        # deterministic, what each head's tail holds is)
+        outs.append((c, [X.lookup_records(b[k], int(c[2 * k]), cap, tcap).tobytes() for k in range(8)]))
+    assert int(outs[0][0][0::2].sum()) == int((~holes).sum()) and (outs[0][0][1::2] == 0).all()
+    # config D's ICMPv6 echo frames (5 %) carry a one-unit tail
+    assert sum(len(r) for r in outs[0][1]) > 0
     for c, s in outs[1:]:
-        assert np.array_equal(c, outs[0][0]) and np.array_equal(s, outs[0][1])
+        assert np.array_equal(c, outs[0][0]) and s == outs[0][1]
+
+
+def test_tail_shard_overflow(rxmod):
+    """A tail shard too small for its units (emurx_parse_route_dev): the send counts report,
+    per region, the units the fullest shard needed (> tail_cap), the heads whose tails did not
+    fit carry EMURX_TAIL_NONE, and the owner's lookups over such a region stay in bounds.  With
+    tail_cap grown to the reported need (exchange.grow_tail) the regions hold every record with
+    its tail, equal to a run with room to spare."""
+    import torch
+    from emurx import exchange as X
+    from gpu_util import to_dev
+    n = 1 << 16
+    w = synth.config_d(n, rank=1)
+    rx = rxmod(0, max_ns=32768, max_clients=1 << 20, max_frames=n)
+    rx.register_all()
+    rx.set_partition(4, 0)
+    synth.load_tables(w, rx)
+    buf, desc = to_dev(w["buf"]), to_dev(w["desc"])
+    rx.desc_keys_dev(buf, desc, n)
+    cap = X.capacity(n, 4)
+    qcap = abi.queue_cap(n)
+
+    def route(tcap):
+        rb = abi.lookup_region_bytes(cap, tcap)
+        ql = torch.empty(abi.NUM_QUEUES * qcap, dtype=torch.int32, device="cuda")
+        tc = torch.empty(abi.ntiles(n) * 16, dtype=torch.int32, device="cuda")
+        hi = torch.zeros(abi.HIST_SHARDS * 2 * abi.HIST_BINS, dtype=torch.int64, device="cuda")
+        sd = torch.full((4 * rb,), 0xEE, dtype=torch.uint8, device="cuda")
+        sc = torch.full((8,), -1, dtype=torch.int32, device="cuda")
+        rx.parse_route_dev(buf, desc, n, None, ql, qcap, tc, hi, 4, 1, cap, sd, sc, tail_cap=tcap)
+        torch.cuda.synchronize()
+        return sd, sc.cpu().numpy(), rb
+
+    sd, c, rb = route(1)
+    need = c[1::2]
+    assert (need > 1).any(), c
+    b = sd.cpu().numpy().reshape(4, rb)
+    lost = 0
+    for k in range(4):
+        hd = b[k, : int(c[2 * k]) * 32].view(abi.LOOKUP_REC_DTYPE)
+        u = X.tail_units(hd["w4"])
+        assert u.sum() > 0
+        lost += int((hd["x"][u > 0] == abi.TAIL_NONE).sum())
+    assert lost > 0
+    # the owner side over the overflowed regions: reads stay inside the buffer
+    out = torch.empty(4 * cap * X.REC_BYTES, dtype=torch.uint8, device="cuda")
+    rx.lookup_dev(sd, torch.from_numpy(c).cuda(), 4, cap, out, tail_cap=1)
+    torch.cuda.synchronize()
+    tcap = X.grow_tail(1, need)
+    sd2, c2, rb2 = route(tcap)
+    assert (c2[1::2] == 0).all() and np.array_equal(c2[0::2], c[0::2])
+    sd3, c3, rb3 = route(tail_cap_max(n))
+    b2, b3 = sd2.cpu().numpy().reshape(4, rb2), sd3.cpu().numpy().reshape(4, rb3)
+    for k in range(4):
+        r2 = X.lookup_records(b2[k], int(c2[2 * k]), cap, tcap)
+        r3 = X.lookup_records(b3[k], int(c3[2 * k]), cap, tail_cap_max(n))
+        assert r2.tobytes() == r3.tobytes()
 
 
 def test_table_allocation_fallback():

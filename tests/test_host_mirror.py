@@ -14,6 +14,17 @@ def _build():
     subprocess.run(["make", "-s", "-C", str(ROOT / "trex-emu_amd")], check=True)
 
 
+def test_mirror_shrink_from_live_entries():
+    """The allocation fallback's table shrink (Mirror::shrink, ADVICE r04): an IPv6 table filled
+    to twice its target load (a DHCPv6 address for most clients, ns_ctx.go:442-533) shrinks
+    from its live entries, keeps one more insert under the 3/4 bound and every address
+    findable, and stops when no denser table is smaller (host-only C++ check)."""
+    _build()
+    r = subprocess.run([str(ROOT / "trex-emu_amd" / "build" / "test_mirror")], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0 and "PASS TestShrinkFromLive" in r.stdout, r.stdout + r.stderr
+
+
 def test_host_mirror_builds():
     _build()
     assert BIN.exists() and KAT.exists()

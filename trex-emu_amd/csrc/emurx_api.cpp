@@ -179,8 +179,9 @@ struct emurx_ctx {
         bool used = false;
         hipEvent_t done = nullptr;                      // recorded after each route on st
         DevBuf<uint32_t> cnt, grp, goff;                // grp: zero between batches
+        DevBuf<uint32_t> tcur;                          // tail cursors of the partitioned source
         void release() {
-            cnt.release(); grp.release(); goff.release();
+            cnt.release(); grp.release(); goff.release(); tcur.release();
             if (done) (void)hipEventDestroy(done);
             done = nullptr;
         }
@@ -447,7 +448,8 @@ int route_scratch(emurx_t* h, uint32_t n, hipStream_t st, emurx_t::RouteScratch*
     if (!r->grp.p) {
         if (r->grp.alloc(gw) || !EMURX_HIP_OK(hipMemset(r->grp.p, 0, gw * sizeof(uint32_t)))) return EMURX_ENOMEM;
     }
-    if (r->cnt.alloc(tiles * 16) || r->goff.alloc(gw)) return EMURX_ENOMEM;
+    if (r->cnt.alloc(tiles * 16) || r->goff.alloc(gw) || r->tcur.alloc(EMURX_MAX_PARTS * EMURX_TAIL_SHARDS * EMURX_TAIL_CURSOR_STRIDE))
+        return EMURX_ENOMEM;
     *out = r;
     return EMURX_OK;
 }
@@ -1090,13 +1092,20 @@ int emurx_classify_route_dev(emurx_t* h, const uint8_t* d_frames, const emurx_de
     return route_done(rs, st);
 }
 
+// the whole send / receive buffer of n_parts lookup regions in 32-byte units fits 32 bits (k_rx
+// kind 2 addresses heads by such units)
+static bool lookup_regions_fit(uint32_t n_parts, uint32_t cap, uint32_t tail_cap) {
+    return EMURX_LOOKUP_REGION_BYTES(cap, tail_cap) / 32 * n_parts < (1ull << 32) &&
+           (uint64_t)EMURX_TAIL_SHARDS * tail_cap < (1ull << 32) - 4;
+}
+
 int emurx_parse_route_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_desc, uint32_t n,
                           const emurx_dev_out* out, uint32_t n_parts, uint32_t my_rank, uint32_t cap,
-                          emurx_lookup_rec* d_send, uint32_t* d_send_count, void* stream) {
+                          uint32_t tail_cap, emurx_lookup_rec* d_send, uint32_t* d_send_count, void* stream) {
     int rc = check_batch_args(h, d_frames, d_desc, n, out);
     if (rc) return rc;
     if (!d_send_count || n_parts == 0 || n_parts > EMURX_MAX_PARTS || my_rank >= n_parts ||
-        (n && (!d_send || cap == 0)) || ((uintptr_t)d_send & 15))
+        (n && (!d_send || cap == 0)) || ((uintptr_t)d_send & 15) || !lookup_regions_fit(n_parts, cap, tail_cap))
         return EMURX_EINVAL;
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
     // before anything is enqueued: nothing of a refused call may end up in the caller's graph
@@ -1104,23 +1113,42 @@ int emurx_parse_route_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc*
     emurx_t::RouteScratch* rs = nullptr;
     if ((rc = route_scratch(h, n, st, &rs))) return rc;
     // owner counts from the L2 headers + group scan, then k_rx packs at those offsets
-    if (emurx_launch_owner_count(d_frames, d_desc, n, n_parts, d_send_count, rs->cnt.p, rs->grp.p, rs->goff.p, st))
+    if (emurx_launch_owner_count(d_frames, d_desc, n, n_parts, d_send_count, rs->cnt.p, rs->grp.p, rs->goff.p,
+                                 rs->tcur.p, st))
         return EMURX_EDEVICE;
-    const emurx_route_args rt{n_parts, my_rank, cap, rs->cnt.p, rs->grp.p, rs->goff.p, d_send};
+    // tcp / udp heads carry their c5tuplekey while ANY client has a TransportCtx: the maps are
+    // complete on every partition's handle, the flow tables only on the owner's
+    const uint32_t tup_on = h->m.n_ctx_all ? 1u : 0u;
+    const emurx_route_args rt{n_parts, my_rank, cap, rs->cnt.p, rs->grp.p, rs->goff.p, d_send,
+                              tail_cap, rs->tcur.p, d_send_count, tup_on};
     if (n && (rc = run_dev(h, d_frames, d_desc, n, out, st, 2, &rt))) return rc;
     return route_done(rs, st);
 }
 
+int emurx_zmq_walk_dev(emurx_t* h, const uint8_t* d_buf, const uint32_t* d_ctl, uint32_t nmsg, emurx_desc* d_desc,
+                       uint32_t* d_msg_stat, uint32_t flags, void* stream) {
+    if (!h || (nmsg && (!d_buf || !d_ctl || !d_desc || !d_msg_stat)) || ((uintptr_t)d_desc & 7) ||
+        ((uintptr_t)d_ctl & 7) || (flags & ~EMURX_WALK_NO_KEYS))
+        return EMURX_EINVAL;
+    int rc = bind(h);
+    if (rc) return rc;
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    if ((rc = not_capturing(st))) return rc;
+    return emurx_launch_zmq_walk(d_buf, d_ctl, nmsg, d_desc, d_msg_stat, st, !(flags & EMURX_WALK_NO_KEYS))
+               ? EMURX_EDEVICE
+               : EMURX_OK;
+}
+
 int emurx_lookup_dev(emurx_t* h, const emurx_lookup_rec* d_recv, const uint32_t* d_recv_count, uint32_t n_parts,
-                     uint32_t cap, emurx_route_rec* d_out, uint32_t* d_flow, void* stream) {
+                     uint32_t cap, uint32_t tail_cap, emurx_route_rec* d_out, uint32_t* d_flow, void* stream) {
     if (!h || !d_recv_count || n_parts == 0 || n_parts > EMURX_MAX_PARTS || (cap && (!d_recv || !d_out)) ||
-        ((uintptr_t)d_recv & 15) || ((uintptr_t)d_out & 7))
+        ((uintptr_t)d_recv & 15) || ((uintptr_t)d_out & 7) || !lookup_regions_fit(n_parts, cap, tail_cap))
         return EMURX_EINVAL;
     int rc = bind(h);
     if (rc) return rc;
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
     if ((rc = not_capturing(st)) || (rc = prepare_read(h, st))) return rc;
-    return emurx_launch_lookup(d_recv, d_recv_count, n_parts, cap, h->tables(), d_out, d_flow, st) ? EMURX_EDEVICE
+    return emurx_launch_lookup(d_recv, d_recv_count, n_parts, cap, tail_cap, h->tables(), d_out, d_flow, st) ? EMURX_EDEVICE
                                                                                                     : EMURX_OK;
 }
 

@@ -35,6 +35,9 @@ __device__ __forceinline__ uint32_t ld_be32(const uint8_t* p) {
     return __builtin_bswap32(__builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(a & 3)));
 }
 
+// kKeys: derive each frame's Namespace-owner key (EMURX_DESC_KEYED) on the way; false only in
+// the measurement of what that costs (emurx_zmq_walk_dev, EMURX_WALK_NO_KEYS)
+template <bool kKeys>
 __global__ __launch_bounds__(kBlock) void k_zmq_walk(const uint8_t* __restrict__ buf,
                                                      const uint32_t* __restrict__ ctl, uint32_t nmsg,
                                                      emurx_desc* __restrict__ desc,
@@ -71,9 +74,12 @@ __global__ __launch_bounds__(kBlock) void k_zmq_walk(const uint8_t* __restrict__
                 if (found >= slots) { err = EMURX_MSG_PANIC; break; }  // unreachable: slots bound the walk
                 // the owner key from the CTunnelKey the parse will leave (l2_vlans: the frame's
                 // bytes 12..19 and its length); bytes past the frame are masked by the length
-                uint32_t v0, v1;
-                l2_vlans(plen, ld_be32(s + h4 + 12), ld_be32(s + h4 + 16), v0, v1);
-                const uint32_t key = emurx_owner_key(emurx_tk_hash(vport, v0, v1));
+                uint32_t key = 0;
+                if constexpr (kKeys) {
+                    uint32_t v0, v1;
+                    l2_vlans(plen, ld_be32(s + h4 + 12), ld_be32(s + h4 + 16), v0, v1);
+                    key = emurx_owner_key(emurx_tk_hash(vport, v0, v1));
+                }
                 reinterpret_cast<uint2*>(desc)[base + found] = make_uint2(M.x + h4, plen | (vport << 16) | (key << 24));
                 ++found;
                 of = e;
@@ -578,11 +584,11 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
 }  // namespace emurx
 
 int emurx_launch_zmq_walk(const uint8_t* buf, const uint32_t* ctl, uint32_t nmsg, emurx_desc* desc,
-                          uint32_t* msg_stat, hipStream_t st) {
+                          uint32_t* msg_stat, hipStream_t st, bool keys) {
     using namespace emurx;
     if (!nmsg) return 0;
-    return EMURX_HIP_OK(emurx_launch(k_zmq_walk, dim3((nmsg + kBlock - 1) / kBlock), dim3(kBlock), 0, st, buf, ctl,
-                                     nmsg, desc, msg_stat))
+    return EMURX_HIP_OK(emurx_launch(keys ? k_zmq_walk<true> : k_zmq_walk<false>, dim3((nmsg + kBlock - 1) / kBlock),
+                                     dim3(kBlock), 0, st, buf, ctl, nmsg, desc, msg_stat))
                ? 0
                : -1;
 }

@@ -46,13 +46,21 @@ inline hipError_t emurx_launch(void (*k)(P...), dim3 grid, dim3 block, size_t ld
 // rt (optional): kind 1: the route count pass fused in (per-(tile, owner) counts into cnt,
 // per-group sums added into grp, as emurx_launch_route's first pass); kind 2 (required): the
 // owner counts cnt / group offsets goff of k_owner_count + k_route_scan, and every frame's
-// 64-byte emurx_lookup_rec (emurx_parse.h pack_lookup) packed into send[owner * cap + ..).
+// 32-byte emurx_lookup_rec head (emurx_parse.h pack_lookup) packed into region `owner` of send
+// (EMURX_LOOKUP_REGION_BYTES(cap, tcap) bytes each), its tail units at the units its wave took
+// from tcur[(owner * EMURX_TAIL_SHARDS + shard) * EMURX_TAIL_CURSOR_STRIDE] (a line each: the
+// atomics of different cursors do not serialise on one line); count: the send counts (stride 2), where an
+// overflowing tail shard records the units it needed.
 struct emurx_route_args {
     uint32_t parts, rank, cap;
     uint32_t* cnt;
     uint32_t* grp;
     const uint32_t* goff;
     emurx_lookup_rec* send;
+    uint32_t tcap;
+    uint32_t* tcur;
+    uint32_t* count;
+    uint32_t tup_on;  // some client has a TransportCtx: tcp / udp heads carry their c5tuplekey tail
 };
 int emurx_launch_batch(const uint8_t* frames, const emurx_desc* desc, uint32_t n,
                        const emurx_dev_tables& T, int kind, const emurx_dev_out& out,
@@ -76,20 +84,24 @@ int emurx_launch_route(const emurx_rec* rec, uint32_t n, uint32_t n_parts, uint3
 // The owner counts of the partitioned source (emurx_parse_route_dev): k_owner_count (the
 // CTunnelKey of every frame from its L2 header alone, counted per (tile, owner) and per group)
 // + k_route_scan -> tile_cnt, grp_off, send_count; k_rx kind 2 then packs.  Two launches.
+// send_count: [2 n_parts] {heads, tail overflow}; tcur [n_parts * EMURX_TAIL_SHARDS] cleared.
 int emurx_launch_owner_count(const uint8_t* frames, const emurx_desc* desc, uint32_t n, uint32_t n_parts,
                              uint32_t* send_count, uint32_t* tile_cnt, uint32_t* grp, uint32_t* grp_off,
-                             hipStream_t st);
+                             uint32_t* tcur, hipStream_t st);
 // The owner keys of device-resident descriptors (emurx_desc_keys_dev), in place.  One launch.
 int emurx_launch_desc_keys(const uint8_t* frames, emurx_desc* desc, uint32_t n, hipStream_t st);
-// The owner side (emurx_lookup_dev): one lane per received slot, n_parts regions of cap.
+// The owner side (emurx_lookup_dev): one lane per received head, n_parts regions of
+// EMURX_LOOKUP_REGION_BYTES(cap, tcap) bytes; recv_count stride 2 (heads, tail overflow).
 int emurx_launch_lookup(const emurx_lookup_rec* recv, const uint32_t* recv_count, uint32_t n_parts, uint32_t cap,
-                        const emurx_dev_tables& T, emurx_route_rec* out, uint32_t* flow, hipStream_t st);
+                        uint32_t tcap, const emurx_dev_tables& T, emurx_route_rec* out, uint32_t* flow,
+                        hipStream_t st);
 
 // Batched ZMQ ingest (emurx_ingest.hip).  zmq_walk: one lane per message; ctl = emurx_msg[nmsg]
 // then slot_base[nmsg + 1]; writes desc[slot_base[m] ..) (holes marked EMURX_DESC_HOLE) and
 // msg_stat[m] = frames | EMURX_MSG_* << 24.  The buffer must be readable 8 bytes past every message.
+// keys = false: descriptors without owner keys (the measurement of their cost only).
 int emurx_launch_zmq_walk(const uint8_t* buf, const uint32_t* ctl, uint32_t nmsg, emurx_desc* desc,
-                          uint32_t* msg_stat, hipStream_t st);
+                          uint32_t* msg_stat, hipStream_t st, bool keys = true);
 // A small batch (at most EMURX_SMALL_TILES tiles, EMURX_SMALL_MSGS messages, every tile's messages within the
 // kernel's LDS budget: emurx_ingest_small_fits) in ONE launch: messages and control words read
 // from pinned host memory, walk + parse + classify + queue packing, every result written into

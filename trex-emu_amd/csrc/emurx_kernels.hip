@@ -191,18 +191,22 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
 
     Rec r;
     r.dlen = 0;
-    // kKind 2: the frame's 64-byte lookup record (emurx_parse.h pack_lookup), parked in the
-    // wave's slab (64 lanes x 64 B = 4 KiB) from the end of the parse until the owner offsets are
-    // known after the tile barrier: no registers held across it
-    uint4* lrec = reinterpret_cast<uint4*>(const_cast<uint32_t*>(slab)) + wv * (kStage / 16) + lane * 4;
-    static_assert(kStage >= kWave * 64, "a wave's lookup records fit its slab");
+    // kKind 2: the frame's lookup record (emurx_parse.h pack_lookup), parked in the wave's slab
+    // from the end of the parse: the 32-byte heads (2 KiB) until the owner offsets are known
+    // after the tile barrier, the tails (up to 48 B per lane, the next 3 KiB) until the wave has
+    // taken their units: no registers held across either
+    uint4* const wslab = reinterpret_cast<uint4*>(const_cast<uint32_t*>(slab)) + wv * (kStage / 16);
+    uint4* lhead = wslab + lane * 2;
+    uint4* ltail = wslab + kWave * 2 + lane * 3;
+    static_assert(kStage >= kWave * (32 + 48), "a wave's lookup heads and tails fit its slab");
+    uint32_t tun = 0;  // kKind 2: the frame's tail units (0, 1 or 3)
     if (sg.staged) {  // wave-uniform branch
         if (valid) {
             LdsSrc s{reinterpret_cast<const uint8_t*>(slab), slab, wv * kStage + (off - sg.start)};
             parse_flat(s, len, vport, T.cb_mask, r);
             STAMP(3);
             if (kClassify) classify(s, len, T, r);
-            if (kKind == 2) pack_lookup(s, len, r, i, r.status == EMURX_ST_OK, lrec);
+            if (kKind == 2) tun = pack_lookup(s, len, r, i, r.status == EMURX_ST_OK, rt.tup_on, lhead, ltail);
         }
     } else {
         const uint32_t head = (uint32_t)((uintptr_t)(a.frames + off) & 15);
@@ -212,9 +216,67 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
         coop_checksum_rows(r, a.frames + off, L.csum[wv]);  // the wave's long L4 spans, converged
         STAMP(3);
         if (valid && kClassify) classify(s, len, T, r);
-        if (kKind == 2 && valid) pack_lookup(s, len, r, i, r.status == EMURX_ST_OK, lrec);
+        if (kKind == 2 && valid) tun = pack_lookup(s, len, r, i, r.status == EMURX_ST_OK, rt.tup_on, lhead, ltail);
     }
     STAMP(4);
+    // kind 2: the frame's owner, its rank among the wave's frames of that owner, and its tail's
+    // units: per (wave, owner) one atomic on the owner's cursor of this tile's shard (a line
+    // each) takes the units of the wave's tails (tails of 1 and 3 units ranked by two ballots).
+    // Issued here, consumed after the tile barrier (store_tails): the histogram, the queue ranks
+    // and the barrier hide the atomic's round trip
+    uint32_t rd = 0xffu, rrank = 0, tofs = 0, tlead = 0, tb = 0;
+    const uint32_t shard = tile & (EMURX_TAIL_SHARDS - 1);
+    if constexpr (kKind == 2) {
+        const uint32_t pad = dd.y >> 24;
+        // the owner the count pass used (a keyed descriptor's key, the same digest of the
+        // CTunnelKey the parse left: packing and counts agree by construction)
+        rd = !valid ? 0xffu
+             : (pad & EMURX_DESC_KEYED) ? emurx_owner_of_key(pad, rt.parts)
+                                        : emurx_owner(emurx_tk_hash(r.vport, r.vlan0, r.vlan1), rt.parts);
+        uint64_t rl = __ballot(rd != 0xffu);
+        while (rl) {
+            const uint32_t lead = (uint32_t)__ffsll((long long)rl) - 1;
+            const uint32_t d2 = (uint32_t)__builtin_amdgcn_readlane((int)rd, (int)lead);
+            const uint64_t m = __ballot(rd == d2);
+            const uint64_t m1 = __ballot(rd == d2 && tun == 1), m3 = __ballot(rd == d2 && tun == 3);
+            if (rd == d2) {
+                rrank = mbcnt(m);
+                tofs = mbcnt(m1) + 3 * mbcnt(m3);
+            }
+            if (lane == lead) L.rcnt[wv][d2] = (uint32_t)__popcll(m);
+            if (m1 | m3) {  // wave-uniform
+                const uint32_t tl = (uint32_t)__ffsll((long long)(m1 | m3)) - 1;
+                if (lane == tl)
+                    tb = atomicAdd(&rt.tcur[(d2 * EMURX_TAIL_SHARDS + shard) * EMURX_TAIL_CURSOR_STRIDE],
+                                   (uint32_t)(__popcll(m1) + 3 * __popcll(m3)));
+                if (rd == d2) tlead = tl;
+            }
+            rl &= ~m;
+        }
+    }
+    // each lane stores its tail at the units its wave took and writes their index into its
+    // parked head (kind 2)
+    auto store_tails = [&]() {
+        if (!__ballot(tun != 0)) return;
+        const uint32_t at = (uint32_t)__shfl((int)tb, (int)tlead) + tofs;
+        if (tun) {
+            uint32_t idx = EMURX_TAIL_NONE;
+            if (at + tun <= rt.tcap) {
+                idx = shard * rt.tcap + at;
+                uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(rt.send) +
+                                                      (uint64_t)rd * (rt.cap + 32ull * rt.tcap) * 32 +
+                                                      (uint64_t)rt.cap * 32) + idx;
+                dst[0] = ltail[0];
+                if (tun == 3) {
+                    dst[1] = ltail[1];
+                    dst[2] = ltail[2];
+                }
+            } else {
+                atomicMax(&rt.count[2 * rd + 1], at + tun);  // the shard overflowed: the caller regrows
+            }
+            reinterpret_cast<uint32_t*>(lhead)[7] = idx;
+        }
+    };
     // outcome histogram into the wave's LDS copy: a wave whose frames all share one
     // (status, proto) bin adds its count (ballot) and byte sum (DPP reduction) once, instead
     // of 64 LDS atomics serialised on one address; mixed waves add per frame
@@ -261,6 +323,11 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
     STAMP(5);
     STAMP(6);
     typedef unsigned v4u __attribute__((ext_vector_type(4)));
+    bool tails_out = false;
+    if (kKind == 2 && a.rec) {  // the records' park below reuses the tails' LDS rows
+        store_tails();
+        tails_out = true;
+    }
     if (a.rec) {
         // The wave's 64 records (32 B each) go out as two contiguous 1 KiB stores: every lane
         // parks its record in the wave's slab (free once the parse, the lookups and the lookup
@@ -270,7 +337,7 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
         // batches: config B +3 %, C +0.5 %, E +1 %; non-temporal beats plain stores either way).
         // An empty descriptor slot gets a record too (no Namespace, status EMURX_ST_HOLE), so
         // every consumer of rec[0, n) sees defined bytes.
-        constexpr uint32_t kPark = kKind == 2 ? 256u : 0u;  // in 16-B units
+        constexpr uint32_t kPark = kKind == 2 ? 2u * kWave : 0u;  // in 16-B units: after the heads (the tails are stored)
         static_assert(kPark * 16 + kWave * 32 <= kStage, "the parked records fit the slab");
         uint4* park = reinterpret_cast<uint4*>(const_cast<uint32_t*>(slab)) + wv * (kStage / 16) + kPark;
         park[2 * lane] = valid ? make_uint4(r.ns, r.cl, r.vlan0, r.vlan1)
@@ -291,23 +358,11 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
     }
     if (a.flow && i < n) a.flow[i] = valid ? r.flow : EMURX_FLOW_NONE;
     // the Namespace owner of the record (classify + route: the records whose Namespace was
-    // found; lookup keys: every frame)
-    uint32_t rd = 0xffu;
-    if ((kKind == 1 && rt.cnt) || kKind == 2) {
-        const bool routed = valid && (kKind == 2 || r.ns != EMURX_ID_NONE);
-        // kind 2: the owner the count pass used (a keyed descriptor's key, the same digest of
-        // the CTunnelKey the parse left: packing and counts agree by construction)
-        const uint32_t pad = dd.y >> 24;
-        rd = !routed ? 0xffu
-             : (kKind == 2 && (pad & EMURX_DESC_KEYED)) ? emurx_owner_of_key(pad, rt.parts)
-                                                        : emurx_owner(emurx_tk_hash(r.vport, r.vlan0, r.vlan1), rt.parts);
-    }
-    // Namespace owners (rt.parts > 0): kind 1 counts the records whose Namespace was found
-    // (the first pass of emurx_route_dev, fused; k_route<false> counts them the same way,
-    // emurx_route.hip); kind 2 packs every frame's lookup record into its owner's region,
-    // ranked by ballots like the queues
-    uint32_t rrank = 0;
-    if ((kKind == 1 && rt.cnt) || kKind == 2) {
+    // found), counted per (tile, owner): the first pass of emurx_route_dev, fused (k_route<false>
+    // counts them the same way, emurx_route.hip); kind 2 ranked its owners above
+    if (kKind == 1 && rt.cnt) {
+        const bool routed = valid && r.ns != EMURX_ID_NONE;
+        rd = !routed ? 0xffu : emurx_owner(emurx_tk_hash(r.vport, r.vlan0, r.vlan1), rt.parts);
 #if EMURX_MATCHRANK
         const uint64_t m = match_lanes<3>(rd, __ballot(rd != 0xffu));
         rrank = mbcnt(m);
@@ -332,23 +387,29 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
         rt.cnt[(size_t)tile * 16 + tid] = c;
         if (c) atomicAdd(&rt.grp[(tile / 64) * 16 + tid], c);
     }
-    if constexpr (kKind == 2) {  // every frame's 64-byte lookup record into its owner's region
-        uint32_t dst = 0xffffffffu;  // the record's slot in send (record units), none on overflow
+    if constexpr (kKind == 2) {  // every frame's 32-byte lookup head into its owner's region
+        if (!tails_out) {
+            store_tails();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the patched heads, read by other lanes
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        // the head's slot in send, in 32-byte units (regions of cap + 32 tcap of them: the
+        // launcher checks that the whole buffer's units fit 32 bits); none on overflow
+        uint32_t dst = 0xffffffffu;
         if (rd != 0xffu) {
             uint32_t pos = L.toff[rd] + rrank;
             for (uint32_t w = 0; w < wv; ++w) pos += L.rcnt[w][rd];
-            if (pos < rt.cap) dst = rd * rt.cap + pos;  // overflow: send_count[d] > cap tells the caller
+            if (pos < rt.cap) dst = rd * (rt.cap + 32u * rt.tcap) + pos;  // overflow: send_count[2 d] > cap
         }
-        // four lanes per record, 16 records per store instruction: a record is one whole line
-        // written by one instruction, and records of one owner ranked next to each other
-        // (every one of them at N = 1) make contiguous 1 KiB stores, instead of each lane
-        // writing its own record as four 16-B pieces 64 B apart
-        const uint4* parked = reinterpret_cast<const uint4*>(slab) + wv * (kStage / 16);
+        // two lanes per head, 32 heads per store instruction: heads of one owner ranked next to
+        // each other (every one of them at N = 1) make contiguous 1 KiB stores
+        const uint4* parked = wslab;
 #pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-            const uint32_t rr = k * (kWave / 4) + lane / 4, part = lane & 3;
+        for (uint32_t k = 0; k < 2; ++k) {
+            const uint32_t rr = k * (kWave / 2) + lane / 2, part = lane & 1;
             const uint32_t to = (uint32_t)__shfl((int)dst, (int)rr);
-            if (to != 0xffffffffu) reinterpret_cast<uint4*>(rt.send + to)[part] = parked[rr * 4 + part];
+            if (to != 0xffffffffu) reinterpret_cast<uint4*>(rt.send + to)[part] = parked[rr * 2 + part];
         }
     }
 

@@ -147,17 +147,31 @@ void Mirror::set_partition(uint32_t n, uint32_t p) {
     nsinfo.resize_blocks(nsinfo.nblocks());
     for (uint32_t i = 0; i < max_ns; ++i)
         if (ns[i].alive) put_nsinfo(i);
-    n_ctx = 0;
+    n_ctx = n_ctx_all = 0;
     for (uint32_t c = 0; c < max_clients; ++c)
-        if (cl[c].alive && cl[c].has_ctx && owned_ns(cl[c].ns)) ++n_ctx;
+        if (cl[c].alive && cl[c].has_ctx) {
+            ++n_ctx_all;
+            if (owned_ns(cl[c].ns)) ++n_ctx;
+        }
 }
 
+// The table sized from its LIVE entries at half the spread (not the old bucket count halved: a
+// table grown to ~2 / spread, e.g. IPv6 sized for one address per client that then got both
+// Ipv6 and Dhcpv6, would land at load 1), never past the 3/4 bound Hash::put relies on with one
+// more insert; false when that is no smaller than the table whose allocation failed (ENOMEM)
 bool Mirror::shrink(int k) {
     Hash& t = *hashes(k);
-    if (t.spread <= 2) return false;
-    t.spread >>= 1;
-    rebuild(k, std::max<uint32_t>(t.buckets / 2, 1));
-    return true;
+    const uint32_t per = t.per();
+    for (uint32_t sp = t.spread >> 1; sp >= 2; sp >>= 1) {  // the first denser spread that is smaller
+        uint64_t slots = pow2_at_least(std::max<uint64_t>((uint64_t)sp * t.live, per));
+        while ((uint64_t)(t.live + 1) * 4 > slots * 3) slots *= 2;
+        const uint64_t nb = std::max<uint64_t>(slots / per, 1);
+        if (nb >= t.buckets) continue;
+        t.spread = sp;
+        rebuild(k, (uint32_t)nb);
+        return true;
+    }
+    return false;
 }
 
 uint32_t Mirror::tk_of(uint32_t ns_id) const {
@@ -418,6 +432,7 @@ void Mirror::drop_transport(uint32_t cid) {
     }
     ClientInfo& c = cl[cid];
     if (c.has_ctx && owned_ns(c.ns)) --n_ctx;
+    if (c.has_ctx) --n_ctx_all;
     c.has_ctx = false;
 }
 
@@ -536,6 +551,7 @@ int Mirror::client_set_transport(uint32_t cid, bool has) {
     if (cid >= max_clients || !cl[cid].alive) return EMURX_ENOENT;
     ClientInfo& c = cl[cid];
     if (c.has_ctx != has && owned_ns(c.ns)) n_ctx += has ? 1 : -1;
+    if (c.has_ctx != has) n_ctx_all += has ? 1 : -1;
     c.has_ctx = has;
     rewrite_client_slots(cid);
     touch_ns(c.ns);

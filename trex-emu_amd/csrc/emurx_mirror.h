@@ -133,6 +133,7 @@ struct Mirror {
     std::unordered_map<std::string, Entry> ft_map;  // (client id, tuple bytes) -> flow id
     std::unordered_map<uint64_t, Entry> srv_map;    // client id << 32 | port | proto << 16
     uint32_t n_ctx = 0;                             // owned live clients with a TransportCtx
+    uint32_t n_ctx_all = 0;                         // live clients with a TransportCtx, all partitions
     Hash ns_t, mac_t, ip4_t, ip6_t, ci_t, ft4_t, ft6_t, srv_t;
     Blocks nsinfo;                                  // 4 words per ns id, dense
     uint64_t gen = 1;

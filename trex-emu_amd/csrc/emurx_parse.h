@@ -1441,19 +1441,28 @@ __device__ __forceinline__ void classify(const S& s, uint32_t len, const emurx_d
     resolve(T, r, k, [&](uint32_t cid) { return flow_probe(T, get_tuple(s, len, r), cid); });
 }
 
-// ---- partitioned path: the lookup record (include/emu_rx.h emurx_lookup_rec, 64 bytes) ---
-// Everything the owner needs to finish the frame, in 16 words:
+// ---- partitioned path: the lookup record (include/emu_rx.h emurx_lookup_rec) -----------
+// Everything the owner needs to finish the frame: a 32-byte head, and for two classes a tail
+// of 16-byte units in the region's tail shards (emu_rx.h).  Head words:
 //   w0  source frame index (the source rank is the region the record arrives in)
 //   w1  the CTunnelKey VLAN words, 14 bits each (vlan_code): TPID 0x8100 / 0x88A8 / none + VID
 //   w2  vport | l3 << 8 | next_hdr << 24          w3  l4 | l7 << 16
 //   w4  l7_len | proto << 16 (4 bits, 15 = none) | status << 20 (5 bits) | RTALERT << 25 |
-//       v6 << 26 | mc6 << 27 | key << 28 (3 bits)  (the parse's own flags bit is RTALERT alone)
-//   w5  destination MAC bytes 0..3                w6  bytes 4..5 | TCP flags << 16
-//   w7  tcp / udp: the ports as on the wire (c5tuplekey bytes 8..11 order)
-//   w8..w15  tcp / udp over IPv4: src, dst; over IPv6: src[4], dst[4] (the c5tuplekey; its
-//       protocol byte is next_hdr); other callbacks: kw[0..3] of the rule's key (MAC / IPv4 /
-//       IPv6 / EUI-64 / chaddr) in w8..w11
+//       v6 << 26 | mc6 << 27 | key << 28 (3 bits) | tuple << 31  (the parse's own flags bit is
+//       RTALERT alone)
+//   w5  destination MAC bytes 0..3                w6  bytes 4..5 | hi << 16
+//   w7  (x) kMac: key bytes 0..3 (hi = bytes 4..5; the destination MAC unless DHCP's chaddr);
+//       kIp4: the address; kIp6 / kEui and tuple records: the first tail unit (EMURX_TAIL_NONE
+//       when it did not fit)
+// kIp6 / kEui (ICMPv6 echo: L7 = L7Len = 0, parser.go:684-717): the client-table hash of the
+// key in place of l7 (bits 0..15) and l7_len (16..31), so the owner issues the client probe
+// with the Namespace probe and the tail load; tail = the IPv6 destination (4 words).
+// tuple (tcp / udp, kMac, while some client has a TransportCtx): hi = the TCP flags byte; tail
+// = {ports, src, dst, 0} over IPv4, {ports, src[0..2]} {src[3], dst[0..2]} {dst[3], 0, 0, 0}
+// over IPv6 (fillv4tuple / fillv6tuple src/emu/plugins/transport/client_ctx.go:720-765; its
+// protocol byte is next_hdr).
 __device__ __forceinline__ bool lk_transport(uint32_t cb) { return cb == EMURX_CB_TCP || cb == EMURX_CB_UDP; }
+__device__ __forceinline__ bool lk_ip6key(uint32_t key) { return key == kIp6 || key == kEui; }
 // a CTunnelKey VLAN word (TPID << 16 | VID, parser.go:810) in 14 bits: ParsePacket only takes
 // tags with TPID 0x8100 or 0x88A8, and an untagged slot is 0
 __device__ __forceinline__ uint32_t vlan_code(uint32_t v) {
@@ -1463,46 +1472,71 @@ __device__ __forceinline__ uint32_t vlan_word(uint32_t c) {
     const uint32_t t = (c >> 12) & 3u;
     return t == 0 ? 0u : ((t == 1 ? 0x8100u : 0x88A8u) << 16) | (c & 0xfffu);
 }
-// the record of a frame; `ok`: it reached a callback (the key words are zero otherwise).
-// Written as four 16-byte stores to dst (LDS: the wave's slab, once the parse is done with it)
+// the MAC of an EUI-64 IPv6 address (ExtractOnlyMac client_ctx.go:314-329) from its words 2, 3
+__device__ __forceinline__ uint2 eui_mac(uint32_t w2, uint32_t w3) {
+    return make_uint2(((w2 & 0xff) ^ 2) | (((w2 >> 8) & 0xff) << 8) | (((w2 >> 16) & 0xff) << 16) | (((w3 >> 8) & 0xff) << 24),
+                      ((w3 >> 16) & 0xff) | ((w3 >> 24) << 8));
+}
+// tail units of a head (0, 1 or 3), from its w4
+__device__ __forceinline__ uint32_t lk_tail_units(uint32_t w4) {
+    const uint32_t key = (w4 >> 28) & 7u;
+    if (((w4 >> 20) & 31u) != EMURX_ST_OK) return 0;
+    if (lk_ip6key(key)) return 1;
+    return (w4 >> 31) ? (((w4 >> 26) & 1u) ? 3u : 1u) : 0u;
+}
+// the record of a frame; `ok`: it reached a callback (the key words are zero otherwise);
+// tup_on: tcp / udp records carry their tuple.  Writes the head (two 16-byte stores) and the
+// tail (up to three; LDS: the wave's slab, once the parse is done with it); returns the tail's
+// units.
 template <class S>
-__device__ __forceinline__ void pack_lookup(const S& s, uint32_t len, const Rec& r, uint32_t frame, bool ok,
-                                            uint4* dst) {
-    uint32_t w[16];
+__device__ __forceinline__ uint32_t pack_lookup(const S& s, uint32_t len, const Rec& r, uint32_t frame, bool ok,
+                                                bool tup_on, uint4* head, uint4* tail) {
     LKey k{};
     Tuple t{};
     bool tr = false;
     if (ok) {
         k = make_key(s, len, r);
-        tr = lk_transport(r.proto) && k.key == kMac;
+        tr = tup_on && lk_transport(r.proto) && k.key == kMac;
         if (tr) t = get_tuple(s, len, r);
     }
-    w[0] = frame;
-    w[1] = vlan_code(r.vlan0) | (vlan_code(r.vlan1) << 14);
-    w[2] = r.vport | (r.l3 << 8) | (r.nh << 24);
-    w[3] = r.l4 | (r.l7 << 16);
-    w[4] = r.l7len | (min(r.proto, 15u) << 16) | (r.status << 20) | ((r.flags & EMURX_FLAG_RTALERT) << 25) |
-           (t.v6 << 26) | (k.mc6 << 27) | (k.key << 28);
-    w[5] = k.dlo;
-    w[6] = k.dhi | (t.flags << 16);
-    w[7] = t.ports;
-    if (!tr) {
-        w[8] = k.kw[0]; w[9] = k.kw[1]; w[10] = k.kw[2]; w[11] = k.kw[3];
-        w[12] = w[13] = w[14] = w[15] = 0;
-    } else if (!t.v6) {
-        w[8] = t.a[0]; w[9] = t.d[0];
-        w[10] = w[11] = w[12] = w[13] = w[14] = w[15] = 0;
-    } else {
-        w[8] = t.a[0]; w[9] = t.a[1]; w[10] = t.a[2]; w[11] = t.a[3];
-        w[12] = t.d[0]; w[13] = t.d[1]; w[14] = t.d[2]; w[15] = t.d[3];
+    const bool i6 = ok && lk_ip6key(k.key);
+    uint32_t l7 = r.l7, l7len = r.l7len, x = k.kw[0], hi = k.kw[1];
+    if (i6) {  // the client-table hash of the key (probe_issue's, with the owner's mask applied there)
+        const uint32_t tk = emurx_tk_hash(r.vport, r.vlan0, r.vlan1);
+        uint32_t h;
+        if (k.key == kEui) {
+            const uint2 m = eui_mac(k.kw[2], k.kw[3]);
+            h = emurx_mac_hash(tk, m.x, m.y);
+        } else {
+            h = emurx_ip6_hash(tk, k.kw[0], k.kw[1], k.kw[2], k.kw[3]);
+        }
+        l7 = h & 0xffffu;
+        l7len = h >> 16;
+        tail[0] = make_uint4(k.kw[0], k.kw[1], k.kw[2], k.kw[3]);
+        hi = 0;
+    } else if (tr) {
+        hi = t.flags;
+        if (!t.v6) {
+            tail[0] = make_uint4(t.ports, t.a[0], t.d[0], 0);
+        } else {
+            tail[0] = make_uint4(t.ports, t.a[0], t.a[1], t.a[2]);
+            tail[1] = make_uint4(t.a[3], t.d[0], t.d[1], t.d[2]);
+            tail[2] = make_uint4(t.d[3], 0, 0, 0);
+        }
+    } else if (k.key != kMac) {
+        hi = 0;
+        if (k.key != kIp4) x = 0;
     }
-    dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
-    dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
-    dst[2] = make_uint4(w[8], w[9], w[10], w[11]);
-    dst[3] = make_uint4(w[12], w[13], w[14], w[15]);
+    const uint32_t w4 = l7len | (min(r.proto, 15u) << 16) | (r.status << 20) | ((r.flags & EMURX_FLAG_RTALERT) << 25) |
+                        (t.v6 << 26) | (k.mc6 << 27) | (k.key << 28) | ((uint32_t)tr << 31);
+    head[0] = make_uint4(frame, vlan_code(r.vlan0) | (vlan_code(r.vlan1) << 14), r.vport | (r.l3 << 8) | (r.nh << 24),
+                         r.l4 | (l7 << 16));
+    head[1] = make_uint4(w4, k.dlo, k.dhi | (hi << 16), x);
+    return i6 ? 1u : tr ? (t.v6 ? 3u : 1u) : 0u;
 }
-// the owner's view: the parsed record (ns / client unset), the lookup key and the flow tuple
-__device__ __forceinline__ LKey unpack_lookup(const uint32_t w[16], Rec& r, Tuple& t) {
+// the owner's view of a head: the parsed record (ns / client unset) and the lookup key (for
+// kIp6 / kEui: its client-table hash in kw[0], the address comes with the tail)
+__device__ __forceinline__ LKey unpack_lookup(const uint32_t w[8], Rec& r, uint32_t& chash) {
     r.ns = EMURX_ID_NONE;
     r.cl = EMURX_ID_NONE;
     r.vlan0 = vlan_word(w[1] & 0x3fffu);
@@ -1524,23 +1558,36 @@ __device__ __forceinline__ LKey unpack_lookup(const uint32_t w[16], Rec& r, Tupl
     k.dhi = w[6] & 0xffffu;
     k.key = (w[4] >> 28) & 7u;
     k.mc6 = (w[4] >> 27) & 1u;
-    t = Tuple{};
-    if (!(lk_transport(r.proto) && k.key == kMac)) {
-        k.kw[0] = w[8]; k.kw[1] = w[9]; k.kw[2] = w[10]; k.kw[3] = w[11];
+    chash = 0;
+    k.kw[2] = k.kw[3] = 0;
+    if (lk_ip6key(k.key)) {
+        chash = r.l7 | (r.l7len << 16);
+        r.l7 = r.l7len = 0;  // ICMPv6 leaves both unset
+        k.kw[0] = k.kw[1] = 0;
+    } else if (w[4] >> 31) {  // tuple record: the key is the destination MAC
+        k.kw[0] = k.dlo;
+        k.kw[1] = k.dhi;
     } else {
-        k.kw[0] = k.dlo; k.kw[1] = k.dhi; k.kw[2] = 0; k.kw[3] = 0;
-        t.v6 = (w[4] >> 26) & 1u;
-        t.ports = w[7];
-        t.flags = (w[6] >> 16) & 0xffu;
-        t.proto = r.nh;  // IPv4: the header's protocol field; IPv6: ParserPacketState.NextHeader
-        if (!t.v6) {
-            t.a[0] = w[8]; t.d[0] = w[9];
-        } else {
-            t.a[0] = w[8]; t.a[1] = w[9]; t.a[2] = w[10]; t.a[3] = w[11];
-            t.d[0] = w[12]; t.d[1] = w[13]; t.d[2] = w[14]; t.d[3] = w[15];
-        }
+        k.kw[0] = w[7];
+        k.kw[1] = w[6] >> 16;
     }
     return k;
+}
+// the c5tuplekey of a tuple head from its tail units
+__device__ __forceinline__ Tuple tail_tuple(const uint32_t w[8], uint4 t0, uint4 t1, uint4 t2) {
+    Tuple t{};
+    t.v6 = (w[4] >> 26) & 1u;
+    t.flags = (w[6] >> 16) & 0xffu;
+    t.proto = w[2] >> 24;  // IPv4: the header's protocol field; IPv6: ParserPacketState.NextHeader
+    t.ports = t0.x;
+    if (!t.v6) {
+        t.a[0] = t0.y;
+        t.d[0] = t0.z;
+    } else {
+        t.a[0] = t0.y; t.a[1] = t0.z; t.a[2] = t0.w; t.a[3] = t1.x;
+        t.d[0] = t1.y; t.d[1] = t1.z; t.d[2] = t1.w; t.d[3] = t2.x;
+    }
+    return t;
 }
 
 }  // namespace emurx

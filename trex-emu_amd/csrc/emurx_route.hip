@@ -93,13 +93,18 @@ __global__ __launch_bounds__(kBlock) void k_route(const emurx_rec* __restrict__ 
     }
 }
 
-// exclusive prefix over groups of grp[g][d], d < n_parts; one lane per group; leaves grp zero
+// exclusive prefix over groups of grp[g][d], d < n_parts; one lane per group; leaves grp zero.
+// send_count[cstride * d] = the total of d (cstride 2: the partitioned source's {heads, tail
+// overflow} pairs, the second word zeroed, and its tail cursors tcur cleared for k_rx kind 2)
 __global__ __launch_bounds__(kScanThreads) void k_route_scan(uint32_t* __restrict__ grp, uint32_t ngroups,
                                                               uint32_t n_parts, uint32_t* __restrict__ grp_off,
-                                                              uint32_t* __restrict__ send_count) {
+                                                              uint32_t* __restrict__ send_count, uint32_t* __restrict__ tcur,
+                                                              uint32_t cstride) {
+    static_assert(EMURX_MAX_PARTS * EMURX_TAIL_SHARDS <= kScanThreads, "one cursor per lane");
     __shared__ uint32_t s_wsum[EMURX_MAX_PARTS][kScanThreads / kWave];
     __shared__ uint32_t s_ex[EMURX_MAX_PARTS][kScanThreads];
     const uint32_t t = threadIdx.x, lane = lane_id(), wv = t / kWave;
+    if (tcur && t < n_parts * EMURX_TAIL_SHARDS) tcur[t * EMURX_TAIL_CURSOR_STRIDE] = 0;
     uint4 x = make_uint4(0, 0, 0, 0), y = x;
     if (t < ngroups) {
         uint4* p = reinterpret_cast<uint4*>(grp + t * 16);
@@ -129,7 +134,8 @@ __global__ __launch_bounds__(kScanThreads) void k_route_scan(uint32_t* __restric
             total += sw;
         }
         if (t < ngroups) grp_off[t * 16 + k] = before + s_ex[k][t];
-        if (t == 0) send_count[k] = total;
+        if (t == 0) send_count[cstride * k] = total;
+        if (t == 0 && cstride == 2) send_count[2 * k + 1] = 0;
     }
 }
 
@@ -260,28 +266,71 @@ __global__ __launch_bounds__(kBlock) void k_desc_keys(const uint8_t* __restrict_
 }
 
 // k_lookup: the owner's half — GetNs + the callback's client rule + the flow decision for
-// every received lookup record, against this partition's tables (classify()'s resolve).
+// every received lookup head, against this partition's tables (classify()'s resolve).
 // Output slot j = the input slot: n_parts regions of cap emurx_route_rec, valid up to
-// recv_count[source].  Grid: (records of a region / kBlock, source region): no division.
+// recv_count[2 source].  Grid: (heads of a region / kBlock, source region): no division.
+// A head with a tail (emurx_parse.h) loads it before the table probes: its units arrive in the
+// probes' memory round trip.  An ICMPv6 key's client bucket comes from the hash in its head,
+// so that probe need not wait for the tail either; a tuple is needed only by the flow probe.
 #ifndef EMURX_LOOKUP_WPE
 #define EMURX_LOOKUP_WPE 6
 #endif
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EMURX_LOOKUP_WPE))) void k_lookup(const emurx_lookup_rec* __restrict__ recv,
+template <class Flow>
+__device__ __forceinline__ void resolve_owner(const emurx_dev_tables& T, Rec& r, LKey k, uint32_t chash, uint4 kw6,
+                                              Flow flow) {
+    Probe p;
+    const uint32_t tk = emurx_tk_hash(r.vport, r.vlan0, r.vlan1);  // CTunnelKey words
+    p.nb = tk & T.ns_mask;
+    p.ne = ld_bucket(T.ns_tab, p.nb);
+    p.mlo = k.kw[0];
+    p.mhi = k.kw[1];
+    p.cbk = 0;
+    p.ctab = nullptr;
+    // the table bases as SGPR values selected per lane (probe_issue)
+    uintptr_t tm = (uintptr_t)T.mac_tab, t4 = (uintptr_t)T.ip4_tab, t6 = (uintptr_t)T.ip6_tab;
+    asm volatile("" : "+s"(tm), "+s"(t4), "+s"(t6));
+    if (k.key == kMac) {
+        p.cbk = emurx_mac_hash(tk, p.mlo, p.mhi) & T.mac_mask;
+        p.ctab = reinterpret_cast<const uint32_t*>(tm);
+    } else if (k.key == kEui) {
+        p.cbk = chash & T.mac_mask;
+        p.ctab = reinterpret_cast<const uint32_t*>(tm);
+    } else if (k.key == kIp4) {
+        p.cbk = emurx_ip4_hash(tk, k.kw[0]) & T.ip4_mask;
+        p.ctab = reinterpret_cast<const uint32_t*>(t4);
+    } else if (k.key == kIp6) {
+        p.cbk = chash & T.ip6_mask;
+        p.ctab = reinterpret_cast<const uint32_t*>(t6);
+    }
+    Bucket ce{};
+    if (p.ctab) ce = ld_bucket(p.ctab, p.cbk);
+    if (lk_ip6key(k.key)) {  // the address from the tail
+        k.kw[0] = kw6.x; k.kw[1] = kw6.y; k.kw[2] = kw6.z; k.kw[3] = kw6.w;
+        if (k.key == kEui) {
+            const uint2 m = eui_mac(kw6.z, kw6.w);
+            p.mlo = m.x;
+            p.mhi = m.y;
+        }
+    }
+    resolve_done(T, r, k, p, ce, flow);
+}
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EMURX_LOOKUP_WPE))) void k_lookup(const uint8_t* __restrict__ recv,
                                                    const uint32_t* __restrict__ recv_count, uint32_t n_parts,
-                                                   uint32_t cap, emurx_dev_tables T,
+                                                   uint32_t cap, uint32_t tcap, emurx_dev_tables T,
                                                    emurx_route_rec* __restrict__ out, uint32_t* __restrict__ flow) {
-    // the wave's 64 records are contiguous: 4 KiB copied into LDS by four fully coalesced
-    // LDS-DMA loads (a lane-strided 64-byte read would touch 32 lines per instruction)
-    __shared__ __attribute__((aligned(16))) uint4 s_rec[kWaves][kWave * 4];
+    // the wave's 64 heads are contiguous: 2 KiB copied into LDS by two fully coalesced LDS-DMA
+    // loads; the rows then hold the wave's 40-byte outputs (2.5 KiB)
+    __shared__ __attribute__((aligned(16))) uint4 s_rec[kWaves][kWave * 40 / 16];
     const uint32_t lane = threadIdx.x % kWave, wv = threadIdx.x / kWave;
     const uint32_t src = blockIdx.y, idx0 = blockIdx.x * kBlock + wv * kWave, idx = idx0 + lane;
-    const uint32_t cnt = min(recv_count[src], cap);
+    const uint32_t cnt = min(recv_count[2 * src], cap);
     if (idx0 >= cnt) return;  // wave-uniform
     const uint64_t j = (uint64_t)src * cap + idx;
-    const uint4* base = reinterpret_cast<const uint4*>(recv + (uint64_t)src * cap + idx0);
-    const uint32_t nvec = min(kWave, cnt - idx0) * 4;  // never past the region's valid records
+    const uint8_t* region = recv + (uint64_t)src * (cap + 32ull * tcap) * 32;
+    const uint4* base = reinterpret_cast<const uint4*>(region) + (uint64_t)idx0 * 2;
+    const uint32_t nvec = min(kWave, cnt - idx0) * 2;  // never past the region's valid heads
 #pragma unroll
-    for (uint32_t k = 0; k < 4; ++k)
+    for (uint32_t k = 0; k < 2; ++k)
         if (k * kWave + lane < nvec)
             __builtin_amdgcn_global_load_lds(base + k * kWave + lane,
                                              (__attribute__((address_space(3))) void*)&s_rec[wv][k * kWave], 16, 0, 0);
@@ -290,15 +339,26 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EMURX_LO
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const bool live = idx < cnt;
-    const uint4* p = &s_rec[wv][lane * 4];
-    const uint4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
-    const uint32_t w[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
-                            q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+    const uint4 q0 = s_rec[wv][lane * 2], q1 = s_rec[wv][lane * 2 + 1];
+    const uint32_t w[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
     Rec r;
-    Tuple t;
-    const LKey k = unpack_lookup(w, r, t);
+    uint32_t chash;
+    const LKey k = unpack_lookup(w, r, chash);
+    // the tail: issued ahead of the table probes (an index past the shards, EMURX_TAIL_NONE
+    // included, is not read: the source reported that overflow and must route the batch again)
+    const uint32_t tun = live ? lk_tail_units(w[4]) : 0u;
+    uint4 t0 = make_uint4(0, 0, 0, 0), t1 = t0, t2 = t0;
+    if (tun && w[7] < EMURX_TAIL_SHARDS * tcap && w[7] + tun <= EMURX_TAIL_SHARDS * tcap) {
+        const uint4* tl = reinterpret_cast<const uint4*>(region + (uint64_t)cap * 32) + w[7];
+        t0 = tl[0];
+        if (tun == 3) {
+            t1 = tl[1];
+            t2 = tl[2];
+        }
+    }
     // frames that reached no callback travel too (their owner keeps their record): no lookup
-    if (live && r.status == EMURX_ST_OK) resolve(T, r, k, [&](uint32_t cid) { return flow_probe(T, t, cid); });
+    if (live && r.status == EMURX_ST_OK)
+        resolve_owner(T, r, k, chash, t0, [&](uint32_t cid) { return flow_probe(T, tail_tuple(w, t0, t1, t2), cid); });
     // The wave's outputs are contiguous: its 40-B records are parked in its (now read) LDS rows
     // and written back as five 8-B pieces per lane, 512 contiguous bytes per store instruction,
     // instead of five 8-B stores per lane 40 B apart
@@ -325,16 +385,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EMURX_LO
 
 int emurx_launch_owner_count(const uint8_t* frames, const emurx_desc* desc, uint32_t n, uint32_t n_parts,
                              uint32_t* send_count, uint32_t* tile_cnt, uint32_t* grp, uint32_t* grp_off,
-                             hipStream_t st) {
+                             uint32_t* tcur, hipStream_t st) {
     using namespace emurx;
     const uint32_t ntiles = (n + kBlock - 1) / kBlock, ngroups = (ntiles + kGroup - 1) / kGroup;
-    if (n == 0) return EMURX_HIP_OK(hipMemsetAsync(send_count, 0, n_parts * sizeof(uint32_t), st)) ? 0 : -1;
+    if (n == 0) return EMURX_HIP_OK(hipMemsetAsync(send_count, 0, 2 * n_parts * sizeof(uint32_t), st)) ? 0 : -1;
     if (ngroups > kScanThreads) return -1;
     if (!EMURX_HIP_OK(emurx_launch(k_owner_count, dim3(ntiles), dim3(kBlock), 0, st, frames, desc, n, n_parts,
                                    tile_cnt, grp)))
         return -1;
     return EMURX_HIP_OK(emurx_launch(k_route_scan, dim3(1), dim3(kScanThreads), 0, st, grp, ngroups, n_parts, grp_off,
-                                     send_count))
+                                     send_count, tcur, 2u))
                ? 0
                : -1;
 }
@@ -348,20 +408,21 @@ int emurx_launch_desc_keys(const uint8_t* frames, emurx_desc* desc, uint32_t n, 
 }
 
 int emurx_launch_lookup(const emurx_lookup_rec* recv, const uint32_t* recv_count, uint32_t n_parts, uint32_t cap,
-                        const emurx_dev_tables& T, emurx_route_rec* out, uint32_t* flow, hipStream_t st) {
+                        uint32_t tcap, const emurx_dev_tables& T, emurx_route_rec* out, uint32_t* flow,
+                        hipStream_t st) {
     using namespace emurx;
     if (!n_parts || !cap) return 0;
     if (n_parts > 65535) return -1;
-// k_lookup's occupancy is capped at 4 workgroups (16 waves) per CU by unused LDS: its 16 KiB of
-// record rows + 24 KiB = 40 KiB of the CU's 160 KiB.  Its probes are random table lines; more
+// k_lookup's occupancy is capped at 4 workgroups (16 waves) per CU by unused LDS: its 10 KiB of
+// record rows + 30 KiB = 40 KiB of the CU's 160 KiB.  Its probes are random table lines; more
 // waves in flight only queue more of them, and beside the next batch's k_rx<2> on the other
 // stream the freed slots serve that kernel (6 workgroups 98.4 us per 2M records,
 // 4: 96.9 us, the pipelined partitioned step +3-4.5 %; at an owner of 8, 74.3 -> 72.3 us)
 #ifndef EMURX_LOOKUP_LDS_PAD
-#define EMURX_LOOKUP_LDS_PAD (24 * 1024)
+#define EMURX_LOOKUP_LDS_PAD (30 * 1024)
 #endif
-    return EMURX_HIP_OK(emurx_launch(k_lookup, dim3((cap + kBlock - 1) / kBlock, n_parts), dim3(kBlock), EMURX_LOOKUP_LDS_PAD, st, recv,
-                                     recv_count, n_parts, cap, T, out, flow))
+    return EMURX_HIP_OK(emurx_launch(k_lookup, dim3((cap + kBlock - 1) / kBlock, n_parts), dim3(kBlock), EMURX_LOOKUP_LDS_PAD, st,
+                                     reinterpret_cast<const uint8_t*>(recv), recv_count, n_parts, cap, tcap, T, out, flow))
                ? 0
                : -1;
 }
@@ -378,7 +439,7 @@ int emurx_launch_route(const emurx_rec* rec, uint32_t n, uint32_t n_parts, uint3
                                    tile_cnt, grp, (const uint32_t*)nullptr, send, cap)))
         return -1;
     if (!EMURX_HIP_OK(emurx_launch(k_route_scan, dim3(1), dim3(kScanThreads), 0, st, grp, ngroups, n_parts, grp_off,
-                                   send_count)))
+                                   send_count, (uint32_t*)nullptr, 1u)))
         return -1;
     return EMURX_HIP_OK(emurx_launch(k_route<true>, dim3(ntiles), dim3(kBlock), 0, st, rec, n, n_parts, my_rank,
                                      tile_cnt, grp, grp_off, send, cap))

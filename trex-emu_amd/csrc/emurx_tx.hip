@@ -157,13 +157,17 @@ __global__ __launch_bounds__(kBlock) void k_tx_csum(uint8_t* __restrict__ frames
     const uint32_t ops = d.w & 0xff, nhx = (d.w >> 8) & 0xff;
     const uint32_t lo = wave_min_u32(live ? d.x : 0xffffffffu);
     const uint32_t hi = wave_max_u32(live ? d.x + len : 0u);
-    const uint32_t start = lo & ~15u, nvec = hi > lo ? (hi - start + 15) >> 4 : 0;
+    // the staged rows start at the 16-byte boundary of the ABSOLUTE address (d_frames need not
+    // be 16-aligned): a frame byte's slab index is then its address mod 16 plus a multiple of 16
+    const uintptr_t fbase = (uintptr_t)frames;
+    const uint32_t skew = (uint32_t)((fbase + lo) & 15u);  // lo's offset in its aligned vector
+    const uint32_t start = lo - skew, nvec = hi > lo ? (hi - start + 15) >> 4 : 0;
     const bool staged = nvec > 0 && nvec <= kTxSlab / 16;  // wave-uniform
     uint32_t hcs = 0, lcs = 0, fo = 0;
     bool ok;
     if (staged) {
         static_assert(kTxSlab % (16 * kWave) == 0, "whole 1 KiB DMA rows");
-        const uint4* src = reinterpret_cast<const uint4*>(frames + start);
+        const uint4* src = reinterpret_cast<const uint4*>(frames + start);  // 16-byte aligned
         uint4* dst = reinterpret_cast<uint4*>(s_slab[wv]);
 #pragma unroll
         for (uint32_t k = 0; k < kTxSlab / 16 / kWave; ++k)

@@ -71,12 +71,28 @@ REC_DTYPE = np.dtype([
 assert REC_DTYPE.itemsize == 32
 ROUTE_REC_DTYPE = np.dtype([("rec", REC_DTYPE), ("src_index", "<u4"), ("src_rank", "<u4")])
 assert ROUTE_REC_DTYPE.itemsize == 40
-# emurx_lookup_rec (owner-partitioned classification, 64 B): the source frame index, the packed
-# parse (VLAN codes, vport / l3 / next header, l4 / l7, l7_len / proto / status / key kind) and
-# the callback rule's key (destination MAC, ports, addresses or kw[0..3]); csrc/emurx_parse.h
+# emurx_lookup_rec (owner-partitioned classification): the 32-byte head of a frame's lookup
+# record: the source frame index, the packed parse (VLAN codes, vport / l3 / next header, l4 /
+# l7, l7_len / proto / status / key kind / tuple bit), the destination MAC, and x (MAC / IPv4
+# key, or the index of the record's first 16-byte tail unit); csrc/emurx_parse.h
 LOOKUP_REC_DTYPE = np.dtype([("frame", "<u4"), ("vlans", "<u4"), ("w2", "<u4"), ("w3", "<u4"), ("w4", "<u4"),
-                             ("dlo", "<u4"), ("dhi", "<u4"), ("ports", "<u4"), ("key", "<u4", 8)])
-assert LOOKUP_REC_DTYPE.itemsize == 64
+                             ("dlo", "<u4"), ("dhi", "<u4"), ("x", "<u4")])
+assert LOOKUP_REC_DTYPE.itemsize == 32
+WALK_NO_KEYS = 1          # EMURX_WALK_NO_KEYS
+TAIL_SHARDS = 64          # EMURX_TAIL_SHARDS: tail cursors (and shards) per region
+TAIL_NONE = 0xFFFFFFFF    # EMURX_TAIL_NONE: a head whose tail did not fit its shard
+
+
+def lookup_region_bytes(cap: int, tail_cap: int) -> int:
+    """EMURX_LOOKUP_REGION_BYTES: one owner's region of 32-byte heads and tail shards."""
+    return cap * 32 + TAIL_SHARDS * tail_cap * 16
+
+
+def tail_capacity(cap: int, frac: float = 1 / 16) -> int:
+    """16-byte tail units per shard for regions of `cap` heads: room for `frac` of them to
+    carry a one-unit tail (config D: the 5 % ICMPv6 echo frames), plus slack for the spread of
+    the shards.  A shard that overflows reports the units it needed (emurx_parse_route_dev)."""
+    return int(cap * frac / TAIL_SHARDS) + 32
 ST_HOLE = 0xFF     # EMURX_ST_HOLE: status of the record of an empty descriptor slot
 MAX_PARTS = 8
 DESC_DTYPE = np.dtype([("off", "<u4"), ("len", "<u2"), ("vport", "u1"), ("pad", "u1")])
@@ -144,6 +160,7 @@ _P = C.c_void_p
 _U8P = C.c_void_p
 SIGNATURES = [
     ("emurx_abi_version", C.c_int, []),
+    ("emurx_build_id", C.c_char_p, []),
     ("emurx_open", C.c_int, [C.POINTER(Cfg), C.POINTER(C.c_void_p)]),
     ("emurx_close", None, [_P]),
     ("emurx_strerror", C.c_char_p, [C.c_int]),
@@ -181,8 +198,9 @@ SIGNATURES = [
     ("emurx_classify_route_dev", C.c_int, [_P, _P, _P, C.c_uint32, C.POINTER(DevOut), C.c_uint32, C.c_uint32,
                                            C.c_uint32, _P, _P, _P]),
     ("emurx_parse_route_dev", C.c_int, [_P, _P, _P, C.c_uint32, C.POINTER(DevOut), C.c_uint32, C.c_uint32,
-                                        C.c_uint32, _P, _P, _P]),
-    ("emurx_lookup_dev", C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint32, _P, _P, _P]),
+                                        C.c_uint32, C.c_uint32, _P, _P, _P]),
+    ("emurx_lookup_dev", C.c_int, [_P, _P, _P, C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P]),
+    ("emurx_zmq_walk_dev", C.c_int, [_P, _P, _P, C.c_uint32, _P, _P, C.c_uint32, _P]),
     ("emurx_set_partition", C.c_int, [_P, C.c_uint32, C.c_uint32]),
     ("emurx_table_gen", C.c_uint64, [_P]),
     ("emurx_recs_stale", C.c_int, [_P, _P, C.c_uint32, C.c_uint64, _P]),
@@ -221,7 +239,29 @@ def load(path: str | os.PathLike | None = None):
         fn.argtypes = args
     if path is None:
         _lib = lib
+        # provenance: which source tree the loaded library was built from (GPU test logs)
+        built, tree = lib.emurx_build_id().decode(), source_id()
+        import sys
+        print(f"emurx: {p} built from source tree {built}" +
+              ("" if tree in (built, None) else f" -- STALE: this tree is {tree}"), file=sys.stderr)
     return lib
+
+
+def source_id() -> str | None:
+    """The id of the source tree (trex-emu_amd/Makefile SRC_ID: sha1 of the concatenated
+    sources, headers and Makefile, first 16 hex digits); None when a file is missing."""
+    import hashlib
+    src = ["emurx_kernels.hip", "emurx_route.hip", "emurx_ingest.hip", "emurx_tx.hip", "emurx_txzmq.hip",
+           "emurx_api.cpp", "emurx_mirror.cpp"]
+    hdr = ["emurx_kernels.h", "emurx_tables.h", "emurx_parse.h", "emurx_mirror.h"]
+    files = [PKG_ROOT / "csrc" / f for f in src + hdr] + [REPO_ROOT / "include" / "emu_rx.h", PKG_ROOT / "Makefile"]
+    h = hashlib.sha1()
+    try:
+        for f in files:
+            h.update(f.read_bytes())
+    except OSError:
+        return None
+    return h.hexdigest()[:16]
 
 
 def check(rc: int, what: str = ""):

@@ -1,10 +1,15 @@
 """Namespace-partitioned exchange between GPUs.
 
-Frames shard by input offset across the ranks of a node.  Each rank classifies its shard
-(emurx_classify_dev), packs the records whose Namespace was found into the send regions of
-the Namespaces' owners (emurx_route_dev), and one equal-split all-to-all delivers them:
-rank r receives, from every source s, `recv_count[s]` valid records at
-`recv[s * cap : s * cap + recv_count[s]]` (frame order of the source).
+Frames shard by input offset across the ranks of a node.  Each rank fills one send region per
+Namespace owner and one equal-split all-to-all delivers them: rank r receives, from every
+source s, region s of its receive buffer and the counts of that region.  Two region kinds:
+
+- replicated tables: emurx_classify_route_dev packs the classified records whose Namespace
+  was found, `cap` emurx_route_rec (40 B) per region, one count per region;
+- partitioned tables: emurx_parse_route_dev packs every frame's lookup record as a 32-byte
+  head plus, for ICMPv6 keys and transport tuples, 16-byte tail units
+  (abi.lookup_region_bytes(cap, tail_cap) per region), two counts per region (heads, tail
+  overflow).
 
 The collectives are plain torch.distributed calls: RCCL over xGMI with the "nccl" backend
 (device tensors, no host synchronisation, the counts travel in their own all-to-all), or
@@ -17,6 +22,7 @@ import numpy as np
 from . import abi
 
 REC_BYTES = abi.ROUTE_REC_DTYPE.itemsize
+LOOKUP_BYTES = abi.LOOKUP_REC_DTYPE.itemsize
 
 
 def capacity(n_frames: int, n_parts: int, slack: float = 1.25) -> int:
@@ -37,19 +43,32 @@ def grow(cap: int, counts) -> int:
     return max(cap, m + m // 16 + 1024)
 
 
-LOOKUP_BYTES = abi.LOOKUP_REC_DTYPE.itemsize
+def grow_tail(tail_cap: int, need) -> int:
+    """Tail units per shard after a shard overflowed: the largest need seen plus 1/4 more."""
+    m = int(max(int(c) for c in need))
+    return max(tail_cap, m + m // 4 + 32)
 
 
-def exchange(send, send_count, cap: int, group=None, rec_bytes: int = REC_BYTES):
-    """Equal-split all-to-all of `send` ([world * cap * rec_bytes] uint8 tensor: emurx_route_rec
-    regions, or emurx_lookup_rec regions with rec_bytes = LOOKUP_BYTES) and `send_count`
-    ([world] int32 tensor).  Returns (recv, recv_count) on the device of the inputs."""
+def region_bytes(cap: int, tail_cap: int | None = None) -> int:
+    """Bytes of one region: lookup regions when tail_cap is given, else route records."""
+    return cap * REC_BYTES if tail_cap is None else abi.lookup_region_bytes(cap, tail_cap)
+
+
+def _check(send, send_count, rbytes, world):
+    assert send.numel() == world * rbytes, (send.numel(), world, rbytes)
+    assert send_count.numel() % world == 0
+
+
+def exchange(send, send_count, rbytes: int, group=None):
+    """Equal-split all-to-all of `send` ([world * rbytes] uint8 tensor: one region per rank)
+    and `send_count` ([world * k] int32 tensor: k counts per region).  Returns (recv,
+    recv_count) on the device of the inputs."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    assert send.numel() == world * cap * rec_bytes and send_count.numel() == world
+    _check(send, send_count, rbytes, world)
     if dist.get_backend(group) == "gloo" and send.is_cuda:
-        r, c = exchange(send.cpu(), send_count.cpu(), cap, group, rec_bytes)
+        r, c = exchange(send.cpu(), send_count.cpu(), rbytes, group)
         return r.to(send.device), c.to(send.device)
     recv = torch.empty_like(send)
     recv_count = torch.empty_like(send_count)
@@ -58,7 +77,7 @@ def exchange(send, send_count, cap: int, group=None, rec_bytes: int = REC_BYTES)
     return recv, recv_count
 
 
-def exchange_start(send, send_count, cap: int, group=None, rec_bytes: int = REC_BYTES):
+def exchange_start(send, send_count, rbytes: int, group=None):
     """exchange() without waiting: the all-to-alls are enqueued on the collective's stream
     behind the work already on the caller's stream, and the caller's stream goes on (the next
     batch's parse overlaps this batch's transfer).  exchange_finish() makes the caller's
@@ -67,9 +86,9 @@ def exchange_start(send, send_count, cap: int, group=None, rec_bytes: int = REC_
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    assert send.numel() == world * cap * rec_bytes and send_count.numel() == world
+    _check(send, send_count, rbytes, world)
     if dist.get_backend(group) == "gloo" and send.is_cuda:
-        return (None,) + exchange(send, send_count, cap, group, rec_bytes)
+        return (None,) + exchange(send, send_count, rbytes, group)
     recv = torch.empty_like(send)
     recv_count = torch.empty_like(send_count)
     works = (dist.all_to_all_single(recv_count, send_count, group=group, async_op=True),
@@ -86,10 +105,48 @@ def exchange_finish(pending):
 
 
 def received(recv: np.ndarray, recv_count: np.ndarray, cap: int) -> np.ndarray:
-    """Valid records of a receive buffer (host copy), source-rank order."""
+    """Valid records of a route receive buffer (host copy), source-rank order."""
     r = np.ascontiguousarray(recv).view(np.uint8).reshape(-1)[: len(recv_count) * cap * REC_BYTES]
     r = r.view(abi.ROUTE_REC_DTYPE).reshape(len(recv_count), cap)
     cnt = np.asarray(recv_count).astype(np.int64)
     if (cnt > cap).any():
         raise RuntimeError(f"exchange region overflow: counts {cnt.tolist()} > cap {cap}")
     return np.concatenate([r[s, : cnt[s]] for s in range(len(cnt))]) if len(cnt) else r[:0, 0]
+
+
+# the canonical form of a lookup record: the head with x replaced by 0 when it names a tail,
+# then the tail's units (zero-padded to 3); what a head's tail holds is deterministic, where
+# the units sit in the shards is not (emu_rx.h)
+LOOKUP_CANON_DTYPE = np.dtype([("head", abi.LOOKUP_REC_DTYPE), ("tail", "<u4", 12)])
+
+
+def tail_units(w4: np.ndarray) -> np.ndarray:
+    """Tail units of heads from their w4 word (emurx_parse.h lk_tail_units)."""
+    w4 = np.asarray(w4, np.uint32)
+    key = (w4 >> 28) & 7
+    ok = ((w4 >> 20) & 31) == abi.ST["OK"]
+    ip6k = (key == 4) | (key == 6)  # kEui, kIp6
+    tup = (w4 >> 31) == 1
+    units = np.where(ip6k, 1, np.where(tup, np.where((w4 >> 26) & 1, 3, 1), 0))
+    return np.where(ok, units, 0).astype(np.int64)
+
+
+def lookup_records(region: np.ndarray, count: int, cap: int, tail_cap: int) -> np.ndarray:
+    """The `count` valid lookup records of one region (host bytes) in canonical form
+    (LOOKUP_CANON_DTYPE): each head with its tail's units attached."""
+    b = np.ascontiguousarray(region).view(np.uint8).reshape(-1)
+    assert b.size == abi.lookup_region_bytes(cap, tail_cap), (b.size, cap, tail_cap)
+    if count > cap:
+        raise RuntimeError(f"lookup region overflow: {count} heads > cap {cap}")
+    heads = b[: cap * 32].view(abi.LOOKUP_REC_DTYPE)[:count].copy()
+    tails = b[cap * 32:].view("<u4").reshape(-1, 4)
+    out = np.zeros(count, LOOKUP_CANON_DTYPE)
+    u = tail_units(heads["w4"])
+    for i in np.nonzero(u)[0]:
+        x = int(heads["x"][i])
+        if x == abi.TAIL_NONE or x + u[i] > len(tails):
+            raise RuntimeError(f"lookup record {i}: tail index {x:#x} outside the shards")
+        out["tail"][i, : 4 * u[i]] = tails[x: x + u[i]].reshape(-1)
+        heads["x"][i] = 0
+    out["head"] = heads
+    return out

@@ -271,12 +271,15 @@ class RxPath:
         return abi.check(self.lib.emurx_set_partition(self.h, n_parts, part), "set_partition")
 
     def parse_route_dev(self, frames, desc, n: int, rec, qlist, qcap: int, tile_cnt, hist, n_parts: int,
-                        my_rank: int, cap: int, send, send_count, stream=None):
-        """Parse + lookup keys, packed into the owners' regions as LOOKUP_REC_DTYPE (64 B)."""
+                        my_rank: int, cap: int, send, send_count, stream=None, tail_cap=None):
+        """Parse + lookup keys, packed into the owners' regions (abi.lookup_region_bytes(cap,
+        tail_cap) bytes each: LOOKUP_REC_DTYPE heads + tail shards); send_count [2 * n_parts]
+        {heads, tail overflow}.  tail_cap defaults to abi.tail_capacity(cap)."""
+        tail_cap = abi.tail_capacity(cap) if tail_cap is None else tail_cap
         out = abi.DevOut(_addr(rec), _addr(qlist), qcap, _addr(tile_cnt), _addr(hist), None)
         return abi.check(self.lib.emurx_parse_route_dev(self.h, _addr(frames), _addr(desc), n, C.byref(out),
-                                                        n_parts, my_rank, cap, _addr(send), _addr(send_count),
-                                                        _stream(stream)), "parse_route_dev")
+                                                        n_parts, my_rank, cap, tail_cap, _addr(send),
+                                                        _addr(send_count), _stream(stream)), "parse_route_dev")
 
     def desc_keys_dev(self, frames, desc, n: int, stream=None):
         """Write every frame's owner key into its descriptor's pad byte, in place
@@ -284,9 +287,18 @@ class RxPath:
         return abi.check(self.lib.emurx_desc_keys_dev(self.h, _addr(frames), _addr(desc), n, _stream(stream)),
                          "desc_keys_dev")
 
-    def lookup_dev(self, recv, recv_count, n_parts: int, cap: int, out, flow=None, stream=None):
-        """The owner's lookups over received LOOKUP_REC_DTYPE regions -> ROUTE_REC_DTYPE slots."""
-        return abi.check(self.lib.emurx_lookup_dev(self.h, _addr(recv), _addr(recv_count), n_parts, cap,
+    def zmq_walk_dev(self, buf, ctl, nmsg: int, desc, msg_stat, keys: bool = True, stream=None):
+        """The framing walk alone on device-resident messages (include/emu_rx.h
+        emurx_zmq_walk_dev): ctl = emurx_msg[nmsg] then slot_base[nmsg + 1] (uint32)."""
+        return abi.check(self.lib.emurx_zmq_walk_dev(self.h, _addr(buf), _addr(ctl), nmsg, _addr(desc),
+                                                     _addr(msg_stat), 0 if keys else abi.WALK_NO_KEYS,
+                                                     _stream(stream)), "zmq_walk_dev")
+
+    def lookup_dev(self, recv, recv_count, n_parts: int, cap: int, out, flow=None, stream=None, tail_cap=None):
+        """The owner's lookups over received lookup regions (parse_route_dev's layout; recv_count
+        [2 * n_parts]) -> ROUTE_REC_DTYPE slots."""
+        tail_cap = abi.tail_capacity(cap) if tail_cap is None else tail_cap
+        return abi.check(self.lib.emurx_lookup_dev(self.h, _addr(recv), _addr(recv_count), n_parts, cap, tail_cap,
                                                    _addr(out), _addr(flow), _stream(stream)), "lookup_dev")
 
     # ---- table generations / image diagnostics -------------------------------------------------
