@@ -468,7 +468,7 @@ int emurx_ingest_wait(emurx_t* h, uint32_t slot, emurx_ingest_result* res);
    count reads instead of the frame), and msg_stat[m] = frames | EMURX_MSG_* << 24.  d_ctl:
    emurx_msg[nmsg] then slot_base[nmsg + 1] (message m's descriptor slots are
    [slot_base[m], slot_base[m + 1]); slots a message announced but did not carry become
-   EMURX_DESC_HOLE).  The buffer must be readable 8 bytes past every message.  flags:
+   EMURX_DESC_HOLE).  The buffer must be readable 32 bytes past every message.  flags:
    EMURX_WALK_NO_KEYS leaves the pad byte 0 (for the measurement of what the keys cost; the
    bench folds the difference into the exchange's rate).  One launch, no host sync. */
 #define EMURX_WALK_NO_KEYS 1u

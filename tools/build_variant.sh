@@ -15,5 +15,6 @@ done
 /opt/rocm/bin/hipcc $F -x hip -c csrc/emurx_api.cpp -o $out/emurx_api.o &
 ${CXX:-g++} -O2 -std=c++17 -fPIC -Wall $flags -c csrc/emurx_mirror.cpp -o $out/emurx_mirror.o &
 wait
-/opt/rocm/bin/hipcc $F -shared -o lib/libemurx_$name.so $objs $out/emurx_api.o $out/emurx_mirror.o
+make -s build/build_id.o
+/opt/rocm/bin/hipcc $F -shared -o lib/libemurx_$name.so $objs $out/emurx_api.o $out/emurx_mirror.o build/build_id.o
 echo lib/libemurx_$name.so

@@ -13,7 +13,7 @@ HDR = ROOT / "include" / "emu_rx.h"
 DOC = ROOT / "INTEGRATION.md"
 
 GROUPS = [
-    ("Lifecycle and errors", ["emurx_abi_version", "emurx_open", "emurx_close", "emurx_strerror"],
+    ("Lifecycle and errors", ["emurx_abi_version", "emurx_build_id", "emurx_open", "emurx_close", "emurx_strerror"],
      "`NewThreadCtx` / `Parser.Init` (`thread_ctx.go`, `parser.go:567-581`)"),
     ("Parser registration", ["emurx_register", "emurx_set_callbacks_mask", "emurx_get_callbacks_mask"],
      "`Parser.Register` `parser.go:528-565`"),
@@ -31,7 +31,7 @@ GROUPS = [
      "(device image of the maps above)"),
     ("Mid-batch mutations", ["emurx_table_gen", "emurx_recs_stale"], "DESIGN.md §2.2, `dhcp.go:718`"),
     ("Batched ingest (primary)", ["emurx_ingest_buffer", "emurx_ingest_submit", "emurx_ingest_wait",
-                                  "emurx_ingest_stream"],
+                                  "emurx_ingest_stream", "emurx_zmq_walk_dev"],
      "`VethIFZmq.OnRxStream` over the rx `select` loop's messages, `thread_ctx.go:409-410`, `veth_zmq.go:277-320`"),
     ("Receive path (device-resident; per-message fallback)",
      ["emurx_classify_dev", "emurx_parse_dev", "emurx_rx_stream", "emurx_zmq_descriptors",

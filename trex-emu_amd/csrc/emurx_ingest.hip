@@ -6,7 +6,7 @@
 //   k_zmq_walk  one lane per message: the offset walk of VethIFZmq.OnRxStream
 //               (veth_zmq.go:277-320, uint16 running offset, abort on a header error) ->
 //               descriptors in the message's slot range, each with its frame's owner key
-//               (EMURX_DESC_KEYED: bytes 12..19 of the frame, loaded beside its header);
+//               (EMURX_DESC_KEYED: bytes 12..19 of the frame, loaded with its header);
 //               slots past the decoded frames are marked EMURX_DESC_HOLE (k_rx skips them);
 //               one status word per message
 //   k_qscan     one workgroup: exclusive offset of every (queue, tile) segment of k_rx's
@@ -64,7 +64,27 @@ __global__ __launch_bounds__(kBlock) void k_zmq_walk(const uint8_t* __restrict__
                 const uint32_t h4 = (of + 4) & 0xffff;
                 if (blen < h4) { err = EMURX_MSG_PARSE_ERR; break; }
                 if (h4 < of) { err = EMURX_MSG_PANIC; break; }  // stream[of:of+4] out of range
-                header = ld_be32(s + of);
+                // the frame's bytes 12..19 for its owner key come with its header: 32 bytes from
+                // the header's aligned dword in two 16-byte loads (one memory round trip per
+                // frame, and two load instructions instead of six: each one touches 64 lines, one
+                // per message of the wave); read before the header's checks, so up to 28 bytes
+                // past a message's end may be read, never used.  (A wave per message guessing 64
+                // equal strides per round, and 512-byte LDS windows of each message, both
+                // measured slower on config D's mixed sizes: DESIGN.md §6 round 5)
+                uint32_t w12 = 0, w16 = 0;
+                const uintptr_t a = (uintptr_t)(s + of);
+                const uint32_t sh = (uint32_t)(a & 3);
+                const uint32_t* wa = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+                if constexpr (kKeys) {
+                    const uint4 x = gld16(wa), y = gld16(wa + 4);
+                    header = __builtin_bswap32(__builtin_amdgcn_alignbyte(x.y, x.x, sh));
+                    w12 = __builtin_bswap32(__builtin_amdgcn_alignbyte(y.y, y.x, sh));  // bytes of+16 .. of+19
+                    w16 = __builtin_bswap32(__builtin_amdgcn_alignbyte(y.z, y.y, sh));  // bytes of+20 .. of+23
+                } else {  // the header's two dwords in one load
+                    typedef unsigned v2u __attribute__((ext_vector_type(2)));
+                    const v2u x = *(const __attribute__((address_space(1))) v2u*)wa;
+                    header = __builtin_bswap32(__builtin_amdgcn_alignbyte(x.y, x.x, sh));
+                }
                 if ((header & 0xff000000u) != 0xAA000000u) { err = EMURX_MSG_PARSE_ERR; break; }
                 const uint32_t vport = (header >> 16) & 0xff, plen = header & 0xffff;
                 const uint32_t e = (of + 4 + plen) & 0xffff;
@@ -77,7 +97,7 @@ __global__ __launch_bounds__(kBlock) void k_zmq_walk(const uint8_t* __restrict__
                 uint32_t key = 0;
                 if constexpr (kKeys) {
                     uint32_t v0, v1;
-                    l2_vlans(plen, ld_be32(s + h4 + 12), ld_be32(s + h4 + 16), v0, v1);
+                    l2_vlans(plen, w12, w16, v0, v1);
                     key = emurx_owner_key(emurx_tk_hash(vport, v0, v1));
                 }
                 reinterpret_cast<uint2*>(desc)[base + found] = make_uint2(M.x + h4, plen | (vport << 16) | (key << 24));

@@ -98,7 +98,7 @@ int emurx_launch_lookup(const emurx_lookup_rec* recv, const uint32_t* recv_count
 
 // Batched ZMQ ingest (emurx_ingest.hip).  zmq_walk: one lane per message; ctl = emurx_msg[nmsg]
 // then slot_base[nmsg + 1]; writes desc[slot_base[m] ..) (holes marked EMURX_DESC_HOLE) and
-// msg_stat[m] = frames | EMURX_MSG_* << 24.  The buffer must be readable 8 bytes past every message.
+// msg_stat[m] = frames | EMURX_MSG_* << 24.  The buffer must be readable 32 bytes past every message.
 // keys = false: descriptors without owner keys (the measurement of their cost only).
 int emurx_launch_zmq_walk(const uint8_t* buf, const uint32_t* ctl, uint32_t nmsg, emurx_desc* desc,
                           uint32_t* msg_stat, hipStream_t st, bool keys = true);

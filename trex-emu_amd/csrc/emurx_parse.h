@@ -547,6 +547,11 @@ __device__ __forceinline__ void first(uint32_t& st, bool cond, uint32_t code) {
     st = (st == EMURX_ST_OK && cond) ? code : st;
 }
 
+// EMURX_DWFIELDS: header fields of the staged path extracted from aligned-dword words (v_alignbyte)
+// instead of byte reads (A/B)
+#ifndef EMURX_DWFIELDS
+#define EMURX_DWFIELDS 0
+#endif
 // Parser.parsePacketL4 parser.go:583-724, flat
 __device__ __forceinline__ void parse_l4_flat(const LdsSrc& s, uint32_t len, Rec& r, uint32_t nextHdr, uint32_t pcs,
                                               uint32_t l4len, bool v6, uint32_t cb_mask) {
@@ -555,8 +560,16 @@ __device__ __forceinline__ void parse_l4_flat(const LdsSrc& s, uint32_t len, Rec
     const bool p1 = nextHdr == 1, p2 = nextHdr == 2, p6 = nextHdr == 6, p17 = nextHdr == 17, p58 = nextHdr == 58;
     const uint32_t L4_8 = (L4 + 8) & 0xffff, L4_4 = (L4 + 4) & 0xffff, L4_12 = (L4 + 12) & 0xffff;
     const bool sok = span_ok(L4, l4len);
+#if EMURX_DWFIELDS
+    // the L4 header's fields from three aligned-dword words (bytes L4..L4+7, L4+12..L4+15)
+    // instead of eight byte reads; a staged frame's L4 + 12 never wraps the uint16
+    const uint32_t P0 = le32(s, L4), P4 = le32(s, L4 + 4), P12 = le32(s, L4 + 12);
+    const uint32_t tcplen = ((P12 & 0xff) >> 4) << 2;
+    const bool ucs = (P4 >> 16) != 0;  // UDP checksum present (bytes L4+6, L4+7)
+#else
     const uint32_t tcplen = (s.u8(L4_12) >> 4) << 2;
     const bool ucs = be16(s, L4 + 6) > 0;  // UDP checksum present
+#endif
     uint32_t st = EMURX_ST_OK;
     bool tcp_hdr = false;  // TCP got past its length checks (L7 / L7Len are set)
     if (p1) {
@@ -586,7 +599,12 @@ __device__ __forceinline__ void parse_l4_flat(const LdsSrc& s, uint32_t len, Rec
     // before it for UDP, L7 only on success for ICMP and UDP)
     r.l7len = tcp_hdr ? ((l4len - tcplen) & 0xffff) : (p17 && len >= L4_8) ? ((l4len - 8) & 0xffff) : 0u;
     r.l7 = tcp_hdr ? ((L4 + tcplen) & 0xffff) : ((p1 || p17) && st == EMURX_ST_OK) ? L4_8 : 0u;
+#if EMURX_DWFIELDS
+    const uint32_t src = ((P0 & 0xff) << 8) | ((P0 >> 8) & 0xff), dst = (((P0 >> 16) & 0xff) << 8) | (P0 >> 24),
+                   t6 = P0 & 0xff;
+#else
     const uint32_t src = be16(s, L4), dst = be16(s, L4 + 2), t6 = s.u8(L4);
+#endif
     uint32_t cb = p1 ? EMURX_CB_ICMP : p2 ? EMURX_CB_IGMP : p6 ? EMURX_CB_TCP : p58 ? EMURX_CB_ICMPV6 : EMURX_CB_UDP;
     if (p17) {
         cb = dst == 5353 ? EMURX_CB_MDNS
@@ -612,7 +630,14 @@ __device__ __forceinline__ void parse_flat(const LdsSrc& s, uint32_t len, uint32
     auto is_ppp = [](uint32_t x) { return x == 0x8863 || x == 0x8864; };
     uint32_t st = EMURX_ST_OK;
     first(st, len < 14, EMURX_ST_PACKET_TOO_SHORT);
+#if EMURX_DWFIELDS
+    // bytes 12..23 as three big-endian words from four aligned dwords (the EtherType / TPID
+    // words and the CTunnelKey VLAN words) instead of six byte reads and two word reads
+    const uint32_t W12 = be32(s, 12), W16 = be32(s, 16), W20 = be32(s, 20);
+    const uint32_t e0 = W12 >> 16, e1 = W16 >> 16, e2 = W20 >> 16;
+#else
     const uint32_t e0 = be16(s, 12), e1 = be16(s, 16), e2 = be16(s, 20);
+#endif
     const bool t0 = st == EMURX_ST_OK && is_tag(e0);
     first(st, t0 && len < 18, EMURX_ST_DOT1Q_TOO_SHORT);
     const bool g0 = t0 && st == EMURX_ST_OK;  // tag 0 parsed
@@ -624,8 +649,13 @@ __device__ __forceinline__ void parse_flat(const LdsSrc& s, uint32_t len, uint32
     const bool t2 = g1 && !ppp1 && is_tag(e2);
     first(st, t2 && len < 26, EMURX_ST_DOT1Q_TOO_SHORT);
     first(st, t2, EMURX_ST_TOO_MANY_DOT1Q);
+#if EMURX_DWFIELDS
+    r.vlan0 = g0 ? (W12 & 0xffff0fffu) : 0u;
+    r.vlan1 = g1 ? (W16 & 0xffff0fffu) : 0u;
+#else
     r.vlan0 = g0 ? (be32(s, 12) & 0xffff0fffu) : 0u;
     r.vlan1 = g1 ? (be32(s, 16) & 0xffff0fffu) : 0u;
+#endif
     if (st != EMURX_ST_OK) { fail(r, st); return; }
     if (ppp0 || ppp1) { invoke(r, EMURX_CB_PPP, cb_mask); return; }
     const uint32_t offset = 14 + (g0 ? 4u : 0u) + (g1 ? 4u : 0u);
@@ -635,7 +665,15 @@ __device__ __forceinline__ void parse_flat(const LdsSrc& s, uint32_t len, uint32
     bool v6 = false;
     if (et == 0x0800) {  // IPv4
         r.l3 = offset;
+#if EMURX_DWFIELDS
+        // version / IHL, total length, flags / fragment offset and protocol from the header's
+        // first three words (the dwords its checksum reads again) instead of six byte reads
+        const uint32_t H0 = le32(s, offset), H4 = le32(s, offset + 4), H8 = le32(s, offset + 8);
+        const uint32_t b0 = H0 & 0xff, totlen = (((H0 >> 16) & 0xff) << 8) | (H0 >> 24),
+                       frag = (((H4 >> 16) & 0xff) << 8) | (H4 >> 24);
+#else
         const uint32_t b0 = s.u8(offset), frag = be16(s, offset + 6), totlen = be16(s, offset + 2);
+#endif
         const uint32_t hdr = (b0 & 0xf) << 2;
         first(st, len < offset + 20, EMURX_ST_IPV4_TOO_SHORT);
         first(st, (b0 >> 4) != 4, EMURX_ST_IPV4_HDR_TOO_SHORT);
@@ -650,7 +688,11 @@ __device__ __forceinline__ void parse_flat(const LdsSrc& s, uint32_t len, uint32
         if (st != EMURX_ST_OK) { fail(r, st); return; }
         l4len = (totlen - hdr) & 0xffff;
         l4 = offset + hdr;
+#if EMURX_DWFIELDS
+        nh = (H8 >> 8) & 0xff;
+#else
         nh = s.u8(offset + 9);
+#endif
         pcs = be_domain(s.template sum_fixed<8>(offset + 12), s.at(offset + 12)) + nh + l4len;  // src, dst, 0|proto, len
     } else if (et == 0x86DD) {  // IPv6
         r.l3 = offset;
@@ -1116,7 +1158,12 @@ __device__ __forceinline__ LKey make_key(const S& s, uint32_t len, const Rec& r)
     const uint32_t cb = r.proto;
     LKey k;
     k.dlo = le32(s, 0);
+#if EMURX_DWFIELDS
+    if constexpr (std::is_same<S, LdsSrc>::value) k.dhi = le32(s, 4) & 0xffffu;  // p[4:6] from a dword word
+    else k.dhi = s.u8(4) | (s.u8(5) << 8);
+#else
     k.dhi = s.u8(4) | (s.u8(5) << 8);  // p[0:6]
+#endif
     k.mc6 = 0;
     const bool bcast = k.dlo == 0xffffffffu && k.dhi == 0xffffu;
     k.key = kMac;
