@@ -963,6 +963,28 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
                          (" + owner lookups (k_lookup)" if mode == "partitioned" else "")),
             "phases": phases,
         }
+        pmc_x = ROOT / "profiles" / "pmc_exchangeD.json"
+        if mode == "partitioned" and cfg == "D" and pmc_x.exists() and phases and phases.get("owner_lookup_ms"):
+            # the owner's k_lookup against ITS roofline: random 64-B probe lines that leave L2
+            # (calibrated PMC, per launch, scaled to this batch) at the measured random-line rate
+            # of an HBM-sized table, plus its streamed records at the copy ceiling (additive, as
+            # the calibration's stream + probes mode measured)
+            try:
+                px = json.loads(pmc_x.read_text())
+                lines = px["k_lookup"]["probe_lines_per_launch"] * n / (1 << 21)
+                rate = px["line_rate_glines_per_s"]["hbm_sized_table"] * 1e9
+                stream_b = (32 + 0.8 + 40) * n
+                floor_ms = (lines / rate + stream_b / (copy_gbs * 1e9)) * 1e3
+                look = phases["owner_lookup_ms"]
+                out["exchange"]["random_line"] = {
+                    "kernel": "k_lookup", "probe_lines_per_launch": int(lines), "line_rate_glines_per_s": rate / 1e9,
+                    "stream_bytes_per_launch": int(stream_b), "floor_ms": round(floor_ms, 5), "measured_ms": look,
+                    "frac": round(floor_ms / look, 4),
+                    "hbm_frac_alg_bytes": round(stream_b / (look * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                    "source": f"{pmc_x.relative_to(ROOT)} (probe lines), profiles/r05/probe_rate/rates.txt (line rate), "
+                              "this run's copy ceiling and phases.owner_lookup_ms"}
+            except Exception as e:  # noqa: BLE001
+                out["exchange"]["random_line"] = {"error": repr(e)[:200]}
         if pipelined is not None:
             # N = 1: the line's value is the pipelined rate, as for the one-launch steps of
             # B / C / E; the back-to-back steps above stay beside it

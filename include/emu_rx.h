@@ -451,6 +451,8 @@ typedef struct emurx_ingest_result {
     uint32_t n_msgs;
     uint32_t qoff[EMURX_NUM_QUEUES + 1];
     emurx_counters delta;        /* ParserStats + VethStats deltas of the batch             */
+    uint32_t one_launch;         /* 1: the batch ran as one kernel (k_ingest_small, the
+                                    small-batch path), 0: the copy + four-launch pipeline     */
 } emurx_ingest_result;
 /* Pinned staging buffer of slot s (0 <= s < EMURX_INGEST_SLOTS) with room for `bytes`
    (grown on demand; not while the slot has a batch in flight). */

@@ -750,6 +750,61 @@ def test_zmq_walk_dev(rxmod):
             assert (seg["pad"][nf:] == abi.DESC_HOLE).all(), m
 
 
+@pytest.mark.parametrize("small", ["1", "0"])
+def test_ingest_small_limits(rxmod, small, monkeypatch):
+    """The one-launch ingest at its limits: 64 tiles of slots exactly (256 messages
+    of 64 frames), 1,024 messages exactly (16 frames each), and a tile whose staged messages
+    take exactly EMURX_SMALL_LDS / 16 vectors (one launch) or one vector more (the pipeline):
+    which path ran (emurx_ingest_result.one_launch), and results equal to the oracle's either
+    way (the sizing of s_mk / s_base / s_cnt and the host's small_fits agree exactly)."""
+    monkeypatch.setenv("EMURX_INGEST_SMALL", small)
+    w = synth.config_b(1 << 14, seed=0xB17)
+    frames = [w["buf"][d["off"]:d["off"] + d["len"]].tobytes() for d in w["desc"]]
+    rx, o = new_pair(rxmod, max_frames=1 << 15)
+    for t in (rx, o):
+        synth.load_tables(w, t)
+    rng = np.random.default_rng(5)
+
+    def run(msgs, offs=None):
+        if offs is None:
+            tab = place_messages(rx, 0, msgs, rng)
+        else:  # exact offsets (the LDS budget depends on each message's offset mod 16)
+            buf = rx.ingest_buffer(0, offs[-1] + len(msgs[-1]) + 64)
+            tab = np.zeros(len(msgs), abi.MSG_DTYPE)
+            for i, (m, at) in enumerate(zip(msgs, offs)):
+                buf[at:at + len(m)] = np.frombuffer(m, np.uint8)
+                tab[i] = (at, len(m))
+        rx.ingest_submit(0, tab)
+        res = rx.ingest_wait(0)
+        check_ingest(res, o, msgs, tab)
+        return res["one_launch"]
+
+    big = [F.zmq_pack(frames[64 * i:64 * i + 64]) for i in range(256)]  # 16,384 slots = 64 tiles
+    assert run(big) == (small == "1")
+    many = [F.zmq_pack(frames[16 * i:16 * i + 16]) for i in range(1024)]  # 1,024 messages
+    assert run(many) == (small == "1")
+    # tile 1 = one message of 255 frames (40,804 bytes at a 16-aligned offset: 2,553 vectors with
+    # the 2 of slack) + one of 1 frame at offset mod 16 = 4: 7 vectors (66 bytes) = 2,560 =
+    # EMURX_SMALL_LDS / 16, or 8 (80 bytes): one over
+    pad = lambda f, n: f + bytes(n - len(f))  # noqa: E731  (bytes past IPv4 totlen: Go ignores them)
+    m1 = F.zmq_pack([pad(frames[300 + i], 156) for i in range(255)])
+    assert len(m1) == 40804
+    head = [F.zmq_pack(frames[64 * i:64 * i + 64]) for i in range(4)]  # tile 0
+    for flen, fits in ((64, True), (72, False)):
+        m2 = F.zmq_pack([pad(frames[900], flen)])
+        msgs = head + [m1, m2]
+        offs, at = [], 0
+        for m in head:
+            offs.append(at)
+            at += len(m)
+        at = (at + 15) & ~15
+        offs += [at, at + len(m1)]
+        assert (offs[-1] & 15) == 4
+        v = (((offs[-1] & 15) + len(m2) + 15) >> 4) + 2 + (len(m1) + 15) // 16 + 2
+        assert v == abi.SMALL_LDS // 16 + (0 if fits else 1), v
+        assert run(msgs, offs) == (small == "1" and fits), (flen, fits)
+
+
 def test_ingest_messages(rxmod):
     """Valid, truncated, corrupted, over-announcing, oversized and > 64 KiB messages in one
     batch at unaligned offsets: records, descriptors, queues, per-message frame counts and
@@ -773,13 +828,14 @@ def test_ingest_messages(rxmod):
 
 @pytest.mark.parametrize("small", ["1", "0"])
 def test_ingest_small_batches(rxmod, small, monkeypatch):
-    """Batches that fit the one-launch path (k_ingest_small: <= 16 tiles, <= 256 messages, each
+    """Batches that fit the one-launch path (k_ingest_small: <= 64 tiles, <= 1024 messages, each
     tile's messages within its LDS budget) and, with EMURX_INGEST_SMALL=0, the same batches
     through the multi-launch pipeline: records, descriptors (owner keys included), queues,
     per-message frame counts and status, and every counter equal the oracle's OnRxStream per
     message.  1 to 300 messages of config C frames and hostile messages (truncated, corrupted,
     over-announcing, empty), so that messages span tiles, some carry no slot and the last
-    tile's status words include the trailing empty messages."""
+    tile's status words include the trailing empty messages; then the limits themselves
+    (test_ingest_small_limits)."""
     import test_abi
     monkeypatch.setenv("EMURX_INGEST_SMALL", small)
     rng = np.random.default_rng(0x5A11 + int(small))

@@ -44,7 +44,7 @@ def main():
     lib, h = rx.lib, rx.h
     res = abi.IngestResult()
     mt = np.ascontiguousarray(np.asarray(msgs)).view(np.uint32).reshape(-1, 2)
-    for nm in (1, 16, 64):
+    for nm in (1, 16, 64, 256):
         tab = np.ascontiguousarray(mt[:nm])
         ptr = tab.ctypes.data
         sub, wt = [], []
@@ -59,10 +59,12 @@ def main():
         out[f"msgs_{nm}"] = {"submit_us": med(sub), "wait_us": med(wt),
                              "total_us": med([a + b for a, b in zip(sub, wt)])}
         if hasattr(lib, "emurx_debug_small_stamps"):  # the EMURX_SMALL_STAMP build: the last batch's phases
-            st = np.zeros(16 * 10, dtype=np.uint64)
-            lib.emurx_debug_small_stamps(st.ctypes.data_as(C.c_void_p))
-            st = st.reshape(16, 10).astype(np.int64)
+            raw = np.zeros(64 * 10 + 16, dtype=np.uint64)
+            lib.emurx_debug_small_stamps(raw.ctypes.data_as(C.c_void_p))
+            st = raw[:640].reshape(64, 10).astype(np.int64)
             t0 = st[st[:, 0] > 0, 0].min()
+            pk = raw[640:646].astype(np.int64)  # the last workgroup's pack phases
+            out[f"msgs_{nm}"]["pack_stamps_us"] = [round((v - t0) / 100.0, 2) if v > 0 else None for v in pk]
             out[f"msgs_{nm}"]["stamps_us_from_first_entry"] = [
                 [round((v - t0) / 100.0, 2) if v > 0 else None for v in row] for row in st if row[0] > 0]
     print(json.dumps(out))

@@ -616,11 +616,11 @@ int ingest_submit(emurx_t* h, uint32_t slot, const emurx_msg* msgs, uint32_t nms
         if (!s.d_ticket.p) {
             if (s.d_qseg.alloc((size_t)EMURX_SMALL_TILES * EMURX_NUM_QUEUES * EMURX_QUEUE_TILE) ||
                 s.d_tcnt.alloc((size_t)EMURX_SMALL_TILES * 16) || s.d_hsmall.alloc(2 * EMURX_HIST_BINS) ||
-                s.h_done.alloc(1) || s.d_ticket.alloc(1))
+                s.h_done.alloc(1) || s.d_ticket.alloc(3))
                 return EMURX_ENOMEM;
             *(volatile uint32_t*)s.h_done.p = s.seq;
             if (!EMURX_HIP_OK(hipMemsetAsync(s.d_hsmall.p, 0, 2 * EMURX_HIST_BINS * sizeof(uint64_t), st)) ||
-                !EMURX_HIP_OK(hipMemsetAsync(s.d_ticket.p, 0, sizeof(uint32_t), st)))
+                !EMURX_HIP_OK(hipMemsetAsync(s.d_ticket.p, 0, 3 * sizeof(uint32_t), st)))
                 return EMURX_EDEVICE;
         }
         if (emurx_launch_ingest_small(s.h_buf.p, ctl, nmsg, n, h->tables(), s.h_rec.p, s.h_desc.p, s.h_qlist.p,
@@ -722,6 +722,7 @@ int ingest_wait(emurx_t* h, uint32_t slot, emurx_ingest_result* res) {
     }
     memcpy(res->qoff, s.h_qoff.p, sizeof(res->qoff));
     if (res->qoff[EMURX_NUM_QUEUES] != nf) return EMURX_EDEVICE;
+    res->one_launch = s.small ? 1u : 0u;
     emurx_hist_to_counters(s.h_hist.p, &d);
     d.rx_pkts = nf;  // VethIFZmq.OnRx veth_zmq.go:233-234
     for (int b = 0; b < EMURX_HIST_BINS; ++b) d.rx_bytes += s.h_hist.p[2 * b + 1];

@@ -256,12 +256,19 @@ struct SmallArgs {
 #define EMURX_SMALL_STAMP 0
 #endif
 #if EMURX_SMALL_STAMP
-__device__ unsigned long long g_small_stamp[EMURX_SMALL_TILES * 10];
+__device__ unsigned long long g_small_stamp[EMURX_SMALL_TILES * 10 + 16];  // + the last workgroup's pack phases
 #define SSTAMP(k)                                                 \
     do {                                                          \
         if (tid == 0) g_small_stamp[t * 10 + (k)] = wall_clock64(); \
     } while (0)
+#define PSTAMP(k)                                                                 \
+    do {                                                                          \
+        if (tid == 0) g_small_stamp[EMURX_SMALL_TILES * 10 + (k)] = wall_clock64(); \
+    } while (0)
 #else
+#define PSTAMP(k) \
+    do {          \
+    } while (0)
 #define SSTAMP(k) \
     do {          \
     } while (0)
@@ -547,46 +554,142 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
         atomicAdd(&a.hist[2 * tid], (unsigned long long)s_hp[tid]);
         atomicAdd(&a.hist[2 * tid + 1], (unsigned long long)s_hb[tid]);
     }
-    // 4. arrival: the workgroup whose ticket is last packs every tile's queues.  Every wave's
-    // write-through stores have completed (vmcnt 0) before the barrier; then one lane releases
-    // and takes a ticket (MI355X_MICROARCH.md, the hand-off table's first row)
+    // queue-major offsets of every (queue, tile) segment from the tiles' published counts:
+    // s_off[q * nt + t], s_off[nseg] = the total; qoff written by the caller's choice
+    __shared__ uint32_t s_cnt[EMURX_SMALL_TILES * EMURX_NUM_QUEUES], s_off[EMURX_SMALL_TILES * EMURX_NUM_QUEUES + 1];
+    const uint32_t nseg = a.nt * EMURX_NUM_QUEUES;  // segment k = (q = k / nt, t = k % nt)
+    auto segment_offsets = [&](bool write_qoff) {
+        for (uint32_t k = tid; k < nseg; k += kBlock) s_cnt[k] = ld_agent(a.tcnt + (k % a.nt) * 16 + k / a.nt);
+        __syncthreads();
+        // exclusive prefix, the whole workgroup: kPer per lane, then the lanes' sums by a wave
+        // scan and the waves' totals (one lane walking 832 segments serially spent ~40 us of a
+        // 16K-frame batch in dependent LDS reads)
+        constexpr uint32_t kPer = (EMURX_SMALL_TILES * EMURX_NUM_QUEUES + kBlock - 1) / kBlock;  // segments per lane
+        __shared__ uint32_t s_wsum[kWaves];
+        uint32_t c4[kPer], sum = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; ++j) {
+            const uint32_t k = kPer * tid + j;
+            c4[j] = k < nseg ? s_cnt[k] : 0u;
+            sum += c4[j];
+        }
+        const uint32_t incl = wave_incl_scan(sum);
+        if (lane == kWave - 1) s_wsum[wv] = incl;
+        __syncthreads();
+        uint32_t at = incl - sum, total = 0;
+        for (uint32_t w2 = 0; w2 < kWaves; ++w2) {
+            at += w2 < wv ? s_wsum[w2] : 0u;
+            total += s_wsum[w2];
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; ++j) {
+            const uint32_t k = kPer * tid + j;
+            if (k < nseg) {
+                s_off[k] = at;
+                if (write_qoff && k % a.nt == 0) a.qoff[k / a.nt] = at;
+            }
+            at += c4[j];
+        }
+        if (tid == 0) {
+            s_off[nseg] = total;
+            if (write_qoff) a.qoff[EMURX_NUM_QUEUES] = total;
+        }
+        __syncthreads();
+    };
+    // 4. the tiles meet: every workgroup publishes its queue counts (write-through stores, then a
+    // release and an arrival count), waits until every tile has arrived, derives the segment
+    // offsets from all the counts and writes its own queue entries straight to their packed
+    // places in the host's qlist (the PCIe writes spread over every workgroup: one workgroup
+    // writing a 16K-frame batch's 64 KiB took 20 us at its outstanding-write limit).  The wait
+    // is bounded (kSpinLimit polls): a workgroup that gives up (its tiles were not all resident,
+    // e.g. beside other kernels) marks the batch degraded, and the last workgroup then packs
+    // the queues from the device scratch every tile also wrote (qseg) as before.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    __shared__ uint32_t s_direct;
+    if (tid == 0) {
+        constexpr uint32_t kSpinLimit = 20000;  // one agent-scope load (~1 us) + s_sleep per poll
+        __atomic_thread_fence(__ATOMIC_RELEASE);  // every wave's stores are behind the barrier
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        atomicAdd(a.ticket + 1, 1u);
+        uint32_t it = 0, seen = 0;
+        while ((seen = ld_agent(a.ticket + 1)) < a.nt && ++it < kSpinLimit) __builtin_amdgcn_s_sleep(2);
+        s_direct = seen >= a.nt;
+        if (!s_direct) atomicOr(a.ticket + 2, 1u);  // before this workgroup's ticket (release below)
+    }
+    __syncthreads();
+    SSTAMP(7);
+    if (s_direct) {
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+        segment_offsets(t == 0);
+        if (q != 0xffu) {
+            uint32_t pos = s_off[q * a.nt + t] + rank;
+            for (uint32_t w = 0; w < wv; ++w) pos += s_wcnt[w][q];
+            a.qlist[pos] = sl;
+        }
+    }
+    // the ticket: every wave's stores (host qlist entries included) have completed first; the
+    // workgroup that takes the last ticket folds the histogram, packs the queues if the batch
+    // was degraded, resets the scratch words and writes the completion word
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-        __atomic_thread_fence(__ATOMIC_RELEASE);  // every wave's stores are behind the barrier
+        __atomic_thread_fence(__ATOMIC_RELEASE);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         s_last = atomicAdd(a.ticket, 1u) == a.nt - 1;
     }
     __syncthreads();
-    SSTAMP(7);
     if (!s_last) return;
+    PSTAMP(0);
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
-    // queue-major offsets of every (queue, tile) segment; lane tid < 13 * nt owns one
-    __shared__ uint32_t s_cnt[EMURX_SMALL_TILES * EMURX_NUM_QUEUES], s_off[EMURX_SMALL_TILES * EMURX_NUM_QUEUES + 1];
-    const uint32_t nseg = a.nt * EMURX_NUM_QUEUES;  // segment k = (q = k / nt, t = k % nt)
-    for (uint32_t k = tid; k < nseg; k += kBlock) s_cnt[k] = ld_agent(a.tcnt + (k % a.nt) * 16 + k / a.nt);
-    __syncthreads();
-    if (tid == 0) {
-        uint32_t at = 0;
-        for (uint32_t k = 0; k < nseg; ++k) {
-            if (k % a.nt == 0) a.qoff[k / a.nt] = at;
-            s_off[k] = at;
-            at += s_cnt[k];
+    PSTAMP(1);
+    const bool degraded = ld_agent(a.ticket + 2) != 0;
+    if (degraded) segment_offsets(true);
+    PSTAMP(2);
+    PSTAMP(3);
+    // The packed queues, entry p by lane p mod 256 in round p / 256: every store instruction
+    // writes 1 KiB of contiguous host memory (PCIe writes of whole lines), and a lane issues
+    // kPackBatch rounds' loads before their stores.  Its segment advances monotonically with p.
+    // (Round 4 copied a segment per wave, 64 entries per step: a batch of one-queue traffic
+    // took one device round trip per 64 entries, 21 us for 16 tiles)
+    if (degraded) {
+        constexpr uint32_t kPackBatch = 16;
+        const uint32_t total = s_off[nseg];
+        uint32_t k = 0;  // the segment of this lane's current entry
+        if (tid < total) {  // its first: the last segment starting at or before it (empty ones skipped)
+            uint32_t lo = 0, hi = nseg;
+            while (hi - lo > 1) {
+                const uint32_t md = (lo + hi) >> 1;
+                if (s_off[md] <= tid) lo = md; else hi = md;
+            }
+            k = lo;
         }
-        a.qoff[EMURX_NUM_QUEUES] = at;
+        for (uint32_t p0 = 0; p0 < total; p0 += kPackBatch * kBlock) {
+            uint32_t v[kPackBatch];
+#pragma unroll
+            for (uint32_t u = 0; u < kPackBatch; ++u) {
+                const uint32_t p = p0 + u * kBlock + tid;
+                v[u] = 0;
+                if (p < total) {
+                    while (s_off[k + 1] <= p) ++k;  // s_off[nseg] = total > p: stops inside
+                    const uint32_t qq = k / a.nt, tt = k % a.nt;
+                    v[u] = ld_agent(a.qseg + ((size_t)tt * EMURX_NUM_QUEUES + qq) * kBlock + (p - s_off[k]));
+                }
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kPackBatch; ++u) {
+                const uint32_t p = p0 + u * kBlock + tid;
+                if (p < total) a.qlist[p] = v[u];
+            }
+        }
     }
-    __syncthreads();
-    for (uint32_t k = wv; k < nseg; k += kWaves) {  // a wave per segment
-        const uint32_t c = s_cnt[k], qq = k / a.nt, tt = k % a.nt;
-        for (uint32_t j = lane; j < c; j += kWave)
-            a.qlist[s_off[k] + j] = ld_agent(a.qseg + ((size_t)tt * EMURX_NUM_QUEUES + qq) * kBlock + j);
-    }
+    PSTAMP(4);
     if (tid < 2 * EMURX_HIST_BINS) {
         unsigned long long* hp = a.hist + tid;
         a.hist_out[tid] = __hip_atomic_load(hp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(hp, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (tid == 0) __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid < 3) __hip_atomic_store(a.ticket + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     SSTAMP(8);
     // 5. the host's completion word, after every result store of this workgroup has completed
     // and a system-scope release (the other workgroups' results are ordered before their
@@ -594,6 +697,7 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
     // the kernel's end-of-dispatch signal
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    PSTAMP(5);
     if (tid == 0) {
         __atomic_thread_fence(__ATOMIC_RELEASE);
         __hip_atomic_store(a.done, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -106,11 +106,14 @@ int emurx_launch_zmq_walk(const uint8_t* buf, const uint32_t* ctl, uint32_t nmsg
 // kernel's LDS budget: emurx_ingest_small_fits) in ONE launch: messages and control words read
 // from pinned host memory, walk + parse + classify + queue packing, every result written into
 // pinned host memory (h_*: the layout of the pipeline's D2H copies).  Device scratch: d_qseg
-// [EMURX_SMALL_TILES * 13 * 256], d_tcnt [EMURX_SMALL_TILES * 16], d_hist [128] and d_ticket,
+// [EMURX_SMALL_TILES * 13 * 256], d_tcnt [EMURX_SMALL_TILES * 16], d_hist [128] and d_ticket [3] (ticket,
+// arrivals, degraded),
 // zero before the first launch (each launch leaves them zero).  h_done (pinned host): seq is
 // written there after every result (the host may spin on it instead of the stream).  trange[t]
 // (emurx_ingest_tile_ranges): tile t's first message | its message count << 16.
+#ifndef EMURX_SMALL_TILES
 #define EMURX_SMALL_TILES 64
+#endif
 #define EMURX_SMALL_LDS 40960
 #define EMURX_SMALL_MSGS 1024
 int emurx_launch_ingest_small(const uint8_t* h_buf, const uint32_t* h_ctl, uint32_t nmsg, uint32_t n,

@@ -100,6 +100,7 @@ assert DESC_DTYPE.itemsize == 8
 DESC_HOLE = 0xFF   # EMURX_DESC_HOLE: an empty descriptor slot
 DESC_KEYED = 0x80  # EMURX_DESC_KEYED | k: the frame's Namespace-owner key
 INGEST_SLOTS = 2   # EMURX_INGEST_SLOTS
+SMALL_TILES, SMALL_LDS, SMALL_MSGS = 64, 40960, 1024  # the one-launch ingest's limits (csrc/emurx_kernels.h)
 MSG_OK, MSG_PARSE_ERR, MSG_PANIC = 0, 1, 2
 MSG_DTYPE = np.dtype([("off", "<u4"), ("len", "<u4")])
 TX_IPV4_HDR, TX_V6_NH, TX_L4_SHIFT = 0x01, 0x02, 4
@@ -138,7 +139,8 @@ class Counters(C.Structure):
 class IngestResult(C.Structure):
     _fields_ = [("rec", C.c_void_p), ("desc", C.c_void_p), ("qlist", C.c_void_p),
                 ("msg_frames", C.c_void_p), ("msg_status", C.c_void_p), ("n_frames", C.c_uint32),
-                ("n_msgs", C.c_uint32), ("qoff", C.c_uint32 * (NUM_QUEUES + 1)), ("delta", Counters)]
+                ("n_msgs", C.c_uint32), ("qoff", C.c_uint32 * (NUM_QUEUES + 1)), ("delta", Counters),
+                ("one_launch", C.c_uint32)]
 
 
 class DevOut(C.Structure):

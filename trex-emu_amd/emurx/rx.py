@@ -233,7 +233,7 @@ class RxPath:
         return dict(rec=view(r.rec, n, abi.REC_DTYPE), desc=view(r.desc, n, abi.DESC_DTYPE),
                     qlist=view(r.qlist, n, np.uint32), qoff=np.array(r.qoff, np.uint32),
                     msg_frames=view(r.msg_frames, m, np.uint32), msg_status=view(r.msg_status, m, np.uint8),
-                    counters=r.delta.as_dict(), n=n)
+                    counters=r.delta.as_dict(), n=n, one_launch=bool(r.one_launch))
 
     # ---- tx-side checksum generation ------------------------------------------------------
     def tx_checksum_dev(self, frames, desc, n: int, status=None, stream=None):
