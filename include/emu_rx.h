@@ -538,11 +538,14 @@ int emurx_tx_checksum_dev(emurx_t* h, uint8_t* d_frames, const emurx_tx_desc* d_
    d_msg_off[n_msgs] the total; capacity n + 1.  d_info = {n_msgs, total bytes}.  Nothing is
    written at or past out_cap; out_cap >= 8 * n + sum(len) always suffices, and d_info
    tells the size needed when it did not.  d_out 16-byte aligned; the frames are read as
-   the aligned 16-byte blocks that hold them.  A stream-ordered sequence of launches, no
-   host synchronisation.  Replaces VethIFZmq.FlushTx's per-frame append loop. */
+   the aligned 16-byte blocks that hold them.  n < EMURX_TX_ZMQ_MAX_FRAMES.  Two launches on
+   `stream` (the chain scan, then the write), no host synchronisation; calls on different
+   streams of one handle share its scratch, so they must not overlap.  Replaces
+   VethIFZmq.FlushTx's per-frame append loop. */
 #define EMURX_ZMQ_TX_BURST 64u            /* ZMQ_TX_PKT_BURST_SIZE  veth_zmq.go:36 */
 #define EMURX_ZMQ_TX_MAX_BUFFER 32768u    /* ZMQ_TX_MAX_BUFFER_SIZE veth_zmq.go:37 */
 #define EMURX_ZMQ_PKT_MAGIC 0xAAu         /* per-frame header tag   veth_zmq.go:167 */
+#define EMURX_TX_ZMQ_MAX_FRAMES (1u << 26) /* n must be below it (else EMURX_EINVAL)       */
 int emurx_tx_zmq_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_desc, uint32_t n,
                      uint8_t* d_out, uint64_t out_cap, uint64_t* d_msg_off, uint64_t* d_info, void* stream);
 

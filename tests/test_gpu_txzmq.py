@@ -63,6 +63,29 @@ def test_tx_zmq_million(rx):
     assert check(rx, buf, d) == (1 << 20) // 64
 
 
+def test_tx_zmq_repeat_and_levels(rx):
+    """Back-to-back calls of different sizes reuse the chain's arrival counters (each call's
+    last arrival resets its own; they sit at fixed places, whatever n lays out after them):
+    64 * 4096 + 7 frames (levels of 4,097 tiles, 65, 2 and 1 units: parents with a partial last
+    child set), a 2-tile batch, 3 level-1 units of 500-1,200-byte frames, after a 1M-frame call
+    (test_tx_zmq_million) laid the scratch out for four levels."""
+    big = U.batch(4096 * 64 + 7, 0, seed=21)
+    mid = U.batch(64 * 64 * 3 + 5, 2, seed=23)
+    small = U.batch(100, 0, seed=22)
+    for buf, d in (big, big, small, mid, big, mid):
+        check(rx, buf, d)
+
+
+def test_tx_zmq_frame_limit(rx):
+    """n >= EMURX_TX_ZMQ_MAX_FRAMES (2^26) is refused before anything is enqueued."""
+    import torch
+    from emurx import abi
+    t = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    off = torch.zeros(2, dtype=torch.int64, device="cuda")
+    with pytest.raises(RuntimeError, match=f"emurx error {abi.EMURX_EINVAL}"):
+        rx.tx_zmq_dev(t, t, 1 << 26, t, 64, off, off)
+
+
 def test_tx_zmq_capacity(rx):
     buf, d = U.batch(2000, 2, seed=4)
     need = 8 * len(d) + int(d["len"].astype(np.int64).sum())

@@ -1265,7 +1265,7 @@ int emurx_tx_zmq_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_de
                      uint8_t* d_out, uint64_t out_cap, uint64_t* d_msg_off, uint64_t* d_info, void* stream) {
     if (!h || !d_msg_off || !d_info || (n && (!d_frames || !d_desc || (!d_out && out_cap))))
         return EMURX_EINVAL;
-    if (n > (1u << 30) || ((uintptr_t)d_out & 15) || ((uintptr_t)d_desc & 7)) return EMURX_EINVAL;
+    if (n >= EMURX_TX_ZMQ_MAX_FRAMES || ((uintptr_t)d_out & 15) || ((uintptr_t)d_desc & 7)) return EMURX_EINVAL;
     int rc = bind(h);
     if (rc) return rc;
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
@@ -1273,6 +1273,8 @@ int emurx_tx_zmq_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_de
     if (need > h->d_txz.n) {  // grows on demand; a launch in flight may still read the old one
         (void)hipStreamSynchronize(st);
         if (h->d_txz.alloc(need)) return EMURX_ENOMEM;
+        // the chain's arrival counters start at zero (each call's last arrival resets its own)
+        if (!EMURX_HIP_OK(hipMemset(h->d_txz.p, 0, need))) return EMURX_EDEVICE;
     }
     return emurx_launch_tx_zmq(d_frames, d_desc, n, d_out, out_cap, d_msg_off, d_info, h->d_txz.p, st)
                ? EMURX_EDEVICE
