@@ -752,15 +752,17 @@ def test_zmq_walk_dev(rxmod):
 
 @pytest.mark.parametrize("small", ["1", "0"])
 def test_ingest_small_limits(rxmod, small, monkeypatch):
-    """The one-launch ingest at its limits: 64 tiles of slots exactly (256 messages
-    of 64 frames), 1,024 messages exactly (16 frames each), and a tile whose staged messages
-    take exactly EMURX_SMALL_LDS / 16 vectors (one launch) or one vector more (the pipeline):
-    which path ran (emurx_ingest_result.one_launch), and results equal to the oracle's either
-    way (the sizing of s_mk / s_base / s_cnt and the host's small_fits agree exactly)."""
+    """The one-launch ingest at its limits (256 tiles since round 5): 256 tiles of
+    slots exactly (1,024 messages of 64 frames: also the message limit), 257 tiles (1,009
+    messages of 65 frames: the pipeline), 1,024 messages of 16 frames, and a tile whose staged
+    messages take exactly EMURX_SMALL_LDS / 16 vectors (one launch) or one vector more (the
+    pipeline): which path ran (emurx_ingest_result.one_launch), and results equal to the
+    oracle's either way (the sizing of s_mk / s_base / s_off and the host's small_fits agree
+    exactly)."""
     monkeypatch.setenv("EMURX_INGEST_SMALL", small)
     w = synth.config_b(1 << 14, seed=0xB17)
     frames = [w["buf"][d["off"]:d["off"] + d["len"]].tobytes() for d in w["desc"]]
-    rx, o = new_pair(rxmod, max_frames=1 << 15)
+    rx, o = new_pair(rxmod, max_frames=1 << 17)
     for t in (rx, o):
         synth.load_tables(w, t)
     rng = np.random.default_rng(5)
@@ -779,8 +781,12 @@ def test_ingest_small_limits(rxmod, small, monkeypatch):
         check_ingest(res, o, msgs, tab)
         return res["one_launch"]
 
-    big = [F.zmq_pack(frames[64 * i:64 * i + 64]) for i in range(256)]  # 16,384 slots = 64 tiles
+    assert abi.SMALL_TILES == 256 and abi.SMALL_MSGS == 1024
+    nf = len(frames)
+    big = [F.zmq_pack([frames[(64 * i + j) % nf] for j in range(64)]) for i in range(1024)]  # 65,536 slots = 256 tiles
     assert run(big) == (small == "1")
+    over = [F.zmq_pack([frames[(65 * i + j) % nf] for j in range(65)]) for i in range(1009)]  # 65,585 slots: 257 tiles
+    assert not run(over)
     many = [F.zmq_pack(frames[16 * i:16 * i + 16]) for i in range(1024)]  # 1,024 messages
     assert run(many) == (small == "1")
     # tile 1 = one message of 255 frames (40,804 bytes at a 16-aligned offset: 2,553 vectors with

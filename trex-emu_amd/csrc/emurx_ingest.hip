@@ -556,23 +556,23 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
     }
     // queue-major offsets of every (queue, tile) segment from the tiles' published counts:
     // s_off[q * nt + t], s_off[nseg] = the total; qoff written by the caller's choice
-    __shared__ uint32_t s_cnt[EMURX_SMALL_TILES * EMURX_NUM_QUEUES], s_off[EMURX_SMALL_TILES * EMURX_NUM_QUEUES + 1];
+    __shared__ uint32_t s_off[EMURX_SMALL_TILES * EMURX_NUM_QUEUES + 1];
     const uint32_t nseg = a.nt * EMURX_NUM_QUEUES;  // segment k = (q = k / nt, t = k % nt)
     auto segment_offsets = [&](bool write_qoff) {
-        for (uint32_t k = tid; k < nseg; k += kBlock) s_cnt[k] = ld_agent(a.tcnt + (k % a.nt) * 16 + k / a.nt);
-        __syncthreads();
-        // exclusive prefix, the whole workgroup: kPer per lane, then the lanes' sums by a wave
-        // scan and the waves' totals (one lane walking 832 segments serially spent ~40 us of a
-        // 16K-frame batch in dependent LDS reads)
+        // exclusive prefix, the whole workgroup: kPer consecutive segments per lane, their counts
+        // loaded straight into registers (all in flight), then the lanes' sums by a wave scan and
+        // the waves' totals (one lane walking 832 segments serially spent ~40 us of a 16K-frame
+        // batch in dependent LDS reads)
         constexpr uint32_t kPer = (EMURX_SMALL_TILES * EMURX_NUM_QUEUES + kBlock - 1) / kBlock;  // segments per lane
         __shared__ uint32_t s_wsum[kWaves];
         uint32_t c4[kPer], sum = 0;
 #pragma unroll
         for (uint32_t j = 0; j < kPer; ++j) {
             const uint32_t k = kPer * tid + j;
-            c4[j] = k < nseg ? s_cnt[k] : 0u;
-            sum += c4[j];
+            c4[j] = k < nseg ? ld_agent(a.tcnt + (k % a.nt) * 16 + k / a.nt) : 0u;
         }
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; ++j) sum += c4[j];
         const uint32_t incl = wave_incl_scan(sum);
         if (lane == kWave - 1) s_wsum[wv] = incl;
         __syncthreads();

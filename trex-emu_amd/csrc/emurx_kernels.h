@@ -112,7 +112,7 @@ int emurx_launch_zmq_walk(const uint8_t* buf, const uint32_t* ctl, uint32_t nmsg
 // written there after every result (the host may spin on it instead of the stream).  trange[t]
 // (emurx_ingest_tile_ranges): tile t's first message | its message count << 16.
 #ifndef EMURX_SMALL_TILES
-#define EMURX_SMALL_TILES 64
+#define EMURX_SMALL_TILES 256
 #endif
 #define EMURX_SMALL_LDS 40960
 #define EMURX_SMALL_MSGS 1024

@@ -100,7 +100,7 @@ assert DESC_DTYPE.itemsize == 8
 DESC_HOLE = 0xFF   # EMURX_DESC_HOLE: an empty descriptor slot
 DESC_KEYED = 0x80  # EMURX_DESC_KEYED | k: the frame's Namespace-owner key
 INGEST_SLOTS = 2   # EMURX_INGEST_SLOTS
-SMALL_TILES, SMALL_LDS, SMALL_MSGS = 64, 40960, 1024  # the one-launch ingest's limits (csrc/emurx_kernels.h)
+SMALL_TILES, SMALL_LDS, SMALL_MSGS = 256, 40960, 1024  # the one-launch ingest's limits (csrc/emurx_kernels.h)
 MSG_OK, MSG_PARSE_ERR, MSG_PANIC = 0, 1, 2
 MSG_DTYPE = np.dtype([("off", "<u4"), ("len", "<u4")])
 TX_IPV4_HDR, TX_V6_NH, TX_L4_SHIFT = 0x01, 0x02, 4
