@@ -272,6 +272,13 @@ __global__ __launch_bounds__(kBlock) void k_desc_keys(const uint8_t* __restrict_
 // A head with a tail (emurx_parse.h) loads it before the table probes: its units arrive in the
 // probes' memory round trip.  An ICMPv6 key's client bucket comes from the hash in its head,
 // so that probe need not wait for the tail either; a tuple is needed only by the flow probe.
+// The heads are read once: non-temporal LDS-DMA (aux nt); the outputs are stored write-through
+// (sc1), so their lines leave this XCD's L2 to the table lines the probes re-read (round 5:
+// config D's partitioned step +1.3 %, k_lookup 111 -> 108 us in the phase times,
+// profiles/r05/ab_lookup/).  EMURX_LOOKUP_NT=0: the default policies
+#ifndef EMURX_LOOKUP_NT
+#define EMURX_LOOKUP_NT 1
+#endif
 #ifndef EMURX_LOOKUP_WPE
 #define EMURX_LOOKUP_WPE 6
 #endif
@@ -333,7 +340,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EMURX_LO
     for (uint32_t k = 0; k < 2; ++k)
         if (k * kWave + lane < nvec)
             __builtin_amdgcn_global_load_lds(base + k * kWave + lane,
-                                             (__attribute__((address_space(3))) void*)&s_rec[wv][k * kWave], 16, 0, 0);
+                                             (__attribute__((address_space(3))) void*)&s_rec[wv][k * kWave], 16, 0,
+                                             EMURX_LOOKUP_NT ? 2 : 0);
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -377,7 +385,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EMURX_LO
     const uint32_t npieces = min(kWave, cnt - idx0) * 5;
 #pragma unroll
     for (uint32_t k5 = 0; k5 < 5; ++k5)
-        if (k5 * kWave + lane < npieces) o[k5 * kWave + lane] = park[k5 * kWave + lane];
+        if (k5 * kWave + lane < npieces) {
+#if EMURX_LOOKUP_NT
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(o) + k5 * kWave + lane,
+                               reinterpret_cast<const unsigned long long*>(park)[k5 * kWave + lane], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);  // sc1: the line leaves this XCD's L2
+#else
+            o[k5 * kWave + lane] = park[k5 * kWave + lane];
+#endif
+        }
     if (flow && live) flow[j] = r.flow;
 }
 
