@@ -977,7 +977,10 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             "phases": phases,
         }
         pmc_x = ROOT / "profiles" / "pmc_exchangeD.json"
-        if mode == "partitioned" and cfg == "D" and pmc_x.exists() and phases and phases.get("owner_lookup_kernel_ms"):
+        # the PMC calibration is of one owner holding every table (N = 1, 2M frames): the block is
+        # reported for that step only (an owner of N holds 1/N of the tables: other line rates)
+        if (mode == "partitioned" and cfg == "D" and world == 1 and pmc_x.exists() and phases
+                and phases.get("owner_lookup_kernel_ms")):
             # the owner's k_lookup against ITS roofline: random 64-B probe lines that leave L2
             # (calibrated PMC, per launch, scaled to this batch) at the measured random-line rate
             # of an HBM-sized table, plus its streamed records at the copy ceiling (additive, as
@@ -1490,9 +1493,24 @@ def tx_csum_rate(rx, w, torch, reps=50):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
     moved = int(d["len"][sel].astype(np.int64).sum()) + 16 * m
+    # the in-place field writes dirty whole lines: the 64-byte sectors that hold a checksum
+    # field's bytes go back to HBM whatever their other bytes (each field's two bytes; the
+    # IPv4 header field where the header checksum is rewritten)
+    base = td["off"].astype(np.int64)
+    kd = td["ops"].astype(np.int64) >> abi.TX_L4_SHIFT
+    fld = np.where((kd == abi.TX_L4_TCP4) | (kd == abi.TX_L4_TCP6), 16,
+                   np.where((kd == abi.TX_L4_UDP4) | (kd == abi.TX_L4_UDP6), 6, 2))
+    a4 = base + td["l4"].astype(np.int64) + fld
+    a3 = (base + td["l3"].astype(np.int64) + 10)[(td["ops"] & abi.TX_IPV4_HDR) != 0]
+    sectors = np.unique(np.concatenate([a4 >> 6, (a4 + 1) >> 6, a3 >> 6, (a3 + 1) >> 6]))
+    wb = 64 * len(sectors)
     return {"frames": m, "ms_per_call": round(ms, 4), "mpkts": round(m / ms / 1e3, 1),
             "gbs_moved": round(moved / ms / 1e6, 1), "frac_of_8tbs": round(moved / ms / 1e6 / 8000.0, 4),
-            "note": "one k_tx_csum launch per call, in place; descriptors from the library's parse"}
+            "written_sector_bytes": wb, "gbs_with_writeback": round((moved + wb) / ms / 1e6, 1),
+            "frac_with_writeback": round((moved + wb) / ms / 1e6 / 8000.0, 4),
+            "note": "one k_tx_csum launch per call, in place; descriptors from the library's parse; "
+                    "gbs_moved counts the frames read and the descriptors, gbs_with_writeback adds the "
+                    "64-byte sectors the in-place field writes dirty (written back to HBM whole)"}
 
 
 if __name__ == "__main__":

@@ -386,7 +386,9 @@ __global__ __launch_bounds__(256) void k_txz_emit(const uint8_t* __restrict__ fr
                     for (uint32_t v = 0; v < 5; ++v) {
                         const uintptr_t a = A + 4 * i0 + 16 * v;  // 4 * i0: i0 is a multiple of 16
                         uint4 x = make_uint4(0, 0, 0, 0);
-                        if (a < Fend) x = *reinterpret_cast<const uint4*>(a);  // holds a frame byte
+                        // only blocks that hold a frame byte are read (the first may lie wholly
+                        // before the frame: G0 is up to 3 bytes before it; those bytes are masked)
+                        if (a < Fend && a + 16 > F) x = *reinterpret_cast<const uint4*>(a);
                         W[4 * v] = x.x; W[4 * v + 1] = x.y; W[4 * v + 2] = x.z; W[4 * v + 3] = x.w;
                     }
 #pragma unroll
