@@ -1443,7 +1443,7 @@ def tx_zmq_rate(rx, w, torch, reps=50):
     moved = fb + total + 8 * n
     return {"frames": n, "msgs": nm, "bytes_out": total, "ms_per_call": round(ms, 4),
             "mpkts": round(n / ms / 1e3, 1), "gbs_moved": round(moved / ms / 1e6, 1),
-            "note": "launch sequence: k_txz_chain (leaf tables + the up-sweep, one launch) + k_txz_write (staged, then long-frame tiles)"}
+            "note": "two launches per call: k_txz_chain (leaf tables + the up-sweep) + k_txz_emit (the write)"}
 
 
 def tx_csum_rate(rx, w, torch, reps=50):

@@ -86,6 +86,41 @@ def test_tx_zmq_frame_limit(rx):
         rx.tx_zmq_dev(t, t, 1 << 26, t, 64, off, off)
 
 
+def test_tx_zmq_under_load(rx):
+    """The chain scan's hand-offs between workgroups (sc1 stores, one atomic per workgroup, the
+    last arrival's sc1 loads) under uneven load: every call runs on its own stream while a
+    copy kernel streams 1 GiB on another, so the chain's workgroups start and finish at
+    different times on busy CUs; 12 calls of 6 sizes and length profiles (1 to 3 levels above
+    the tiles), every output word checked."""
+    import torch
+    import pyoracle
+    from gpu_util import to_dev
+    noise = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+    sink = torch.empty_like(noise)
+    s_noise, s_tx = torch.cuda.Stream(), torch.cuda.Stream()
+    cases = [(64 * 4096 + 1, 0), (1000, 1), (64 * 64 * 5 + 33, 2), (200000, 0), (4096 * 64 * 3 + 9, 3), (3000, 1)]
+    for k in range(12):
+        buf, d = U.batch(*cases[k % len(cases)], seed=100 + k)
+        n = len(d)
+        need = 8 * n + int(d["len"].astype(np.int64).sum())
+        with torch.cuda.stream(s_tx):
+            tb, td = to_dev(buf), to_dev(d)
+            out = torch.full((need,), 0xEE, dtype=torch.uint8, device="cuda")
+            off = torch.full((n + 1,), -1, dtype=torch.int64, device="cuda")
+            info = torch.full((2,), -1, dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        with torch.cuda.stream(s_noise):
+            for _ in range(3):
+                sink.copy_(noise)
+        rx.tx_zmq_dev(tb, td, n, out, need, off, info, stream=s_tx.cuda_stream)
+        torch.cuda.synchronize()
+        want, woff, wtotal = pyoracle.tx_zmq(buf, d, None)
+        nm, total = (int(x) for x in info.cpu().numpy())
+        assert total == wtotal and nm == len(woff) - 1, (k, n)
+        assert np.array_equal(off.cpu().numpy()[: nm + 1].astype(np.uint64), woff), k
+        assert out.cpu().numpy()[:total].tobytes() == want.tobytes(), k
+
+
 def test_tx_zmq_capacity(rx):
     buf, d = U.batch(2000, 2, seed=4)
     need = 8 * len(d) + int(d["len"].astype(np.int64).sum())
