@@ -65,6 +65,10 @@ def parse_args():
                          "(default for D: partitioned, with the replicated alternative measured too)")
     ap.add_argument("--table-updates", action="store_true",
                     help="also time batches with 1 / 64 / 4096 table mutations between them")
+    ap.add_argument("--a2a", choices=("v", "equal"), default="v",
+                    help="the exchange's transfer: v = counts, then only the spans that carry data (grouped "
+                         "sends / receives, SURVEY §8e's all-to-all-v; default); equal = whole regions by one "
+                         "equal-split all-to-all (round 4)")
     ap.add_argument("--exchange-frames", type=int, default=1 << 21,
                     help="frames per GPU of the config-D Namespace-exchange measurement beside the headline")
     ap.add_argument("--no-exchange-run", action="store_true",
@@ -510,6 +514,22 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
                        out=xch["sets"][0].get("out"))
         alloc_regions()
 
+        def x_start(b):
+            """batch b's transfer enqueued behind its stream (the v form waits on the host for
+            the batch's counts first)"""
+            with torch.cuda.stream(b["st"]):  # the collective waits for this set's stream
+                if a.a2a == "v":
+                    b["pending"] = X.exchange_v_start(b["send"], b["send_count"], xch["region"], xch["cap"], rb)
+                else:
+                    b["pending"] = X.exchange_start(b["send"], b["send_count"], xch["region"])
+
+        def x_sync(send, send_count):
+            """(recv, recv_count, bytes sent to other ranks) of one blocking transfer"""
+            if a.a2a == "v":
+                return X.exchange_v(send, send_count, xch["region"], xch["cap"], rb)
+            r, c = X.exchange(send, send_count, xch["region"])
+            return r, c, (world - 1) * xch["region"]
+
         def produce(b, k):
             b["k"] = k
             fb, fd = inputs[k % R]
@@ -537,36 +557,50 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
                 xch["dump"].append(dict(k=b["k"], cnt=cnt, recs=np.concatenate(
                     [res[sr, : min(int(cnt[sr]), xch["cap"]) * X.REC_BYTES] for sr in range(world)])))
 
+        def finish(b):
+            consume(b)
+            if b["ev"] is not None:
+                b["ev"][1].record(b["st"])
+                xch["ev"].append(b["ev"])
+                b["ev"] = None
+
         def step_overlapped():
-            """Batch k on set k mod 2's stream: parse + pack, then its all-to-all starts on the
-            collective stream (behind that parse); then the previous batch's owner lookups are
-            queued on ITS stream behind its own all-to-all.  So batch k's parse, batch k-1's
-            transfer and batch k-2's lookups overlap.  Events time a batch from its parse to its
-            lookups' end, on its stream."""
+            """Batch k on set k mod 2's stream.  equal: parse + pack, then its all-to-all starts
+            on the collective stream (behind that parse), then the previous batch's owner lookups
+            are queued on ITS stream behind its own all-to-all.  v: the lookups of batch k-2 (the
+            set's last batch, whose transfer started a step ago) are queued first, then batch k's
+            parse + pack, and only then batch k-1's transfer, whose counts the host waits for:
+            by then batch k's parse is queued behind it, so the GPU does not idle while the host
+            waits.  Either way batch k's parse, batch k-1's transfer and batch k-2's lookups
+            overlap.  Events time a batch from its parse to its lookups' end, on its stream."""
             k = xch["k"]
             xch["k"] += 1
             b, prev = xch["sets"][k % 2], xch["sets"][(k + 1) % 2]
+            if a.a2a == "v" and b["pending"] is not None:
+                finish(b)  # batch k - 2
             if xch["timing"] and k % a.time_stride == 0 and xch["pool"]:
                 b["ev"] = xch["pool"].pop()
                 b["ev"][0].record(b["st"])
             produce(b, k)
-            with torch.cuda.stream(b["st"]):  # the collective waits for this set's stream
-                b["pending"] = X.exchange_start(b["send"], b["send_count"], xch["region"])
-            if prev["pending"] is not None:
-                consume(prev)
-                if prev["ev"] is not None:
-                    prev["ev"][1].record(prev["st"])
-                    xch["ev"].append(prev["ev"])
-                    prev["ev"] = None
+            if a.a2a == "equal":
+                x_start(b)
+                if prev["pending"] is not None:
+                    finish(prev)
+                return
+            b["await_x"] = True
+            if prev.get("await_x"):  # batch k - 1
+                prev["await_x"] = False
+                x_start(prev)
 
         def drain():
-            for b in sorted(xch["sets"], key=lambda x: x.get("k", 0)):
+            order = sorted(xch["sets"], key=lambda x: x.get("k", 0))
+            for b in order:
+                if b.get("await_x"):
+                    b["await_x"] = False
+                    x_start(b)
+            for b in order:
                 if b["pending"] is not None:
-                    consume(b)
-                    if b["ev"] is not None:
-                        b["ev"][1].record(b["st"])
-                        xch["ev"].append(b["ev"])
-                        b["ev"] = None
+                    finish(b)
 
     kk = [0]
 
@@ -617,7 +651,7 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         xch["k"] += 1
         produce(xch["sets"][0], k)
         if world > 1:
-            xch["recv"], xch["recv_count"] = X.exchange(xch["send"], xch["send_count"], xch["region"])
+            xch["recv"], xch["recv_count"], _ = x_sync(xch["send"], xch["send_count"])
         else:
             xch["recv"], xch["recv_count"] = xch["send"], xch["send_count"]
         if mode == "partitioned":
@@ -652,7 +686,7 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             produce(b, k)
             e[1].record(stream)
             if world > 1:
-                recv, rc = X.exchange(b["send"], b["send_count"], xch["region"])
+                recv, rc, sent = x_sync(b["send"], b["send_count"])
             else:
                 recv, rc = b["send"], b["send_count"]
             e[2].record(stream)
@@ -679,7 +713,9 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         k_rx_ms = float(np.mean(krx[1:])) if len(krx) > 1 else float("nan")
         sc = b["send_count"].cpu().numpy().astype(np.int64)[0::xch["cs"]]
         others = [d for d in range(world) if d != rank]
-        moved = len(others) * (xch["region"] + 4 * xch["cs"])
+        # what crossed to other ranks: the counts and, per --a2a, the spans that carry data (v)
+        # or whole regions (equal); the last step's, as every step of one batch sends the same
+        moved = (sent if world > 1 else 0) + len(others) * 4 * xch["cs"]
         # payload per region: the heads (or routed records) and, partitioned, their tail units
         units = [0] * world
         if mode == "partitioned":
@@ -695,6 +731,8 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
                "owner_lookup_kernel_ms": round(look_b2b, 5) if look_b2b is not None else None,
                "record_bytes": rb, "tail_units_per_shard": xch["tcap"], "region_bytes": xch["region"],
                "tail_bytes_per_frame": round(16 * sum(units) / max(int(sc.sum()), 1), 3),
+               "transfer": ("counts, then the spans that carry data (grouped sends / receives)" if a.a2a == "v"
+                            else "one equal-split all-to-all of whole regions"),
                "bytes_to_other_ranks": moved, "payload_bytes_to_other_ranks": payload,
                "frames_to_other_ranks": to_others,
                "bytes_per_frame_to_other_ranks": round(moved / to_others, 2) if to_others else None,
@@ -970,7 +1008,9 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             "record_bytes": xch["rb"],
             "tail_units_per_shard": xch["tcap"],
             "region_bytes": xch["region"],
-            "collective": f"all_to_all_single x2 ({a.backend})" if world > 1 else "none (1 rank)",
+            "collective": ((f"all_to_all_single of the counts + batch_isend_irecv of the spans that carry data "
+                            f"({a.backend})") if a.a2a == "v" else f"all_to_all_single x2 ({a.backend})")
+                           if world > 1 else "none (1 rank)",
             "overlapped": overlapped,  # batch k's all-to-all beside batch k+1's parse (two buffer sets)
             "includes": ("k_rx + group scan + pack" + (" + all-to-all" if world > 1 else "") +
                          (" + owner lookups (k_lookup)" if mode == "partitioned" else "")),

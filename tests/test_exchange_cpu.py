@@ -71,6 +71,24 @@ def _worker(rank, world, port, out_dir):
         ra, ca = X.exchange_finish(pa)
         ok = ok and bool((cb == 0).all()) and torch.equal(ca, recv_count)
         ok = ok and X.received(ra.numpy(), ca.numpy(), cap).tobytes() == got.tobytes()
+        # the payload-sized exchange (counts, then only the valid records): junk past every
+        # region's count stays home; the records are the same; the bytes sent are the payload
+        jsend = junk.numpy().reshape(world, cap * X.REC_BYTES).copy()
+        sv = send.view(np.uint8).reshape(world, -1)
+        for d in range(world):
+            jsend[d, : cnt[d] * X.REC_BYTES] = sv[d, : cnt[d] * X.REC_BYTES]
+        rv, cv, moved = X.exchange_v(torch.from_numpy(jsend.reshape(-1)), torch.from_numpy(cnt), cap * X.REC_BYTES,
+                                     cap, X.REC_BYTES)
+        ok = ok and torch.equal(cv, recv_count) and X.received(rv.numpy(), cv.numpy(), cap).tobytes() == got.tobytes()
+        ok = ok and moved == sum(int(cnt[d]) * X.REC_BYTES for d in range(world) if d != rank)
+        # two in flight (started A then B, finished B then A)
+        pa = X.exchange_v_start(torch.from_numpy(jsend.reshape(-1)), torch.from_numpy(cnt), cap * X.REC_BYTES,
+                                cap, X.REC_BYTES)
+        pb = X.exchange_v_start(junk, torch.zeros(world, dtype=torch.int32), cap * X.REC_BYTES, cap, X.REC_BYTES)
+        rb2, cb2 = X.exchange_finish(pb)
+        ra2, ca2 = X.exchange_finish(pa)
+        ok = ok and bool((cb2 == 0).all()) and pb[3] == 0
+        ok = ok and X.received(ra2.numpy(), ca2.numpy(), cap).tobytes() == got.tobytes()
         Path(out_dir, f"r{rank}").write_text(f"{int(ok)} {len(got)}")
     finally:
         dist.destroy_process_group()
@@ -151,6 +169,16 @@ def _worker_partitioned(rank, world, port, out_dir):
         want = np.concatenate([lookup_regions(recs[s], world, s, cap, tcap)[2][rank] for s in range(world)])
         ok = got.tobytes() == want.tobytes() and len(got) > 0 and (c[1::2] == 0).all()
         ok = ok and int((X.tail_units(got["head"]["w4"]) > 0).sum()) > 0
+        # payload-sized: the valid heads and the tail shards of every region, nothing else
+        noise = np.random.default_rng(7 + rank).integers(0, 256, send.shape, dtype=np.uint8)
+        for d in range(world):
+            noise[d, : int(cnt[2 * d]) * 32] = send[d, : int(cnt[2 * d]) * 32]
+            noise[d, cap * 32:] = send[d, cap * 32:]
+        rv, cv, moved = X.exchange_v(torch.from_numpy(noise.reshape(-1).copy()), torch.from_numpy(cnt), rb, cap, 32)
+        r2 = rv.numpy().reshape(world, rb)
+        got2 = np.concatenate([X.lookup_records(r2[s], int(cv[2 * s]), cap, tcap) for s in range(world)])
+        ok = ok and got2.tobytes() == want.tobytes() and torch.equal(cv, recv_count)
+        ok = ok and moved == sum(int(cnt[2 * d]) * 32 + (rb - cap * 32) for d in range(world) if d != rank)
         w = synth.config_c(N_FRAMES)
         full = RxPath(-1, max_ns=4096, max_clients=65536, max_frames=64)
         part = RxPath(-1, max_ns=4096, max_clients=65536, max_frames=64)

@@ -1,8 +1,11 @@
 """Namespace-partitioned exchange between GPUs.
 
 Frames shard by input offset across the ranks of a node.  Each rank fills one send region per
-Namespace owner and one equal-split all-to-all delivers them: rank r receives, from every
-source s, region s of its receive buffer and the counts of that region.  Two region kinds:
+Namespace owner; the counts travel first (an all-to-all of 1-2 words per region), then only the
+bytes that carry data (exchange_v_start: one grouped send / receive per peer and span, the
+all-to-all-v of SURVEY §8e); rank r receives, from every source s, region s of its receive
+buffer and the counts of that region.  exchange() / exchange_start() move whole regions (one
+equal-split all-to-all; the round-4 protocol, kept for comparison).  Two region kinds:
 
 - replicated tables: emurx_classify_route_dev packs the classified records whose Namespace
   was found, `cap` emurx_route_rec (40 B) per region, one count per region;
@@ -97,11 +100,78 @@ def exchange_start(send, send_count, rbytes: int, group=None):
 
 
 def exchange_finish(pending):
-    """(recv, recv_count) of an exchange_start(), the caller's stream ordered after it."""
-    works, recv, recv_count = pending
+    """(recv, recv_count) of an exchange_start() or exchange_v_start(), the caller's stream
+    ordered after it."""
+    works, recv, recv_count = pending[:3]
     for w in works or ():
         w.wait()
     return recv, recv_count
+
+
+# ---- payload-sized exchange (round 5): counts first, then only the bytes that carry data ----
+def payload_spans(count: int, cap: int, rec_bytes: int, rbytes: int):
+    """The byte spans of one region that carry data: its first min(count, cap) records and,
+    for lookup regions, the tail shards [cap * rec_bytes, rbytes) (their units are taken by
+    atomics, so which of them are used is known on the device only)."""
+    heads = min(int(count), cap) * rec_bytes
+    spans = [(0, heads)] if heads else []
+    if rbytes > cap * rec_bytes:
+        spans.append((cap * rec_bytes, rbytes))
+    return spans
+
+
+def _v_ops(send, recv, sc, rc, cs: int, rbytes: int, cap: int, rec_bytes: int, group):
+    """The P2P operations of one payload-sized exchange, the own region copied in place; the
+    bytes sent to other ranks."""
+    import torch.distributed as dist
+    world, me = dist.get_world_size(group), dist.get_rank(group)
+    ops, moved = [], 0
+    for p in range(world):
+        peer = dist.get_global_rank(group, p) if group is not None else p
+        out_spans = payload_spans(sc[p * cs], cap, rec_bytes, rbytes)
+        if p == me:
+            for a, b in out_spans:
+                recv[p * rbytes + a: p * rbytes + b].copy_(send[p * rbytes + a: p * rbytes + b])
+            continue
+        for a, b in out_spans:
+            ops.append(dist.P2POp(dist.isend, send[p * rbytes + a: p * rbytes + b], peer, group))
+            moved += b - a
+        for a, b in payload_spans(rc[p * cs], cap, rec_bytes, rbytes):
+            ops.append(dist.P2POp(dist.irecv, recv[p * rbytes + a: p * rbytes + b], peer, group))
+    return ops, moved
+
+
+def exchange_v_start(send, send_count, rbytes: int, cap: int, rec_bytes: int, group=None):
+    """The payload-sized exchange (all-to-all-v, counts then records): the
+    counts' all-to-all, the counts to the host (this waits for the caller's stream: the batch's
+    packing), then one grouped send / receive per peer and span that carries data (RCCL
+    groups them as its own all-to-all does), enqueued behind the caller's stream; the receive
+    buffer keeps the equal-split layout (region s at s * rbytes), its bytes outside the spans
+    undefined.  Returns the pending (works, recv, recv_count, moved) for exchange_finish();
+    `moved` = the bytes sent to other ranks.  gloo on device tensors (CPU rehearsals) runs on
+    host copies and completes here."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    _check(send, send_count, rbytes, world)
+    cs = send_count.numel() // world
+    if dist.get_backend(group) == "gloo" and send.is_cuda:
+        r, c, moved = exchange_v(send.cpu(), send_count.cpu(), rbytes, cap, rec_bytes, group)
+        return None, r.to(send.device), c.to(send.device), moved
+    recv = torch.empty_like(send)
+    recv_count = torch.empty_like(send_count)
+    dist.all_to_all_single(recv_count, send_count, group=group)
+    sc, rc = send_count.cpu().numpy(), recv_count.cpu().numpy()
+    ops, moved = _v_ops(send, recv, sc, rc, cs, rbytes, cap, rec_bytes, group)
+    works = dist.batch_isend_irecv(ops) if ops else []
+    return works, recv, recv_count, moved
+
+
+def exchange_v(send, send_count, rbytes: int, cap: int, rec_bytes: int, group=None):
+    """exchange_v_start() + exchange_finish(): (recv, recv_count, moved)."""
+    pending = exchange_v_start(send, send_count, rbytes, cap, rec_bytes, group)
+    recv, recv_count = exchange_finish(pending)
+    return recv, recv_count, pending[3]
 
 
 def received(recv: np.ndarray, recv_count: np.ndarray, cap: int) -> np.ndarray:
