@@ -128,10 +128,13 @@ __device__ __forceinline__ void tx_block_sync() {
     __syncthreads();
 }
 
-// Compose unit p of level k from the children's tables in S.t / S.b (cn of them): 8 blocks of 8
-// children walked by waves 0-7 (8 dependent LDS steps), the block prefixes by wave 0 (8 steps),
-// then the running rows by a gather.  Writes R/RB/T/B of (k, p); the root writes info too.
-__device__ void tx_compose_unit(const TxChain& c, uint32_t k, uint32_t p, uint32_t cn, TxChainLds& S) {
+// Compose unit p of level k from the children's tables in S.t / S.b (cn of them), in two parts:
+// tx_compose_table -- 8 blocks of 8 children walked by waves 0-7 (8 dependent LDS steps, the
+// running state kept in LDS), the block prefixes by wave 0 (8 steps): the unit's table T and
+// bytes B (write-through: the parent's composer reads them) and RB; tx_compose_rows -- the
+// running rows R by a gather (read by the write kernel only, so they are stored while the
+// unit's arrival is in flight), and the root's message count and total size.
+__device__ void tx_compose_table(const TxChain& c, uint32_t k, uint32_t p, uint32_t cn, TxChainLds& S) {
     const uint32_t wv = threadIdx.x / kWave, lane = lane_id();
     if (wv < kTxBlocks) {  // running state within the block, from every entry
         uint32_t x = lane, m = 0;
@@ -169,6 +172,9 @@ __device__ void tx_compose_unit(const TxChain& c, uint32_t k, uint32_t p, uint32
         if (lane == kWave - 1) __hip_atomic_store(&c.B[k][p], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     tx_block_sync();
+}
+__device__ void tx_compose_rows(const TxChain& c, uint32_t k, uint32_t p, uint32_t cn, TxChainLds& S) {
+    const uint32_t wv = threadIdx.x / kWave, lane = lane_id();
     if (wv < kTxBlocks) {  // R[ch][e] = the block's running state from the block's entry
         const uint32_t pe = S.u.up.p[wv][lane], x0 = pe & 63u, m0 = pe >> 6;
         uint32_t* R = c.R[k] + (size_t)p * 4096;
@@ -259,35 +265,46 @@ __global__ __launch_bounds__(kTxUnitWaves * kWave) void k_txz_chain(const emurx_
         if (lane == 0) S.b[ch] = tot;
     }
     tx_block_sync();
-    const uint32_t cn = min(c.ntiles - p * 64, 64u);
-    tx_compose_unit(c, 1, p, cn, S);
-    // ---- up the levels: the workgroup that completes a parent's last child composes it
+    uint32_t cn = min(c.ntiles - p * 64, 64u);
+    tx_compose_table(c, 1, p, cn, S);
+    // ---- up the levels: the workgroup that completes a parent's last child composes it; a
+    // unit's running rows are stored while its arrival's atomic is in flight
     uint32_t up = p;
+    for (uint32_t k = 1;; ++k) {
+        const bool top = k == c.L - 1;
 #if EMURX_TXC_NOUP
-    return;  // timing of the leaf + level-1 compose alone (wrong results past one level)
-#endif
-    for (uint32_t k = 2; k < c.L; ++k) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores of T / B
-        tx_block_sync();
-        const uint32_t par = up >> 6, kids = min(c.units[k - 1] - par * 64, 64u);
-        if (threadIdx.x == 0) {
-            const uint32_t old = __hip_atomic_fetch_add(&c.cnt[k][par], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            S.last = old == kids - 1;
-            if (S.last) tx_st_agent(&c.cnt[k][par], 0u);  // all arrived: ready for the next call
+        if (!top) {  // timing of the leaf + level-1 compose alone (wrong results past one level)
+            tx_compose_rows(c, k, up, cn, S);
+            return;
         }
-        tx_block_sync();
+#endif
+        const uint32_t par = up >> 6, kids = top ? 0u : min(c.units[k] - par * 64, 64u);
+        if (!top) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores of T / B
+            tx_block_sync();
+            if (threadIdx.x == 0) {
+                const uint32_t old =
+                    __hip_atomic_fetch_add(&c.cnt[k + 1][par], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                S.last = old == kids - 1;
+                if (S.last) tx_st_agent(&c.cnt[k + 1][par], 0u);  // all arrived: ready for the next call
+            }
+        }
+        tx_compose_rows(c, k, up, cn, S);
+        if (top) return;
+        tx_block_sync();      // S.last, and the rows are done with the LDS the parent's compose reuses
         if (!S.last) return;  // workgroup-uniform
         // the children's tables into LDS (sc1 vector loads: written in this launch, write-through)
         for (uint32_t r = wv; r < kids; r += kTxUnitWaves)
-            S.t[r][lane] = __hip_atomic_load(&c.T[k - 1][((size_t)par * 64 + r) * 64 + lane], __ATOMIC_RELAXED,
+            S.t[r][lane] = __hip_atomic_load(&c.T[k][((size_t)par * 64 + r) * 64 + lane], __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT);
         if (threadIdx.x < 64)
-            S.b[threadIdx.x] = threadIdx.x < kids ? __hip_atomic_load(&c.B[k - 1][(size_t)par * 64 + threadIdx.x],
+            S.b[threadIdx.x] = threadIdx.x < kids ? __hip_atomic_load(&c.B[k][(size_t)par * 64 + threadIdx.x],
                                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                                   : 0ull;
         tx_block_sync();
-        tx_compose_unit(c, k, par, kids, S);
         up = par;
+        cn = kids;
+        tx_compose_table(c, k + 1, up, cn, S);
     }
 }
 
