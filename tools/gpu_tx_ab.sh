@@ -16,7 +16,7 @@ done
 for rep in 1 2; do
   for v in default "$@"; do
     lib=$PWD/trex-emu_amd/lib/libemurx.so; [ $v != default ] && lib=$PWD/trex-emu_amd/lib/libemurx_$v.so
-    for c in B E; do
+    for c in ${TX_CONFIGS:-B E}; do
       EMURX_LIB=$lib timeout -k 10 300 python -u bench.py --config $c --steps 20 --warmup 5 --tx-path --no-exchange-run \
         --no-cpu-baseline --no-check > $out/tx_${c}_${v}_$rep.log 2>&1 || { tail -5 $out/tx_${c}_${v}_$rep.log; exit 1; }
       grep '^{' $out/tx_${c}_${v}_$rep.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print("'$c' '$v' '$rep'", json.dumps(d["tx_zmq"]))'

@@ -337,8 +337,11 @@ __device__ __forceinline__ void lds_or4(uint32_t* o32, uint32_t p, uint32_t v) {
 // blocks that hold the frame, funnel-shifted into the image's dwords -- so that twice as many
 // waves are resident as with the staged source; tiles whose output does not fit the image take
 // the long-frame path in the same launch, its arrays carved from the same LDS
-constexpr uint32_t kTxImg = 6144 + 32;  // output bytes per wave (headers + frames, 16-B rows)
-__global__ __launch_bounds__(256) void k_txz_emit(const uint8_t* __restrict__ frames, const emurx_desc* __restrict__ d,
+#ifndef EMURX_TXIMG  // output bytes per wave (headers + frames, 16-B rows)
+#define EMURX_TXIMG 6144
+#endif
+constexpr uint32_t kTxImg = EMURX_TXIMG;
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kTxImg <= 4608 ? 8 : 6))) void k_txz_emit(const uint8_t* __restrict__ frames, const emurx_desc* __restrict__ d,
                                                   uint32_t n, uint32_t ntiles, const TxChain c,
                                                   uint8_t* __restrict__ out, unsigned long long cap,
                                                   unsigned long long* __restrict__ msg_off) {
@@ -357,10 +360,6 @@ __global__ __launch_bounds__(256) void k_txz_emit(const uint8_t* __restrict__ fr
     unsigned long long tbb;
     tx_tile_base(c, t, te, tmb, tbb);
     const uint32_t len = dl.len;
-    const uint32_t tot = wave_reduce(len, [](uint32_t x, uint32_t y) { return x + y; });
-    // the output range is at most the frame bytes + 8 per frame (its header and, at most, a
-    // message header): within the image, the staged path
-    const bool fits = tot + 8 * lim + 32 <= kTxImg;  // wave-uniform
     const uint32_t er = tx_endrel_v(len, lnext, n, base, s_q[wv]);
     uint64_t starts = 0;  // the chain's starts inside this tile: a scalar walk from the tile's entry
     for (uint32_t s = (uint32_t)__builtin_amdgcn_readfirstlane((int)te); s < lim;
@@ -381,9 +380,10 @@ __global__ __launch_bounds__(256) void k_txz_emit(const uint8_t* __restrict__ fr
          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)fo, (int)last)) + 4 +
         (uint32_t)__builtin_amdgcn_readlane((int)len, (int)last);
     uint32_t* o32 = s_img[wv];
-    if (fits) {
-        const unsigned long long obase = o0 & ~15ull;
-        const uint32_t nrow = (uint32_t)(((o1 + 15) & ~15ull) - obase) >> 4;
+    const unsigned long long obase = o0 & ~15ull;
+    const uint32_t nrow = (uint32_t)(((o1 + 15) & ~15ull) - obase) >> 4;
+    if (nrow * 16 <= kTxImg) {  // wave-uniform: the tile's output rows fit the image
+
         for (uint32_t r = lane; r < nrow; r += kWave) reinterpret_cast<uint4*>(o32)[r] = make_uint4(0, 0, 0, 0);
         tx_wave_sync();
         if (valid) {
@@ -462,7 +462,7 @@ __global__ __launch_bounds__(256) void k_txz_emit(const uint8_t* __restrict__ fr
         sg[5][lane] = st ? ((uint32_t)EMURX_ZMQ_MAGIC << 16) + er : 0u;
     }
     tx_wave_sync();
-    const uint32_t head = (uint32_t)(o0 & 15), nrow = (head + R + 15) >> 4;
+    const uint32_t head = (uint32_t)(o0 & 15);  // nrow (above) = (head + R + 15) / 16
     const unsigned long long xb = o0 - head;  // 16-byte aligned (d_out is)
     auto row_byte = [&](uint32_t r, uint32_t j, uint32_t kk) {
         const int y = (int)(16 * r + j) - (int)head;
