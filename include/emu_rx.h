@@ -575,6 +575,11 @@ const char* emurx_build_id(void);
    at emurx_open forces one.  Results never depend on it.  No ABI replacement: a tuning
    observable of this implementation. */
 uint32_t emurx_last_stage(const emurx_t* h);
+/* LDS image (bytes per wave) of the most recent tx framing write (emurx_tx_zmq_dev): 6144,
+   4608 or 0 (every tile on the rows-over-lanes path); -1 before the first.  Chosen per call from
+   the tile sizes an earlier call's chain kernel saw; EMURX_TXZ=wide|narrow|long at emurx_open
+   forces one.  Results never depend on it.  A tuning observable, no ABI replacement. */
+int32_t emurx_last_txz(const emurx_t* h);
 
 /* HBM copy ceiling of this GPU for the roofline context (bench.py): a streaming 16-byte copy
    of `bytes` (a multiple of 16, 16-byte aligned device pointers) on `stream`, one launch.

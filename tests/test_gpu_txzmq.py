@@ -121,6 +121,44 @@ def test_tx_zmq_under_load(rx):
         assert out.cpu().numpy()[:total].tobytes() == want.tobytes(), k
 
 
+@pytest.mark.parametrize("img", ["wide", "narrow", "long"])
+def test_tx_zmq_write_variants(img, monkeypatch, oracle_built):
+    """Every write image (EMURX_TXZ forces it at emurx_open) writes every tile bit-exactly:
+    tiles that do not fit the image take the rows-over-lanes path in the same launch."""
+    from emurx.rx import RxPath
+    monkeypatch.setenv("EMURX_TXZ", img)
+    rx2 = RxPath(0, max_ns=16, max_clients=16, max_frames=1 << 10)
+    try:
+        for n, kind in ((64 * 64 * 3 + 5, 3), (5000, 0), (3000, 1), (2000, 2), (130, 0)):
+            check(rx2, *U.batch(n, kind, seed=31 + n))
+            assert rx2.last_txz() == {"wide": 6144, "narrow": 4608, "long": 0}[img]
+    finally:
+        rx2.close()
+
+
+def test_tx_zmq_write_choice(oracle_built):
+    """The write image follows the tile sizes earlier calls saw (a copy-back behind a call every
+    8th call or less often, read once it has landed): 64-byte frames -> the 4.5 KiB image,
+    frames of 0..200 bytes -> 6 KiB, IMIX-sized frames -> no image, each reached within 20
+    calls of the traffic changing; results bit-exact throughout."""
+    import torch
+    from emurx.rx import RxPath
+    rx2 = RxPath(0, max_ns=16, max_clients=16, max_frames=1 << 10)
+    try:
+        for (n, kind), want in (((64 * 64 * 4, 3), 4608), ((64 * 64 * 4, 0), 6144), ((3000, 1), 0)):
+            buf, d = U.batch(n, kind, seed=41 + kind)
+            seen = []
+            for _ in range(20):  # a sample every 8th call or less often; the call after it decides
+                check(rx2, buf, d)
+                torch.cuda.synchronize()
+                seen.append(rx2.last_txz())
+                if seen[-1] == want:
+                    break
+            assert seen[-1] == want, (n, kind, seen)
+    finally:
+        rx2.close()
+
+
 def test_tx_zmq_capacity(rx):
     buf, d = U.batch(2000, 2, seed=4)
     need = 8 * len(d) + int(d["len"].astype(np.int64).sum())

@@ -170,6 +170,18 @@ struct emurx_ctx {
 
     // tx ZMQ framing scratch (emurx_tx_zmq_dev): per-level chain transfer tables
     DevBuf<uint8_t> d_txz;
+    // the tx write kernel's image per call (EMURX_TXZ_*), from the bounds of the tiles' output
+    // rows an earlier call's chain kernel folded into two scratch words: copied back behind that
+    // call (an event, no synchronisation) as the staging slab's feedback is, the first call and
+    // then at most every txz_every-th (8, doubled when a decision repeats, up to 256).  Every
+    // image writes every tile correctly; the choice is speed only.  EMURX_TXZ=wide|narrow|long
+    // forces one.
+    PinBuf<uint32_t> txz_fb;
+    hipEvent_t txz_ev = nullptr;
+    bool txz_pending = false;
+    int txz_variant = EMURX_TXZ_WIDE, txz_mode = -1;
+    uint32_t txz_calls = 0, txz_last_copy = 0, txz_every = 8, txz_same = 0;
+    int last_txz = -1;
 
     // Namespace-partition packing scratch (emurx_route_dev / emurx_classify_route_dev /
     // emurx_parse_route_dev): one set per stream, so routes of batches pipelined over several
@@ -777,6 +789,9 @@ int emurx_open(const emurx_cfg* cfg, emurx_t** out) {
     if (!EMURX_HIP_OK(hipStreamCreate(&h->stream))) { delete h; return EMURX_EDEVICE; }
     if (const char* e = getenv("EMURX_STAGE")) h->stage_mode = !strcmp(e, "wide") ? 1 : !strcmp(e, "narrow") ? 2 : 0;
     if (const char* e = getenv("EMURX_INGEST_SMALL")) h->ingest_small = strcmp(e, "0") != 0;
+    if (const char* e = getenv("EMURX_TXZ"))
+        h->txz_mode = !strcmp(e, "wide") ? EMURX_TXZ_WIDE : !strcmp(e, "narrow") ? EMURX_TXZ_NARROW
+                    : !strcmp(e, "long") ? EMURX_TXZ_LONG : -1;
     if (const char* e = getenv("EMURX_INGEST_SPIN")) h->ingest_spin = strcmp(e, "0") != 0;
     if (h->stage_fb.alloc(256) || h->d_stage_fb.alloc(256) ||
         !EMURX_HIP_OK(hipEventCreateWithFlags(&h->stage_ev, hipEventDisableTiming)) ||
@@ -822,6 +837,8 @@ void emurx_close(emurx_t* h) {
     h->d_nsinfo.release();
     for (auto& r : h->route) r.release();
     h->d_txz.release();
+    h->txz_fb.release();
+    if (h->txz_ev) (void)hipEventDestroy(h->txz_ev);
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
     h->ev.clear();
@@ -1230,6 +1247,10 @@ int emurx_set_timing(emurx_t* h, uint32_t slots, uint32_t stride) {
 }
 
 uint32_t emurx_last_stage(const emurx_t* h) { return h ? h->last_stage : 0; }
+int32_t emurx_last_txz(const emurx_t* h) {
+    if (!h || h->last_txz < 0) return -1;
+    return h->last_txz == EMURX_TXZ_NARROW ? 4608 : h->last_txz == EMURX_TXZ_LONG ? 0 : 6144;
+}
 
 int emurx_kernel_times(emurx_t* h, float* batch_ms, uint32_t cap, uint32_t* n_out) {
     if (!h || !n_out || (cap && !batch_ms)) return EMURX_EINVAL;
@@ -1273,12 +1294,45 @@ int emurx_tx_zmq_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc* d_de
     if (need > h->d_txz.n) {  // grows on demand; a launch in flight may still read the old one
         (void)hipStreamSynchronize(st);
         if (h->d_txz.alloc(need)) return EMURX_ENOMEM;
-        // the chain's arrival counters start at zero (each call's last arrival resets its own)
+        // the chain's arrival counters (and the feedback words) start at zero (each call's last
+        // arrival resets its own counter)
         if (!EMURX_HIP_OK(hipMemset(h->d_txz.p, 0, need))) return EMURX_EDEVICE;
+        h->txz_pending = false;
     }
-    return emurx_launch_tx_zmq(d_frames, d_desc, n, d_out, out_cap, d_msg_off, d_info, h->d_txz.p, st)
-               ? EMURX_EDEVICE
-               : EMURX_OK;
+    if (!h->txz_ev && (h->txz_fb.alloc(2) || !EMURX_HIP_OK(hipEventCreateWithFlags(&h->txz_ev, hipEventDisableTiming))))
+        return EMURX_ENOMEM;
+    if (h->txz_pending && hipEventQuery(h->txz_ev) == hipSuccess) {  // "not ready" is no error
+        h->txz_pending = false;
+        // hi: the largest upper bound of a sampled tile's output rows; lo: the smallest lower
+        // bound (0 words: nothing sampled, the choice stands)
+        const uint32_t hi = h->txz_fb.p[0], lo = ~h->txz_fb.p[1];
+        const int v = !hi                                ? h->txz_variant
+                      : hi <= emurx_txz_img_narrow_rows ? EMURX_TXZ_NARROW
+                      : lo > emurx_txz_img_wide_rows    ? EMURX_TXZ_LONG
+                                                        : EMURX_TXZ_WIDE;
+        if (v != h->txz_variant) {
+            h->txz_same = 0;
+            h->txz_every = 8;
+        } else if (++h->txz_same >= 2 && h->txz_every < 256) {
+            h->txz_every *= 2;
+        }
+        h->txz_variant = v;
+    }
+    const bool fb = h->txz_mode < 0 && n && !h->txz_pending && (!h->txz_calls || h->txz_calls - h->txz_last_copy >= h->txz_every);
+    ++h->txz_calls;
+    const int variant = h->txz_mode >= 0 ? h->txz_mode : h->txz_variant;
+    if (emurx_launch_tx_zmq(d_frames, d_desc, n, d_out, out_cap, d_msg_off, d_info, h->d_txz.p, st, variant, fb))
+        return EMURX_EDEVICE;
+    h->last_txz = variant;
+    if (fb) {  // the two words behind this call, then cleared for the next sample
+        if (!EMURX_HIP_OK(hipMemcpyAsync(h->txz_fb.p, h->d_txz.p, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st)) ||
+            !EMURX_HIP_OK(hipMemsetAsync(h->d_txz.p, 0, 2 * sizeof(uint32_t), st)) ||
+            !EMURX_HIP_OK(hipEventRecord(h->txz_ev, st)))
+            return EMURX_EDEVICE;
+        h->txz_pending = true;
+        h->txz_last_copy = h->txz_calls;
+    }
+    return EMURX_OK;
 }
 
 uint32_t emurx_ns_owner(const uint8_t key[12], uint32_t n_parts) {

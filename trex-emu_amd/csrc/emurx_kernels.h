@@ -134,5 +134,12 @@ int emurx_launch_tx_csum(uint8_t* frames, const emurx_tx_desc* desc, uint32_t n,
 
 // Tx ZMQ framing (emurx_txzmq.hip): see emurx_tx_zmq_dev.  scratch: emurx_txz_scratch_bytes(n).
 size_t emurx_txz_scratch_bytes(uint32_t n);
+// variant: the write kernel's image (EMURX_TXZ_*, emurx_tx_zmq_dev's feedback choice); feedback:
+// the chain kernel also folds the bounds of its tiles' output rows into scratch words 0 (largest
+// upper bound, atomicMax) and 1 (~ the smallest lower bound), which the caller copies back and
+// clears (emurx_txz_feedback_words)
+enum { EMURX_TXZ_WIDE = 0, EMURX_TXZ_NARROW = 1, EMURX_TXZ_LONG = 2 };
+constexpr uint32_t emurx_txz_img_narrow_rows = 4608 / 16, emurx_txz_img_wide_rows = 6144 / 16;
 int emurx_launch_tx_zmq(const uint8_t* frames, const emurx_desc* desc, uint32_t n, uint8_t* out, uint64_t cap,
-                        uint64_t* msg_off, uint64_t* info, void* scratch, hipStream_t st);
+                        uint64_t* msg_off, uint64_t* info, void* scratch, hipStream_t st, int variant = EMURX_TXZ_WIDE,
+                        bool feedback = false);

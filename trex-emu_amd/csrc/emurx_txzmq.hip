@@ -94,6 +94,7 @@ struct TxChain {
     unsigned long long* RB[kTxMaxLevels];    // k >= 1: [units][64]
     uint32_t* cnt[kTxMaxLevels];             // k >= 2: [units] children finished (reset by the last)
     unsigned long long *msg_off, *info;
+    uint32_t* fb;  // non-null: the largest bound of a tile's output rows and ~ the smallest, atomicMax
 };
 struct TxChainLds {
     uint32_t t[64][64];         // the children's tables
@@ -109,6 +110,7 @@ struct TxChainLds {
             uint32_t p[kTxBlocks + 1][64];
         } up;
     } u;
+    uint32_t fbw[kTxUnitWaves][2];  // the size feedback's per-wave bounds
     uint32_t last;
 };
 __device__ __forceinline__ void tx_wave_sync() {
@@ -264,7 +266,32 @@ __global__ __launch_bounds__(kTxUnitWaves * kWave) void k_txz_chain(const emurx_
         const uint32_t tot = q[j * kWave + kWave - 1] - (j ? q[j * kWave - 1] : 0u);
         if (lane == 0) S.b[ch] = tot;
     }
+    if (c.fb) {  // the write's variant feedback (emurx_launch_tx_zmq): bounds of the tiles' output rows
+        uint32_t hi = 0, lo = 0xffffffffu;
+#pragma unroll
+        for (uint32_t j = 0; j < kTxTilesPerWave; ++j) {
+            const uint32_t tot = q[j * kWave + kWave - 1] - (j ? q[j * kWave - 1] : 0u);
+            const uint32_t mm = wave_max_u32(m[j]);  // messages started inside, the most over the entries
+            if (lim[j]) {
+                hi = max(hi, (tot + 4 * lim[j] + 4 * mm + 30) / 16 + 1);
+                lo = min(lo, (tot + 4 * lim[j]) / 16);
+            }
+        }
+        if (lane == 0) {
+            S.fbw[wv][0] = hi;
+            S.fbw[wv][1] = lo;
+        }
+    }
     tx_block_sync();
+    if (c.fb && threadIdx.x == 0) {
+        uint32_t hi = 0, lo = 0xffffffffu;
+        for (uint32_t w = 0; w < kTxUnitWaves; ++w) {
+            hi = max(hi, S.fbw[w][0]);
+            lo = min(lo, S.fbw[w][1]);
+        }
+        atomicMax(&c.fb[0], hi);
+        atomicMax(&c.fb[1], ~lo);  // the smallest lower bound, as the largest complement
+    }
     uint32_t cn = min(c.ntiles - p * 64, 64u);
     tx_compose_table(c, 1, p, cn, S);
     // ---- up the levels: the workgroup that completes a parent's last child composes it; a
@@ -337,15 +364,18 @@ __device__ __forceinline__ void lds_or4(uint32_t* o32, uint32_t p, uint32_t v) {
 // blocks that hold the frame, funnel-shifted into the image's dwords -- so that twice as many
 // waves are resident as with the staged source; tiles whose output does not fit the image take
 // the long-frame path in the same launch, its arrays carved from the same LDS
-#ifndef EMURX_TXIMG  // output bytes per wave (headers + frames, 16-B rows)
-#define EMURX_TXIMG 6144
-#endif
-constexpr uint32_t kTxImg = EMURX_TXIMG;
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kTxImg <= 4608 ? 8 : 6))) void k_txz_emit(const uint8_t* __restrict__ frames, const emurx_desc* __restrict__ d,
+// kTxImg: output bytes per wave (headers + frames, 16-B rows) of the image path, chosen per launch
+// from the tile sizes earlier calls saw (emurx_launch_tx_zmq): 6 KiB (6 waves per SIMD), 4.5 KiB
+// (8), or none (every tile takes the long path; its arrays alone, 8 waves).  Every variant
+// writes every tile correctly: a tile that does not fit the image takes the long path.
+constexpr uint32_t kTxImgWide = 6144, kTxImgNarrow = 4608, kTxLongLds = 6 * kWave * 4 + 512 * 4;
+template <uint32_t kTxImg>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kTxImg == kTxImgWide ? 6 : 8))) void k_txz_emit(const uint8_t* __restrict__ frames, const emurx_desc* __restrict__ d,
                                                   uint32_t n, uint32_t ntiles, const TxChain c,
                                                   uint8_t* __restrict__ out, unsigned long long cap,
                                                   unsigned long long* __restrict__ msg_off) {
-    __shared__ __attribute__((aligned(16))) uint32_t s_img[4][kTxImg / 4];
+    constexpr uint32_t kLds = kTxImg > kTxLongLds ? kTxImg : kTxLongLds;
+    __shared__ __attribute__((aligned(16))) uint32_t s_img[4][kLds / 4];
     __shared__ uint32_t s_q[4][2 * kWave];
     const uint32_t wv = threadIdx.x / kWave, lane = lane_id();
     const uint32_t t = blockIdx.x * 4 + wv;
@@ -382,7 +412,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kTxImg <= 4
     uint32_t* o32 = s_img[wv];
     const unsigned long long obase = o0 & ~15ull;
     const uint32_t nrow = (uint32_t)(((o1 + 15) & ~15ull) - obase) >> 4;
-    if (nrow * 16 <= kTxImg) {  // wave-uniform: the tile's output rows fit the image
+    if (kTxImg && nrow * 16 <= kTxImg) {  // wave-uniform: the tile's output rows fit the image
 
         for (uint32_t r = lane; r < nrow; r += kWave) reinterpret_cast<uint4*>(o32)[r] = make_uint4(0, 0, 0, 0);
         tx_wave_sync();
@@ -450,7 +480,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kTxImg <= 4
     // The segment table and the slow-row list live in this wave's image space
     uint32_t(*sg)[kWave] = reinterpret_cast<uint32_t(*)[kWave]>(o32);  // [6][64]
     uint32_t* slow = o32 + 6 * kWave;                                   // [kTxSlow]
-    static_assert(6 * kWave * 4 + kTxSlow * 4 <= kTxImg, "long path's arrays in the image space");
+    static_assert(6 * kWave * 4 + kTxSlow * 4 <= kLds, "long path's arrays in the image space");
     const uint32_t R = (uint32_t)(o1 - o0);  // output bytes of the tile
     if (valid) {
         const uint32_t fr = (uint32_t)(fo - o0);  // the frame header, relative to o0
@@ -560,7 +590,7 @@ size_t emurx_txz_scratch_bytes(uint32_t n) {
 }
 
 int emurx_launch_tx_zmq(const uint8_t* frames, const emurx_desc* desc, uint32_t n, uint8_t* out, uint64_t cap,
-                        uint64_t* msg_off, uint64_t* info, void* scratch, hipStream_t st) {
+                        uint64_t* msg_off, uint64_t* info, void* scratch, hipStream_t st, int variant, bool feedback) {
     using namespace emurx;
     unsigned long long* mo = reinterpret_cast<unsigned long long*>(msg_off);
     unsigned long long* inf = reinterpret_cast<unsigned long long*>(info);
@@ -573,6 +603,7 @@ int emurx_launch_tx_zmq(const uint8_t* frames, const emurx_desc* desc, uint32_t 
     c.units[0] = c.ntiles;
     c.msg_off = mo;
     c.info = inf;
+    c.fb = feedback ? static_cast<uint32_t*>(scratch) : nullptr;  // level 0's counter words (unused)
     uint8_t* p = static_cast<uint8_t*>(scratch) + kTxCntBytes;
     uint32_t L = 1;
     for (uint32_t u = (c.ntiles + 63) / 64;; u = (u + 63) / 64) {
@@ -593,7 +624,9 @@ int emurx_launch_tx_zmq(const uint8_t* frames, const emurx_desc* desc, uint32_t 
     const uint32_t nt = c.ntiles;
     hipError_t e = emurx_launch(k_txz_chain, dim3(c.units[1]), dim3(kTxUnitWaves * kWave), 0, st, desc, c);
     if (e == hipSuccess)
-        e = emurx_launch(k_txz_emit, dim3((nt + 3) / 4), dim3(256), 0, st, frames, desc, n, nt, c, out,
-                         (unsigned long long)cap, mo);
+        e = emurx_launch(variant == EMURX_TXZ_NARROW ? k_txz_emit<kTxImgNarrow>
+                         : variant == EMURX_TXZ_LONG ? k_txz_emit<0>
+                                                     : k_txz_emit<kTxImgWide>,
+                         dim3((nt + 3) / 4), dim3(256), 0, st, frames, desc, n, nt, c, out, (unsigned long long)cap, mo);
     return EMURX_HIP_OK(e) ? 0 : -1;
 }

@@ -192,6 +192,7 @@ SIGNATURES = [
     ("emurx_set_timing", C.c_int, [_P, C.c_uint32, C.c_uint32]),
     ("emurx_kernel_times", C.c_int, [_P, _P, C.c_uint32, C.POINTER(C.c_uint32)]),
     ("emurx_last_stage", C.c_uint32, [_P]),
+    ("emurx_last_txz", C.c_int32, [_P]),
     ("emurx_copy_ceiling_dev", C.c_int, [_P, _P, C.c_size_t, _P]),
     ("emurx_ns_owner", C.c_uint32, [_U8P, C.c_uint32]),
     ("emurx_owner_key", C.c_uint8, [_U8P]),

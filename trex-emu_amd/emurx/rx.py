@@ -195,6 +195,9 @@ class RxPath:
         """LDS staging bytes per wave of the most recent k_rx launch (7168 or 6144)."""
         return int(self.lib.emurx_last_stage(self.h))
 
+    def last_txz(self) -> int:
+        """LDS image bytes per wave of the last tx framing write (6144, 4608, 0; -1 before)."""
+        return int(self.lib.emurx_last_txz(self.h))
 
     # ---- batched host ingest (many ZMQ messages per GPU round trip) -------------------------
     def ingest_buffer(self, slot: int, nbytes: int) -> np.ndarray:
