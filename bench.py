@@ -990,6 +990,26 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             "source": f"the timed region: a HIP event pair on each of the {S} streams (no cross-stream waits), "
                       "earliest start to latest end / launches = the launch interval in steady state (each launch "
                       "overlaps its neighbours)"}
+    if mode == "none" and cfg == "D" and world == 1 and pmc.exists():
+        # D classification (k_rx probing 1.75 GB of sparse tables) against the random-line bound,
+        # as the owner's k_lookup: the excess FETCH of the calibrated PMC is probe lines
+        # (pmc_summary.py's rule for this config), per launch, at the measured random-line rate of an
+        # HBM-sized table, plus the algorithmic bytes at the copy ceiling (additive)
+        try:
+            pj = json.loads(pmc.read_text())
+            lines = pj["excess_fetch_bytes"] / 64 * n / (1 << 21)
+            rate = 48.8e9  # profiles/r05/probe_rate/rates.txt, 512 MB table
+            floor_ms = (lines / rate + alg_bytes / (copy_gbs * 1e9)) * 1e3
+            look = parse_s * 1e3
+            out["roofline"]["random_line"] = {
+                "kernel": "k_rx (parse + classify, full tables)", "probe_lines_per_launch": int(lines),
+                "line_rate_glines_per_s": rate / 1e9, "stream_bytes_per_launch": int(alg_bytes),
+                "floor_ms": round(floor_ms, 5), "measured_ms": round(look, 5), "frac": round(floor_ms / look, 4),
+                "source": f"{pmc.relative_to(ROOT)} (excess FETCH as 64-byte probe lines), "
+                          "profiles/r05/probe_rate/rates.txt (line rate), this run's copy ceiling and kernel_ms_mean "
+                          "(one launch); frac >= 1 where probe lines hit the Infinity Cache"}
+        except Exception as e:  # noqa: BLE001
+            out["roofline"]["random_line"] = {"error": repr(e)[:200]}
     if replay is not None:
         out["roofline"]["cache_resident_replay"] = {
             "interval_ms": round(replay, 5), "value": round(n / (replay * 1e-3) / 1e6, 2),
