@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 out=gpurun_out/txab; mkdir -p $out
 for v in default "$@"; do
-  case $v in noup*) continue ;; esac  # timing-only builds (wrong results by design)
+  case $v in noup*) continue ;; esac  # timing-only builds (wrong results by design): noup*
   lib=$PWD/trex-emu_amd/lib/libemurx.so; [ $v != default ] && lib=$PWD/trex-emu_amd/lib/libemurx_$v.so
   EMURX_LIB=$lib timeout -k 10 400 python -u -m pytest tests/test_gpu_txzmq.py -m gpu -x -q -p no:cacheprovider \
     --timeout 200 --timeout-method thread > $out/pytest_$v.log 2>&1

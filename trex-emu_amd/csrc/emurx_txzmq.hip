@@ -564,7 +564,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kTxImg == k
         }
     }
     tx_wave_sync();
+#ifdef EMURX_TX_NOPASS2  // timing only: the long path without its byte-by-byte rows (wrong output)
+    const uint32_t nb = 0;
+#else
     const uint32_t nb = min(nslow, kTxSlow) * 16;
+#endif
     for (uint32_t i = lane; i < nb; i += kWave) {
         const uint32_t e = slow[i >> 4];
         row_byte(e >> 6, i & 15, e & 63);
