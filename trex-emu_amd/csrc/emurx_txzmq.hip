@@ -510,7 +510,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kTxImg == k
         out[x] = (uint8_t)v;
     };
     uint32_t nslow = 0, k = 0;
-    constexpr uint32_t kU = 4;  // rows per lane per round, their loads in flight together
+#ifndef EMURX_TX_KU
+#define EMURX_TX_KU 4
+#endif
+    constexpr uint32_t kU = EMURX_TX_KU;  // rows per lane per round, their loads in flight together
     for (uint32_t r0 = 0; r0 < nrow; r0 += kU * kWave) {  // wave-uniform trip count
         uint4 cur[kU], nxt[kU];
         uint32_t sh[kU], kk[kU];
