@@ -524,9 +524,17 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
                     b["pending"] = X.exchange_start(b["send"], b["send_count"], xch["region"])
 
         def x_sync(send, send_count):
-            """(recv, recv_count, bytes sent to other ranks) of one blocking transfer"""
+            """(recv, recv_count, bytes sent to other ranks) of one blocking transfer.  The first
+            runs in the warmup: should the grouped sends / receives fail on this backend, every
+            rank falls back to whole regions before the timed steps, and the line says so"""
             if a.a2a == "v":
-                return X.exchange_v(send, send_count, xch["region"], xch["cap"], rb)
+                try:
+                    return X.exchange_v(send, send_count, xch["region"], xch["cap"], rb)
+                except Exception as e:  # noqa: BLE001 - keep the exchange measured (a backend without
+                    # point-to-point support fails the same call on every rank)
+                    xch["a2a_fallback"] = repr(e)[:300]
+                    progress(rank, f"payload-sized transfer failed ({repr(e)[:120]}): whole regions from here on")
+                    a.a2a = "equal"
             r, c = X.exchange(send, send_count, xch["region"])
             return r, c, (world - 1) * xch["region"]
 
@@ -1028,6 +1036,7 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             "record_bytes": xch["rb"],
             "tail_units_per_shard": xch["tcap"],
             "region_bytes": xch["region"],
+            "a2a_fallback": xch.get("a2a_fallback"),
             "collective": ((f"all_to_all_single of the counts + batch_isend_irecv of the spans that carry data "
                             f"({a.backend})") if a.a2a == "v" else f"all_to_all_single x2 ({a.backend})")
                            if world > 1 else "none (1 rank)",
