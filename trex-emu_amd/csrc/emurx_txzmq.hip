@@ -525,7 +525,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kTxImg == k
             kk[u] = k;
             cur[u] = nxt[u] = make_uint4(0, 0, 0, 0);
             sh[u] = 0;
+#ifdef EMURX_TX_PURECOPY  // timing only: every row a copy from the frames buffer's first 256 MiB
+            if (r < nrow && xb + 16ull * r + 16 <= cap) {
+                const uintptr_t sa = (uintptr_t)(frames + (((uint32_t)xb + 16 * r) & 0x0ffffff0u) + 5);
+                const uint4* sv = reinterpret_cast<const uint4*>(sa & ~(uintptr_t)15);
+                sh[u] = 5;
+                cur[u] = sv[0];
+                nxt[u] = sv[1];
+                fast[u] = true;
+            }
+            if (false) {
+#else
             if (r < nrow) {
+#endif
                 const int y0 = (int)(16 * r) - (int)head;
                 const uint32_t yc = y0 < 0 ? 0u : (uint32_t)y0;
                 while (k < last && sg[0][k + 1] <= yc) ++k;
