@@ -527,11 +527,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kTxImg == k
             sh[u] = 0;
 #ifdef EMURX_TX_PURECOPY  // timing only: every row a copy from the frames buffer's first 256 MiB
             if (r < nrow && xb + 16ull * r + 16 <= cap) {
-                const uintptr_t sa = (uintptr_t)(frames + (((uint32_t)xb + 16 * r) & 0x0ffffff0u) + 5);
+#ifndef EMURX_TX_PC_OFF
+#define EMURX_TX_PC_OFF 5
+#endif
+                const uintptr_t sa = (uintptr_t)(frames + (((uint32_t)xb + 16 * r) & 0x0ffffff0u) + EMURX_TX_PC_OFF);
                 const uint4* sv = reinterpret_cast<const uint4*>(sa & ~(uintptr_t)15);
-                sh[u] = 5;
+                sh[u] = EMURX_TX_PC_OFF;
                 cur[u] = sv[0];
-                nxt[u] = sv[1];
+                if (EMURX_TX_PC_OFF) nxt[u] = sv[1];
                 fast[u] = true;
             }
             if (false) {
