@@ -13,7 +13,9 @@ and the interval (last end - first start) / launches, which is what the bench's 
 around a group measures.  With --batches <= --streams there is no replay group: pass
 `--no-replay` as the third argument.  `--kernel <text>` keeps only the k_rx dispatches whose name
 holds <text> (the default command also runs config D's exchange after the headline: pass
-`--kernel "k_rx<1, 6144u>"` for config B's narrow-slab launches).
+`--kernel "k_rx<1, 6144u>"` for config B's narrow-slab launches).  `--trim-isolated` drops the
+trailing isolated launches of the default line's host_inclusive block (ingest batches, each on its
+own after its copies).
 """
 import csv
 import json
@@ -27,7 +29,7 @@ def col(row, *names):
     raise KeyError(names)
 
 
-def main(path, steps, replay=True, old_order=False, one=None, kernel="k_rx"):
+def main(path, steps, replay=True, old_order=False, one=None, kernel="k_rx", trim=False):
     one = max(steps, 100) if one is None else one  # bench.py times one launch alone over max(--steps, 100)
     ks = []
     for row in csv.DictReader(open(path)):
@@ -38,6 +40,12 @@ def main(path, steps, replay=True, old_order=False, one=None, kernel="k_rx"):
                    int(col(row, "End_Timestamp", "End-Timestamp", "EndNs"))))
     ks.sort()
     out = {"k_rx_dispatches": len(ks), "steps": steps}
+    if trim:  # the default command's host_inclusive block runs after the headline: its batches'
+        # k_rx launches each start > 30 us after the previous one ended; drop them from the end
+        n0 = len(ks)
+        while len(ks) > 1 and ks[-1][0] - ks[-2][1] > 30000:
+            ks.pop()
+        out["trimmed_isolated_dispatches"] = n0 - len(ks)
     if old_order:
         g = [ks[len(ks) - (i + 1) * steps:len(ks) - i * steps] for i in range(3)]  # last, second to last, ...
         groups = [("timed_region", g[0])]
@@ -64,4 +72,4 @@ if __name__ == "__main__":
     one = int(rest[rest.index("--one") + 1]) if "--one" in rest else None  # traces before max(steps, 100): --one <steps>
     kernel = rest[rest.index("--kernel") + 1] if "--kernel" in rest else "k_rx"
     main(sys.argv[1], int(sys.argv[2]), replay="--no-replay" not in rest, old_order="--old-order" in rest, one=one,
-         kernel=kernel)
+         kernel=kernel, trim="--trim-isolated" in rest)
