@@ -513,7 +513,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kTxImg == k
         out[x] = (uint8_t)byte_at((uint32_t)y, kk);
     };
     uint32_t nslow = 0, k = 0;
-#if defined(EMURX_TX_P2ROUND) || defined(EMURX_TX_P2ROW)
+#ifndef EMURX_TX_P2ROUND  // 0: the slow rows after the tile's last round (rounds 1-4)
+#define EMURX_TX_P2ROUND 1
+#endif
+#if EMURX_TX_P2ROUND
     uint32_t p2done = 0;
 #endif
 #ifndef EMURX_TX_KU
@@ -565,11 +568,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kTxImg == k
 #pragma unroll
         for (uint32_t u = 0; u < kU; ++u) {
             const uint32_t r = r0 + u * kWave + lane;
-#ifdef EMURX_TX_PC_HOLES  // timing only: the pure copy leaves every 16th row unwritten
-            if (fast[u] && (r & 15) != 7) {
-#else
             if (fast[u]) {
-#endif
                 const uint32_t q = sh[u] >> 2, b = sh[u] & 3;
                 const uint32_t w[8] = {cur[u].x, cur[u].y, cur[u].z, cur[u].w, nxt[u].x, nxt[u].y, nxt[u].z, nxt[u].w};
                 uint32_t o[4];
@@ -590,100 +589,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kTxImg == k
             }
             nslow += (uint32_t)__popcll(m);
         }
-#ifdef EMURX_TX_P2LDS
-        // this round's byte-by-byte rows now, assembled in LDS and stored as whole 16-byte rows
-        // (a row written in pieces, or late, leaves partly written lines: every such line costs
-        // HBM a read-modify-write); the list holds this round's rows only (<= kU * 64)
-        tx_wave_sync();
-        {
-            static_assert(kU * kWave <= 256 && 256 * 4 + 64 * 16 <= kTxSlow * 4, "round list + row buffers");
-            uint8_t* rb = reinterpret_cast<uint8_t*>(slow + 256);
-            auto whole = [&](uint32_t r) {
-                return 16 * r >= head && 16 * r + 16 - head <= R && xb + 16ull * r + 16 <= cap;
-            };
-            for (uint32_t i = lane; i < nslow * 16; i += kWave) {
-                const uint32_t e = slow[i >> 4], r = e >> 6, j = i & 15;
-                if ((i >> 4) < 64 && whole(r)) rb[i] = (uint8_t)byte_at(16 * r + j - head, e & 63);
-                else row_byte(r, j, e & 63);
-            }
-            tx_wave_sync();
-            for (uint32_t q = lane; q < min(nslow, 64u); q += kWave) {
-                const uint32_t r = slow[q] >> 6;
-                if (whole(r))
-                    *reinterpret_cast<uint4*>(out + xb + 16ull * r) = reinterpret_cast<const uint4*>(rb)[q];
-            }
-            nslow = 0;
-            tx_wave_sync();
-        }
-#endif
-#ifdef EMURX_TX_P2ROW
-        // this round's slow rows now, one lane per row: a row that lies inside this tile and
-        // touches at most two segments takes each segment's frame bytes by (at most) two aligned
-        // 16-byte loads, all issued before any is used, and is stored as one 16-byte row; other
-        // rows byte by byte.  (Byte per lane took one load latency per 64 bytes of slow rows.)
-        tx_wave_sync();
-        {
-            const uint32_t nl = min(nslow, kTxSlow);
-            for (uint32_t q = p2done + lane; q < nl; q += kWave) {
-                const uint32_t e = slow[q], r = e >> 6;
-                uint32_t k0 = e & 63;
-                const bool whole = 16 * r >= head && 16 * r + 16 - head <= R && xb + 16ull * r + 16 <= cap;
-                const uint32_t y0 = 16 * r - head;  // valid when whole
-                if (whole) while (k0 < last && sg[0][k0 + 1] <= y0) ++k0;
-                const uint32_t k1 = min(k0 + 1, last);
-                const bool two = k0 < last && sg[0][k1] < y0 + 16;
-                const bool fits = whole && (!two || k1 == last || sg[0][k1 + 1] >= y0 + 16);
-                if (!fits) {
-                    for (uint32_t j = 0; j < 16; ++j) row_byte(r, j, e & 63);
-                    continue;
-                }
-                uint4 a0 = make_uint4(0, 0, 0, 0), b0 = a0, a1 = a0, b1 = a0;
-                uint32_t win0 = 0, win1 = 0;
-                // segment s's frame bytes within the row: output [fs, fe) from frames + off + fs - ds
-                auto load_win = [&](uint32_t ks, uint4& wa, uint4& wb, uint32_t& win) {
-                    const uint32_t ds = sg[1][ks], de = ds + sg[3][ks];
-                    const uint32_t fs = max(y0, ds), fe = min(y0 + 16, de);
-                    if (fs >= fe) return;
-                    const uintptr_t ad = (uintptr_t)(frames + sg[2][ks] + (fs - ds));
-                    const uint4* v = reinterpret_cast<const uint4*>(ad & ~(uintptr_t)15);
-                    win = fs - (uint32_t)(ad & 15);  // the output byte at the window's first byte
-                    wa = v[0];
-                    if ((ad & 15) + (fe - fs) > 16) wb = v[1];
-                };
-                load_win(k0, a0, b0, win0);
-                if (two) load_win(k1, a1, b1, win1);
-                const uint32_t s1 = two ? sg[0][k1] : 0xffffffffu;
-                const uint32_t st0 = sg[0][k0], mh0 = sg[5][k0], hd0 = sg[4][k0];
-                const uint32_t mh1 = sg[5][k1], hd1 = sg[4][k1];
-                auto pick = [](const uint4 wa, const uint4 wb, uint32_t i) {
-                    const uint32_t d = i >> 2;
-                    uint32_t v = wa.x;
-                    v = d == 1 ? wa.y : v; v = d == 2 ? wa.z : v; v = d == 3 ? wa.w : v;
-                    v = d == 4 ? wb.x : v; v = d == 5 ? wb.y : v; v = d == 6 ? wb.z : v;
-                    v = d == 7 ? wb.w : v;
-                    return (v >> (8 * (i & 3))) & 0xffu;
-                };
-                unsigned long long lo = 0, hi = 0;
-                for (uint32_t j = 0; j < 16; ++j) {
-                    const uint32_t y = y0 + j;
-                    const bool in1 = y >= s1;
-                    const uint32_t rel = y - (in1 ? s1 : st0), mh = in1 ? mh1 : mh0, hd = in1 ? hd1 : hd0;
-                    const uint32_t rel2 = mh ? rel - 4 : rel;
-                    uint32_t v;
-                    if (mh && rel < 4) v = (mh >> (24 - 8 * rel)) & 0xffu;
-                    else if (rel2 < 4) v = (hd >> (24 - 8 * rel2)) & 0xffu;
-                    else v = in1 ? pick(a1, b1, y - win1) : pick(a0, b0, y - win0);
-                    if (j < 8) lo |= (unsigned long long)v << (8 * j);
-                    else hi |= (unsigned long long)v << (8 * (j - 8));
-                }
-                *reinterpret_cast<uint4*>(out + xb + 16ull * r) =
-                    make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
-            }
-            p2done = nl;
-        }
-#endif
-#ifdef EMURX_TX_P2ROUND
-        // this round's byte-by-byte rows now, while the lines its full rows wrote are in L2
+#if EMURX_TX_P2ROUND && !defined(EMURX_TX_NOPASS2)
+        // this round's byte-by-byte rows now, while the lines its full rows wrote are in L2 (a
+        // line left partly written costs its write-back a read-modify-write)
         tx_wave_sync();
         const uint32_t nl = min(nslow, kTxSlow);
         for (uint32_t i = p2done * 16 + lane; i < nl * 16; i += kWave) {
@@ -699,7 +607,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kTxImg == k
 #else
     const uint32_t nb = min(nslow, kTxSlow) * 16;
 #endif
-#if defined(EMURX_TX_P2ROUND) || defined(EMURX_TX_P2ROW)
+#if EMURX_TX_P2ROUND
     for (uint32_t i = p2done * 16 + lane; i < nb; i += kWave) {
 #else
     for (uint32_t i = lane; i < nb; i += kWave) {
