@@ -65,10 +65,15 @@ def parse_args():
                          "(default for D: partitioned, with the replicated alternative measured too)")
     ap.add_argument("--table-updates", action="store_true",
                     help="also time batches with 1 / 64 / 4096 table mutations between them")
-    ap.add_argument("--a2a", choices=("v", "equal"), default="v",
-                    help="the exchange's transfer: v = counts, then only the spans that carry data (grouped "
-                         "sends / receives, SURVEY §8e's all-to-all-v; default); equal = whole regions by one "
-                         "equal-split all-to-all (round 4)")
+    ap.add_argument("--a2a", choices=("auto", "v", "equal"), default="auto",
+                    help="the exchange's transfer at N > 1: equal = whole regions, no host synchronisation; v = "
+                         "counts, then only the spans that carry data (SURVEY §8e's all-to-all-v; the host waits "
+                         "for the counts); auto (default) = both timed after the warmup, the faster one runs the "
+                         "timed steps (namespace_exchange.exchange.a2a_choice)")
+    ap.add_argument("--comm", choices=("library", "torch"), default="library",
+                    help="N > 1 over nccl: library = the exchange through the C-ABI's own RCCL communicator "
+                         "(emurx_comm_init + emurx_exchange_dev, what a Go caller drives; default); torch = "
+                         "torch.distributed collectives.  gloo (CPU rehearsals) always uses torch.distributed")
     ap.add_argument("--exchange-frames", type=int, default=1 << 21,
                     help="frames per GPU of the config-D Namespace-exchange measurement beside the headline")
     ap.add_argument("--no-exchange-run", action="store_true",
@@ -498,6 +503,17 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         # beside batch k's all-to-all AND beside batch k-1's owner lookups
         nsets = 2 if world > 1 and not a.no_overlap else 1
         side = torch.cuda.Stream(dev) if nsets > 1 else None
+        # the transfer: the library's own communicator (RCCL through the C-ABI) at N > 1 over
+        # nccl, else torch.distributed (gloo rehearsals); whole regions or payload spans
+        xch["lib"] = world > 1 and a.backend == "nccl" and a.comm == "library"
+        xch["payload"] = a.a2a == "v"
+        if xch["lib"]:
+            from emurx.rx import comm_unique_id
+            uid = torch.zeros(128, dtype=torch.uint8, device=dev)
+            if rank == 0:
+                uid.copy_(torch.frombuffer(bytearray(comm_unique_id()), dtype=torch.uint8))
+            dist.broadcast(uid, 0)  # the id out of band (a Go caller sends it its own way)
+            rx.comm_init(bytes(uid.cpu().numpy()), world, rank)
 
         def alloc_regions():
             xch["sets"] = []
@@ -507,6 +523,8 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
                          st=stream if j == 0 else side, ev=None)
                 # set 0 writes the handle's record / queue buffers (the sanity checks read them)
                 b["rec"], b["qlist"], b["tile_cnt"] = (rec, qlist, tile_cnt) if j == 0 else outputs()
+                if xch["lib"]:  # the library exchange's receive buffers (stream-ordered reuse)
+                    b["recv"], b["recv_count"] = torch.empty_like(b["send"]), torch.empty_like(b["send_count"])
                 if mode == "partitioned":
                     b["out"] = torch.empty(world * xch["cap"] * X.REC_BYTES, dtype=torch.uint8, device=dev)
                 xch["sets"].append(b)
@@ -514,28 +532,33 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
                        out=xch["sets"][0].get("out"))
         alloc_regions()
 
+        def lib_exchange(b, st):
+            """batch b's transfer through the library's communicator, enqueued on st"""
+            return rx.exchange_dev(b["send"], b["send_count"], b["recv"], b["recv_count"], xch["cap"],
+                                   xch["tcap"] or 0, payload=xch["payload"], route=mode == "replicated", stream=st)
+
         def x_start(b):
-            """batch b's transfer enqueued behind its stream (the v form waits on the host for
-            the batch's counts first)"""
+            """batch b's transfer enqueued behind its stream (the payload form waits on the host
+            for the batch's counts first)"""
+            if xch["lib"]:
+                b["pending"] = (None, b["recv"], b["recv_count"], lib_exchange(b, b["st"]))
+                return
             with torch.cuda.stream(b["st"]):  # the collective waits for this set's stream
-                if a.a2a == "v":
+                if xch["payload"]:
                     b["pending"] = X.exchange_v_start(b["send"], b["send_count"], xch["region"], xch["cap"], rb)
                 else:
                     b["pending"] = X.exchange_start(b["send"], b["send_count"], xch["region"])
 
-        def x_sync(send, send_count):
-            """(recv, recv_count, bytes sent to other ranks) of one blocking transfer.  The first
-            runs in the warmup: should the grouped sends / receives fail on this backend, every
-            rank falls back to whole regions before the timed steps, and the line says so"""
-            if a.a2a == "v":
-                try:
-                    return X.exchange_v(send, send_count, xch["region"], xch["cap"], rb)
-                except Exception as e:  # noqa: BLE001 - keep the exchange measured (a backend without
-                    # point-to-point support fails the same call on every rank)
-                    xch["a2a_fallback"] = repr(e)[:300]
-                    progress(rank, f"payload-sized transfer failed ({repr(e)[:120]}): whole regions from here on")
-                    a.a2a = "equal"
-            r, c = X.exchange(send, send_count, xch["region"])
+        def x_sync(b):
+            """(recv, recv_count, bytes sent to other ranks) of set b's transfer, on the launch
+            stream, waited for.  A failure fails the run on every rank (no per-rank fallback:
+            ranks that changed protocol alone would hang in mismatched collectives)"""
+            if xch["lib"]:
+                moved = lib_exchange(b, stream)
+                return b["recv"], b["recv_count"], moved
+            if xch["payload"]:
+                return X.exchange_v(b["send"], b["send_count"], xch["region"], xch["cap"], rb)
+            r, c = X.exchange(b["send"], b["send_count"], xch["region"])
             return r, c, (world - 1) * xch["region"]
 
         def produce(b, k):
@@ -584,13 +607,13 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             k = xch["k"]
             xch["k"] += 1
             b, prev = xch["sets"][k % 2], xch["sets"][(k + 1) % 2]
-            if a.a2a == "v" and b["pending"] is not None:
+            if xch["payload"] and b["pending"] is not None:
                 finish(b)  # batch k - 2
             if xch["timing"] and k % a.time_stride == 0 and xch["pool"]:
                 b["ev"] = xch["pool"].pop()
                 b["ev"][0].record(b["st"])
             produce(b, k)
-            if a.a2a == "equal":
+            if not xch["payload"]:
                 x_start(b)
                 if prev["pending"] is not None:
                     finish(prev)
@@ -659,7 +682,7 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         xch["k"] += 1
         produce(xch["sets"][0], k)
         if world > 1:
-            xch["recv"], xch["recv_count"], _ = x_sync(xch["send"], xch["send_count"])
+            xch["recv"], xch["recv_count"], _ = x_sync(xch["sets"][0])
         else:
             xch["recv"], xch["recv_count"] = xch["send"], xch["send_count"]
         if mode == "partitioned":
@@ -694,7 +717,7 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             produce(b, k)
             e[1].record(stream)
             if world > 1:
-                recv, rc, sent = x_sync(b["send"], b["send_count"])
+                recv, rc, sent = x_sync(b)
             else:
                 recv, rc = b["send"], b["send_count"]
             e[2].record(stream)
@@ -739,8 +762,8 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
                "owner_lookup_kernel_ms": round(look_b2b, 5) if look_b2b is not None else None,
                "record_bytes": rb, "tail_units_per_shard": xch["tcap"], "region_bytes": xch["region"],
                "tail_bytes_per_frame": round(16 * sum(units) / max(int(sc.sum()), 1), 3),
-               "transfer": ("counts, then the spans that carry data (grouped sends / receives)" if a.a2a == "v"
-                            else "one equal-split all-to-all of whole regions"),
+               "transfer": ("counts, then the spans that carry data (grouped sends / receives)" if xch["payload"]
+                            else "whole regions and counts in one grouped exchange"),
                "bytes_to_other_ranks": moved, "payload_bytes_to_other_ranks": payload,
                "frames_to_other_ranks": to_others,
                "bytes_per_frame_to_other_ranks": round(moved / to_others, 2) if to_others else None,
@@ -791,9 +814,42 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             xcheck(xch, rec, n, world, rank, dist, torch, dev, mode)
     if not a.no_check and warmup > 0:
         sanity()
+    def choose_a2a(k_steps):
+        """--a2a auto at N > 1: the two transfers timed one after the other over the same
+        pipeline as the timed steps (k_steps each after 4 untimed, max over ranks), the faster
+        kept.  Every rank decides on the same reduced times."""
+        over = len(xch["sets"]) > 1
+        res = {}
+        for name, pl in (("equal", False), ("payload", True)):
+            xch["payload"] = pl
+            for reps in (4, k_steps):
+                torch.cuda.synchronize()
+                dist.barrier()
+                xch["k"] = 0
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    step_overlapped() if over else step()
+                if over:
+                    drain()
+                t_sub = time.perf_counter() - t0
+                torch.cuda.synchronize()
+                el = time.perf_counter() - t0
+            t = torch.tensor([el, t_sub], dtype=torch.float64)
+            t = t.to(dev) if dist.get_backend() == "nccl" else t
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el, t_sub = (float(x) for x in t.cpu())
+            res[name] = {"value": round(n * world * k_steps / el / 1e6, 2), "ms_per_step": round(el / k_steps * 1e3, 4),
+                         "host_submit_ms_per_step": round(t_sub / k_steps * 1e3, 4)}
+        return a2a_choice_block(res, k_steps)
+
     # the time-based warmup last, right before the measurements: the host-side check above
     # leaves the GPU idle long enough for its clocks to drop, which a 20-step region would time
     warm_s = warm_for_time()
+    if xch is not None and world > 1 and a.a2a == "auto":
+        xch["a2a_choice"] = choose_a2a(max(10, min(steps, 40)))
+        xch["payload"] = xch["a2a_choice"]["chosen"] == "payload"
+        progress(rank, f"transfer: {xch['a2a_choice']['chosen']} ({xch['a2a_choice']})")
+        warm_s += warm_for_time()
 
     progress(rank, f"config {cfg} {mode}: tables and batches ready, warmed up ({time.perf_counter() - t_start:.1f} s)")
     region = xch is None and a.kernel_timing == "region"
@@ -1036,10 +1092,13 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             "record_bytes": xch["rb"],
             "tail_units_per_shard": xch["tcap"],
             "region_bytes": xch["region"],
-            "a2a_fallback": xch.get("a2a_fallback"),
-            "collective": ((f"all_to_all_single of the counts + batch_isend_irecv of the spans that carry data "
-                            f"({a.backend})") if a.a2a == "v" else f"all_to_all_single x2 ({a.backend})")
-                           if world > 1 else "none (1 rank)",
+            "collective": (("emurx_exchange_dev over the library's own RCCL communicator (emurx_comm_init; "
+                            "ncclSend / ncclRecv to every peer in one group), " if xch["lib"] else
+                            f"torch.distributed ({a.backend}): ") +
+                           ("counts, host waits, then the spans that carry data" if xch["payload"]
+                            else "whole regions, no host synchronisation")) if world > 1 else "none (1 rank)",
+            "transfer_mode": ("payload" if xch["payload"] else "equal") if world > 1 else None,
+            "a2a_choice": xch.get("a2a_choice"),
             "overlapped": overlapped,  # batch k's all-to-all beside batch k+1's parse (two buffer sets)
             "includes": ("k_rx + group scan + pack" + (" + all-to-all" if world > 1 else "") +
                          (" + owner lookups (k_lookup)" if mode == "partitioned" else "")),
@@ -1094,6 +1153,16 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             ms = out["ms_per_step"] + key_ms
             out["value"], out["ms_per_step"] = round(n * world / (ms * 1e-3) / 1e6, 2), round(ms, 4)
     return out, rx, w
+
+
+def a2a_choice_block(res, k_steps):
+    """The namespace_exchange line's record of --a2a auto: both transfers' rates (frames over all
+    ranks / the slowest rank's time), their host submit time per step, and the one chosen (the
+    lower ms_per_step; ties keep the sync-free whole regions)."""
+    chosen = "payload" if res["payload"]["ms_per_step"] < res["equal"]["ms_per_step"] else "equal"
+    return dict(res, chosen=chosen, steps_each=k_steps,
+                source="after the warmup: 4 untimed + steps_each timed steps of each transfer over the timed steps' "
+                       "pipeline, wall clock, max over ranks; the faster runs the timed steps")
 
 
 def key_derivation(rx, w, torch, dev, stream, keyed_desc, per_msg=64, reps=30):
@@ -1305,15 +1374,53 @@ def xcheck(xch, rec, n, world, rank, dist, torch, dev, mode):
     assert routed[0] == routed[1], f"sent {routed[0]} != received {routed[1]}"
 
 
+class ReceiveFill:
+    """Stands in for the ZMQ receive (veth_zmq.go:132-143 rxThread: RecvBytes per message): the
+    batch's messages land straight in the slot's pinned staging buffer that emurx_ingest_buffer
+    handed out, written by `threads` receiver threads over disjoint message ranges (ctypes.memmove
+    drops the GIL, as a cgo zmq_recv into the slot does).  threads = 1 is the
+    round-5 single np.copyto."""
+
+    def __init__(self, threads):
+        from concurrent.futures import ThreadPoolExecutor
+        self.threads = max(1, int(threads))
+        self.pool = ThreadPoolExecutor(self.threads) if self.threads > 1 else None
+
+    def fill(self, dst, src):
+        import ctypes
+        import numpy as np
+        if self.pool is None:
+            np.copyto(dst[: src.size], src)
+            return
+        n = src.nbytes
+        chunk = ((n + self.threads - 1) // self.threads + 4095) & ~4095
+        d, s = dst.ctypes.data, src.ctypes.data
+        futs = [self.pool.submit(ctypes.memmove, d + o, s + o, min(chunk, n - o)) for o in range(0, n, chunk)]
+        for f in futs:
+            f.result()
+
+    def close(self):
+        if self.pool is not None:
+            self.pool.shutdown()
+
+
+def fill_threads():
+    """Receiver threads of the host-inclusive passes: the job's cores, at most 16
+    (EMURX_BENCH_FILL_THREADS overrides, for the measurement of the choice)."""
+    e = os.environ.get("EMURX_BENCH_FILL_THREADS")
+    return max(1, int(e)) if e and e.isdigit() else max(1, min(16, host_cores()))
+
+
 def host_inclusive_block(rx, w, rank, world, dist, torch, backend, per_msg=64, budget_s=1.0):
     """The host-inclusive rate of the default line, at every N: the
     headline batch as ZMQ messages of `per_msg` frames (veth_zmq.go:36-37,132-143,277-320)
     through the batched ingest (emurx_ingest_*), both slots alternating: pinned staging -> H2D
     -> framing walk -> k_rx -> queue packing -> D2H of records, descriptors, queues and
-    counters.  Two passes of `budget_s` each, every rank at once after a barrier: with the copy
-    of the messages into the slot's pinned staging (the receive copy the caller makes anyway),
-    and with the staging prefilled (PCIe + GPU only).  Per pass the node's aggregate = all
-    ranks' frames / the slowest rank's time (max over ranks, as the headline)."""
+    counters.  Passes of `budget_s` each, every rank at once after a barrier: with the messages
+    received into the slot's pinned staging by the receiver threads (ReceiveFill: the receive
+    copy the caller makes anyway, straight into the slot), the same with one thread, and with
+    the staging prefilled (PCIe + GPU only).  Per pass the node's aggregate = all ranks' frames
+    / the slowest rank's time (max over ranks, as the headline)."""
     import numpy as np
     from emurx import frames as F
     zs, msgs = F.zmq_messages(w["buf"], w["desc"], per_msg)
@@ -1326,7 +1433,7 @@ def host_inclusive_block(rx, w, rank, world, dist, torch, backend, per_msg=64, b
     out = {"frames_per_batch": n, "frames_per_msg": per_msg, "msgs_per_batch": len(msgs), "bytes_per_batch": total,
            "budget_s_per_pass": budget_s}
 
-    def one_pass(copy):
+    def one_pass(fill):
         if world > 1:
             dist.barrier()
         pending, k, t0 = [False, False], 0, time.perf_counter()
@@ -1334,8 +1441,8 @@ def host_inclusive_block(rx, w, rank, world, dist, torch, backend, per_msg=64, b
             s = k & 1
             if pending[s]:
                 rx.ingest_wait(s, copy=False)
-            if copy:
-                np.copyto(bufs[s], zs)
+            if fill is not None:
+                fill.fill(bufs[s], zs)
             rx.ingest_submit(s, msgs)
             pending[s] = True
             k += 1
@@ -1358,11 +1465,18 @@ def host_inclusive_block(rx, w, rank, world, dist, torch, backend, per_msg=64, b
         return {"mpkts": round(frames / el_max / 1e6, 2), "gbs_in": round(nbytes / el_max / 1e9, 2),
                 "rank0_mpkts": round(per_rank, 2), "batches_rank0": k}
 
-    out["with_host_copy"] = one_pass(True)
-    out["prefilled"] = one_pass(False)
+    fills = [ReceiveFill(fill_threads()), ReceiveFill(1)]
+    out["with_host_copy"] = one_pass(fills[0])
+    out["with_host_copy"]["fill_threads"] = fills[0].threads
+    out["with_host_copy_1_thread"] = one_pass(fills[1])
+    out["prefilled"] = one_pass(None)
+    for f in fills:
+        f.close()
     out["n_gpus"] = world
     out["source"] = ("emurx_ingest_submit/wait on both slots of every rank, wall clock per rank after a barrier; "
-                     "node aggregate = all ranks' frames / the slowest rank's time")
+                     "node aggregate = all ranks' frames / the slowest rank's time; with_host_copy: the messages "
+                     "received straight into the slot's pinned buffer (emurx_ingest_buffer) by fill_threads receiver "
+                     "threads while the other slot is in flight")
     return out
 
 
@@ -1381,6 +1495,9 @@ def host_path_rate(rx, w, per_msg=64, budget_s=3.0):
     out = {"frames_per_batch": n, "frames_per_msg": per_msg, "msgs_per_batch": len(msgs),
            "bytes_per_batch": total}
 
+    fill = ReceiveFill(fill_threads())
+    out["fill_threads"] = fill.threads
+
     def run(copy):
         pending = [False, False]
         for s in range(2):  # warm
@@ -1394,7 +1511,7 @@ def host_path_rate(rx, w, per_msg=64, budget_s=3.0):
             if pending[s]:
                 rx.ingest_wait(s, copy=False)
             if copy:
-                np.copyto(bufs[s], stream)
+                fill.fill(bufs[s], stream)
             rx.ingest_submit(s, msgs)
             pending[s] = True
             k += 1
@@ -1410,6 +1527,7 @@ def host_path_rate(rx, w, per_msg=64, budget_s=3.0):
     out["mpkts_with_host_copy"] = round(k * n / el / 1e6, 2)
     out["gbs_in_with_host_copy"] = round(k * total / el / 1e9, 2)
     k, el = run(False)
+    fill.close()
     out["mpkts_prefilled"] = round(k * n / el / 1e6, 2)
     out["gbs_in_prefilled"] = round(k * total / el / 1e9, 2)
     # latency of one batch by its size in messages (one slot, nothing else in flight): submit

@@ -18,6 +18,9 @@
  *   emurx_client_update_*    CNSCtx.UpdateClientIpv4/Ipv6/DIpv6 src/emu/core/ns_ctx.go:442-533
  *   emurx_client_set_ra()    CClient.Ipv6Router prefix      src/emu/core/client_ctx.go:60-66,279-295
  *   emurx_hist_to_counters() ParserStats accumulation       src/emu/core/parser.go:67-119
+ *   emurx_comm_* / emurx_exchange_dev   no Go counterpart: the one MapNsT of the single main
+ *                            goroutine (thread_ctx.go:139,397-419,772-784) split by Namespace
+ *                            owner over the GPUs, joined by an RCCL exchange
  *
  * Conventions: plain C types, no exceptions or aborts cross the ABI; every call returns
  * EMURX_OK (0) or a negative EMURX_E* code (mirrors PARSER_OK/PARSER_ERR, parser.go:41-44).
@@ -34,7 +37,7 @@
 extern "C" {
 #endif
 
-#define EMURX_ABI_VERSION 5
+#define EMURX_ABI_VERSION 6
 
 /* ---- return codes -------------------------------------------------------------------- */
 #define EMURX_OK 0
@@ -274,6 +277,9 @@ typedef struct emurx_dev_out {
 #define EMURX_FLOW_NO_SYN 0xFFFFFFF1u    /* new TCP flow without a bare SYN (ft_new_tcp_no_syn) :840-844 */
 #define EMURX_FLOW_NO_SERVER 0xFFFFFFF2u /* new flow, no listener on the port (ft_new_no_cb) :848-853,884-887 */
 #define EMURX_FLOW_NEW 0xFFFFFFF3u       /* new flow with a listener: OnAccept runs in Go :855-868,890-903 */
+#define EMURX_FLOW_UNKNOWN 0xFFFFFFF4u   /* emurx_lookup_dev only: the handler is reached but the head came
+                                            without its c5tuplekey (the source's handle saw no TransportCtx,
+                                            or the tuple did not fit its tail shard): the caller decides */
 #define EMURX_FLOW_ID_MAX 0xFFFFFFEFu    /* flow ids are 0 .. EMURX_FLOW_ID_MAX                */
 
 typedef struct emurx_ctx emurx_t;
@@ -453,6 +459,12 @@ typedef struct emurx_ingest_result {
     emurx_counters delta;        /* ParserStats + VethStats deltas of the batch             */
     uint32_t one_launch;         /* 1: the batch ran as one kernel (k_ingest_small, the
                                     small-batch path), 0: the copy + four-launch pipeline     */
+    uint32_t degraded;           /* 1: a one-launch batch whose workgroups did not all arrive
+                                    within the wait bound (EMURX_INGEST_SPIN_US, default 200 us,
+                                    read at emurx_open, plus 0.1 ns per byte of the batch's
+                                    messages: at most 1.2 ms; 0 forces it): its queues were
+                                    packed by the last workgroup from device scratch.  Same
+                                    results.                                                    */
 } emurx_ingest_result;
 /* Pinned staging buffer of slot s (0 <= s < EMURX_INGEST_SLOTS) with room for `bytes`
    (grown on demand; not while the slot has a batch in flight). */
@@ -690,6 +702,53 @@ int emurx_parse_route_dev(emurx_t* h, const uint8_t* d_frames, const emurx_desc*
 int emurx_lookup_dev(emurx_t* h, const emurx_lookup_rec* d_recv, const uint32_t* d_recv_count,
                      uint32_t n_parts, uint32_t cap, uint32_t tail_cap, emurx_route_rec* d_out,
                      uint32_t* d_flow, void* stream);
+
+/* ---- the exchange behind the C-ABI: a library-owned communicator (RCCL over xGMI) -------
+   The reference is one process whose main goroutine owns every table (MapNsT / GetNs
+   thread_ctx.go:139,772-784, MainLoop :397-419).  Sharded over the GPUs of a node, the one new
+   step is the exchange of every frame's lookup record to its Namespace owner; these calls run
+   it from the caller's thread (cgo) with no Python or torch in between:
+     one process per GPU:  rank 0 calls emurx_comm_unique_id and hands the 128 bytes to every
+                           rank out of band; each rank calls emurx_comm_init(h, id, nranks, rank)
+                           on its handle (ncclCommInitRank: blocks until every rank has joined)
+     one process, N GPUs:  emurx_comm_init_all(handles, n) (ncclCommInitAll over the handles'
+                           devices, one per GPU), the reference's process model; the exchanges of
+                           the N handles are then issued between emurx_group_start and
+                           emurx_group_end (whole-region mode only)
+   The communicator's nranks is the n_parts of the exchange; handle k of emurx_comm_init_all is
+   rank k.  emurx_close destroys it. */
+#define EMURX_ECOMM (-71)          /* RCCL error (init, send / receive, group) */
+#define EMURX_COMM_ID_BYTES 128    /* ncclUniqueId */
+int emurx_comm_unique_id(uint8_t id[EMURX_COMM_ID_BYTES]);
+int emurx_comm_init(emurx_t* h, const uint8_t id[EMURX_COMM_ID_BYTES], uint32_t nranks, uint32_t rank);
+int emurx_comm_init_all(emurx_t* const* hs, uint32_t n);
+int emurx_comm_destroy(emurx_t* h);
+/* EMURX_ENOENT when the handle has no communicator */
+int emurx_comm_info(emurx_t* h, uint32_t* nranks, uint32_t* rank);
+/* The RCCL library the communicators use, bound at the first communicator call (dlopen of
+   librccl.so.1: the copy already in the process if any, else the system's); its path into
+   `path`.  EMURX_ECOMM when none loads. */
+int emurx_comm_library(char* path, size_t cap);
+int emurx_group_start(void);
+int emurx_group_end(void);
+/* One exchange of the regions emurx_parse_route_dev packed (lookup regions of
+   EMURX_LOOKUP_REGION_BYTES(cap, tail_cap) bytes, two counts each) or, with EMURX_XCH_ROUTE,
+   those emurx_classify_route_dev packed (cap emurx_route_rec, one count each): rank r receives
+   region r of every source s into region s of d_recv, and its counts into d_recv_count, the
+   layout emurx_lookup_dev reads.  Enqueued on `stream` (NULL = the handle's stream):
+     EMURX_XCH_EQUAL    whole regions and counts in one group (ncclSend / ncclRecv to every
+                        peer, the own region by a device copy); no host synchronisation
+     EMURX_XCH_PAYLOAD  the counts first, then the host waits for them (the stream up to the
+                        batch's packing) and only the spans that carry data travel: the first
+                        min(count, cap) records and the tail shards (not inside a group)
+   *bytes_moved (optional): bytes sent to other ranks by this call.  A count > cap (the sources'
+   overflow, emurx_parse_route_dev) is delivered as is, so every rank sees it. */
+#define EMURX_XCH_EQUAL 0u
+#define EMURX_XCH_PAYLOAD 1u
+#define EMURX_XCH_ROUTE 2u
+int emurx_exchange_dev(emurx_t* h, const void* d_send, const uint32_t* d_send_count, void* d_recv,
+                       uint32_t* d_recv_count, uint32_t cap, uint32_t tail_cap, uint32_t flags,
+                       uint64_t* bytes_moved, void* stream);
 
 #ifdef __cplusplus
 }

@@ -90,6 +90,11 @@ def test_two_rank_exchange_fields(gpu_ok):
     assert ph["bytes_per_frame_to_other_ranks"] <= 40, ph
     assert 32 < ph["payload_bytes_per_frame_to_other_ranks"] < 34, ph  # config D: 5 % one-unit tails
     assert ph["xgmi_gbs"] > 0
+    # --a2a auto: both transfers timed, their host submit time, the faster one chosen and run
+    ch = x["exchange"]["a2a_choice"]
+    assert ch["chosen"] in ("equal", "payload") and x["exchange"]["transfer_mode"] == ch["chosen"]
+    for k in ("equal", "payload"):
+        assert ch[k]["value"] > 0 and ch[k]["host_submit_ms_per_step"] > 0, ch
     # its N = 1 twin, measured in the same job on rank 0: the ratio the >= 6x target is judged by
     t = x["exchange_scaling_target"]
     assert t["n1_value"] > 0 and t["ratio"] > 0 and t["target"] == 6.0 and t["n_gpus"] == 2

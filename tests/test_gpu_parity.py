@@ -897,6 +897,46 @@ def test_ingest_small_batches(rxmod, small, monkeypatch):
         check_ingest(rx.ingest_wait(0), o, msgs, tab)
 
 
+@pytest.mark.parametrize("spin_us", ["0", "200"])
+def test_ingest_small_degraded(rxmod, spin_us, monkeypatch):
+    """the one-launch ingest's degraded pack (a workgroup that stops
+    waiting for the other tiles marks the batch, and the last workgroup packs the queues from
+    device scratch).  EMURX_INGEST_SPIN_US=0 takes it on every multi-tile batch; the default
+    bound (200 us + 0.1 ns per message byte) on an idle GPU takes the direct pack.  Records, descriptors, queues,
+    per-message status and every counter equal the oracle either way, from 2 tiles to the
+    256-tile limit, with hostile messages mixed in (OnRxStream veth_zmq.go:277-320)."""
+    import test_abi
+    monkeypatch.setenv("EMURX_INGEST_SMALL", "1")
+    monkeypatch.setenv("EMURX_INGEST_SPIN_US", spin_us)
+    rng = np.random.default_rng(0xDE6 + int(spin_us))
+    w = synth.config_c(16384, seed=0xC0DF)
+    frames = [w["buf"][d["off"]:d["off"] + d["len"]].tobytes() for d in w["desc"]]
+    vp = [int(v) for v in w["desc"]["vport"]]
+    rx, o = new_pair(rxmod, max_frames=1 << 17)
+    for t in (rx, o):
+        synth.load_tables(w, t)
+    nf = len(frames) - 64
+    for nm in (1, 9, 40, 300, 1024):
+        msgs = []
+        k = int(rng.integers(0, nf))
+        for _ in range(nm - (4 if nm > 8 else 0)):
+            per = 64 if nm == 1024 else int(rng.integers(1, 65))
+            msgs.append(F.zmq_pack([frames[(k + j) % nf] for j in range(per)], [vp[(k + j) % nf] for j in range(per)]))
+            k = (k + per) % nf
+        if nm > 8:
+            msgs += test_abi._rand_msgs(rng, 4)[:4]
+        msgs = [msgs[i] for i in rng.permutation(len(msgs))]
+        tab = place_messages(rx, 0, msgs, rng)
+        rx.ingest_submit(0, tab)
+        res = rx.ingest_wait(0)
+        check_ingest(res, o, msgs, tab)
+        assert res["one_launch"], nm
+        if nm != 9:  # one tile (nm = 1: at most 64 frames), or many (> 1,000 frames)
+            multi = nm > 1
+            assert res["n"] > abi.QUEUE_TILE or not multi
+            assert res["degraded"] == (multi and spin_us == "0"), (nm, res["n"], res["degraded"])
+
+
 def test_ingest_two_slots_pipelined(rxmod):
     """Config C frames as 64-frame messages, three batches over the two slots with one batch
     always in flight while the next is staged; each equals the oracle."""
@@ -984,6 +1024,32 @@ def test_tx_checksum_unaligned_frames(rxmod):
         got, st = run_tx(rx, zeroed, d, skew)
         assert (st == abi.TX_OK).all(), skew
         assert got.tobytes() == want.tobytes(), skew
+
+
+def test_tx_checksum_unaligned_first_frame_at_zero(rxmod):
+    """a staged wave whose first frame starts at d_frames + 0..15 with
+    d_frames itself unaligned.  The slab's aligned start must come from the absolute address
+    (frame offset lo - skew wrapped below zero and pointed ~4 GiB past the buffer).  Small
+    frames packed with no header, so wave 0's first frame is at offset 0; every skew 1..15,
+    against the oracle, nothing before d_frames written."""
+    import pyoracle
+    from emurx import frames as F
+    rng = np.random.default_rng(0xA1)
+    n = 300  # several waves, each one staged (about 64 x 60 B < the 6 KiB slab)
+    frames = [rng.integers(0, 256, int(l), dtype=np.uint8).tobytes() for l in rng.integers(40, 80, n)]
+    buf, desc = F.pack_frames(frames, header=0)
+    assert int(desc["off"][0]) == 0
+    d = np.zeros(n, abi.TX_DESC_DTYPE)
+    d["off"], d["len"] = desc["off"], desc["len"]
+    d["l3"] = 14
+    d["l4"] = 34
+    d["ops"] = abi.TX_IPV4_HDR | (rng.choice([abi.TX_L4_TCP4, abi.TX_L4_UDP4, abi.TX_L4_ICMP4], n) << abi.TX_L4_SHIFT)
+    want, wst = pyoracle.tx_checksum(buf, d)
+    rx, _ = new_pair(rxmod)
+    for skew in range(1, 16):
+        got, st = run_tx(rx, buf, d, skew)
+        assert np.array_equal(st, wst), skew
+        assert got.tobytes() == np.asarray(want).tobytes(), skew
 
 
 def test_tx_checksum_fuzz_vs_oracle(rxmod):

@@ -545,3 +545,48 @@ def test_table_allocation_fallback():
                          env={**os.environ, "EMURX_DEBUG_TABLE_LIMIT": str(64 << 20)})
     assert out.returncode == 0 and "ok" in out.stdout, out.stderr[-3000:]
     assert int(out.stdout.split()[-1]) < (400 << 20)  # every table at most 64 MiB
+
+
+def test_owner_flags_heads_without_tuple(rxmod):
+    """a source whose handle has no TransportCtx routes tcp / udp heads without
+    their c5tuplekey; an owner whose tables hold flows must not probe them with a zero tuple.
+    Those frames' flow is EMURX_FLOW_UNKNOWN (the caller decides); every other flow decision
+    and every record equal the oracle's."""
+    import pyoracle
+    import torch
+    from emurx import exchange as X
+    from gpu_util import to_dev
+    n = 30000
+    w = synth.config_c(n, rank=0, syn=0.3)
+    o = pyoracle.Oracle()
+    src = rxmod(0, max_ns=4096, max_clients=65536, max_frames=n)
+    own = rxmod(0, max_ns=4096, max_clients=65536, max_frames=n)
+    for t in (o, src, own):
+        synth.load_tables(w, t)
+        if t is not o:
+            t.register_all()
+    orec0 = o.rx_batch(w["buf"], w["desc"])[0]
+    transport_state([w])([o, own], [orec0])  # flows and listeners on the owner only
+    orec = o.rx_batch(w["buf"], w["desc"])[0]
+    want_flow = o.flows(w["buf"], w["desc"], orec)
+    cap, tcap = n, tail_cap_max(n)
+    rb = abi.lookup_region_bytes(cap, tcap)
+    buf, desc = to_dev(w["buf"]), to_dev(w["desc"])
+    qcap = abi.queue_cap(n)
+    ql = torch.empty(abi.NUM_QUEUES * qcap, dtype=torch.int32, device="cuda")
+    tc = torch.empty(abi.ntiles(n) * 16, dtype=torch.int32, device="cuda")
+    hi = torch.zeros(abi.HIST_SHARDS * 2 * abi.HIST_BINS, dtype=torch.int64, device="cuda")
+    sd = torch.full((rb,), 0xEE, dtype=torch.uint8, device="cuda")
+    sc = torch.full((2,), -1, dtype=torch.int32, device="cuda")
+    src.parse_route_dev(buf, desc, n, None, ql, qcap, tc, hi, 1, 0, cap, sd, sc, tail_cap=tcap)
+    out = torch.full((cap * X.REC_BYTES,), 0xEE, dtype=torch.uint8, device="cuda")
+    flow = torch.full((cap,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    own.lookup_dev(sd, sc, 1, cap, out, flow, tail_cap=tcap)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(abi.ROUTE_REC_DTYPE)[:n]
+    assert got["rec"].tobytes() == orec.tobytes(), rec_diff(got["rec"], orec)
+    fl = flow.cpu().numpy().view(np.uint32)[:n]
+    decided = (want_flow != abi.FLOW_NONE) & (want_flow != abi.FLOW_NO_CTX)
+    assert decided.sum() > 1000
+    assert (fl[decided] == abi.FLOW_UNKNOWN).all()
+    assert np.array_equal(fl[~decided], want_flow[~decided])

@@ -40,9 +40,16 @@ GROUPS = [
     ("Several GPUs", ["emurx_set_partition", "emurx_route_dev", "emurx_classify_route_dev", "emurx_parse_route_dev",
                       "emurx_lookup_dev", "emurx_owner_key", "emurx_desc_keys_dev"],
      "`GetNs` `thread_ctx.go:772-784` on the Namespace owner (SURVEY §8e)"),
+    ("Exchange (library-owned RCCL communicator)",
+     ["emurx_comm_unique_id", "emurx_comm_init", "emurx_comm_init_all", "emurx_comm_destroy", "emurx_comm_info",
+      "emurx_comm_library",
+      "emurx_group_start", "emurx_group_end", "emurx_exchange_dev"],
+     "no Go counterpart: the single goroutine's `MapNsT` (`thread_ctx.go:139,397-419,772-784`) split by owner "
+     "(SURVEY §8e)"),
     ("Tx path", ["emurx_tx_checksum_dev", "emurx_tx_zmq_dev"],
      "gopacket checksum updates; `VethIFZmq.Send/FlushTx` `veth_zmq.go:149-200`"),
-    ("Measurement", ["emurx_set_timing", "emurx_kernel_times", "emurx_copy_ceiling_dev", "emurx_last_stage"],
+    ("Measurement", ["emurx_set_timing", "emurx_kernel_times", "emurx_copy_ceiling_dev", "emurx_last_stage",
+                     "emurx_last_txz"],
      "(bench.py; `emurx_copy_ceiling_dev` is the measured HBM copy ceiling beside the roofline)"),
 ]
 

@@ -167,6 +167,14 @@ struct emurx_ctx {
     IngestSlot ing[EMURX_INGEST_SLOTS + 1];
     bool ingest_small = true;  // small batches in one launch (k_ingest_small); EMURX_INGEST_SMALL=0: never
     bool ingest_spin = true;   // wait for them on their completion word; EMURX_INGEST_SPIN=0: on the event
+    // the one-launch path's bounds: its tiles must all be resident (the device's capacity for
+    // k_ingest_small, measured at emurx_open), and a workgroup waits for the others at most
+    // EMURX_INGEST_SPIN_US (default 200 us) plus 0.1 ns per byte of the batch's messages (the
+    // tiles read them over PCIe at 20-50 GB/s, so a bigger batch's tiles arrive further apart:
+    // at most 1.2 ms for the largest one-launch batch); 0 forces the degraded pack (tests)
+    uint32_t small_tiles = EMURX_SMALL_TILES;
+    double spin_base_us = 200.0;
+    uint32_t wall_khz = 100000;  // the GPU's wall clock (hipDeviceAttributeWallClockRate)
 
     // tx ZMQ framing scratch (emurx_tx_zmq_dev): per-level chain transfer tables
     DevBuf<uint8_t> d_txz;
@@ -223,6 +231,9 @@ struct emurx_ctx {
     hipEvent_t stage_ev = nullptr;
     bool stage_narrow = false;
     uint32_t last_stage = 0;
+
+    // the Namespace-owner exchange's communicator (emurx_comm.cpp), or none
+    emurx_comm_state* comm = nullptr;
 
     // timing ring: 2 events per batch (around the k_rx launch)
     std::vector<hipEvent_t> ev;
@@ -524,8 +535,8 @@ int ingest_buffer(emurx_t* h, uint32_t slot, size_t bytes, uint8_t** buf) {
 // it, and those whose status word it writes: tile min(base / 256, tiles - 1)) within the
 // kernel's LDS budget, counted exactly as the kernel stages them: 16-byte vectors from the
 // message's aligned start, plus two of slack.
-bool small_fits(const uint32_t* ctl, uint32_t nmsg, uint32_t n, uint32_t trange[EMURX_SMALL_TILES]) {
-    if (nmsg > EMURX_SMALL_MSGS || n > (uint32_t)EMURX_SMALL_TILES * EMURX_QUEUE_TILE) return false;
+bool small_fits(const uint32_t* ctl, uint32_t nmsg, uint32_t n, uint32_t max_tiles, uint32_t trange[EMURX_SMALL_TILES]) {
+    if (nmsg > EMURX_SMALL_MSGS || n > std::min<uint32_t>(max_tiles, EMURX_SMALL_TILES) * EMURX_QUEUE_TILE) return false;
     const uint32_t nt = std::max<uint32_t>(ntiles(n), 1);
     const uint32_t* base = ctl + 2 * (size_t)nmsg;
     uint64_t vec[EMURX_SMALL_TILES] = {0};
@@ -622,7 +633,7 @@ int ingest_submit(emurx_t* h, uint32_t slot, const emurx_msg* msgs, uint32_t nms
     // the pipeline's histogram shards start zeroed (k_qscan leaves them zero)
     if (fresh_hist && !EMURX_HIP_OK(hipMemsetAsync(s.d_hist.p, 0, hw * sizeof(uint64_t), st))) return EMURX_EDEVICE;
     uint32_t trange[EMURX_SMALL_TILES];
-    if (h->ingest_small && small_fits(ctl, nmsg, n, trange)) {
+    if (h->ingest_small && small_fits(ctl, nmsg, n, h->small_tiles, trange)) {
         // one launch: control words and messages read from the pinned buffers, every result
         // written into the pinned result buffers (no copies)
         if (!s.d_ticket.p) {
@@ -637,10 +648,12 @@ int ingest_submit(emurx_t* h, uint32_t slot, const emurx_msg* msgs, uint32_t nms
         }
         if (emurx_launch_ingest_small(s.h_buf.p, ctl, nmsg, n, h->tables(), s.h_rec.p, s.h_desc.p, s.h_qlist.p,
                                       s.h_stat.p, s.h_qoff.p, s.h_hist.p, s.d_qseg.p, s.d_tcnt.p, s.d_hsmall.p,
-                                      s.d_ticket.p, s.h_done.p, s.seq + 1, trange, st) ||
+                                      s.d_ticket.p, s.h_done.p, (s.seq + 1) & 0x7fffffffu,
+                                      h->spin_base_us > 0 ? (uint32_t)((h->spin_base_us + 1e-4 * (double)end) * h->wall_khz / 1000.0) : 0u,
+                                      trange, st) ||
             !EMURX_HIP_OK(hipEventRecord(s.done, st)))
             return EMURX_EDEVICE;
-        ++s.seq;
+        s.seq = (s.seq + 1) & 0x7fffffffu;  // bit 31 of the completion word: the batch was degraded
         s.small = true;
         s.pending = true;
         s.nmsg = nmsg;
@@ -681,7 +694,7 @@ bool spin_done(const uint32_t* word, uint32_t seq) {
     const volatile uint32_t* w = word;
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t k = 1;; ++k) {
-        if (*w == seq) {
+        if ((*w & 0x7fffffffu) == seq) {
             std::atomic_thread_fence(std::memory_order_acquire);
             return true;
         }
@@ -735,6 +748,7 @@ int ingest_wait(emurx_t* h, uint32_t slot, emurx_ingest_result* res) {
     memcpy(res->qoff, s.h_qoff.p, sizeof(res->qoff));
     if (res->qoff[EMURX_NUM_QUEUES] != nf) return EMURX_EDEVICE;
     res->one_launch = s.small ? 1u : 0u;
+    res->degraded = s.small ? (*(volatile uint32_t*)s.h_done.p >> 31) : 0u;
     emurx_hist_to_counters(s.h_hist.p, &d);
     d.rx_pkts = nf;  // VethIFZmq.OnRx veth_zmq.go:233-234
     for (int b = 0; b < EMURX_HIST_BINS; ++b) d.rx_bytes += s.h_hist.p[2 * b + 1];
@@ -750,6 +764,12 @@ int ingest_wait(emurx_t* h, uint32_t slot, emurx_ingest_result* res) {
 
 }  // namespace
 
+// handle internals for emurx_comm.cpp (emurx_kernels.h)
+int emurx_handle_bind(emurx_t* h) { return bind(h); }
+int emurx_handle_device(const emurx_t* h) { return h->host_only ? -1 : h->cfg.device; }
+hipStream_t emurx_handle_stream(emurx_t* h) { return h->stream; }
+emurx_comm_state*& emurx_handle_comm(emurx_t* h) { return h->comm; }
+
 extern "C" {
 
 int emurx_abi_version(void) { return EMURX_ABI_VERSION; }
@@ -763,6 +783,7 @@ const char* emurx_strerror(int code) {
     case EMURX_ENOENT: return "not found";
     case EMURX_EDEVICE: return "HIP runtime error";
     case EMURX_ENOSPC: return "output buffer too small";
+    case EMURX_ECOMM: return "RCCL communication error";
     default: return "unknown error";
     }
 }
@@ -793,6 +814,15 @@ int emurx_open(const emurx_cfg* cfg, emurx_t** out) {
         h->txz_mode = !strcmp(e, "wide") ? EMURX_TXZ_WIDE : !strcmp(e, "narrow") ? EMURX_TXZ_NARROW
                     : !strcmp(e, "long") ? EMURX_TXZ_LONG : -1;
     if (const char* e = getenv("EMURX_INGEST_SPIN")) h->ingest_spin = strcmp(e, "0") != 0;
+    {
+        // the one-launch ingest's wait bound in wall-clock ticks, and its grid cap
+        int khz = 100000;
+        if (EMURX_HIP_OK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, cfg->device)) && khz > 0)
+            h->wall_khz = (uint32_t)khz;
+        if (const char* e = getenv("EMURX_INGEST_SPIN_US")) h->spin_base_us = std::min(std::max(0.0, strtod(e, nullptr)), 1e6);
+        const uint32_t cap = emurx_ingest_small_capacity(cfg->device);
+        h->small_tiles = std::min<uint32_t>(EMURX_SMALL_TILES, cap);
+    }
     if (h->stage_fb.alloc(256) || h->d_stage_fb.alloc(256) ||
         !EMURX_HIP_OK(hipEventCreateWithFlags(&h->stage_ev, hipEventDisableTiming)) ||
         !EMURX_HIP_OK(hipEventCreateWithFlags(&h->ship_ev, hipEventDisableTiming)) ||
@@ -823,6 +853,8 @@ void emurx_close(emurx_t* h) {
     }
     bind(h);
     (void)hipDeviceSynchronize();
+    emurx_comm_free(h->comm);
+    h->comm = nullptr;
     for (auto& s : h->ing) s.release();
     h->stage_fb.release();
     h->d_stage_fb.release();

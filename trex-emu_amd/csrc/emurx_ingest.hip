@@ -246,7 +246,9 @@ struct SmallArgs {
     unsigned long long* hist;    // [2 * EMURX_HIST_BINS], zero between batches
     uint32_t* ticket;            // zero between batches
     uint32_t* done;              // pinned host: the batch's sequence number, written last
-    uint32_t seq;
+    uint32_t seq;                // < 2^31: bit 31 of the completion word says "degraded"
+    uint32_t spin_ticks;         // wall-clock ticks a workgroup waits for every tile to arrive
+                                 // (0: none, the degraded pack at once: tests of that path)
     uint32_t trange[EMURX_SMALL_TILES];  // per tile: its first message | message count << 16
 };
 
@@ -601,20 +603,25 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
     // offsets from all the counts and writes its own queue entries straight to their packed
     // places in the host's qlist (the PCIe writes spread over every workgroup: one workgroup
     // writing a 16K-frame batch's 64 KiB took 20 us at its outstanding-write limit).  The wait
-    // is bounded (kSpinLimit polls): a workgroup that gives up (its tiles were not all resident,
-    // e.g. beside other kernels) marks the batch degraded, and the last workgroup then packs
-    // the queues from the device scratch every tile also wrote (qseg) as before.
+    // is bounded in time (spin_ticks of the 100 MHz wall clock, the host's EMURX_INGEST_SPIN_US):
+    // a workgroup that gives up (its tiles were not all resident, e.g. beside other kernels)
+    // marks the batch degraded, and the last workgroup then packs the queues from the device
+    // scratch every tile also wrote (qseg) as before.  The host caps the grid at the workgroups
+    // the GPU holds at once (emurx_ingest_small_capacity), so the wait ends early but for
+    // co-tenancy; its worst case is spin_ticks per batch.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     __shared__ uint32_t s_direct;
     if (tid == 0) {
-        constexpr uint32_t kSpinLimit = 20000;  // one agent-scope load (~1 us) + s_sleep per poll
         __atomic_thread_fence(__ATOMIC_RELEASE);  // every wave's stores are behind the barrier
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         atomicAdd(a.ticket + 1, 1u);
-        uint32_t it = 0, seen = 0;
-        while ((seen = ld_agent(a.ticket + 1)) < a.nt && ++it < kSpinLimit) __builtin_amdgcn_s_sleep(2);
-        s_direct = seen >= a.nt;
+        uint32_t seen = 0;
+        const uint64_t t_0 = (uint64_t)wall_clock64();
+        while (a.spin_ticks && (seen = ld_agent(a.ticket + 1)) < a.nt &&
+               (uint64_t)wall_clock64() - t_0 < a.spin_ticks)
+            __builtin_amdgcn_s_sleep(2);
+        s_direct = a.spin_ticks && seen >= a.nt;
         if (!s_direct) atomicOr(a.ticket + 2, 1u);  // before this workgroup's ticket (release below)
     }
     __syncthreads();
@@ -700,7 +707,7 @@ __global__ __launch_bounds__(kBlock) void k_ingest_small(const SmallArgs a) {
     PSTAMP(5);
     if (tid == 0) {
         __atomic_thread_fence(__ATOMIC_RELEASE);
-        __hip_atomic_store(a.done, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(a.done, a.seq | (degraded ? 0x80000000u : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     SSTAMP(9);
 }
@@ -721,15 +728,26 @@ int emurx_launch_ingest_small(const uint8_t* h_buf, const uint32_t* h_ctl, uint3
                               const emurx_dev_tables& T, emurx_rec* h_rec, emurx_desc* h_desc, uint32_t* h_qlist,
                               uint32_t* h_stat, uint32_t* h_qoff, uint64_t* h_hist, uint32_t* d_qseg, uint32_t* d_tcnt,
                               uint64_t* d_hist, uint32_t* d_ticket, uint32_t* h_done, uint32_t seq,
-                              const uint32_t* trange, hipStream_t st) {
+                              uint32_t spin_ticks, const uint32_t* trange, hipStream_t st) {
     using namespace emurx;
     const uint32_t nt = std::max<uint32_t>((n + kBlock - 1) / kBlock, 1);
-    if (nt > EMURX_SMALL_TILES || nmsg > kSmallMsgs) return -1;
+    if (nt > EMURX_SMALL_TILES || nmsg > kSmallMsgs || (seq >> 31)) return -1;
     SmallArgs args{h_buf, h_ctl, nmsg, n, nt, T, h_rec, h_desc, h_qlist, h_stat, h_qoff,
                    reinterpret_cast<unsigned long long*>(h_hist), d_qseg, d_tcnt,
-                   reinterpret_cast<unsigned long long*>(d_hist), d_ticket, h_done, seq, {}};
+                   reinterpret_cast<unsigned long long*>(d_hist), d_ticket, h_done, seq, spin_ticks, {}};
     for (uint32_t t = 0; t < nt; ++t) args.trange[t] = trange[t];
     return EMURX_HIP_OK(emurx_launch(k_ingest_small, dim3(nt), dim3(kBlock), 0, st, args)) ? 0 : -1;
+}
+
+// Workgroups of k_ingest_small the device holds at once (occupancy x compute units): the
+// one-launch path's tiles must all be resident for its direct queue pack.
+uint32_t emurx_ingest_small_capacity(int device) {
+    using namespace emurx;
+    int per_cu = 0, cus = 0;
+    if (!EMURX_HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_ingest_small, kBlock, 0)) ||
+        !EMURX_HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device)))
+        return 0;
+    return (uint32_t)std::max(per_cu, 0) * (uint32_t)std::max(cus, 0);
 }
 
 #if EMURX_SMALL_STAMP

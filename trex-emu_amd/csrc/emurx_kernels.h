@@ -108,8 +108,10 @@ int emurx_launch_zmq_walk(const uint8_t* buf, const uint32_t* ctl, uint32_t nmsg
 // pinned host memory (h_*: the layout of the pipeline's D2H copies).  Device scratch: d_qseg
 // [EMURX_SMALL_TILES * 13 * 256], d_tcnt [EMURX_SMALL_TILES * 16], d_hist [128] and d_ticket [3] (ticket,
 // arrivals, degraded),
-// zero before the first launch (each launch leaves them zero).  h_done (pinned host): seq is
-// written there after every result (the host may spin on it instead of the stream).  trange[t]
+// zero before the first launch (each launch leaves them zero).  h_done (pinned host): seq
+// (< 2^31) is written there after every result, bit 31 set when the batch was degraded (the
+// host may spin on it instead of the stream).  spin_ticks: the 100 MHz wall-clock ticks a
+// workgroup waits for every tile's arrival before it takes the degraded pack (0: at once).  trange[t]
 // (emurx_ingest_tile_ranges): tile t's first message | its message count << 16.
 #ifndef EMURX_SMALL_TILES
 #define EMURX_SMALL_TILES 256
@@ -120,13 +122,23 @@ int emurx_launch_ingest_small(const uint8_t* h_buf, const uint32_t* h_ctl, uint3
                               const emurx_dev_tables& T, emurx_rec* h_rec, emurx_desc* h_desc, uint32_t* h_qlist,
                               uint32_t* h_stat, uint32_t* h_qoff, uint64_t* h_hist, uint32_t* d_qseg, uint32_t* d_tcnt,
                               uint64_t* d_hist, uint32_t* d_ticket, uint32_t* h_done, uint32_t seq,
-                              const uint32_t* trange, hipStream_t st);
+                              uint32_t spin_ticks, const uint32_t* trange, hipStream_t st);
+// k_ingest_small's workgroups resident at once on `device` (0 when unknown)
+uint32_t emurx_ingest_small_capacity(int device);
 // Concatenate k_rx's per-tile queue segments (queue-major, frame order) into `packed`, write
 // qoff[EMURX_NUM_QUEUES + 1], fold the histogram shards into hist_out[2 * EMURX_HIST_BINS] and
 // clear the shards.  Scratch seg_off: [ceil(n / 256) * 16].  Two launches.
 int emurx_launch_queue_pack(const uint32_t* qlist, uint32_t qcap, const uint32_t* tile_cnt, uint32_t n,
                             uint32_t* seg_off, uint32_t* packed, uint32_t* qoff, uint64_t* hist,
                             uint64_t* hist_out, hipStream_t st);
+
+// The handle internals the communicator (emurx_comm.cpp) uses; defined in emurx_api.cpp.
+struct emurx_comm_state;
+int emurx_handle_bind(emurx_t* h);           // make the handle's device current (EMURX_OK / error)
+int emurx_handle_device(const emurx_t* h);   // its device ordinal (< 0: host-only handle)
+hipStream_t emurx_handle_stream(emurx_t* h);  // its own stream
+emurx_comm_state*& emurx_handle_comm(emurx_t* h);
+void emurx_comm_free(emurx_comm_state* c);   // emurx_comm.cpp: destroy a communicator
 
 // Tx checksum generation (emurx_tx.hip): one launch, in place; status may be null.
 int emurx_launch_tx_csum(uint8_t* frames, const emurx_tx_desc* desc, uint32_t n, uint8_t* status,

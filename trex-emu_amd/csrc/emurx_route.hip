@@ -356,7 +356,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EMURX_LO
     // included, is not read: the source reported that overflow and must route the batch again)
     const uint32_t tun = live ? lk_tail_units(w[4]) : 0u;
     uint4 t0 = make_uint4(0, 0, 0, 0), t1 = t0, t2 = t0;
-    if (tun && w[7] < EMURX_TAIL_SHARDS * tcap && w[7] + tun <= EMURX_TAIL_SHARDS * tcap) {
+    const bool tail_ok = tun && w[7] < EMURX_TAIL_SHARDS * tcap && w[7] + tun <= EMURX_TAIL_SHARDS * tcap;
+    // a tcp / udp head without its c5tuplekey (the source's handle saw no TransportCtx when it
+    // routed, or the tuple's tail did not fit its shard) cannot take the flow decision here: its
+    // flow is EMURX_FLOW_UNKNOWN instead of a probe with a zero tuple
+    const bool has_tuple = (w[4] >> 31) && tail_ok;
+    if (tail_ok) {
         const uint4* tl = reinterpret_cast<const uint4*>(region + (uint64_t)cap * 32) + w[7];
         t0 = tl[0];
         if (tun == 3) {
@@ -366,7 +371,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EMURX_LO
     }
     // frames that reached no callback travel too (their owner keeps their record): no lookup
     if (live && r.status == EMURX_ST_OK)
-        resolve_owner(T, r, k, chash, t0, [&](uint32_t cid) { return flow_probe(T, tail_tuple(w, t0, t1, t2), cid); });
+        resolve_owner(T, r, k, chash, t0, [&](uint32_t cid) {
+            return has_tuple ? flow_probe(T, tail_tuple(w, t0, t1, t2), cid) : EMURX_FLOW_UNKNOWN;
+        });
     // The wave's outputs are contiguous: its 40-B records are parked in its (now read) LDS rows
     // and written back as five 8-B pieces per lane, 512 contiguous bytes per store instruction,
     // instead of five 8-B stores per lane 40 B apart

@@ -159,15 +159,17 @@ __global__ __launch_bounds__(kBlock) void k_tx_csum(uint8_t* __restrict__ frames
     const uint32_t hi = wave_max_u32(live ? d.x + len : 0u);
     // the staged rows start at the 16-byte boundary of the ABSOLUTE address (d_frames need not
     // be 16-aligned): a frame byte's slab index is then its address mod 16 plus a multiple of 16
-    const uintptr_t fbase = (uintptr_t)frames;
-    const uint32_t skew = (uint32_t)((fbase + lo) & 15u);  // lo's offset in its aligned vector
-    const uint32_t start = lo - skew, nvec = hi > lo ? (hi - start + 15) >> 4 : 0;
+    // (built from the absolute address: lo - skew in frame offsets would wrap below d_frames
+    // when the wave's first frame sits within its first 16 bytes)
+    const uintptr_t abs_lo = (uintptr_t)frames + lo;
+    const uint32_t skew = (uint32_t)(abs_lo & 15u);  // lo's offset in its aligned vector
+    const uint32_t nvec = hi > lo ? (hi - lo + skew + 15) >> 4 : 0;
     const bool staged = nvec > 0 && nvec <= kTxSlab / 16;  // wave-uniform
     uint32_t hcs = 0, lcs = 0, fo = 0;
     bool ok;
     if (staged) {
         static_assert(kTxSlab % (16 * kWave) == 0, "whole 1 KiB DMA rows");
-        const uint4* src = reinterpret_cast<const uint4*>(frames + start);  // 16-byte aligned
+        const uint4* src = reinterpret_cast<const uint4*>(abs_lo & ~(uintptr_t)15);  // 16-byte aligned
         uint4* dst = reinterpret_cast<uint4*>(s_slab[wv]);
 #pragma unroll
         for (uint32_t k = 0; k < kTxSlab / 16 / kWave; ++k)
@@ -178,7 +180,7 @@ __global__ __launch_bounds__(kBlock) void k_tx_csum(uint8_t* __restrict__ frames
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const TxLds s{reinterpret_cast<const uint8_t*>(s_slab[wv]), s_slab[wv], d.x - start};
+        const TxLds s{reinterpret_cast<const uint8_t*>(s_slab[wv]), s_slab[wv], d.x - lo + skew};
         ok = live && tx_sums(s, len, l3, l4, osize, ops, nhx, hcs, lcs, fo);
     } else {
         // frames too wide to stage whole (long L4 spans): each lane's first kTxWinVec vectors in

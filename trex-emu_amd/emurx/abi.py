@@ -19,6 +19,9 @@ LIB_PATH = PKG_ROOT / "lib" / "libemurx.so"
 EMURX_OK = 0
 EMURX_EINVAL, EMURX_ENOMEM, EMURX_EEXIST, EMURX_ENOENT = -22, -12, -17, -2
 EMURX_EDEVICE, EMURX_ENOSPC = -5, -28
+EMURX_ECOMM = -71      # RCCL error of the library-owned communicator
+COMM_ID_BYTES = 128    # EMURX_COMM_ID_BYTES (ncclUniqueId)
+XCH_EQUAL, XCH_PAYLOAD, XCH_ROUTE = 0, 1, 2  # emurx_exchange_dev flags
 ID_NONE = 0xFFFFFFFF
 MAX_FRAME = 9216
 
@@ -109,6 +112,7 @@ TX_OK, TX_RANGE = 0, 1
 ZMQ_TX_BURST, ZMQ_TX_MAX_BUFFER, ZMQ_PKT_MAGIC = 64, 32768, 0xAA  # veth_zmq.go:36-37, :167
 FLOW_NONE, FLOW_NO_CTX, FLOW_NO_SYN, FLOW_NO_SERVER, FLOW_NEW = (0xFFFFFFFF, 0xFFFFFFF0, 0xFFFFFFF1,
                                                                 0xFFFFFFF2, 0xFFFFFFF3)
+FLOW_UNKNOWN = 0xFFFFFFF4  # emurx_lookup_dev: the head came without its c5tuplekey
 FLOW_ID_MAX = 0xFFFFFFEF
 # emurx_client_spec (ctx_client_add list entry)
 CLIENT_SPEC_DTYPE = np.dtype([("ns_id", "<u4"), ("client_id", "<u4"), ("plugin_mask", "<u4"), ("mac", "u1", 6),
@@ -140,7 +144,7 @@ class IngestResult(C.Structure):
     _fields_ = [("rec", C.c_void_p), ("desc", C.c_void_p), ("qlist", C.c_void_p),
                 ("msg_frames", C.c_void_p), ("msg_status", C.c_void_p), ("n_frames", C.c_uint32),
                 ("n_msgs", C.c_uint32), ("qoff", C.c_uint32 * (NUM_QUEUES + 1)), ("delta", Counters),
-                ("one_launch", C.c_uint32)]
+                ("one_launch", C.c_uint32), ("degraded", C.c_uint32)]
 
 
 class DevOut(C.Structure):
@@ -221,6 +225,16 @@ SIGNATURES = [
     ("emurx_server_add", C.c_int, [_P, C.c_uint32, C.c_uint16, C.c_uint8]),
     ("emurx_server_remove", C.c_int, [_P, C.c_uint32, C.c_uint16, C.c_uint8]),
     ("emurx_client_set_transport", C.c_int, [_P, C.c_uint32, C.c_int]),
+    ("emurx_comm_unique_id", C.c_int, [_P]),
+    ("emurx_comm_init", C.c_int, [_P, _P, C.c_uint32, C.c_uint32]),
+    ("emurx_comm_init_all", C.c_int, [_P, C.c_uint32]),
+    ("emurx_comm_destroy", C.c_int, [_P]),
+    ("emurx_comm_info", C.c_int, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+    ("emurx_comm_library", C.c_int, [C.c_char_p, C.c_size_t]),
+    ("emurx_group_start", C.c_int, []),
+    ("emurx_group_end", C.c_int, []),
+    ("emurx_exchange_dev", C.c_int, [_P, _P, _P, _P, _P, C.c_uint32, C.c_uint32, C.c_uint32,
+                                     C.POINTER(C.c_uint64), _P]),
 ]
 
 _lib = None
@@ -255,7 +269,7 @@ def source_id() -> str | None:
     sources, headers and Makefile, first 16 hex digits); None when a file is missing."""
     import hashlib
     src = ["emurx_kernels.hip", "emurx_route.hip", "emurx_ingest.hip", "emurx_tx.hip", "emurx_txzmq.hip",
-           "emurx_api.cpp", "emurx_mirror.cpp"]
+           "emurx_api.cpp", "emurx_mirror.cpp", "emurx_comm.cpp"]
     hdr = ["emurx_kernels.h", "emurx_tables.h", "emurx_parse.h", "emurx_mirror.h"]
     files = [PKG_ROOT / "csrc" / f for f in src + hdr] + [REPO_ROOT / "include" / "emu_rx.h", PKG_ROOT / "Makefile"]
     h = hashlib.sha1()

@@ -121,20 +121,26 @@ class RxPath:
     # transport flow tables (TransportCtx.addFlowv4/6, serverCb; include/emu_rx.h)
     def flow_add(self, cid, tuple_bytes, flow_id) -> int:
         t = np.frombuffer(bytes(tuple_bytes), np.uint8).copy()
-        return self.lib.emurx_flow_add(self.h, cid, _p(t), len(t), flow_id)
+        rc = self.lib.emurx_flow_add(self.h, cid, _p(t), len(t), flow_id)
+        self._transport = self.any_transport or rc == 0
+        return rc
 
     def flow_remove(self, cid, tuple_bytes) -> int:
         t = np.frombuffer(bytes(tuple_bytes), np.uint8).copy()
         return self.lib.emurx_flow_remove(self.h, cid, _p(t), len(t))
 
     def server_add(self, cid, port, proto) -> int:
-        return self.lib.emurx_server_add(self.h, cid, port, proto)
+        rc = self.lib.emurx_server_add(self.h, cid, port, proto)
+        self._transport = self.any_transport or rc == 0
+        return rc
 
     def server_remove(self, cid, port, proto) -> int:
         return self.lib.emurx_server_remove(self.h, cid, port, proto)
 
     def client_set_transport(self, cid, has_ctx) -> int:
-        return self.lib.emurx_client_set_transport(self.h, cid, int(has_ctx))
+        rc = self.lib.emurx_client_set_transport(self.h, cid, int(has_ctx))
+        self._transport = self.any_transport or (rc == 0 and bool(has_ctx))
+        return rc
 
     def sync(self, stream=None):
         return abi.check(self.lib.emurx_sync(self.h, stream), "sync")
@@ -236,7 +242,7 @@ class RxPath:
         return dict(rec=view(r.rec, n, abi.REC_DTYPE), desc=view(r.desc, n, abi.DESC_DTYPE),
                     qlist=view(r.qlist, n, np.uint32), qoff=np.array(r.qoff, np.uint32),
                     msg_frames=view(r.msg_frames, m, np.uint32), msg_status=view(r.msg_status, m, np.uint8),
-                    counters=r.delta.as_dict(), n=n, one_launch=bool(r.one_launch))
+                    counters=r.delta.as_dict(), n=n, one_launch=bool(r.one_launch), degraded=bool(r.degraded))
 
     # ---- tx-side checksum generation ------------------------------------------------------
     def tx_checksum_dev(self, frames, desc, n: int, status=None, stream=None):
@@ -277,12 +283,26 @@ class RxPath:
                         my_rank: int, cap: int, send, send_count, stream=None, tail_cap=None):
         """Parse + lookup keys, packed into the owners' regions (abi.lookup_region_bytes(cap,
         tail_cap) bytes each: LOOKUP_REC_DTYPE heads + tail shards); send_count [2 * n_parts]
-        {heads, tail overflow}.  tail_cap defaults to abi.tail_capacity(cap)."""
-        tail_cap = abi.tail_capacity(cap) if tail_cap is None else tail_cap
+        {heads, tail overflow}.  tail_cap defaults to default_tail_cap(cap)."""
+        if tail_cap is None:
+            tail_cap = self.default_tail_cap(cap)
         out = abi.DevOut(_addr(rec), _addr(qlist), qcap, _addr(tile_cnt), _addr(hist), None)
         return abi.check(self.lib.emurx_parse_route_dev(self.h, _addr(frames), _addr(desc), n, C.byref(out),
                                                         n_parts, my_rank, cap, tail_cap, _addr(send),
                                                         _addr(send_count), _stream(stream)), "parse_route_dev")
+
+    def default_tail_cap(self, cap: int) -> int:
+        """Tail units per shard when the caller gives none: room for a sixteenth of
+        the heads to carry one unit (ICMPv6 keys), or, once any client has a TransportCtx (tcp /
+        udp heads then carry their c5tuplekey: 1 unit over IPv4, 3 over IPv6), for every head to
+        carry three.  A shard that still overflows is reported in send_count[2 d + 1]."""
+        return abi.tail_capacity(cap, 3.0 if self.any_transport else 1 / 16)
+
+    @property
+    def any_transport(self) -> bool:
+        """Some client has a TransportCtx on this handle (flows, listeners or the mark): what
+        makes the source attach tuples (emurx_parse_route_dev)."""
+        return bool(getattr(self, "_transport", False))
 
     def desc_keys_dev(self, frames, desc, n: int, stream=None):
         """Write every frame's owner key into its descriptor's pad byte, in place
@@ -300,9 +320,42 @@ class RxPath:
     def lookup_dev(self, recv, recv_count, n_parts: int, cap: int, out, flow=None, stream=None, tail_cap=None):
         """The owner's lookups over received lookup regions (parse_route_dev's layout; recv_count
         [2 * n_parts]) -> ROUTE_REC_DTYPE slots."""
-        tail_cap = abi.tail_capacity(cap) if tail_cap is None else tail_cap
+        if tail_cap is None:
+            tail_cap = self.default_tail_cap(cap)
         return abi.check(self.lib.emurx_lookup_dev(self.h, _addr(recv), _addr(recv_count), n_parts, cap, tail_cap,
                                                    _addr(out), _addr(flow), _stream(stream)), "lookup_dev")
+
+    # ---- the library-owned communicator (include/emu_rx.h emurx_comm_*, emurx_exchange_dev) ----
+    def comm_init(self, uid: bytes, nranks: int, rank: int):
+        """Join the exchange's communicator (ncclCommInitRank; blocks until every rank joined).
+        uid: comm_unique_id() of one rank, handed to every rank out of band."""
+        u = _u8(uid, abi.COMM_ID_BYTES)
+        return abi.check(self.lib.emurx_comm_init(self.h, _p(u), nranks, rank), "comm_init")
+
+    def comm_destroy(self):
+        return abi.check(self.lib.emurx_comm_destroy(self.h), "comm_destroy")
+
+    def comm_info(self):
+        """(nranks, rank) of the handle's communicator, or None."""
+        a, b = C.c_uint32(), C.c_uint32()
+        rc = self.lib.emurx_comm_info(self.h, C.byref(a), C.byref(b))
+        if rc == abi.EMURX_ENOENT:
+            return None
+        abi.check(rc, "comm_info")
+        return a.value, b.value
+
+    def exchange_dev(self, send, send_count, recv, recv_count, cap: int, tail_cap=None, payload: bool = False,
+                     route: bool = False, stream=None) -> int:
+        """One exchange of the owners' regions over the handle's communicator (RCCL): region r
+        of every rank's send into region s of rank r's recv, counts alongside.  Lookup regions
+        (parse_route_dev) unless route (classify_route_dev's route records).  Returns the bytes
+        sent to other ranks."""
+        tail_cap = (self.default_tail_cap(cap) if tail_cap is None else tail_cap) if not route else 0
+        moved = C.c_uint64()
+        flags = (abi.XCH_PAYLOAD if payload else abi.XCH_EQUAL) | (abi.XCH_ROUTE if route else 0)
+        abi.check(self.lib.emurx_exchange_dev(self.h, _addr(send), _addr(send_count), _addr(recv), _addr(recv_count),
+                                              cap, tail_cap, flags, C.byref(moved), _stream(stream)), "exchange_dev")
+        return moved.value
 
     # ---- table generations / image diagnostics -------------------------------------------------
     def table_gen(self) -> int:
@@ -336,6 +389,29 @@ class RxPath:
         a, b, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
         abi.check(self.lib.emurx_table_stats(self.h, C.byref(a), C.byref(b), C.byref(c)), "table_stats")
         return dict(delta_blocks=a.value, whole_tables=b.value, table_bytes=c.value)
+
+
+def comm_unique_id() -> bytes:
+    """A fresh communicator id (emurx_comm_unique_id, ncclGetUniqueId): one rank makes it, every
+    rank passes it to RxPath.comm_init."""
+    b = np.zeros(abi.COMM_ID_BYTES, np.uint8)
+    abi.check(abi.load().emurx_comm_unique_id(_p(b)), "comm_unique_id")
+    return b.tobytes()
+
+
+def comm_init_all(paths) -> None:
+    """One communicator over several handles of this process, one GPU each (emurx_comm_init_all):
+    handle k is rank k."""
+    hs = (C.c_void_p * len(paths))(*[p.h.value for p in paths])
+    abi.check(abi.load().emurx_comm_init_all(hs, len(paths)), "comm_init_all")
+
+
+def group_start():
+    abi.check(abi.load().emurx_group_start(), "group_start")
+
+
+def group_end():
+    abi.check(abi.load().emurx_group_end(), "group_end")
 
 
 def owner_key(key: bytes) -> int:
