@@ -355,7 +355,8 @@ def exchange_block(xo):
     """The namespace_exchange entry of the line: the exchange step's own measurement (value =
     frames over all ranks / max-over-ranks time; at N = 1 the two-stream pipelined rate, with
     the one-stream steps beside it in exchange.one_stream_steps) and its per-phase times."""
-    b = {k: xo[k] for k in ("value", "unit", "n_gpus", "ms_per_step", "steps", "warmup", "config", "exchange")}
+    b = {k: xo[k] for k in ("value", "unit", "n_gpus", "ms_per_step", "steps", "warmup", "config", "exchange",
+                            "host_submit_ms_per_step")}
     b["k_rx_ms_mean"] = xo["roofline"]["kernel_ms_mean"]
     b["roofline"] = {k: xo["roofline"][k] for k in ("kernel", "achieved", "frac", "alg_bytes_per_launch")}
     return b

@@ -50,6 +50,11 @@ __device__ unsigned long long* g_stamp;
 
 // k_rx's arguments as one struct (a single kernarg block; 91 SGPRs and 76 VGPRs against 106
 // and 79 for the same arguments passed one by one)
+// EMURX_TOL_PREFETCH (default 1): k_rx<2> issues the tile's owner-offset loads before the
+// staging wait (0, A/B builds: wave 0 loads them inside the tile body, one more round trip)
+#ifndef EMURX_TOL_PREFETCH
+#define EMURX_TOL_PREFETCH 1
+#endif
 struct RxArgs {
     const uint8_t* frames;
     const emurx_desc* desc;
@@ -157,7 +162,7 @@ struct TileLds {
 // workgroup's kWaves slabs of kStage bytes): parse, classify, record, queue segment, counts.
 template <int kKind, uint32_t kStage>
 __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 dd, Stage sg, const uint32_t* slab,
-                                          TileLds& L, const unsigned long long* pre = nullptr) {
+                                          TileLds& L, const TileOffLoads& tol, const unsigned long long* pre = nullptr) {
     constexpr bool kClassify = kKind == 1;
     constexpr uint32_t kWinVec = kStage / 16 / kWave;
     const emurx_dev_tables& T = a.T;
@@ -177,8 +182,12 @@ __device__ __forceinline__ void tile_body(const RxArgs& a, uint32_t tile, uint2 
     const uint32_t i = tile * EMURX_QUEUE_TILE + tid;
     if (lane < 16) L.wcnt[wv][lane] = 0;
     if (lane < EMURX_MAX_PARTS) L.rcnt[wv][lane] = 0;
-    if (kKind == 2 && wv == 0)
-        tile_offsets(rt.cnt, rt.goff, rt.parts, tile, lane, L.toff, [](uint32_t v) { return wave_sum_u32(v); });
+    // kind 2: the tile's offset in every owner region, from the loads issued before the staging
+    // wait (k_rx): in flight beside the tile's LDS-DMA instead of one more round trip here
+    if (kKind == 2 && wv == 0) {
+        const TileOffLoads t = EMURX_TOL_PREFETCH ? tol : tile_offsets_issue(rt.cnt, rt.goff, rt.parts, tile, lane);
+        tile_offsets_sum(t, rt.parts, lane, L.toff, [](uint32_t v) { return wave_sum_u32(v); });
+    }
     const bool valid = (dd.y >> 24) != EMURX_DESC_HOLE;
     const uint32_t off = dd.x, len = dd.y & 0xffff, vport = (dd.y >> 16) & 0xff;
     // stage-size feedback from every 64th tile (the launcher's choice, emurx_api.cpp): one
@@ -461,6 +470,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
     pre[0] = __builtin_amdgcn_s_memtime();
 #endif
     const uint2 dd = load_desc(a.desc, a.n, tile * EMURX_QUEUE_TILE + threadIdx.x);
+    TileOffLoads tol{make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), 0u};
+    if (EMURX_TOL_PREFETCH && kKind == 2 && wv == 0) tol = tile_offsets_issue(a.rt.cnt, a.rt.goff, a.rt.parts, tile, lane_id());
 #if EMURX_STAMP
     wait_vm0();
     pre[1] = __builtin_amdgcn_s_memtime();
@@ -469,9 +480,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kStage =
     stage_wait();
 #if EMURX_STAMP
     pre[2] = __builtin_amdgcn_s_memtime();
-    tile_body<kKind, kStage>(a, tile, dd, sg, slab, L, pre);
+    tile_body<kKind, kStage>(a, tile, dd, sg, slab, L, tol, pre);
 #else
-    tile_body<kKind, kStage>(a, tile, dd, sg, slab, L);
+    tile_body<kKind, kStage>(a, tile, dd, sg, slab, L, tol);
 #endif
 }
 

@@ -69,6 +69,37 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 // region = its group's offset (grp_off, k_route_scan) + the counts of the group's earlier
 // tiles (tile_cnt[t][owner], 64 tiles per group).  Called by one whole wave; lane 0 writes
 // s_toff[0 .. parts).
+// The loads of tile_offsets alone (x, y: the counts of the group's earlier tiles, lane l's
+// tile; g: lane l's group offset for owner l), so that a kernel can issue them ahead of a
+// wait it makes anyway (k_rx<2>: before its staging wait) and finish with tile_offsets_sum.
+struct TileOffLoads {
+    uint4 x, y;
+    uint32_t g;
+};
+__device__ __forceinline__ TileOffLoads tile_offsets_issue(const uint32_t* tile_cnt, const uint32_t* grp_off,
+                                                           uint32_t parts, uint32_t tile, uint32_t lane) {
+    TileOffLoads t{make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), 0u};
+    const uint32_t g0 = tile & ~63u;
+    if (g0 + lane < tile) {
+        const uint4* q = reinterpret_cast<const uint4*>(tile_cnt + (size_t)(g0 + lane) * 16);
+        t.x = q[0];
+        t.y = q[1];
+    }
+    if (lane < parts) t.g = grp_off[(tile / 64) * 16 + lane];
+    return t;
+}
+template <class R>
+__device__ __forceinline__ void tile_offsets_sum(const TileOffLoads& t, uint32_t parts, uint32_t lane, uint32_t* s_toff,
+                                                 R reduce_sum) {
+    const uint32_t c[EMURX_MAX_PARTS] = {t.x.x, t.x.y, t.x.z, t.x.w, t.y.x, t.y.y, t.y.z, t.y.w};
+#pragma unroll
+    for (uint32_t k = 0; k < EMURX_MAX_PARTS; ++k) {
+        if (k >= parts) break;
+        const uint32_t sum = reduce_sum(c[k]);
+        const uint32_t g = (uint32_t)__builtin_amdgcn_readlane((int)t.g, (int)k);
+        if (lane == 0) s_toff[k] = g + sum;
+    }
+}
 template <class R>
 __device__ __forceinline__ void tile_offsets(const uint32_t* tile_cnt, const uint32_t* grp_off, uint32_t parts,
                                              uint32_t tile, uint32_t lane, uint32_t* s_toff, R reduce_sum) {
