@@ -52,3 +52,43 @@ def test_kat_fixture_is_current():
         n = name.encode()
         b += struct.pack("<H", len(n)) + n + struct.pack("<HI", vp, len(f)) + bytes(f)
     assert KAT.read_bytes() == bytes(b)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_exchange_from_cpp_on_gpu(gpu_ok, oracle_built, tmp_path):
+    """The Namespace-owner exchange driven from C++ through the C-ABI alone (host/test_exchange.cpp:
+    no Python or torch in that process): a 1-rank communicator made both ways (emurx_comm_init_all,
+    the one-process model, with its exchange in a group; emurx_comm_unique_id + emurx_comm_init with
+    the payload-sized transfer), config D frames on config D's full tables, the owner's records
+    byte-equal to the oracle's."""
+    import struct
+    import numpy as np
+    import pyoracle
+    from emurx import abi, synth
+    _build()
+    n = 1 << 16
+    w = synth.config_d(n, rank=5)
+    o = pyoracle.Oracle()
+    synth.load_tables(w, o)
+    orec = o.rx_batch(w["buf"], w["desc"])[0]
+    want = np.zeros(n, abi.ROUTE_REC_DTYPE)
+    want["rec"], want["src_index"], want["src_rank"] = orec, np.arange(n), 0
+    specs = synth.client_specs(w)
+    f = tmp_path / "exchange_fixture.bin"
+    with open(f, "wb") as fh:
+        buf = np.ascontiguousarray(w["buf"], np.uint8)
+        fh.write(struct.pack("<6I", n, buf.size, len(w["ns"]), len(specs), 32768, 1 << 20))
+        fh.write(buf.tobytes())
+        fh.write(np.ascontiguousarray(w["desc"]).tobytes())
+        for key, ns_id in w["ns"]:
+            fh.write(bytes(key) + struct.pack("<I", ns_id))
+        fh.write(np.ascontiguousarray(specs).tobytes())
+        fh.write(want.tobytes())
+    r = subprocess.run([str(ROOT / "trex-emu_amd" / "build" / "test_exchange"), str(f)], capture_output=True,
+                       text=True, timeout=500)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    for name in ("TestExchangeOneProcess", "TestExchangeCommInit"):
+        assert f"PASS {name}" in r.stdout
+    assert "rccl: " in r.stdout and "librccl" in r.stdout

@@ -13,8 +13,10 @@ for f in emurx_kernels emurx_route emurx_ingest emurx_tx emurx_txzmq; do
   objs="$objs $out/$f.o"
 done
 /opt/rocm/bin/hipcc $F -x hip -c csrc/emurx_api.cpp -o $out/emurx_api.o &
+/opt/rocm/bin/hipcc $F -c csrc/emurx_comm.cpp -o $out/emurx_comm.o &
 ${CXX:-g++} -O2 -std=c++17 -fPIC -Wall $flags -c csrc/emurx_mirror.cpp -o $out/emurx_mirror.o &
 wait
 make -s build/build_id.o
-/opt/rocm/bin/hipcc $F -shared -o lib/libemurx_$name.so $objs $out/emurx_api.o $out/emurx_mirror.o build/build_id.o
+/opt/rocm/bin/hipcc $F -shared -o lib/libemurx_$name.so $objs $out/emurx_api.o $out/emurx_mirror.o $out/emurx_comm.o \
+  build/build_id.o -ldl
 echo lib/libemurx_$name.so

@@ -330,6 +330,7 @@ class RxPath:
         """Join the exchange's communicator (ncclCommInitRank; blocks until every rank joined).
         uid: comm_unique_id() of one rank, handed to every rank out of band."""
         u = _u8(uid, abi.COMM_ID_BYTES)
+        _torch_first()
         return abi.check(self.lib.emurx_comm_init(self.h, _p(u), nranks, rank), "comm_init")
 
     def comm_destroy(self):
@@ -391,9 +392,21 @@ class RxPath:
         return dict(delta_blocks=a.value, whole_tables=b.value, table_bytes=c.value)
 
 
+def _torch_first():
+    """Before the library binds RCCL (its first communicator call): torch, when installed, is
+    imported first, so that the process has one ROCm runtime and one RCCL (torch's bundled
+    ones).  The system's RCCL bound ahead of a later torch import mixes two copies of ROCm's
+    libraries, and such a process aborts at exit."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def comm_unique_id() -> bytes:
     """A fresh communicator id (emurx_comm_unique_id, ncclGetUniqueId): one rank makes it, every
     rank passes it to RxPath.comm_init."""
+    _torch_first()
     b = np.zeros(abi.COMM_ID_BYTES, np.uint8)
     abi.check(abi.load().emurx_comm_unique_id(_p(b)), "comm_unique_id")
     return b.tobytes()
@@ -402,11 +415,13 @@ def comm_unique_id() -> bytes:
 def comm_init_all(paths) -> None:
     """One communicator over several handles of this process, one GPU each (emurx_comm_init_all):
     handle k is rank k."""
+    _torch_first()
     hs = (C.c_void_p * len(paths))(*[p.h.value for p in paths])
     abi.check(abi.load().emurx_comm_init_all(hs, len(paths)), "comm_init_all")
 
 
 def group_start():
+    _torch_first()
     abi.check(abi.load().emurx_group_start(), "group_start")
 
 
