@@ -113,6 +113,9 @@ def parse_args():
                     help="rendezvous + max-over-ranks reduction only, no GPU (CPU test of the launch path)")
     ap.add_argument("--no-host-inclusive", action="store_true",
                     help="skip the default line's bounded host-inclusive block (every N)")
+    ap.add_argument("--ingest-slots", type=int, default=3,
+                    help="ingest slots the host-inclusive passes rotate through (one filled while the others "
+                         "are in flight; at most EMURX_INGEST_SLOTS)")
     ap.add_argument("--host-path", action="store_true",
                     help="also time the host-inclusive path (pinned H2D + kernels + D2H)")
     ap.add_argument("--unkeyed", action="store_true",
@@ -290,11 +293,12 @@ def main():
         # the north star's host-in / host-out rate, at every N (each rank through its own two
         # ingest slots, the node's aggregate): bounded to ~2 s, on the headline's handle
         try:
-            out["host_inclusive"] = host_inclusive_block(rx, w, rank, world, dist, torch, a.backend)
+            out["host_inclusive"] = host_inclusive_block(rx, w, rank, world, dist, torch, a.backend,
+                                                         slots=a.ingest_slots)
         except Exception as e:  # noqa: BLE001 - report, keep the headline line
             out["host_inclusive"] = {"error": repr(e)[:300]}
     if a.host_path:
-        out["host_inclusive"] = host_path_rate(rx, w)
+        out["host_inclusive"] = host_path_rate(rx, w, slots=a.ingest_slots)
     if a.config == "D" and not a.no_exchange_run:
         # SURVEY.md §8e asks for both: the Namespace-partitioned lookups (the headline of D)
         # and the "replicas only" alternative (every GPU holds every table)
@@ -1412,7 +1416,7 @@ def fill_threads():
     return max(1, int(e)) if e and e.isdigit() else max(1, min(16, host_cores()))
 
 
-def host_inclusive_block(rx, w, rank, world, dist, torch, backend, per_msg=64, budget_s=1.0):
+def host_inclusive_block(rx, w, rank, world, dist, torch, backend, per_msg=64, budget_s=1.0, slots=3):
     """The host-inclusive rate of the default line, at every N: the
     headline batch as ZMQ messages of `per_msg` frames (veth_zmq.go:36-37,132-143,277-320)
     through the batched ingest (emurx_ingest_*), both slots alternating: pinned staging -> H2D
@@ -1420,26 +1424,31 @@ def host_inclusive_block(rx, w, rank, world, dist, torch, backend, per_msg=64, b
     counters.  Passes of `budget_s` each, every rank at once after a barrier: with the messages
     received into the slot's pinned staging by the receiver threads (ReceiveFill: the receive
     copy the caller makes anyway, straight into the slot), the same with one thread, and with
-    the staging prefilled (PCIe + GPU only).  Per pass the node's aggregate = all ranks' frames
-    / the slowest rank's time (max over ranks, as the headline)."""
+    the staging prefilled (PCIe + GPU only).  The batches rotate over `slots` ingest slots: a
+    slot is filled while the others' batches are in flight (with two, a slot's fill waits for
+    its own previous batch's H2D + kernels + D2H, ~2.4 ms at 1M frames, and the fill does not
+    overlap it).  Per pass the node's aggregate = all ranks' frames / the slowest rank's time
+    (max over ranks, as the headline)."""
+    from emurx import abi
+    slots = max(2, min(int(slots), abi.INGEST_SLOTS))
     import numpy as np
     from emurx import frames as F
     zs, msgs = F.zmq_messages(w["buf"], w["desc"], per_msg)
     n, total = len(w["desc"]), len(zs)
-    bufs = [rx.ingest_buffer(s, total) for s in range(2)]
-    for s in range(2):  # warm both slots
+    bufs = [rx.ingest_buffer(s, total) for s in range(slots)]
+    for s in range(slots):  # warm every slot
         np.copyto(bufs[s], zs)
         rx.ingest_submit(s, msgs)
         assert rx.ingest_wait(s, copy=False)["n"] == n
     out = {"frames_per_batch": n, "frames_per_msg": per_msg, "msgs_per_batch": len(msgs), "bytes_per_batch": total,
-           "budget_s_per_pass": budget_s}
+           "budget_s_per_pass": budget_s, "slots": slots}
 
     def one_pass(fill):
         if world > 1:
             dist.barrier()
-        pending, k, t0 = [False, False], 0, time.perf_counter()
+        pending, k, t0 = [False] * slots, 0, time.perf_counter()
         while True:
-            s = k & 1
+            s = k % slots
             if pending[s]:
                 rx.ingest_wait(s, copy=False)
             if fill is not None:
@@ -1447,9 +1456,9 @@ def host_inclusive_block(rx, w, rank, world, dist, torch, backend, per_msg=64, b
             rx.ingest_submit(s, msgs)
             pending[s] = True
             k += 1
-            if time.perf_counter() - t0 > budget_s and k >= 4:
+            if time.perf_counter() - t0 > budget_s and k >= 2 * slots:
                 break
-        for s in range(2):
+        for s in range(slots):
             if pending[s]:
                 rx.ingest_wait(s, copy=False)
         el = time.perf_counter() - t0
@@ -1474,41 +1483,43 @@ def host_inclusive_block(rx, w, rank, world, dist, torch, backend, per_msg=64, b
     for f in fills:
         f.close()
     out["n_gpus"] = world
-    out["source"] = ("emurx_ingest_submit/wait on both slots of every rank, wall clock per rank after a barrier; "
+    out["source"] = (f"emurx_ingest_submit/wait over {slots} slots of every rank, wall clock per rank after a barrier; "
                      "node aggregate = all ranks' frames / the slowest rank's time; with_host_copy: the messages "
                      "received straight into the slot's pinned buffer (emurx_ingest_buffer) by fill_threads receiver "
-                     "threads while the other slot is in flight")
+                     "threads while the other slots are in flight")
     return out
 
 
-def host_path_rate(rx, w, per_msg=64, budget_s=3.0):
+def host_path_rate(rx, w, per_msg=64, budget_s=3.0, slots=3):
     """Host-inclusive rate of the batched ingest (emurx_ingest_*): the batch as ZMQ messages
-    of `per_msg` frames (TRex sends at most 64 per message, veth_zmq.go:36-37), two slots in
-    flight.  Timed per batch: copy of the messages into the slot's pinned staging (the
+    of `per_msg` frames (TRex sends at most 64 per message, veth_zmq.go:36-37), `slots` slots in
+    rotation.  Timed per batch: copy of the messages into the slot's pinned staging (the
     receive copy the caller makes anyway) + H2D + framing walk + k_rx + queue packing + D2H
     of records, descriptors, queues and counters.  Also timed with the staging pre-filled
     (PCIe + GPU only), and one message per call through emurx_rx_stream."""
     import numpy as np
     from emurx import frames as F
     stream, msgs = F.zmq_messages(w["buf"], w["desc"], per_msg)
+    from emurx import abi
     total, n = len(stream), len(w["desc"])
-    bufs = [rx.ingest_buffer(s, total) for s in range(2)]
+    slots = max(2, min(int(slots), abi.INGEST_SLOTS))
+    bufs = [rx.ingest_buffer(s, total) for s in range(slots)]
     out = {"frames_per_batch": n, "frames_per_msg": per_msg, "msgs_per_batch": len(msgs),
-           "bytes_per_batch": total}
+           "bytes_per_batch": total, "slots": slots}
 
     fill = ReceiveFill(fill_threads())
     out["fill_threads"] = fill.threads
 
     def run(copy):
-        pending = [False, False]
-        for s in range(2):  # warm
+        pending = [False] * slots
+        for s in range(slots):  # warm
             np.copyto(bufs[s], stream)
             rx.ingest_submit(s, msgs)
             res = rx.ingest_wait(s, copy=False)
             assert res["n"] == n
         k, t0 = 0, time.perf_counter()
         while True:
-            s = k & 1
+            s = k % slots
             if pending[s]:
                 rx.ingest_wait(s, copy=False)
             if copy:
@@ -1516,9 +1527,9 @@ def host_path_rate(rx, w, per_msg=64, budget_s=3.0):
             rx.ingest_submit(s, msgs)
             pending[s] = True
             k += 1
-            if time.perf_counter() - t0 > budget_s and k >= 4:
+            if time.perf_counter() - t0 > budget_s and k >= 2 * slots:
                 break
-        for s in range(2):
+        for s in range(slots):
             if pending[s]:
                 rx.ingest_wait(s, copy=False)
         el = time.perf_counter() - t0

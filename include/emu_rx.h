@@ -428,8 +428,9 @@ int emurx_zmq_descriptors(const uint8_t* msg, size_t len, emurx_desc* out, uint3
    The per-message loop of VethIFZmq.OnRxStream (veth_zmq.go:277-320) over a whole batch of
    messages, with the framing walk on the GPU (one lane per message, same uint16 offset and
    abort-on-header-error rules as emurx_zmq_descriptors), then parse + classify (k_rx), then
-   the per-callback queues packed on the GPU.  Two slots let the caller fill one pinned
-   staging buffer while the other slot's batch is in flight:
+   the per-callback queues packed on the GPU.  Several slots let the caller fill one pinned
+   staging buffer while the other slots' batches are in flight (a slot's buffers are allocated
+   at its first emurx_ingest_buffer: unused slots cost nothing):
 
        buf = emurx_ingest_buffer(h, s, bytes)    pinned host memory owned by the library
        ... the caller writes ZMQ messages into buf (the receive copy it does anyway) ...
@@ -439,7 +440,7 @@ int emurx_zmq_descriptors(const uint8_t* msg, size_t len, emurx_desc* out, uint3
    Frames are numbered in message order, then wire order (the order the Go loop handles
    them).  res.desc[i].off is the frame's offset in the slot's buffer.  Counters in res.delta
    are those of OnRxStream called once per message (RxBatch = nmsg). */
-#define EMURX_INGEST_SLOTS 2
+#define EMURX_INGEST_SLOTS 4
 #define EMURX_MSG_OK 0u          /* every announced frame decoded                           */
 #define EMURX_MSG_PARSE_ERR 1u   /* RxParseErr: the walk stopped on a header error           */
 #define EMURX_MSG_PANIC 2u       /* the reference panics: frame > 9216 B or offset wrap      */

@@ -102,7 +102,7 @@ DESC_DTYPE = np.dtype([("off", "<u4"), ("len", "<u2"), ("vport", "u1"), ("pad", 
 assert DESC_DTYPE.itemsize == 8
 DESC_HOLE = 0xFF   # EMURX_DESC_HOLE: an empty descriptor slot
 DESC_KEYED = 0x80  # EMURX_DESC_KEYED | k: the frame's Namespace-owner key
-INGEST_SLOTS = 2   # EMURX_INGEST_SLOTS
+INGEST_SLOTS = 4   # EMURX_INGEST_SLOTS
 SMALL_TILES, SMALL_LDS, SMALL_MSGS = 256, 40960, 1024  # the one-launch ingest's limits (csrc/emurx_kernels.h)
 MSG_OK, MSG_PARSE_ERR, MSG_PANIC = 0, 1, 2
 MSG_DTYPE = np.dtype([("off", "<u4"), ("len", "<u4")])
