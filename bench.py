@@ -113,9 +113,9 @@ def parse_args():
                     help="rendezvous + max-over-ranks reduction only, no GPU (CPU test of the launch path)")
     ap.add_argument("--no-host-inclusive", action="store_true",
                     help="skip the default line's bounded host-inclusive block (every N)")
-    ap.add_argument("--ingest-slots", type=int, default=3,
+    ap.add_argument("--ingest-slots", type=int, default=2,
                     help="ingest slots the host-inclusive passes rotate through (one filled while the others "
-                         "are in flight; at most EMURX_INGEST_SLOTS)")
+                         "are in flight; at most EMURX_INGEST_SLOTS; 3 and 4 measured slower, DESIGN.md §6)")
     ap.add_argument("--host-path", action="store_true",
                     help="also time the host-inclusive path (pinned H2D + kernels + D2H)")
     ap.add_argument("--unkeyed", action="store_true",
@@ -1416,7 +1416,7 @@ def fill_threads():
     return max(1, int(e)) if e and e.isdigit() else max(1, min(16, host_cores()))
 
 
-def host_inclusive_block(rx, w, rank, world, dist, torch, backend, per_msg=64, budget_s=1.0, slots=3):
+def host_inclusive_block(rx, w, rank, world, dist, torch, backend, per_msg=64, budget_s=1.0, slots=2):
     """The host-inclusive rate of the default line, at every N: the
     headline batch as ZMQ messages of `per_msg` frames (veth_zmq.go:36-37,132-143,277-320)
     through the batched ingest (emurx_ingest_*), both slots alternating: pinned staging -> H2D
@@ -1425,9 +1425,7 @@ def host_inclusive_block(rx, w, rank, world, dist, torch, backend, per_msg=64, b
     received into the slot's pinned staging by the receiver threads (ReceiveFill: the receive
     copy the caller makes anyway, straight into the slot), the same with one thread, and with
     the staging prefilled (PCIe + GPU only).  The batches rotate over `slots` ingest slots: a
-    slot is filled while the others' batches are in flight (with two, a slot's fill waits for
-    its own previous batch's H2D + kernels + D2H, ~2.4 ms at 1M frames, and the fill does not
-    overlap it).  Per pass the node's aggregate = all ranks' frames / the slowest rank's time
+    slot is filled while the others' batches are in flight.  Per pass the node's aggregate = all ranks' frames / the slowest rank's time
     (max over ranks, as the headline)."""
     from emurx import abi
     slots = max(2, min(int(slots), abi.INGEST_SLOTS))
@@ -1490,7 +1488,7 @@ def host_inclusive_block(rx, w, rank, world, dist, torch, backend, per_msg=64, b
     return out
 
 
-def host_path_rate(rx, w, per_msg=64, budget_s=3.0, slots=3):
+def host_path_rate(rx, w, per_msg=64, budget_s=3.0, slots=2):
     """Host-inclusive rate of the batched ingest (emurx_ingest_*): the batch as ZMQ messages
     of `per_msg` frames (TRex sends at most 64 per message, veth_zmq.go:36-37), `slots` slots in
     rotation.  Timed per batch: copy of the messages into the slot's pinned staging (the
