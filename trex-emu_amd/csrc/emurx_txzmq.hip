@@ -351,6 +351,14 @@ __device__ __forceinline__ void tx_tile_base(const TxChain& c, uint32_t t, uint3
 }
 
 constexpr uint32_t kTxSlow = 512;  // long-frame tiles: rows assembled byte by byte, listed per wave
+// Waves per tile of the long variant (EMURX_TXZ_LONG), A/B knob: split, every wave makes the
+// tile's segments itself and copies a contiguous part of its rows.  Measured on config E (1M
+// IMIX frames): 1 wave 263 us per call, 2 waves 262-268, 4 waves 288:
+// the launch's tail is not what E's write pays for.  1 (one wave per tile) kept.
+#ifndef EMURX_TX_SPLIT
+#define EMURX_TX_SPLIT 1
+#endif
+constexpr uint32_t kTxSplit = EMURX_TX_SPLIT;
 
 // OR a little-endian word v into LDS bytes [p, p + 4) (dwords at p >> 2 and the next one)
 __device__ __forceinline__ void lds_or4(uint32_t* o32, uint32_t p, uint32_t v) {
@@ -378,7 +386,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kTxImg == k
     __shared__ __attribute__((aligned(16))) uint32_t s_img[4][kLds / 4];
     __shared__ uint32_t s_q[4][2 * kWave];
     const uint32_t wv = threadIdx.x / kWave, lane = lane_id();
-    const uint32_t t = blockIdx.x * 4 + wv;
+    // the long variant (no image): kTxSplit waves per tile, each making the tile's segments itself
+    // and copying its share of the tile's rows
+    constexpr uint32_t kSplit = kTxImg == 0 ? kTxSplit : 1u;
+    const uint32_t gw = blockIdx.x * 4 + wv, t = gw / kSplit, part = gw % kSplit;
     if (t >= ntiles) return;  // wave-uniform
     const uint32_t base = t * kTxTile;
     // loads that wait on nothing first: this and the next tile's descriptors, the tile base
@@ -523,7 +534,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kTxImg == k
 #define EMURX_TX_KU 4
 #endif
     constexpr uint32_t kU = EMURX_TX_KU;  // rows per lane per round, their loads in flight together
-    for (uint32_t r0 = 0; r0 < nrow; r0 += kU * kWave) {  // wave-uniform trip count
+    // this wave's share of the rows: kSplit contiguous parts, whole 64-row groups each
+    const uint32_t per = kSplit == 1 ? nrow : ((nrow + kSplit - 1) / kSplit + kWave - 1) & ~(kWave - 1);
+    const uint32_t rbeg = min(nrow, part * per), rend = min(nrow, rbeg + per);
+    for (uint32_t r0 = rbeg; r0 < rend; r0 += kU * kWave) {  // wave-uniform trip count
         uint4 cur[kU], nxt[kU];
         uint32_t sh[kU], kk[kU];
         bool fast[kU];
@@ -535,7 +549,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kTxImg == k
             cur[u] = nxt[u] = make_uint4(0, 0, 0, 0);
             sh[u] = 0;
 #ifdef EMURX_TX_PURECOPY  // timing only: every row a copy from the frames buffer's first 256 MiB
-            if (r < nrow && xb + 16ull * r + 16 <= cap) {
+            if (r < rend && xb + 16ull * r + 16 <= cap) {
 #ifndef EMURX_TX_PC_OFF
 #define EMURX_TX_PC_OFF 5
 #endif
@@ -548,7 +562,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kTxImg == k
             }
             if (false) {
 #else
-            if (r < nrow) {
+            if (r < rend) {
 #endif
                 const int y0 = (int)(16 * r) - (int)head;
                 const uint32_t yc = y0 < 0 ? 0u : (uint32_t)y0;
@@ -580,7 +594,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kTxImg == k
                 }
                 *reinterpret_cast<uint4*>(out + xb + 16ull * r) = make_uint4(o[0], o[1], o[2], o[3]);
             }
-            const bool slw = r < nrow && !fast[u];
+            const bool slw = r < rend && !fast[u];
             const uint64_t m = __ballot(slw);
             const uint32_t at = nslow + mbcnt(m);
             if (slw) {
@@ -669,10 +683,12 @@ int emurx_launch_tx_zmq(const uint8_t* frames, const emurx_desc* desc, uint32_t 
     c.L = L;
     const uint32_t nt = c.ntiles;
     hipError_t e = emurx_launch(k_txz_chain, dim3(c.units[1]), dim3(kTxUnitWaves * kWave), 0, st, desc, c);
-    if (e == hipSuccess)
+    if (e == hipSuccess) {
+        const uint32_t waves = variant == EMURX_TXZ_LONG ? nt * kTxSplit : nt;  // the long variant: kTxSplit waves per tile
         e = emurx_launch(variant == EMURX_TXZ_NARROW ? k_txz_emit<kTxImgNarrow>
                          : variant == EMURX_TXZ_LONG ? k_txz_emit<0>
                                                      : k_txz_emit<kTxImgWide>,
-                         dim3((nt + 3) / 4), dim3(256), 0, st, frames, desc, n, nt, c, out, (unsigned long long)cap, mo);
+                         dim3((waves + 3) / 4), dim3(256), 0, st, frames, desc, n, nt, c, out, (unsigned long long)cap, mo);
+    }
     return EMURX_HIP_OK(e) ? 0 : -1;
 }
