@@ -513,6 +513,17 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         xch["lib"] = world > 1 and a.backend == "nccl" and a.comm == "library"
         xch["payload"] = a.a2a == "v"
         if xch["lib"]:
+            # every rank binds RCCL before any joins the communicator (ncclCommInitRank waits for
+            # all ranks): should one fail to, every rank takes torch.distributed instead, together
+            from emurx.rx import comm_library
+            xch["comm_library"] = comm_library()
+            lib_ok = torch.tensor([1 if xch["comm_library"] else 0], dtype=torch.int64, device=dev)
+            dist.all_reduce(lib_ok, op=dist.ReduceOp.MIN)
+            if not int(lib_ok.item()):
+                xch["lib"] = False
+                xch["comm_fallback"] = "a rank could not bind RCCL (emurx_comm_library): torch.distributed"
+                progress(rank, xch["comm_fallback"])
+        if xch["lib"]:
             from emurx.rx import comm_unique_id
             uid = torch.zeros(128, dtype=torch.uint8, device=dev)
             if rank == 0:
@@ -1103,6 +1114,8 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
                            ("counts, host waits, then the spans that carry data" if xch["payload"]
                             else "whole regions, no host synchronisation")) if world > 1 else "none (1 rank)",
             "transfer_mode": ("payload" if xch["payload"] else "equal") if world > 1 else None,
+            "comm_fallback": xch.get("comm_fallback"),
+            "comm_library": xch.get("comm_library"),
             "a2a_choice": xch.get("a2a_choice"),
             "overlapped": overlapped,  # batch k's all-to-all beside batch k+1's parse (two buffer sets)
             "includes": ("k_rx + group scan + pack" + (" + all-to-all" if world > 1 else "") +

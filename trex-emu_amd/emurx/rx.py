@@ -392,6 +392,15 @@ class RxPath:
         return dict(delta_blocks=a.value, whole_tables=b.value, table_bytes=c.value)
 
 
+def comm_library():
+    """Path of the RCCL the library's communicators use (emurx_comm_library: bound at the first
+    call), or None when none loads."""
+    _torch_first()
+    b = C.create_string_buffer(1024)
+    rc = abi.load().emurx_comm_library(b, 1024)
+    return b.value.decode() if rc == abi.EMURX_OK else None
+
+
 def _torch_first():
     """Before the library binds RCCL (its first communicator call): torch, when installed, is
     imported first, so that the process has one ROCm runtime and one RCCL (torch's bundled
