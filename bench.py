@@ -31,7 +31,8 @@ regions, with the per-region counts in a second all-to-all, and the owner resolv
 The JSON line carries `roofline` (algorithmic bytes per frame = frame_len + 8 B descriptor
 + 32 B record + 4 B queue entry, over k_rx's duration with each launch alone: the same --steps
 launches back to back on one stream over the rotating slots, one HIP event pair around them;
-`roofline.pipelined` is the timed region's launch interval on the S streams, and
+`roofline.pipelined` is the launch interval on the S streams of a second region of the same
+steps right after the timed one (the wall-timed region itself carries no events), and
 `roofline.cache_resident_replay` the round-2 replay of one batch per stream, labelled as such)
 and `cpu_baseline` (the oracle, a single-threaded C restatement of the Go path, timed on this
 host's cores over a bounded sample of the same workload; rank 0 at N=1 only).
@@ -83,12 +84,13 @@ def parse_args():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--time-stride", type=int, default=4,
-                    help="record HIP events around every N-th launch of the timed region")
+                    help="record HIP events around every N-th launch of the timing pass (the timed region's steps once "
+                         "more, after it)")
     ap.add_argument("--kernel-timing", default="region", choices=["region", "launch", "off"],
-                    help="steps that are one k_rx launch (no exchange): region = one HIP event pair "
-                         "around the whole timed region, duration = elapsed / launches; launch = "
-                         "events around every --time-stride-th launch (each pair adds ~1.5 us to "
-                         "the step it brackets); off = wall clock only")
+                    help="steps that are one k_rx launch (no exchange): region = an event pair per stream around "
+                         "a second region of the same steps (the launch interval) and one around launches "
+                         "back to back on one stream (each launch alone); launch = events around every "
+                         "--time-stride-th launch of a timing pass; off = wall clock only")
     ap.add_argument("--streams", type=int, default=2,
                     help="steps without an exchange: consecutive batches go round-robin to this many "
                          "streams, each with its own output buffers, so a batch's k_rx runs beside the "
@@ -869,10 +871,11 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
 
     progress(rank, f"config {cfg} {mode}: tables and batches ready, warmed up ({time.perf_counter() - t_start:.1f} s)")
     region = xch is None and a.kernel_timing == "region"
-    if xch is not None or a.kernel_timing == "launch":
-        rx.set_timing(steps + 8, a.time_stride)
+    # per-launch / per-batch HIP events (the exchange's phases, --kernel-timing launch) are
+    # recorded in a second pass of the same steps after the timed region, never inside it
+    timed_pass = xch is not None or a.kernel_timing == "launch"
     if xch is not None:
-        xch["timing"] = True
+        xch["timing"] = False
         xch["ev"] = []
         xch["pool"] = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                        for _ in range(steps // a.time_stride + 1)]
@@ -910,15 +913,14 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
     overlapped = xch is not None and len(xch["sets"]) > 1
     if overlapped:
         xch["k"] = 0
-    if region:
-        region_open()
+    # the timed region holds the steps alone: its launch-interval events come from a second
+    # region of the same steps right after it (an event pair per stream inside the wall-timed
+    # region cost the 20-step command ~3 %, profiles/r06/ab_events/)
     t0 = time.perf_counter()
     for _ in range(steps):
         step_overlapped() if overlapped else step()
     if overlapped:
         drain()
-    if region:
-        region_close()
     t_submit = time.perf_counter() - t0
     torch.cuda.synchronize()
     if world > 1:
@@ -928,6 +930,13 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         sanity()
     interval = None
     if region:
+        # the launch interval: the same steps again (the batch rotation continuing), an event
+        # pair on every stream, earliest start to latest end
+        region_open()
+        for _ in range(steps):
+            step()
+        region_close()
+        torch.cuda.synchronize()
         interval = region_ms() / steps
         # each launch alone (after the timed region, which runs straight after the time-based
         # warmup): the same rotation of batch slots, back to back on one stream
@@ -950,8 +959,25 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             replay = region_ms() / steps
         pk = [one]
     else:
-        pk = rx.kernel_times()
-        rx.set_timing(0)
+        pk = []
+        if timed_pass:
+            # the timing pass: the timed region's steps once more with the library's launch
+            # events (every --time-stride-th launch) and the batches' event pairs on
+            rx.set_timing(steps + 8, a.time_stride)
+            if xch is not None:
+                xch["timing"] = True
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            for _ in range(steps):
+                step_overlapped() if overlapped else step()
+            if overlapped:
+                drain()
+            torch.cuda.synchronize()
+            pk = rx.kernel_times()
+            rx.set_timing(0)
+            if xch is not None:
+                xch["timing"] = False
     if xch is not None and any(exchange_overflow(dict(xch, send_count=b["send_count"]), world, dist, torch, dev)
                                for b in xch["sets"]):
         raise RuntimeError("exchange region overflow in the timed region")
@@ -1058,7 +1084,8 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
                                    "region: elapsed / launches = each launch alone (what rocprofv3's kernel "
                                    "trace times, plus the ~1 us dispatch gap between launches)" if region else
                                    f"HIP events on the launch stream around every {a.time_stride}-th "
-                                   "k_rx launch of the timed region"),
+                                   "k_rx launch of a second pass of the timed region's steps (the timed region "
+                                   "itself carries no events)"),
         },
         "warmup_seconds": round(warm_s, 3),
         "host_submit_ms_per_step": round(t_submit / steps * 1e3, 5),
@@ -1067,9 +1094,10 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         out["roofline"]["pipelined"] = {
             "interval_ms": round(interval, 5), "achieved": round(alg_bytes / (interval * 1e-3) / 1e9, 1),
             "frac": round(alg_bytes / (interval * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "streams": S,
-            "source": f"the timed region: a HIP event pair on each of the {S} streams (no cross-stream waits), "
-                      "earliest start to latest end / launches = the launch interval in steady state (each launch "
-                      "overlaps its neighbours)"}
+            "source": f"a second region of the timed region's steps right after it: a HIP event pair on each of the "
+                      f"{S} streams (no cross-stream waits), earliest start to latest end / launches = the launch "
+                      "interval in steady state (each launch overlaps its neighbours); the wall-timed region itself "
+                      "carries no events"}
     if mode == "none" and cfg == "D" and world == 1 and pmc.exists():
         # D classification (k_rx probing 1.75 GB of sparse tables) against the random-line bound,
         # as the owner's k_lookup: the excess FETCH of the calibrated PMC is probe lines
