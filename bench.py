@@ -711,54 +711,57 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
             xch["ev"].append(ev)
 
     def phase_breakdown(reps=None):
-        """Device time per phase of the exchange step, each phase bracketed by HIP events on the
-        launch stream, over `reps` steps run one after the other (no overlap): the source side
-        (owner counts + group scan + k_rx packing the lookup records, or k_rx + scan + route
-        packing), k_rx alone (the library's events around its launch), the all-to-all (counts +
+        """Device time per phase of the exchange step, each phase as `reps` calls back to back
+        on the launch stream between one HIP event pair (an event between two phases adds a
+        barrier and a cache write-back of its own: round 6 measured the old per-phase events
+        inflating the owner-count + scan phase from 12 to 69 us): the source side (owner counts +
+        group scan + k_rx packing the lookup records, or k_rx + scan + route packing), k_rx alone
+        (the library's events around its launch, a second pass), the all-to-all (counts +
         regions; RCCL's stream joined back into the launch stream), the owner's k_lookup; and
         the bytes that crossed to other ranks (whole regions: the all-to-all is equal-split) and
         the payload among them (heads + tail units, or routed records)."""
         reps = reps or max(4, min(steps, 30))
-        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(reps)]
-        rx.set_timing(reps + 8, 1)
         b = xch["sets"][0]
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        # hold the launch stream (a ~20 ms spin) while the host enqueues every step, so the
-        # events time the device work back to back, not the host's enqueue of each call
-        with torch.cuda.stream(stream):
-            torch.cuda._sleep(50_000_000)
-        for k in range(reps):
-            e = ev[k]
-            e[0].record(stream)
-            produce(b, k)
-            e[1].record(stream)
+        pairs = {}
+
+        def group(name, fn):
+            """fn(k) for k < reps between one event pair on the launch stream (one warm call
+            first); the host enqueues them behind a spin so the pair times the device work"""
+            fn(0)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
             if world > 1:
-                recv, rc, sent = x_sync(b)
-            else:
-                recv, rc = b["send"], b["send_count"]
-            e[2].record(stream)
-            if mode == "partitioned":
-                rx.lookup_dev(recv, rc, world, xch["cap"], b["out"], stream=stream, tail_cap=xch["tcap"])
-            e[3].record(stream)
-        look_b2b = None
+                dist.barrier()
+            with torch.cuda.stream(stream):
+                torch.cuda._sleep(20_000_000)
+            e0.record(stream)
+            for k in range(reps):
+                fn(k)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            pairs[name] = e0.elapsed_time(e1) / reps
+
+        res = {}
+
+        def a2a(k):
+            res["x"] = x_sync(b) if world > 1 else (b["send"], b["send_count"], 0)
+
+        group("src", lambda k: produce(b, k))
+        a2a(0)
+        recv, rc, sent = res["x"]
+        if world > 1:
+            group("a2a", a2a)
         if mode == "partitioned":
-            # the owner's k_lookup alone: `reps` launches back to back between one event pair (the
-            # phase events above add their own barrier to every phase they bracket), per launch
-            # what rocprofv3's kernel trace times plus the dispatch gap
-            l0, l1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            l0.record(stream)
-            for _ in range(reps):
-                rx.lookup_dev(recv, rc, world, xch["cap"], b["out"], stream=stream, tail_cap=xch["tcap"])
-            l1.record(stream)
-        torch.cuda.synchronize()
-        if look_b2b is None and mode == "partitioned":
-            look_b2b = l0.elapsed_time(l1) / reps
+            group("look", lambda k: rx.lookup_dev(recv, rc, world, xch["cap"], b["out"], stream=stream,
+                                                  tail_cap=xch["tcap"]))
+        # k_rx alone: the library's events around each launch of a second source-side group
+        rx.set_timing(reps + 8, 1)
+        group("src_timed", lambda k: produce(b, k))
         krx = rx.kernel_times()
         rx.set_timing(0)
-        ms = np.array([[e[j].elapsed_time(e[j + 1]) for j in range(3)] for e in ev[1:]])  # the first: warm
-        src, a2a, look = (float(np.mean(ms[:, j])) for j in range(3))
+        src, a2a_ms = pairs["src"], pairs.get("a2a", 0.0)
+        look = pairs.get("look")
+        look_b2b = look
         k_rx_ms = float(np.mean(krx[1:])) if len(krx) > 1 else float("nan")
         sc = b["send_count"].cpu().numpy().astype(np.int64)[0::xch["cs"]]
         others = [d for d in range(world) if d != rank]
@@ -774,9 +777,9 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
                 units[d] = int(X.tail_units(hd["w4"]).sum())
         payload = int(sum(int(sc[d]) * rb + 16 * units[d] for d in others))
         to_others = int(sum(int(sc[d]) for d in others))
-        out = {"steps": reps - 1, "source_side_ms": round(src, 5), "k_rx_ms": round(k_rx_ms, 5),
+        out = {"steps": reps, "source_side_ms": round(src, 5), "k_rx_ms": round(k_rx_ms, 5),
                ("owner_count_scan_ms" if mode == "partitioned" else "scan_pack_ms"): round(src - k_rx_ms, 5),
-               "all_to_all_ms": round(a2a, 5), "owner_lookup_ms": round(look, 5) if mode == "partitioned" else 0.0,
+               "all_to_all_ms": round(a2a_ms, 5), "owner_lookup_ms": round(look, 5) if mode == "partitioned" else 0.0,
                "owner_lookup_kernel_ms": round(look_b2b, 5) if look_b2b is not None else None,
                "record_bytes": rb, "tail_units_per_shard": xch["tcap"], "region_bytes": xch["region"],
                "tail_bytes_per_frame": round(16 * sum(units) / max(int(sc.sum()), 1), 3),
@@ -786,11 +789,12 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
                "frames_to_other_ranks": to_others,
                "bytes_per_frame_to_other_ranks": round(moved / to_others, 2) if to_others else None,
                "payload_bytes_per_frame_to_other_ranks": round(payload / to_others, 2) if to_others else None,
-               "source": "HIP events on the launch stream between the phases of non-overlapped steps; k_rx by the "
-                         "library's events around its launch"}
-        if world > 1 and a2a > 0:
-            out["xgmi_gbs"] = round(moved / (a2a * 1e-3) / 1e9, 2)
-            out["xgmi_payload_gbs"] = round(payload / (a2a * 1e-3) / 1e9, 2)
+               "source": f"each phase as {reps} calls back to back on the launch stream between one HIP event pair "
+                         "(no events between phases); k_rx by the library's events around each launch of a "
+                         "second source-side group"}
+        if world > 1 and a2a_ms > 0:
+            out["xgmi_gbs"] = round(moved / (a2a_ms * 1e-3) / 1e9, 2)
+            out["xgmi_payload_gbs"] = round(payload / (a2a_ms * 1e-3) / 1e9, 2)
         return out
 
     def warm_for_time():
