@@ -1270,8 +1270,10 @@ int emurx_set_timing(emurx_t* h, uint32_t slots, uint32_t stride) {
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
     h->ev.assign((size_t)slots * 2, nullptr);
+    // timing only: no system-scope fence at the record (on gfx950 that fence is a cache
+    // write-back and invalidate, which both inflated the bracketed launch and slowed the next)
     for (auto& e : h->ev)
-        if (!EMURX_HIP_OK(hipEventCreate(&e))) { h->slots = 0; return EMURX_EDEVICE; }
+        if (!EMURX_HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence))) { h->slots = 0; return EMURX_EDEVICE; }
     h->slots = slots;
     h->stride = stride ? stride : 1;
     h->ev_head = h->ev_count = h->batch_seq = 0;

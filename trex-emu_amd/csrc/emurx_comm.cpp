@@ -135,11 +135,18 @@ int new_state(emurx_t* h, uint32_t nranks, uint32_t rank, emurx_comm_state** out
     c->rank = rank;
     const char* e = getenv("EMURX_COMM_SELF");
     c->self_rccl = e && !strcmp(e, "rccl");
+    // ev_in / ev_out order two streams of one device (the caller's and the communicator's): a
+    // device-scope release is enough, and the default system-scope one writes back and
+    // invalidates the caches at every exchange (EMURX_COMM_FENCE=system restores it).  The
+    // counts event (payload mode) is waited for by the host after a copy to pinned memory:
+    // system scope
+    const char* f = getenv("EMURX_COMM_FENCE");
+    const unsigned order = hipEventDisableTiming | (f && !strcmp(f, "system") ? 0u : hipEventDisableSystemFence);
     if (!EMURX_HIP_OK(hipHostMalloc((void**)&c->h_counts, 4 * EMURX_MAX_PARTS * sizeof(uint32_t), hipHostMallocDefault)) ||
         !EMURX_HIP_OK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking)) ||
         !EMURX_HIP_OK(hipEventCreateWithFlags(&c->ev, hipEventDisableTiming)) ||
-        !EMURX_HIP_OK(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming)) ||
-        !EMURX_HIP_OK(hipEventCreateWithFlags(&c->ev_out, hipEventDisableTiming))) {
+        !EMURX_HIP_OK(hipEventCreateWithFlags(&c->ev_in, order)) ||
+        !EMURX_HIP_OK(hipEventCreateWithFlags(&c->ev_out, order))) {
         emurx_comm_free(c);
         return EMURX_EDEVICE;
     }
