@@ -267,10 +267,19 @@ def spawn_ranks(a):
     return rc
 
 
+JSON_OUT = sys.stdout  # main() points it at the process's original stdout
+
+
 def main():
     a = parse_args()
     if a.gpus > 1 and "RANK" not in os.environ:
         sys.exit(spawn_ranks(a))
+    # stdout carries the one JSON line and nothing else: the rest of what this process writes
+    # there (RCCL prints a version banner on stdout when a communicator is created) goes to stderr
+    global JSON_OUT
+    sys.stdout.flush()
+    JSON_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", str(a.gpus)))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -344,7 +353,7 @@ def main():
         if "host_inclusive" in out and a.config == "B" and "batch_latency_by_msgs" in out["host_inclusive"]:
             out["host_inclusive"]["crossover"] = crossover(out["host_inclusive"], out["cpu_baseline"]["value"])
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=JSON_OUT, flush=True)
     rx.close()
     if world > 1:
         dist.destroy_process_group()
@@ -397,6 +406,8 @@ def launch_check(a, rank, world, dist, torch):
         return 3  # test hook: a rank that dies before the rendezvous completes
     if os.environ.get("EMURX_BENCH_HANG"):
         time.sleep(600)  # test hook: every rank stuck (as in a collective whose peer is gone)
+    if os.environ.get("EMURX_BENCH_STDOUT_NOISE"):
+        os.write(1, b"RCCL version : banner\n")  # test hook: a library writing to the stdout fd
     if world > 1:
         dist.init_process_group("gloo")
         dist.barrier()
@@ -405,7 +416,7 @@ def launch_check(a, rank, world, dist, torch):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     if rank == 0:
         print(json.dumps({"launch_check": "ok", "n_gpus": world, "max_over_ranks": float(t.item()),
-                          "master": os.environ.get("MASTER_ADDR")}), flush=True)
+                          "master": os.environ.get("MASTER_ADDR")}), file=JSON_OUT, flush=True)
     if world > 1:
         dist.destroy_process_group()
     return 0

@@ -34,6 +34,17 @@ def test_spawned_ranks_gloo(n):
 
 
 @pytest.mark.timeout(180)
+def test_stdout_holds_the_json_line_only():
+    """What a library writes to the stdout descriptor (RCCL's version banner at communicator
+    creation) lands on stderr: the driver reads one JSON line from rank 0's stdout."""
+    p = run(["--gpus", "2", "--backend", "gloo", "--launch-check"], env={"EMURX_BENCH_STDOUT_NOISE": "1"})
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert len(p.stdout.splitlines()) == 1, p.stdout
+    assert json.loads(p.stdout)["launch_check"] == "ok"
+    assert p.stderr.count("RCCL version : banner") == 2  # both ranks'
+
+
+@pytest.mark.timeout(180)
 def test_failed_rank_ends_the_run():
     p = run(["--gpus", "2", "--backend", "gloo", "--launch-check"], env={"EMURX_BENCH_FAIL_RANK": "1"})
     assert p.returncode == 3, (p.returncode, p.stderr[-2000:])

@@ -320,6 +320,11 @@ int emurx_exchange_dev(emurx_t* h, const void* d_send, const uint32_t* d_send_co
     if (!EMURX_HIP_OK(hipEventRecord(c->ev_in, user)) || !EMURX_HIP_OK(hipStreamWaitEvent(c->st, c->ev_in, 0)))
         return EMURX_EDEVICE;
     hipStream_t st = c->st;
+    // whole regions: the own region's device copy goes on the caller's stream, beside the
+    // peers' transfers on the communicator's (the caller's stream waits for those anyway
+    // before it reads the receive buffer); payload mode copies its spans on the communicator's
+    // stream, behind the counts the host waits for
+    hipStream_t self_st = payload ? st : user;
     const uint32_t P = c->nranks, me = c->rank, cs = route ? 1u : 2u;
     const uint64_t rb = route ? sizeof(emurx_route_rec) : sizeof(emurx_lookup_rec);
     const uint64_t heads_end = (uint64_t)cap * rb;
@@ -335,8 +340,8 @@ int emurx_exchange_dev(emurx_t* h, const void* d_send, const uint32_t* d_send_co
     for (uint32_t p = 0; p < P && ok; ++p) {
         const bool self = p == me;
         if (self && !c->self_rccl) {
-            ok = EMURX_HIP_OK(hipMemcpyAsync(d_recv_count + p * cs, d_send_count + p * cs, cs * 4, D2D, st));
-            if (ok && !payload) ok = EMURX_HIP_OK(hipMemcpyAsync(rbp(p), sb(p), region, D2D, st));
+            ok = EMURX_HIP_OK(hipMemcpyAsync(d_recv_count + p * cs, d_send_count + p * cs, cs * 4, D2D, self_st));
+            if (ok && !payload) ok = EMURX_HIP_OK(hipMemcpyAsync(rbp(p), sb(p), region, D2D, self_st));
             continue;
         }
         ok = nccl_ok(R->Send(d_send_count + p * cs, cs, ncclUint32, (int)p, c->comm, st), "ncclSend") &&
