@@ -155,3 +155,82 @@ def test_comm_init_all_group(dtabs):
         assert recv.tobytes() == send.tobytes()
     finally:
         rx.comm_destroy()
+
+
+def _comm(rx):
+    from emurx.rx import comm_unique_id
+    rx.comm_init(comm_unique_id(), 1, 0)
+
+
+def test_route_records_exchange(dtabs):
+    """EMURX_XCH_ROUTE: the replicated alternative's 40-byte route records (emurx_classify_route_dev's
+    regions, one count per region) through the library communicator, both transfer modes: the
+    counts and every routed record arrive as sent, and they are the host restatement's routing of
+    the oracle's records."""
+    import torch
+    import route_ref
+    from emurx import exchange as X
+    rx, o, shards = dtabs
+    w = shards[0]
+    n = len(w["desc"])
+    orec = o.rx_batch(w["buf"], w["desc"])[0]
+    want = route_ref.route(orec, 1, 0)[0]
+    buf, desc = to_dev(w["buf"]), to_dev(w["desc"])
+    qcap = abi.queue_cap(n)
+    ql = torch.empty(abi.NUM_QUEUES * qcap, dtype=torch.int32, device="cuda")
+    tc = torch.empty(abi.ntiles(n) * 16, dtype=torch.int32, device="cuda")
+    hi = torch.zeros(abi.HIST_SHARDS * 2 * abi.HIST_BINS, dtype=torch.int64, device="cuda")
+    rec = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    cap = X.capacity(n, 1)
+    send = torch.full((cap * X.REC_BYTES,), 0xEE, dtype=torch.uint8, device="cuda")
+    sc = torch.full((1,), -1, dtype=torch.int32, device="cuda")
+    rx.classify_route_dev(buf, desc, n, rec, ql, qcap, tc, hi, 1, 0, cap, send, sc)
+    _comm(rx)
+    try:
+        for payload in (False, True):
+            recv = torch.full_like(send, 0x5A)
+            rc = torch.full_like(sc, -1)
+            moved = rx.exchange_dev(send, sc, recv, rc, cap, payload=payload, route=True)
+            torch.cuda.synchronize()
+            c = int(sc.cpu()[0])
+            assert moved == 0 and int(rc.cpu()[0]) == c == len(want)
+            got = recv.cpu().numpy()[: c * X.REC_BYTES].view(abi.ROUTE_REC_DTYPE)
+            assert got.tobytes() == send.cpu().numpy()[: c * X.REC_BYTES].tobytes()
+            assert got.tobytes() == np.asarray(want, dtype=abi.ROUTE_REC_DTYPE).tobytes()
+    finally:
+        rx.comm_destroy()
+
+
+def test_exchange_overflow_reports_the_full_count(dtabs):
+    """A region sized below the batch (cap = n / 2): the source packs cap heads and reports the
+    full count, the exchange moves the cap heads that exist (whole regions, or the spans
+    min(count, cap) in payload mode) and delivers the full count, which is how the caller sees
+    the overflow and regrows (bench.py exchange_overflow)."""
+    import torch
+    rx, o, shards = dtabs
+    w = shards[1]
+    n = len(w["desc"])
+    cap = n // 2
+    tcap = abi.tail_capacity(cap)
+    buf, desc = to_dev(w["buf"]), to_dev(w["desc"])
+    qcap = abi.queue_cap(n)
+    ql = torch.empty(abi.NUM_QUEUES * qcap, dtype=torch.int32, device="cuda")
+    tc = torch.empty(abi.ntiles(n) * 16, dtype=torch.int32, device="cuda")
+    hi = torch.zeros(abi.HIST_SHARDS * 2 * abi.HIST_BINS, dtype=torch.int64, device="cuda")
+    send = torch.full((abi.lookup_region_bytes(cap, tcap),), 0xEE, dtype=torch.uint8, device="cuda")
+    sc = torch.full((2,), -1, dtype=torch.int32, device="cuda")
+    rx.parse_route_dev(buf, desc, n, None, ql, qcap, tc, hi, 1, 0, cap, send, sc, tail_cap=tcap)
+    _comm(rx)
+    try:
+        for payload in (False, True):
+            recv = torch.full_like(send, 0x5A)
+            rc = torch.full_like(sc, -1)
+            rx.exchange_dev(send, sc, recv, rc, cap, tcap, payload=payload)
+            torch.cuda.synchronize()
+            s, r = send.cpu().numpy(), recv.cpu().numpy()
+            assert int(sc.cpu()[0]) == n > cap
+            assert np.array_equal(rc.cpu().numpy(), sc.cpu().numpy())
+            assert r[: cap * 32].tobytes() == s[: cap * 32].tobytes()
+            assert r[cap * 32:].tobytes() == s[cap * 32:].tobytes()  # the tail shards (whole in both modes)
+    finally:
+        rx.comm_destroy()
