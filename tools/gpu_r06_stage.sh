@@ -1,4 +1,5 @@
 #!/bin/bash
+# (Record of a trial: emurx_ingest_stage and the staged pass were removed after this run.)
 # emurx_ingest_stage: the ingest GPU tests, then the host-inclusive passes of config B with the
 # receive staging every 1/parts of the batch (parts 4, 8, 16; two runs each, interleaved).
 set -u
