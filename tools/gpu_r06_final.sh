@@ -20,3 +20,11 @@ step bench_default 500 python -u bench.py
 step bench_N2_gloo 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
   --master-port 29571 bench.py --gpus 2 --backend gloo --steps 20 --warmup 5 --no-cpu-baseline
 echo "done $(date +%T)"
+# the driver's command under rocprofv3 kernel stats (the same bench, profiled)
+if [ "${PROF:-0}" = 1 ]; then
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $out/prof -o run --output-format csv \
+    -- python -u bench.py --gpus 1 --steps 20 --warmup 5 > $out/prof_driver.log 2>&1 || exit $?
+  f=$(ls $out/prof/*/run_kernel_stats.csv $out/prof/run_kernel_stats.csv 2>/dev/null | head -n 1)
+  cp "$f" $out/prof_driver_kernel_stats.csv && rm -rf $out/prof
+  echo "prof done $(date +%T)"
+fi
