@@ -155,7 +155,15 @@ __global__ __launch_bounds__(kScanThreads) void k_route_scan(uint32_t* __restric
 #ifndef EMURX_OC_STAGE
 #define EMURX_OC_STAGE 2048
 #endif
+// Tiles per workgroup: every tile's descriptors are loaded at the top (EMURX_OC_TPW loads in
+// flight per lane), the tiles then counted one after the other, and the workgroup's counts
+// added to its group once (its tiles share one group of 64)
+#ifndef EMURX_OC_TPW
+#define EMURX_OC_TPW 1
+#endif
 constexpr uint32_t kOcStage = EMURX_OC_STAGE;
+constexpr uint32_t kOcTpw = EMURX_OC_TPW;
+static_assert(kOcTpw >= 1 && kGroup % kOcTpw == 0, "a workgroup's tiles in one group");
 __global__ __launch_bounds__(kBlock) void k_owner_count(const uint8_t* __restrict__ frames,
                                                         const emurx_desc* __restrict__ desc, uint32_t n,
                                                         uint32_t n_parts, uint32_t* __restrict__ tile_cnt,
@@ -163,84 +171,98 @@ __global__ __launch_bounds__(kBlock) void k_owner_count(const uint8_t* __restric
     __shared__ uint32_t s_wcnt[kWaves][16];
     // the wave's staged bytes + 32 bytes of slack for the aligned dword reads past its end
     __shared__ __attribute__((aligned(16))) uint32_t s_stage[kWaves][(kOcStage + 32) / 4];
-    const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / kWave, tile = blockIdx.x;
-    const uint32_t i = tile * kBlock + tid;
-    if (lane < 16) s_wcnt[wv][lane] = 0;
-    const uint2 dd = i < n ? *reinterpret_cast<const uint2*>(desc + i) : make_uint2(0, EMURX_DESC_HOLE << 24);
-    const uint32_t pad = dd.y >> 24;
-    const bool valid = pad != EMURX_DESC_HOLE, keyed = valid && (pad & EMURX_DESC_KEYED);
-    const bool need = valid && !keyed;  // the owner must come from the frame's bytes
-    const uint32_t off = dd.x, len = dd.y & 0xffff;
-    uint32_t start = 0, nvec = 0;
-    if (__ballot(need)) {  // wave-uniform: a wave of keyed descriptors reads no frame byte
-        const uint32_t lo = wave_min_u32(need ? off : 0xffffffffu);
-        const uint32_t hi = wave_max_u32(need ? off + len : 0u);
-        start = lo & ~15u;
-        nvec = hi > lo ? (hi - start + 15) >> 4 : 0;
-    }
-    const bool staged = nvec > 0 && nvec <= kOcStage / 16;  // wave-uniform
-    if (staged) {
-        static_assert(kOcStage % (16 * kWave) == 0, "whole 1 KiB DMA rows");
-        const uint4* src = reinterpret_cast<const uint4*>(frames + start);
-        uint4* dst = reinterpret_cast<uint4*>(s_stage[wv]);
+    const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / kWave, t0 = blockIdx.x * kOcTpw;
+    const uint32_t ntiles = (n + kBlock - 1) / kBlock, tn = min(kOcTpw, ntiles - t0);
+    uint2 dds[kOcTpw];
 #pragma unroll
-        for (uint32_t k = 0; k < kOcStage / 16 / kWave; ++k)
-            if (k * kWave < nvec)
-                __builtin_amdgcn_global_load_lds(src + min(lane + k * kWave, nvec - 1),
-                                                 (__attribute__((address_space(3))) void*)(dst + k * kWave), 16, 0, 2);
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the wave's DMA landed
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (uint32_t k = 0; k < kOcTpw; ++k) {
+        const uint32_t i = (t0 + k) * kBlock + tid;
+        dds[k] = k < tn && i < n ? *reinterpret_cast<const uint2*>(desc + i) : make_uint2(0, EMURX_DESC_HOLE << 24);
     }
-    uint32_t d = keyed ? emurx_owner_of_key(pad, n_parts) : 0xffu;
-    if (need) {
-        const uint32_t vport = (dd.y >> 16) & 0xff;
-        uint32_t w0 = 0, w1 = 0, w2 = 0, sh;
-        if (staged) {
-            // bytes past the frame are the next frame's or stale: l2_vlans reads a word only
-            // where len says its bytes exist
-            const uint32_t rel = off - start + 12;
-            sh = rel & 3;
-            const uint32_t* q = s_stage[wv] + (rel >> 2);
-            w0 = q[0]; w1 = q[1]; w2 = q[2];
-        } else {
-            // bytes 12..19 from the three aligned dwords around them, each loaded only when it
-            // holds a byte of the frame (an aligned dword never crosses the 64-byte boundary the
-            // buffer contract guarantees past the last byte, emu_rx.h): one 12-byte load for every
-            // frame of 21 bytes or more; l2_vlans reads a word only where len says its bytes exist
-            const uintptr_t a = (uintptr_t)(frames + off + 12);
-            sh = (uint32_t)(a & 3);
-            const uint32_t lim = len + sh;  // dword k holds a frame byte iff 12 + 4k < lim
-            const void* wa = reinterpret_cast<const void*>(a & ~(uintptr_t)3);
-            if (lim > 20) {
-                const uint3 w3 = gld12(wa);  // one 12-byte load
-                w0 = w3.x; w1 = w3.y; w2 = w3.z;
-            } else {
-                if (lim > 12) w0 = gld4(wa);
-                if (lim > 16) w1 = gld4(reinterpret_cast<const uint8_t*>(wa) + 4);
-            }
+    uint32_t gacc = 0;  // tid < 16: the workgroup's frames of owner tid
+#pragma unroll
+    for (uint32_t k = 0; k < kOcTpw; ++k) {
+        if (k >= tn) break;
+        const uint32_t tile = t0 + k;
+        if (lane < 16) s_wcnt[wv][lane] = 0;
+        const uint2 dd = dds[k];
+        const uint32_t pad = dd.y >> 24;
+        const bool valid = pad != EMURX_DESC_HOLE, keyed = valid && (pad & EMURX_DESC_KEYED);
+        const bool need = valid && !keyed;  // the owner must come from the frame's bytes
+        const uint32_t off = dd.x, len = dd.y & 0xffff;
+        uint32_t start = 0, nvec = 0;
+        if (__ballot(need)) {  // wave-uniform: a wave of keyed descriptors reads no frame byte
+            const uint32_t lo = wave_min_u32(need ? off : 0xffffffffu);
+            const uint32_t hi = wave_max_u32(need ? off + len : 0u);
+            start = lo & ~15u;
+            nvec = hi > lo ? (hi - start + 15) >> 4 : 0;
         }
-        const uint32_t b12 = __builtin_bswap32(__builtin_amdgcn_alignbyte(w1, w0, sh));
-        const uint32_t b16 = __builtin_bswap32(__builtin_amdgcn_alignbyte(w2, w1, sh));
-        uint32_t v0, v1;
-        l2_vlans(len, b12, b16, v0, v1);
-        d = emurx_owner(emurx_tk_hash(vport, v0, v1), n_parts);
+        const bool staged = nvec > 0 && nvec <= kOcStage / 16;  // wave-uniform
+        if (staged) {
+            static_assert(kOcStage % (16 * kWave) == 0, "whole 1 KiB DMA rows");
+            const uint4* src = reinterpret_cast<const uint4*>(frames + start);
+            uint4* dst = reinterpret_cast<uint4*>(s_stage[wv]);
+#pragma unroll
+            for (uint32_t j = 0; j < kOcStage / 16 / kWave; ++j)
+                if (j * kWave < nvec)
+                    __builtin_amdgcn_global_load_lds(src + min(lane + j * kWave, nvec - 1),
+                                                     (__attribute__((address_space(3))) void*)(dst + j * kWave), 16, 0, 2);
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the wave's DMA landed
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        uint32_t d = keyed ? emurx_owner_of_key(pad, n_parts) : 0xffu;
+        if (need) {
+            const uint32_t vport = (dd.y >> 16) & 0xff;
+            uint32_t w0 = 0, w1 = 0, w2 = 0, sh;
+            if (staged) {
+                // bytes past the frame are the next frame's or stale: l2_vlans reads a word only
+                // where len says its bytes exist
+                const uint32_t rel = off - start + 12;
+                sh = rel & 3;
+                const uint32_t* q = s_stage[wv] + (rel >> 2);
+                w0 = q[0]; w1 = q[1]; w2 = q[2];
+            } else {
+                // bytes 12..19 from the three aligned dwords around them, each loaded only when it
+                // holds a byte of the frame (an aligned dword never crosses the 64-byte boundary the
+                // buffer contract guarantees past the last byte, emu_rx.h): one 12-byte load for every
+                // frame of 21 bytes or more; l2_vlans reads a word only where len says its bytes exist
+                const uintptr_t a = (uintptr_t)(frames + off + 12);
+                sh = (uint32_t)(a & 3);
+                const uint32_t lim = len + sh;  // dword k holds a frame byte iff 12 + 4k < lim
+                const void* wa = reinterpret_cast<const void*>(a & ~(uintptr_t)3);
+                if (lim > 20) {
+                    const uint3 w3 = gld12(wa);  // one 12-byte load
+                    w0 = w3.x; w1 = w3.y; w2 = w3.z;
+                } else {
+                    if (lim > 12) w0 = gld4(wa);
+                    if (lim > 16) w1 = gld4(reinterpret_cast<const uint8_t*>(wa) + 4);
+                }
+            }
+            const uint32_t b12 = __builtin_bswap32(__builtin_amdgcn_alignbyte(w1, w0, sh));
+            const uint32_t b16 = __builtin_bswap32(__builtin_amdgcn_alignbyte(w2, w1, sh));
+            uint32_t v0, v1;
+            l2_vlans(len, b12, b16, v0, v1);
+            d = emurx_owner(emurx_tk_hash(vport, v0, v1), n_parts);
+        }
+        uint64_t left = __ballot(d != 0xffu);
+        while (left) {
+            const uint32_t lead = (uint32_t)__ffsll((long long)left) - 1;
+            const uint32_t q = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)lead);
+            const uint64_t m = __ballot(d == q);
+            if (lane == lead) s_wcnt[wv][q] = (uint32_t)__popcll(m);
+            left &= ~m;
+        }
+        __syncthreads();
+        if (tid < 16) {
+            const uint32_t c = s_wcnt[0][tid] + s_wcnt[1][tid] + s_wcnt[2][tid] + s_wcnt[3][tid];
+            tile_cnt[tile * 16 + tid] = c;
+            gacc += c;
+        }
+        if (kOcTpw > 1) __syncthreads();  // s_wcnt and the slabs are reused by the next tile
     }
-    uint64_t left = __ballot(d != 0xffu);
-    while (left) {
-        const uint32_t lead = (uint32_t)__ffsll((long long)left) - 1;
-        const uint32_t q = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)lead);
-        const uint64_t m = __ballot(d == q);
-        if (lane == lead) s_wcnt[wv][q] = (uint32_t)__popcll(m);
-        left &= ~m;
-    }
-    __syncthreads();
-    if (tid < 16) {
-        const uint32_t c = s_wcnt[0][tid] + s_wcnt[1][tid] + s_wcnt[2][tid] + s_wcnt[3][tid];
-        tile_cnt[tile * 16 + tid] = c;
-        if (c) atomicAdd(&grp[(tile / kGroup) * 16 + tid], c);
-    }
+    if (tid < 16 && gacc) atomicAdd(&grp[(t0 / kGroup) * 16 + tid], gacc);
 }
 
 // k_desc_keys: the owner key of every frame into its descriptor's pad byte (what the device
@@ -413,8 +435,8 @@ int emurx_launch_owner_count(const uint8_t* frames, const emurx_desc* desc, uint
     const uint32_t ntiles = (n + kBlock - 1) / kBlock, ngroups = (ntiles + kGroup - 1) / kGroup;
     if (n == 0) return EMURX_HIP_OK(hipMemsetAsync(send_count, 0, 2 * n_parts * sizeof(uint32_t), st)) ? 0 : -1;
     if (ngroups > kScanThreads) return -1;
-    if (!EMURX_HIP_OK(emurx_launch(k_owner_count, dim3(ntiles), dim3(kBlock), 0, st, frames, desc, n, n_parts,
-                                   tile_cnt, grp)))
+    if (!EMURX_HIP_OK(emurx_launch(k_owner_count, dim3((ntiles + kOcTpw - 1) / kOcTpw), dim3(kBlock), 0, st, frames,
+                                   desc, n, n_parts, tile_cnt, grp)))
         return -1;
     return EMURX_HIP_OK(emurx_launch(k_route_scan, dim3(1), dim3(kScanThreads), 0, st, grp, ngroups, n_parts, grp_off,
                                      send_count, tcur, 2u))
