@@ -730,6 +730,10 @@ int emurx_comm_info(emurx_t* h, uint32_t* nranks, uint32_t* rank);
    librccl.so.1: the copy already in the process if any, else the system's); its path into
    `path`.  EMURX_ECOMM when none loads. */
 int emurx_comm_library(char* path, size_t cap);
+/* A group is per OS thread (RCCL's ncclGroupStart / ncclGroupEnd are): emurx_group_start, the
+   group's exchanges and emurx_group_end must run on one thread (from Go: between
+   runtime.LockOSThread and runtime.UnlockOSThread).  emurx_group_end returns EMURX_EINVAL on a
+   thread with no open group. */
 int emurx_group_start(void);
 int emurx_group_end(void);
 /* One exchange of the regions emurx_parse_route_dev packed (lookup regions of
