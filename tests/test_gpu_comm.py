@@ -234,3 +234,39 @@ def test_exchange_overflow_reports_the_full_count(dtabs):
             assert r[cap * 32:].tobytes() == s[cap * 32:].tobytes()  # the tail shards (whole in both modes)
     finally:
         rx.comm_destroy()
+
+
+def test_empty_batch_exchange(dtabs):
+    """An empty batch through the whole owner step (emurx_parse_route_dev with n = 0 writes zero
+    counts, the exchange moves the counts and nothing to look up, k_lookup writes nothing), both
+    transfer modes; then a one-frame batch on the same buffers, bit-exact."""
+    import torch
+    rx, o, shards = dtabs
+    cap = 1024
+    tcap = abi.tail_capacity(cap)
+    send = torch.full((abi.lookup_region_bytes(cap, tcap),), 0xEE, dtype=torch.uint8, device="cuda")
+    sc = torch.full((2,), -1, dtype=torch.int32, device="cuda")
+    qcap = abi.queue_cap(256)
+    ql = torch.empty(abi.NUM_QUEUES * qcap, dtype=torch.int32, device="cuda")
+    tc = torch.empty(16, dtype=torch.int32, device="cuda")
+    hi = torch.zeros(abi.HIST_SHARDS * 2 * abi.HIST_BINS, dtype=torch.int64, device="cuda")
+    buf = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    desc = torch.zeros(8, dtype=torch.uint8, device="cuda")
+    rx.parse_route_dev(buf, desc, 0, None, ql, qcap, tc, hi, 1, 0, cap, send, sc, tail_cap=tcap)
+    _comm(rx)
+    try:
+        for payload in (False, True):
+            recv = torch.full_like(send, 0x5A)
+            rc = torch.full_like(sc, -1)
+            out = torch.full((cap * 40,), 0xEE, dtype=torch.uint8, device="cuda")
+            assert rx.exchange_dev(send, sc, recv, rc, cap, tcap, payload=payload) == 0
+            rx.lookup_dev(recv, rc, 1, cap, out, tail_cap=tcap)
+            torch.cuda.synchronize()
+            assert rc.cpu().tolist() == [0, 0]
+            assert (out.cpu().numpy() == 0xEE).all()  # nothing written
+        w = shards[0]
+        one = {"buf": w["buf"], "desc": w["desc"][:1]}
+        got, rc, moved, s, r, c = owner_step(rx, one, cap, tcap, False)
+        check_owner(o, one, got, rc, cap)
+    finally:
+        rx.comm_destroy()
