@@ -291,7 +291,7 @@ def transport_state(shards):
     return flows
 
 
-@pytest.mark.parametrize("parts", [2, 4])
+@pytest.mark.parametrize("parts", [2, 3, 4])
 def test_partitioned_lookups_equal_replicated(rxmod, parts):
     """Config C shards with bare SYNs, flows and listeners: records and flow decisions."""
     n = 40000
