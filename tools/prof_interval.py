@@ -3,8 +3,9 @@
     python tools/prof_interval.py <run_kernel_trace.csv> <steps>
 
 bench.py's pipelined steps (--streams 2, --batches 8) enqueue: the warmup launches, then the
-`steps` launches of the timed region alternating between the streams over the rotating slots
-(roofline.pipelined), then max(`steps`, 100) launches back to back on one stream over the
+`steps` launches of the timed region alternating between the streams over the rotating slots,
+then (since round 6) the same `steps` again between the interval events (roofline.pipelined;
+the group this tool reports as timed_region: the same pipeline), then max(`steps`, 100) launches back to back on one stream over the
 rotating batch slots (each launch alone: roofline.kernel_ms_mean / frac), then `steps` launches
 replaying one batch per stream (roofline.cache_resident_replay).  (Before the end of round 3 the timed region
 came last: --old-order.)  For those three groups of

@@ -45,7 +45,9 @@ for ph in $phases; do
         f=$(ls $out/prof_$c/*/run_kernel_stats.csv $out/prof_$c/run_kernel_stats.csv 2>/dev/null | head -n 1)
         [ -n "$f" ] && cut -d, -f1-4 "$f" | head -n 12
         t=$(ls $out/prof_$c/*/run_kernel_trace.csv $out/prof_$c/run_kernel_trace.csv 2>/dev/null | head -n 1)
-        [ -n "$t" ] && python tools/prof_interval.py "$t" $(args $c | sed 's/.*--steps \([0-9]*\).*/\1/') \
+        # B's default line ends with the host-inclusive block's isolated ingest launches: trimmed
+        trim=""; [ "$c" = B ] && trim="--kernel k_rx<1, --trim-isolated"
+        [ -n "$t" ] && python tools/prof_interval.py "$t" $(args $c | sed 's/.*--steps \([0-9]*\).*/\1/') $trim \
           | tee $out/prof_${c}_interval.json ;;
       pmc)
         for k in FETCH_SIZE WRITE_SIZE; do
