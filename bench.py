@@ -938,9 +938,12 @@ def measure(a, cfg, n, mode, steps, warmup, rank, world, local, dist, torch):
         drain()
     t_submit = time.perf_counter() - t0
     torch.cuda.synchronize()
+    # this rank's time: its K steps up to the synchronize that drains them.  The closing barrier
+    # aligns the ranks after it and stays out of the interval (its own latency, tens of us on
+    # nccl, is not step work); the max over ranks below is the slowest rank's time
+    el = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    el = time.perf_counter() - t0
     if not a.no_check and warmup == 0 and steps > 0:  # no warmup: check the timed steps' outputs
         sanity()
     interval = None
